@@ -1,0 +1,158 @@
+#!/usr/bin/env python3
+"""Training-throughput benchmark: RAFT-base, FlyingChairs-shaped synthetic pairs.
+
+Config (BASELINE.json config #2/#3): RAFT base, 368x496 crops, 12 GRU
+iterations, bf16 autocast, full training step = forward + sequence loss +
+backward + grad-clip + fused AdamW + OneCycle step.  Weak scaling: the
+per-GPU batch (``--batch``, default 8 = train_mixed.sh's chairs batch) is fixed
+and the global batch is ``batch * N``.  Multi-GPU runs are one process per GPU
+(torchrun) with DistributedDataParallel over RCCL.
+
+Prints ONE JSON line on rank 0 (see README "bench contract").  ``value`` is
+whole-job image pairs per second.  ``vs_baseline`` divides by the eager
+PyTorch baseline of the reference algorithm measured on the same MI355X
+("measured" row), when present.
+
+    python bench.py                      # 1 GPU, defaults
+    python bench.py --impl reference     # the reference's eager op sequence (baseline)
+    torchrun --nproc-per-node 8 bench.py --gpus 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from argparse import Namespace
+
+import torch
+import torch.distributed as dist
+
+METRIC = "image-pairs/sec training + Sintel-clean EPE, RAFT base at 1/2/4/8 MI355X"
+# Eager PyTorch baseline of the reference algorithm on 1x MI355X (pairs/s), see BASELINE.md
+BASELINE_PAIRS_PER_SEC = None
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--image_size", type=int, nargs=2, default=[368, 496])
+    ap.add_argument("--iters", type=int, default=12)
+    ap.add_argument("--impl", choices=["native", "reference"], default="native")
+    ap.add_argument("--small", action="store_true")
+    ap.add_argument("--amp_dtype", default="bf16", choices=["bf16", "fp16"])
+    ap.add_argument("--lr", type=float, default=4e-4)
+    ap.add_argument("--bucket_mb", type=float, default=32.0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if distributed:
+        dist.init_process_group("nccl", device_id=device)
+
+    from raft_ros_amd.data.synthetic import synthetic_batch
+    from raft_ros_amd.models import RAFT
+    from raft_ros_amd.ops import _ext
+    from raft_ros_amd.train.loss import sequence_loss
+    from raft_ros_amd.train.optim import fetch_optimizer
+
+    _ext.set_backend(args.impl)
+    torch.backends.cudnn.benchmark = True
+    torch.manual_seed(1234 + rank)
+    margs = Namespace(small=args.small, mixed_precision=True, amp_dtype=args.amp_dtype, alternate_corr=False,
+                      dropout=0.0, channels_last=args.impl == "native")
+    model = RAFT(margs).to(device)
+    if args.impl == "native":
+        model = model.to(memory_format=torch.channels_last)
+    model.train()
+    oargs = Namespace(lr=args.lr, wdecay=1e-4, epsilon=1e-8, num_steps=100000)
+    if distributed:
+        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=args.bucket_mb,
+                                                        gradient_as_bucket_view=True, static_graph=True)
+    else:
+        ddp = model
+    optimizer, scheduler = fetch_optimizer(oargs, model)
+    scaler = torch.amp.GradScaler("cuda", enabled=args.amp_dtype == "fp16")
+
+    H, W = args.image_size
+    pool = [synthetic_batch(args.batch, H, W, seed=rank * 97 + i, device=device) for i in range(4)]
+
+    def step(i):
+        i1, i2, flow, valid = pool[i % len(pool)]
+        optimizer.zero_grad(set_to_none=True)
+        preds = ddp(i1, i2, iters=args.iters)
+        loss, metrics = sequence_loss(preds, flow, valid, gamma=0.8)
+        scaler.scale(loss).backward()
+        scaler.unscale_(optimizer)
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        scaler.step(optimizer)
+        scheduler.step()
+        scaler.update()
+        return loss, metrics
+
+    for i in range(args.warmup):
+        loss, metrics = step(i)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss, metrics = step(args.warmup + i)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    pairs = args.batch * world * args.steps
+    value = pairs / elapsed
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "image-pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(value / (BASELINE_PAIRS_PER_SEC * world), 3)
+                            if BASELINE_PAIRS_PER_SEC and args.impl == "native" else None),
+            "dtype": args.amp_dtype,
+            "data": "synthetic (textured pairs warped by known smooth flow; random-init weights)",
+            "config": {
+                "model": "RAFT-small" if args.small else "RAFT-base",
+                "global_batch": args.batch * world,
+                "seq_len": args.iters,
+                "image_size": [H, W],
+                "iters": args.iters,
+                "parallelism": f"dp{world}",
+                "impl": args.impl,
+            },
+            "final_loss": round(float(loss.item()), 4),
+            "epe_synthetic": round(float(metrics["epe"].item()), 4),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    sys.exit(main())

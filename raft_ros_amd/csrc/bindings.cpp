@@ -1,0 +1,400 @@
+// Torch dispatcher registration of the raft_ros_amd native ops.
+//
+// The reference exposes its single native extension through pybind11
+// (alt_cuda_corr/correlation.cpp:51-54, forward/backward of the on-the-fly
+// correlation).  Here every native op is a TORCH_LIBRARY schema with a HIP
+// implementation on the CUDA(=HIP) dispatch key, launched on the current torch
+// HIP stream with error checks.  Autograd wiring lives in raft_ros_amd/ops/.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+namespace raft_amd {
+
+struct PyrDesc {
+  float* ptr[4];
+  int H[4];
+  int W[4];
+  int levels;
+};
+
+enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
+
+// launchers (defined in the .hip translation units)
+hipError_t launch_gemm_nt_bf16(const void* A, long lda, long strideA, const void* B, long ldb,
+                               long strideB, void* C, int out_dtype, long ldc, long strideC, int M,
+                               int N, int K, float alpha, int batch, hipStream_t stream);
+hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int W, hipStream_t s);
+hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void* out, int out_dtype,
+                                  int B, int H, int W, int r, hipStream_t s);
+hipError_t launch_corr_lookup_bwd(const PyrDesc& dpyr, const float* coords, const void* gout,
+                                  int g_dtype, int B, int H, int W, int r, hipStream_t s);
+hipError_t launch_pyramid_grad_combine(const PyrDesc& dpyr, void* dC, void* dCt, int B, int H,
+                                       int W, int ldp, float alpha, hipStream_t s);
+hipError_t launch_convex_up_fwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
+                                long msH, long msW, float* out, int B, int H, int W, hipStream_t s);
+hipError_t launch_convex_up_bwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
+                                long msH, long msW, const float* gout, void* dmask, float* part,
+                                float* dflow, int B, int H, int W, hipStream_t s);
+hipError_t launch_local_corr_fwd(const void* f1, const void* f2, int dtype, const float* coords,
+                                 float* out, int B, int H1, int W1, int H2, int W2, int C, int r,
+                                 float scale, hipStream_t s);
+hipError_t launch_local_corr_bwd(const void* f1, const void* f2, int dtype, const float* coords,
+                                 const float* gout, float* g1, float* g2, int B, int H1, int W1,
+                                 int H2, int W2, int C, int r, float scale, hipStream_t s);
+
+hipError_t launch_gru_gates_fwd(int dtype, const void* zr, const void* h, void* z, void* rh, long npix,
+                                int C, hipStream_t s);
+hipError_t launch_gru_gates_bwd(int dtype, const void* zr, const void* h, const void* gz,
+                                const void* grh, void* dzr, void* dh, long npix, int C, hipStream_t s);
+hipError_t launch_gru_blend_fwd(int dtype, const void* z, const void* q, const void* h, void* out,
+                                long numel, hipStream_t s);
+hipError_t launch_gru_blend_bwd(int dtype, const void* z, const void* q, const void* h, const void* g,
+                                void* dz, void* dq, void* dh, long numel, hipStream_t s);
+
+namespace {
+
+#define HIP_OK(expr)                                                                     \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    TORCH_CHECK(_e == hipSuccess, "raft_amd HIP error: ", hipGetErrorString(_e), " at ", \
+                __FILE__, ":", __LINE__);                                                  \
+  } while (0)
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int dtype_code(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return kF32;
+    case at::kBFloat16: return kBF16;
+    case at::kHalf: return kF16;
+    default: TORCH_CHECK(false, "raft_amd: unsupported dtype ", t);
+  }
+  return -1;
+}
+
+void check_gpu(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "raft_amd: ", name, " must be a GPU tensor");
+}
+
+PyrDesc make_desc(const std::vector<at::Tensor>& levels, long rows) {
+  TORCH_CHECK(levels.size() >= 1 && levels.size() <= 4, "raft_amd: 1..4 pyramid levels supported");
+  PyrDesc d{};
+  d.levels = static_cast<int>(levels.size());
+  for (size_t l = 0; l < levels.size(); ++l) {
+    const auto& t = levels[l];
+    check_gpu(t, "pyramid level");
+    TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous() && t.dim() == 3,
+                "raft_amd: pyramid levels must be contiguous fp32 (B*H*W, Hl, Wl)");
+    TORCH_CHECK(t.size(0) == rows, "raft_amd: pyramid level rows mismatch");
+    d.ptr[l] = t.data_ptr<float>();
+    d.H[l] = static_cast<int>(t.size(1));
+    d.W[l] = static_cast<int>(t.size(2));
+  }
+  return d;
+}
+
+// ---------------------------------------------------------------- GEMM
+at::Tensor gemm_nt(const at::Tensor& A, const at::Tensor& B, double alpha, at::ScalarType out_dtype) {
+  check_gpu(A, "A");
+  check_gpu(B, "B");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16,
+              "raft_amd::gemm_nt expects bf16 operands");
+  TORCH_CHECK(A.dim() == 3 && B.dim() == 3, "raft_amd::gemm_nt expects (batch, rows, K)");
+  TORCH_CHECK(A.stride(2) == 1 && B.stride(2) == 1, "raft_amd::gemm_nt: K must be contiguous");
+  const long batch = A.size(0), M = A.size(1), K = A.size(2), N = B.size(1);
+  TORCH_CHECK(B.size(0) == batch && B.size(2) == K, "raft_amd::gemm_nt: shape mismatch");
+  TORCH_CHECK(K % 64 == 0, "raft_amd::gemm_nt: K must be a multiple of 64 (got ", K, ")");
+  TORCH_CHECK(A.stride(1) % 8 == 0 && B.stride(1) % 8 == 0 && A.stride(0) % 8 == 0 &&
+                  B.stride(0) % 8 == 0,
+              "raft_amd::gemm_nt: row strides must be multiples of 8 elements");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
+              "raft_amd::gemm_nt: operands must be 16-byte aligned");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16,
+              "raft_amd::gemm_nt: out dtype must be fp32 or bf16");
+  const c10::DeviceGuard guard(A.device());
+  auto C = at::empty({batch, M, N}, A.options().dtype(out_dtype));
+  if (batch == 0 || M == 0 || N == 0) return C;
+  HIP_OK(launch_gemm_nt_bf16(A.data_ptr(), A.stride(1), A.stride(0), B.data_ptr(), B.stride(1),
+                             B.stride(0), C.data_ptr(), dtype_code(out_dtype), N, M * N, M, N, K,
+                             static_cast<float>(alpha), batch, cur_stream()));
+  return C;
+}
+
+// ---------------------------------------------------------------- pyramid
+at::Tensor avgpool2x2(const at::Tensor& x) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.dim() == 3, "raft_amd::avgpool2x2 expects fp32 (R,H,W)");
+  auto xc = x.contiguous();
+  const c10::DeviceGuard guard(x.device());
+  auto out = at::empty({x.size(0), x.size(1) / 2, x.size(2) / 2}, x.options());
+  HIP_OK(launch_avgpool2x2(xc.data_ptr<float>(), out.data_ptr<float>(), x.size(0), x.size(1),
+                           x.size(2), cur_stream()));
+  return out;
+}
+
+void check_coords(const at::Tensor& coords) {
+  check_gpu(coords, "coords");
+  TORCH_CHECK(coords.scalar_type() == at::kFloat && coords.is_contiguous() && coords.dim() == 4 &&
+                  coords.size(1) == 2,
+              "raft_amd: coords must be contiguous fp32 (B, 2, H, W)");
+}
+
+at::Tensor corr_lookup(at::TensorList pyramid, const at::Tensor& coords, int64_t radius,
+                       at::ScalarType out_dtype) {
+  check_coords(coords);
+  const long B = coords.size(0), H = coords.size(2), W = coords.size(3);
+  std::vector<at::Tensor> lv(pyramid.begin(), pyramid.end());
+  PyrDesc d = make_desc(lv, B * H * W);
+  const long win = (2 * radius + 1) * (2 * radius + 1);
+  const c10::DeviceGuard guard(coords.device());
+  auto out = at::empty({B, H, W, d.levels * win}, coords.options().dtype(out_dtype));
+  HIP_OK(launch_corr_lookup_fwd(d, coords.data_ptr<float>(), out.data_ptr(), dtype_code(out_dtype),
+                                B, H, W, static_cast<int>(radius), cur_stream()));
+  return out;
+}
+
+void corr_lookup_backward_(at::TensorList dpyr, const at::Tensor& coords, const at::Tensor& grad,
+                           int64_t radius) {
+  check_coords(coords);
+  const long B = coords.size(0), H = coords.size(2), W = coords.size(3);
+  std::vector<at::Tensor> lv(dpyr.begin(), dpyr.end());
+  PyrDesc d = make_desc(lv, B * H * W);
+  const long win = (2 * radius + 1) * (2 * radius + 1);
+  check_gpu(grad, "grad");
+  TORCH_CHECK(grad.dim() == 4 && grad.size(0) == B && grad.size(1) == H && grad.size(2) == W &&
+                  grad.size(3) == d.levels * win,
+              "raft_amd::corr_lookup_backward_: grad must be (B, H, W, L*(2r+1)^2)");
+  auto g = grad.contiguous();
+  const c10::DeviceGuard guard(coords.device());
+  HIP_OK(launch_corr_lookup_bwd(d, coords.data_ptr<float>(), g.data_ptr(),
+                                dtype_code(g.scalar_type()), B, H, W, static_cast<int>(radius),
+                                cur_stream()));
+}
+
+std::tuple<at::Tensor, at::Tensor> pyramid_grad_combine(at::TensorList dpyr, int64_t B, int64_t H,
+                                                        int64_t W, int64_t ldp, double alpha) {
+  std::vector<at::Tensor> lv(dpyr.begin(), dpyr.end());
+  PyrDesc d = make_desc(lv, B * H * W);
+  TORCH_CHECK(lv[0].size(1) == H && lv[0].size(2) == W, "raft_amd: level 0 must be (B*H*W, H, W)");
+  TORCH_CHECK(ldp >= H * W && ldp % 64 == 0, "raft_amd: ldp must be >= H*W and a multiple of 64");
+  const c10::DeviceGuard guard(lv[0].device());
+  auto opts = lv[0].options().dtype(at::kBFloat16);
+  auto dC = at::empty({B, H * W, ldp}, opts);
+  auto dCt = at::empty({B, H * W, ldp}, opts);
+  HIP_OK(launch_pyramid_grad_combine(d, dC.data_ptr(), dCt.data_ptr(), B, H, W, ldp,
+                                     static_cast<float>(alpha), cur_stream()));
+  return {dC, dCt};
+}
+
+// ---------------------------------------------------------------- convex upsampling
+void check_up_inputs(const at::Tensor& flow, const at::Tensor& mask) {
+  check_gpu(flow, "flow");
+  check_gpu(mask, "mask");
+  TORCH_CHECK(flow.scalar_type() == at::kFloat && flow.is_contiguous() && flow.dim() == 4 &&
+                  flow.size(1) == 2,
+              "raft_amd::convex_upsample: flow must be contiguous fp32 (B, 2, H, W)");
+  TORCH_CHECK(mask.dim() == 4 && mask.size(0) == flow.size(0) && mask.size(1) == 576 &&
+                  mask.size(2) == flow.size(2) && mask.size(3) == flow.size(3),
+              "raft_amd::convex_upsample: mask must be (B, 576, H, W)");
+}
+
+at::Tensor convex_upsample(const at::Tensor& flow, const at::Tensor& mask) {
+  check_up_inputs(flow, mask);
+  const long B = flow.size(0), H = flow.size(2), W = flow.size(3);
+  const c10::DeviceGuard guard(flow.device());
+  auto out = at::empty({B, 2, 8 * H, 8 * W}, flow.options());
+  HIP_OK(launch_convex_up_fwd(flow.data_ptr<float>(), mask.data_ptr(), dtype_code(mask.scalar_type()),
+                              mask.stride(0), mask.stride(1), mask.stride(2), mask.stride(3),
+                              out.data_ptr<float>(), B, H, W, cur_stream()));
+  return out;
+}
+
+std::tuple<at::Tensor, at::Tensor> convex_upsample_backward(const at::Tensor& flow,
+                                                            const at::Tensor& mask,
+                                                            const at::Tensor& grad) {
+  check_up_inputs(flow, mask);
+  const long B = flow.size(0), H = flow.size(2), W = flow.size(3);
+  TORCH_CHECK(grad.dim() == 4 && grad.size(0) == B && grad.size(1) == 2 && grad.size(2) == 8 * H &&
+                  grad.size(3) == 8 * W,
+              "raft_amd::convex_upsample_backward: bad grad shape");
+  auto g = grad.to(at::kFloat).contiguous();
+  const c10::DeviceGuard guard(flow.device());
+  auto dmask = at::empty_strided(mask.sizes(), mask.strides(), mask.options());
+  auto part = at::empty({B, 18, H, W}, flow.options());
+  auto dflow = at::empty_like(flow);
+  HIP_OK(launch_convex_up_bwd(flow.data_ptr<float>(), mask.data_ptr(), dtype_code(mask.scalar_type()),
+                              mask.stride(0), mask.stride(1), mask.stride(2), mask.stride(3),
+                              g.data_ptr<float>(), dmask.data_ptr(), part.data_ptr<float>(),
+                              dflow.data_ptr<float>(), B, H, W, cur_stream()));
+  return {dflow, dmask};
+}
+
+// ---------------------------------------------------------------- local (alternate) correlation
+void check_local(const at::Tensor& f1, const at::Tensor& f2, const at::Tensor& coords) {
+  check_gpu(f1, "fmap1");
+  check_gpu(f2, "fmap2");
+  check_coords(coords);
+  TORCH_CHECK(f1.dim() == 4 && f2.dim() == 4 && f1.is_contiguous() && f2.is_contiguous(),
+              "raft_amd::local_corr: fmaps must be contiguous NHWC (B, H, W, C)");
+  TORCH_CHECK(f1.scalar_type() == f2.scalar_type(), "raft_amd::local_corr: fmap dtypes differ");
+  TORCH_CHECK(f1.size(0) == f2.size(0) && f1.size(3) == f2.size(3), "raft_amd::local_corr: shape mismatch");
+  TORCH_CHECK(f1.size(3) % 8 == 0, "raft_amd::local_corr: C must be a multiple of 8");
+  TORCH_CHECK(coords.size(0) == f1.size(0) && coords.size(2) == f1.size(1) &&
+                  coords.size(3) == f1.size(2),
+              "raft_amd::local_corr: coords must be (B, 2, H1, W1)");
+}
+
+at::Tensor local_corr(const at::Tensor& f1, const at::Tensor& f2, const at::Tensor& coords,
+                      int64_t radius, double scale) {
+  check_local(f1, f2, coords);
+  const long B = f1.size(0), H1 = f1.size(1), W1 = f1.size(2), C = f1.size(3);
+  const long H2 = f2.size(1), W2 = f2.size(2);
+  const long rd = 2 * radius + 1;
+  const c10::DeviceGuard guard(f1.device());
+  auto out = at::empty({B, H1, W1, rd * rd}, f1.options().dtype(at::kFloat));
+  HIP_OK(launch_local_corr_fwd(f1.data_ptr(), f2.data_ptr(), dtype_code(f1.scalar_type()),
+                               coords.data_ptr<float>(), out.data_ptr<float>(), B, H1, W1, H2, W2, C,
+                               static_cast<int>(radius), static_cast<float>(scale), cur_stream()));
+  return out;
+}
+
+std::tuple<at::Tensor, at::Tensor> local_corr_backward(const at::Tensor& f1, const at::Tensor& f2,
+                                                       const at::Tensor& coords,
+                                                       const at::Tensor& grad, int64_t radius,
+                                                       double scale) {
+  check_local(f1, f2, coords);
+  const long B = f1.size(0), H1 = f1.size(1), W1 = f1.size(2), C = f1.size(3);
+  const long H2 = f2.size(1), W2 = f2.size(2);
+  auto g = grad.to(at::kFloat).contiguous();
+  const long rd = 2 * radius + 1;
+  TORCH_CHECK(g.dim() == 4 && g.size(0) == B && g.size(1) == H1 && g.size(2) == W1 && g.size(3) == rd * rd,
+              "raft_amd::local_corr_backward: bad grad shape");
+  const c10::DeviceGuard guard(f1.device());
+  auto g1 = at::empty({B, H1, W1, C}, f1.options().dtype(at::kFloat));
+  auto g2 = at::zeros({B, H2, W2, C}, f1.options().dtype(at::kFloat));
+  HIP_OK(launch_local_corr_bwd(f1.data_ptr(), f2.data_ptr(), dtype_code(f1.scalar_type()),
+                               coords.data_ptr<float>(), g.data_ptr<float>(), g1.data_ptr<float>(),
+                               g2.data_ptr<float>(), B, H1, W1, H2, W2, C, static_cast<int>(radius),
+                               static_cast<float>(scale), cur_stream()));
+  return {g1, g2};
+}
+
+// ---------------------------------------------------------------- fused GRU gates
+void check_cl(const at::Tensor& t, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.dim() == 4 && t.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "raft_amd gru: ", name, " must be a channels-last contiguous 4-D tensor");
+}
+
+at::Tensor empty_cl(at::IntArrayRef sizes, const at::TensorOptions& o) {
+  return at::empty(sizes, o.memory_format(at::MemoryFormat::ChannelsLast));
+}
+
+std::tuple<at::Tensor, at::Tensor> gru_gates(const at::Tensor& zr, const at::Tensor& h) {
+  check_cl(zr, "zr");
+  check_cl(h, "h");
+  TORCH_CHECK(zr.scalar_type() == h.scalar_type(), "raft_amd gru_gates: dtype mismatch");
+  const long C = h.size(1);
+  TORCH_CHECK(zr.size(1) == 2 * C && zr.size(0) == h.size(0) && zr.size(2) == h.size(2) &&
+                  zr.size(3) == h.size(3),
+              "raft_amd gru_gates: zr must be (B, 2C, H, W) for h (B, C, H, W)");
+  const c10::DeviceGuard guard(h.device());
+  auto z = empty_cl(h.sizes(), h.options());
+  auto rh = empty_cl(h.sizes(), h.options());
+  HIP_OK(launch_gru_gates_fwd(dtype_code(h.scalar_type()), zr.data_ptr(), h.data_ptr(), z.data_ptr(),
+                              rh.data_ptr(), h.size(0) * h.size(2) * h.size(3), C, cur_stream()));
+  return {z, rh};
+}
+
+std::tuple<at::Tensor, at::Tensor> gru_gates_backward(const at::Tensor& zr, const at::Tensor& h,
+                                                      const at::Tensor& gz, const at::Tensor& grh) {
+  check_cl(zr, "zr");
+  check_cl(h, "h");
+  auto gzc = gz.to(h.scalar_type()).contiguous(at::MemoryFormat::ChannelsLast);
+  auto grc = grh.to(h.scalar_type()).contiguous(at::MemoryFormat::ChannelsLast);
+  const c10::DeviceGuard guard(h.device());
+  auto dzr = empty_cl(zr.sizes(), zr.options());
+  auto dh = empty_cl(h.sizes(), h.options());
+  HIP_OK(launch_gru_gates_bwd(dtype_code(h.scalar_type()), zr.data_ptr(), h.data_ptr(), gzc.data_ptr(),
+                              grc.data_ptr(), dzr.data_ptr(), dh.data_ptr(),
+                              h.size(0) * h.size(2) * h.size(3), h.size(1), cur_stream()));
+  return {dzr, dh};
+}
+
+at::Tensor gru_blend(const at::Tensor& z, const at::Tensor& q, const at::Tensor& h) {
+  check_cl(z, "z");
+  check_cl(q, "q");
+  check_cl(h, "h");
+  TORCH_CHECK(z.sizes() == q.sizes() && z.sizes() == h.sizes(), "raft_amd gru_blend: shape mismatch");
+  TORCH_CHECK(z.scalar_type() == q.scalar_type() && z.scalar_type() == h.scalar_type(),
+              "raft_amd gru_blend: dtype mismatch");
+  const c10::DeviceGuard guard(h.device());
+  auto out = empty_cl(h.sizes(), h.options());
+  HIP_OK(launch_gru_blend_fwd(dtype_code(h.scalar_type()), z.data_ptr(), q.data_ptr(), h.data_ptr(),
+                              out.data_ptr(), h.numel(), cur_stream()));
+  return out;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> gru_blend_backward(const at::Tensor& z,
+                                                                  const at::Tensor& q,
+                                                                  const at::Tensor& h,
+                                                                  const at::Tensor& g) {
+  check_cl(z, "z");
+  check_cl(q, "q");
+  check_cl(h, "h");
+  auto gc = g.to(h.scalar_type()).contiguous(at::MemoryFormat::ChannelsLast);
+  const c10::DeviceGuard guard(h.device());
+  auto dz = empty_cl(h.sizes(), h.options());
+  auto dq = empty_cl(h.sizes(), h.options());
+  auto dh = empty_cl(h.sizes(), h.options());
+  HIP_OK(launch_gru_blend_bwd(dtype_code(h.scalar_type()), z.data_ptr(), q.data_ptr(), h.data_ptr(),
+                              gc.data_ptr(), dz.data_ptr(), dq.data_ptr(), dh.data_ptr(), h.numel(),
+                              cur_stream()));
+  return {dz, dq, dh};
+}
+
+}  // namespace
+}  // namespace raft_amd
+
+TORCH_LIBRARY(raft_amd, m) {
+  m.def("gru_gates(Tensor zr, Tensor h) -> (Tensor, Tensor)");
+  m.def("gru_gates_backward(Tensor zr, Tensor h, Tensor gz, Tensor grh) -> (Tensor, Tensor)");
+  m.def("gru_blend(Tensor z, Tensor q, Tensor h) -> Tensor");
+  m.def("gru_blend_backward(Tensor z, Tensor q, Tensor h, Tensor g) -> (Tensor, Tensor, Tensor)");
+  m.def("gemm_nt(Tensor A, Tensor B, float alpha, ScalarType out_dtype) -> Tensor");
+  m.def("avgpool2x2(Tensor x) -> Tensor");
+  m.def("corr_lookup(Tensor[] pyramid, Tensor coords, int radius, ScalarType out_dtype) -> Tensor");
+  m.def("corr_lookup_backward_(Tensor(a!)[] dpyramid, Tensor coords, Tensor grad, int radius) -> ()");
+  m.def(
+      "pyramid_grad_combine(Tensor[] dpyramid, int B, int H, int W, int ldp, float alpha) -> (Tensor, "
+      "Tensor)");
+  m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");
+  m.def("convex_upsample_backward(Tensor flow, Tensor mask, Tensor grad) -> (Tensor, Tensor)");
+  m.def("local_corr(Tensor fmap1, Tensor fmap2, Tensor coords, int radius, float scale) -> Tensor");
+  m.def(
+      "local_corr_backward(Tensor fmap1, Tensor fmap2, Tensor coords, Tensor grad, int radius, float "
+      "scale) -> (Tensor, Tensor)");
+}
+
+TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
+  m.impl("gemm_nt", &raft_amd::gemm_nt);
+  m.impl("avgpool2x2", &raft_amd::avgpool2x2);
+  m.impl("corr_lookup", &raft_amd::corr_lookup);
+  m.impl("corr_lookup_backward_", &raft_amd::corr_lookup_backward_);
+  m.impl("pyramid_grad_combine", &raft_amd::pyramid_grad_combine);
+  m.impl("convex_upsample", &raft_amd::convex_upsample);
+  m.impl("convex_upsample_backward", &raft_amd::convex_upsample_backward);
+  m.impl("local_corr", &raft_amd::local_corr);
+  m.impl("local_corr_backward", &raft_amd::local_corr_backward);
+  m.impl("gru_gates", &raft_amd::gru_gates);
+  m.impl("gru_gates_backward", &raft_amd::gru_gates_backward);
+  m.impl("gru_blend", &raft_amd::gru_blend);
+  m.impl("gru_blend_backward", &raft_amd::gru_blend_backward);
+}

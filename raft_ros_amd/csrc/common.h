@@ -1,0 +1,60 @@
+// Shared device helpers for the raft_ros_amd CDNA4 (gfx950) kernels.
+//
+// Everything here is written for wave64 / MFMA hardware directly: there is no
+// CUDA compatibility layer and no dual-platform path.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace raft_amd {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// dtype codes shared with bindings.cpp
+enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(__bf16 v) { return static_cast<float>(v); }
+__device__ __forceinline__ float to_f32(_Float16 v) { return static_cast<float>(v); }
+
+template <typename T>
+__device__ __forceinline__ T from_f32(float v);
+template <>
+__device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ __bf16 from_f32<__bf16>(float v) { return static_cast<__bf16>(v); }
+template <>
+__device__ __forceinline__ _Float16 from_f32<_Float16>(float v) { return static_cast<_Float16>(v); }
+
+// Full-wave (64 lane) butterfly sum.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// Bijective XCD-aware remap of a flat workgroup id (MI355X: 8 XCDs, blocks
+// b and b+8 share an XCD's L2).  Consecutive logical tiles land on the same
+// XCD so that tiles sharing an operand panel share that L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (orig >> 3);
+}
+
+inline int cdiv(long a, long b) { return static_cast<int>((a + b - 1) / b); }
+
+}  // namespace raft_amd
+
+#define RAFT_HIP_CHECK(expr)                                                   \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess) return _e;                                           \
+  } while (0)

@@ -1,0 +1,190 @@
+// Fused convex 8x upsampling of the flow field (reference RAFT.upsample_flow,
+// core/raft.py:72-83):
+//   out[b, c, 8y+i, 8x+j] = sum_k softmax_k(mask[b, k*64 + i*8 + j, y, x]) * 8 * flow[b, c, y+ky-1, x+kx-1]
+// with k = ky*3 + kx (F.unfold order) and zero padding outside the field.
+//
+// One wave64 per low-resolution pixel: lane = i*8 + j owns one of the 64
+// sub-pixels, so the 9-way softmax, the gather and the pixel shuffle are a
+// single pass with no intermediate tensors (the reference materialises the
+// (N,1,9,8,8,H,W) softmax, the unfold and a permute copy every iteration).
+// The mask may be in any memory format (strides are passed), so the
+// channels-last output of the mask head is consumed without a copy.
+//
+// Backward: dmask is produced in the same pass; the flow gradient is reduced
+// across the wave per neighbour (deterministic, no atomics) into a
+// (B, 9, 2, H, W) partial buffer that a second tiny kernel gathers.
+#include "common.h"
+
+namespace raft_amd {
+namespace {
+
+template <typename MT>
+__global__ __launch_bounds__(256) void convex_up_fwd_kernel(const float* __restrict__ flow,
+                                                            const MT* __restrict__ mask, long msN,
+                                                            long msC, long msH, long msW,
+                                                            float* __restrict__ out, int B, int H,
+                                                            int W) {
+  const int lane = threadIdx.x & 63;
+  const long pix = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pix >= (long)B * H * W) return;
+  const int x = pix % W;
+  const int y = (pix / W) % H;
+  const int b = pix / ((long)H * W);
+  const int i = lane >> 3, j = lane & 7;
+  const MT* m = mask + b * msN + y * msH + x * msW;
+  float logit[9];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    logit[k] = to_f32(m[(long)(k * 64 + lane) * msC]);
+    mx = fmaxf(mx, logit[k]);
+  }
+  float den = 0.f, o0 = 0.f, o1 = 0.f;
+  const long HW = (long)H * W;
+  const float* f0 = flow + (long)b * 2 * HW;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const float e = __expf(logit[k] - mx);
+    den += e;
+    const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+      o0 += e * f0[yy * W + xx];
+      o1 += e * f0[HW + yy * W + xx];
+    }
+  }
+  const float inv = 8.f / den;
+  const long W8 = 8L * W;
+  const long oHW = 64L * HW;
+  float* o = out + (long)b * 2 * oHW + (8L * y + i) * W8 + 8L * x + j;
+  o[0] = o0 * inv;
+  o[oHW] = o1 * inv;
+}
+
+template <typename MT>
+__global__ __launch_bounds__(256) void convex_up_bwd_kernel(
+    const float* __restrict__ flow, const MT* __restrict__ mask, long msN, long msC, long msH,
+    long msW, const float* __restrict__ gout, MT* __restrict__ dmask, float* __restrict__ part,
+    int B, int H, int W) {
+  const int lane = threadIdx.x & 63;
+  const long pix = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pix >= (long)B * H * W) return;
+  const int x = pix % W;
+  const int y = (pix / W) % H;
+  const int b = pix / ((long)H * W);
+  const int i = lane >> 3, j = lane & 7;
+  const long HW = (long)H * W;
+  const long moff = b * msN + y * msH + x * msW;
+  float p[9];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    p[k] = to_f32(mask[moff + (long)(k * 64 + lane) * msC]);
+    mx = fmaxf(mx, p[k]);
+  }
+  float den = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    p[k] = __expf(p[k] - mx);
+    den += p[k];
+  }
+  const float inv = 1.f / den;
+  const long W8 = 8L * W, oHW = 64L * HW;
+  const float* g = gout + (long)b * 2 * oHW + (8L * y + i) * W8 + 8L * x + j;
+  const float g0 = g[0], g1 = g[oHW];
+  const float* f0 = flow + (long)b * 2 * HW;
+  float gv[9];
+  float dot = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    p[k] *= inv;
+    const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
+    float v0 = 0.f, v1 = 0.f;
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+      v0 = 8.f * f0[yy * W + xx];
+      v1 = 8.f * f0[HW + yy * W + xx];
+    }
+    gv[k] = g0 * v0 + g1 * v1;
+    dot += p[k] * gv[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+    dmask[moff + (long)(k * 64 + lane) * msC] = from_f32<MT>(p[k] * (gv[k] - dot));
+  // d flow(neighbour k, c) = sum over the 64 sub-pixels of 8 * p_k * g_c
+  float* pt = part + (long)b * 18 * HW + (long)y * W + x;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const float s0 = wave_sum(8.f * p[k] * g0);
+    const float s1 = wave_sum(8.f * p[k] * g1);
+    if (lane == 0) {
+      pt[(k * 2 + 0) * HW] = s0;
+      pt[(k * 2 + 1) * HW] = s1;
+    }
+  }
+}
+
+// dflow[b, c, y', x'] = sum_k part[b, k, c, y'-ky+1, x'-kx+1]
+__global__ __launch_bounds__(256) void convex_up_gather_kernel(const float* __restrict__ part,
+                                                               float* __restrict__ dflow, int B,
+                                                               int H, int W) {
+  const long HW = (long)H * W;
+  const long total = (long)B * 2 * HW;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int x = idx % W;
+  const int y = (idx / W) % H;
+  const int c = (idx / HW) % 2;
+  const int b = idx / (2 * HW);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int yy = y - (k / 3) + 1, xx = x - (k % 3) + 1;
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W) s += part[((long)b * 18 + k * 2 + c) * HW + yy * W + xx];
+  }
+  dflow[idx] = s;
+}
+
+}  // namespace
+
+hipError_t launch_convex_up_fwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
+                                long msH, long msW, float* out, int B, int H, int W, hipStream_t s) {
+  const long npix = (long)B * H * W;
+  if (npix == 0) return hipSuccess;
+  const dim3 g((npix + 3) / 4), blk(256);
+  if (m_dtype == kBF16)
+    hipLaunchKernelGGL(convex_up_fwd_kernel<__bf16>, g, blk, 0, s, flow,
+                       static_cast<const __bf16*>(mask), msN, msC, msH, msW, out, B, H, W);
+  else if (m_dtype == kF16)
+    hipLaunchKernelGGL(convex_up_fwd_kernel<_Float16>, g, blk, 0, s, flow,
+                       static_cast<const _Float16*>(mask), msN, msC, msH, msW, out, B, H, W);
+  else
+    hipLaunchKernelGGL(convex_up_fwd_kernel<float>, g, blk, 0, s, flow,
+                       static_cast<const float*>(mask), msN, msC, msH, msW, out, B, H, W);
+  return hipGetLastError();
+}
+
+hipError_t launch_convex_up_bwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
+                                long msH, long msW, const float* gout, void* dmask, float* part,
+                                float* dflow, int B, int H, int W, hipStream_t s) {
+  const long npix = (long)B * H * W;
+  if (npix == 0) return hipSuccess;
+  const dim3 g((npix + 3) / 4), blk(256);
+  if (m_dtype == kBF16)
+    hipLaunchKernelGGL(convex_up_bwd_kernel<__bf16>, g, blk, 0, s, flow,
+                       static_cast<const __bf16*>(mask), msN, msC, msH, msW, gout,
+                       static_cast<__bf16*>(dmask), part, B, H, W);
+  else if (m_dtype == kF16)
+    hipLaunchKernelGGL(convex_up_bwd_kernel<_Float16>, g, blk, 0, s, flow,
+                       static_cast<const _Float16*>(mask), msN, msC, msH, msW, gout,
+                       static_cast<_Float16*>(dmask), part, B, H, W);
+  else
+    hipLaunchKernelGGL(convex_up_bwd_kernel<float>, g, blk, 0, s, flow,
+                       static_cast<const float*>(mask), msN, msC, msH, msW, gout,
+                       static_cast<float*>(dmask), part, B, H, W);
+  RAFT_HIP_CHECK(hipGetLastError());
+  const long tot = (long)B * 2 * H * W;
+  hipLaunchKernelGGL(convex_up_gather_kernel, dim3((tot + 255) / 256), blk, 0, s, part, dflow, B, H,
+                     W);
+  return hipGetLastError();
+}
+
+}  // namespace raft_amd

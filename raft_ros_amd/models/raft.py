@@ -1,0 +1,155 @@
+"""RAFT: Recurrent All-Pairs Field Transforms, MI355X-native execution.
+
+Behaviour and API follow the reference orchestrator (core/raft.py:24-144):
+
+* ``RAFT(args)`` with ``args.small``, ``args.mixed_precision``,
+  ``args.alternate_corr``, ``args.dropout`` (the constructor sets
+  ``args.corr_levels`` / ``args.corr_radius`` like the reference, :29-45);
+* ``forward(image1, image2, iters=12, flow_init=None, upsample=True,
+  test_mode=False)`` -> list of ``iters`` full-resolution flows, or
+  ``(flow_lowres, flow_up)`` in test mode;
+* identical parameter names, so ``raft-*.pth`` checkpoints load.
+
+Execution differences (GPU):
+
+* the correlation pyramid build / lookup / backward, the convex upsampler and
+  the GRU gate math are native HIP kernels (``raft_ros_amd.ops``);
+* the lookup emits channels-last features already in the autocast dtype;
+* mixed precision uses ``args.amp_dtype`` (default bf16 on MI355X; 'fp16'
+  reproduces the reference's fp16 autocast);
+* ``args.channels_last`` (default True on GPU) keeps every conv in NHWC.
+"""
+from __future__ import annotations
+
+from argparse import Namespace
+
+import torch
+import torch.nn as nn
+
+from ..ops import CorrPyramid, LocalCorrPyramid, convex_upsample, upflow8
+from ..ops.reference import coords_grid
+from .extractor import BasicEncoder, SmallEncoder
+from .update import BasicUpdateBlock, SmallUpdateBlock
+
+_AMP_DTYPES = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp16": torch.float16,
+               "float16": torch.float16, "half": torch.float16}
+
+
+def _arg(args, name, default):
+    return getattr(args, name) if name in args else default
+
+
+class RAFT(nn.Module):
+    def __init__(self, args):
+        super().__init__()
+        if isinstance(args, dict):
+            args = Namespace(**args)
+        self.args = args
+        if _arg(args, "small", False):
+            self.hidden_dim = hdim = 96
+            self.context_dim = cdim = 64
+            args.corr_levels = 4
+            args.corr_radius = 3
+        else:
+            self.hidden_dim = hdim = 128
+            self.context_dim = cdim = 128
+            args.corr_levels = 4
+            args.corr_radius = 4
+        if "dropout" not in args:
+            args.dropout = 0
+        if "alternate_corr" not in args:
+            args.alternate_corr = False
+        if "mixed_precision" not in args:
+            args.mixed_precision = False
+        if "small" not in args:
+            args.small = False
+        self.amp_dtype = _AMP_DTYPES[str(_arg(args, "amp_dtype", "bf16")).lower()]
+
+        if args.small:
+            self.fnet = SmallEncoder(output_dim=128, norm_fn="instance", dropout=args.dropout)
+            self.cnet = SmallEncoder(output_dim=hdim + cdim, norm_fn="none", dropout=args.dropout)
+            self.update_block = SmallUpdateBlock(args, hidden_dim=hdim)
+        else:
+            self.fnet = BasicEncoder(output_dim=256, norm_fn="instance", dropout=args.dropout)
+            self.cnet = BasicEncoder(output_dim=hdim + cdim, norm_fn="batch", dropout=args.dropout)
+            self.update_block = BasicUpdateBlock(args, hidden_dim=hdim)
+
+    # ------------------------------------------------------------------ helpers
+    def freeze_bn(self):
+        for m in self.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.eval()
+
+    def initialize_flow(self, img):
+        """flow = coords1 - coords0, both (N, 2, H/8, W/8) pixel grids."""
+        N, _, H, W = img.shape
+        coords0 = coords_grid(N, H // 8, W // 8, device=img.device)
+        coords1 = coords_grid(N, H // 8, W // 8, device=img.device)
+        return coords0, coords1
+
+    def upsample_flow(self, flow, mask):
+        """[H/8, W/8] -> [H, W] flow by convex combination (fused HIP kernel on GPU)."""
+        return convex_upsample(flow, mask)
+
+    def _autocast(self, device_type: str):
+        enabled = bool(self.args.mixed_precision)
+        if device_type == "cpu" and self.amp_dtype == torch.float16:
+            enabled = False  # fp16 autocast is a GPU feature
+        return torch.autocast(device_type=device_type, dtype=self.amp_dtype, enabled=enabled)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, image1, image2, iters: int = 12, flow_init=None, upsample: bool = True,
+                test_mode: bool = False):
+        H, W = image1.shape[-2:]
+        if min(H, W) < 128:
+            # below 128 px the coarsest pyramid level degenerates (reference: NaN at
+            # 64..127 px, a crash below 64 px -- SURVEY.md 2.6); refuse loudly instead
+            raise ValueError(f"RAFT needs inputs of at least 128x128 pixels, got {H}x{W}")
+        dev = image1.device.type
+        cl = dev == "cuda" and _arg(self.args, "channels_last", True)
+        fmt = torch.channels_last if cl else torch.contiguous_format
+
+        image1 = (2 * (image1 / 255.0) - 1.0).contiguous(memory_format=fmt)
+        image2 = (2 * (image2 / 255.0) - 1.0).contiguous(memory_format=fmt)
+        hdim, cdim = self.hidden_dim, self.context_dim
+        amp = bool(self.args.mixed_precision)
+
+        with self._autocast(dev):
+            fmap1, fmap2 = self.fnet([image1, image2])
+        fmap1, fmap2 = fmap1.float(), fmap2.float()
+        if self.args.alternate_corr:
+            corr_fn = LocalCorrPyramid(fmap1, fmap2, radius=self.args.corr_radius)
+        else:
+            corr_fn = CorrPyramid(fmap1, fmap2, radius=self.args.corr_radius)
+
+        with self._autocast(dev):
+            cnet = self.cnet(image1)
+            net, inp = torch.split(cnet, [hdim, cdim], dim=1)
+            net = torch.tanh(net)
+            inp = torch.relu(inp)
+
+        coords0, coords1 = self.initialize_flow(image1)
+        if flow_init is not None:
+            coords1 = coords1 + flow_init
+
+        corr_dtype = self.amp_dtype if (amp and dev == "cuda") else None
+        flow_predictions = []
+        flow_up = None
+        for _ in range(iters):
+            coords1 = coords1.detach()
+            corr = corr_fn(coords1, out_dtype=corr_dtype)
+            flow = coords1 - coords0
+            if cl:
+                flow = flow.contiguous(memory_format=fmt)
+            with self._autocast(dev):
+                net, up_mask, delta_flow = self.update_block(net, inp, corr, flow)
+            coords1 = coords1 + delta_flow.float()
+            if up_mask is None:
+                flow_up = upflow8(coords1 - coords0)
+            else:
+                flow_up = self.upsample_flow(coords1 - coords0, up_mask)
+            flow_predictions.append(flow_up)
+
+        if test_mode:
+            return coords1 - coords0, flow_up
+        return flow_predictions

@@ -1,0 +1,175 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from raft_ros_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from raft_ros_amd.ops._ext import ops
+
+    return ops()
+
+
+@pytest.mark.parametrize("M,N,K,batch", [(2852, 2852, 256, 2), (100, 70, 128, 1), (257, 129, 64, 3)])
+def test_gemm_nt_bf16(cuda, M, N, K, batch):
+    torch.manual_seed(0)
+    A = torch.randn(batch, M, K, device=cuda).bfloat16()
+    B = torch.randn(batch, N, K, device=cuda).bfloat16()
+    C = _ops().gemm_nt(A, B, 0.5, torch.float32)
+    R = 0.5 * torch.matmul(A.float(), B.float().transpose(1, 2))
+    torch.testing.assert_close(C, R, rtol=1e-3, atol=1e-3)
+    # asymmetric operands catch a transposed C/D write
+    Cb = _ops().gemm_nt(A, B, 1.0, torch.bfloat16)
+    torch.testing.assert_close(Cb.float(), 2 * R, rtol=2e-2, atol=5e-2)
+
+
+def test_gemm_nt_identity_asymmetric(cuda):
+    M, K = 128, 128
+    A = torch.eye(M, K, device=cuda).bfloat16()[None]
+    B = (torch.arange(M * K, device=cuda).reshape(M, K) % 7 - 3).float().bfloat16()[None]
+    C = _ops().gemm_nt(A, B, 1.0, torch.float32)
+    torch.testing.assert_close(C[0], B[0].float().t())
+
+
+def test_avgpool(cuda):
+    x = torch.randn(37, 23, 31, device=cuda)
+    torch.testing.assert_close(_ops().avgpool2x2(x), F.avg_pool2d(x[:, None], 2, 2)[:, 0])
+
+
+def _pyramid(B, C, H, W, dev, levels=4):
+    f1 = torch.randn(B, C, H, W, device=dev)
+    f2 = torch.randn(B, C, H, W, device=dev)
+    corr = ref.corr_volume(f1, f2)
+    return f1, f2, ref.build_pyramid(corr, levels)
+
+
+@pytest.mark.parametrize("radius,shape", [(4, (2, 46, 62)), (3, (1, 17, 23))])
+def test_corr_lookup_fwd(cuda, radius, shape):
+    torch.manual_seed(1)
+    B, H, W = shape
+    _, _, pyr = _pyramid(B, 64, H, W, cuda)
+    coords = ref.coords_grid(B, H, W, cuda) + 6 * torch.randn(B, 2, H, W, device=cuda)
+    coords[0, :, 0, 0] = torch.tensor([-30.0, 500.0])  # fully out of range
+    want = ref.pyramid_lookup(pyr, coords, radius)
+    got = _ops().corr_lookup([p[:, 0].contiguous() for p in pyr], coords.contiguous(), radius, torch.float32)
+    torch.testing.assert_close(got.permute(0, 3, 1, 2), want, rtol=1e-4, atol=1e-4)
+    got16 = _ops().corr_lookup([p[:, 0].contiguous() for p in pyr], coords.contiguous(), radius, torch.bfloat16)
+    torch.testing.assert_close(got16.permute(0, 3, 1, 2).float(), want, rtol=2e-2, atol=2e-2)
+
+
+def test_corr_lookup_window_order_is_x_major(cuda):
+    # a volume that is a pure ramp in x: tap channel ix*(2r+1)+iy must move x with ix
+    B, H, W, r = 1, 16, 16, 2
+    xs = torch.arange(W, device=cuda, dtype=torch.float32).view(1, 1, W).expand(B * H * W, H, W).contiguous()
+    coords = ref.coords_grid(B, H, W, cuda)
+    out = _ops().corr_lookup([xs], coords, r, torch.float32)  # (B, H, W, 25)
+    rd = 2 * r + 1
+    px = out[0, 8, 8].view(rd, rd)  # [ix, iy]
+    assert torch.allclose(px[:, 0], torch.arange(8 - r, 8 + r + 1, device=cuda, dtype=torch.float32))
+    assert torch.allclose(px[2], torch.full((rd,), 8.0, device=cuda))
+
+
+def test_corr_pyramid_autograd_matches_reference(cuda):
+    torch.manual_seed(2)
+    from raft_ros_amd.ops.corr import CorrPyramid
+
+    B, C, H, W, r = 2, 256, 20, 28, 4
+    f1 = torch.randn(B, C, H, W, device=cuda, requires_grad=True)
+    f2 = torch.randn(B, C, H, W, device=cuda, requires_grad=True)
+    coords_list = [ref.coords_grid(B, H, W, cuda) + 3 * torch.randn(B, 2, H, W, device=cuda) for _ in range(3)]
+    gouts = [torch.randn(B, 4 * (2 * r + 1) ** 2, H, W, device=cuda) for _ in range(3)]
+
+    cp = CorrPyramid(f1, f2, 4, r)
+    loss = sum((cp(c) * g).sum() for c, g in zip(coords_list, gouts))
+    loss.backward()
+    g1, g2 = f1.grad.clone(), f2.grad.clone()
+
+    f1r = f1.detach().clone().requires_grad_(True)
+    f2r = f2.detach().clone().requires_grad_(True)
+    pyr = ref.build_pyramid(ref.corr_volume(f1r, f2r), 4)
+    outs = [ref.pyramid_lookup(pyr, c, r) for c in coords_list]
+    with torch.no_grad():
+        for o, c in zip(outs, [cp(c) for c in coords_list]):
+            # bf16 MFMA volume vs fp32 reference
+            assert (o - c.float()).abs().max() < 0.05 * o.abs().max()
+    lr = sum((o * g).sum() for o, g in zip(outs, gouts))
+    lr.backward()
+    for got, want in ((g1, f1r.grad), (g2, f2r.grad)):
+        err = (got - want).norm() / want.norm()
+        assert err < 1e-2, err
+
+
+def test_convex_upsample_fwd_bwd(cuda):
+    torch.manual_seed(3)
+    from raft_ros_amd.ops.upsample import convex_upsample
+
+    B, H, W = 2, 13, 17
+    flow = torch.randn(B, 2, H, W, device=cuda, requires_grad=True)
+    mask = torch.randn(B, 576, H, W, device=cuda).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    out = convex_upsample(flow, mask)
+    want = ref.convex_upsample(flow, mask)
+    torch.testing.assert_close(out, want, rtol=1e-4, atol=1e-4)
+    g = torch.randn_like(out)
+    df, dm = torch.autograd.grad(out, (flow, mask), g)
+    rf, rm = torch.autograd.grad(want, (flow, mask), g)
+    torch.testing.assert_close(df, rf, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dm, rm, rtol=1e-4, atol=1e-4)
+    # bf16 mask (autocast output of the mask head)
+    mb = mask.detach().bfloat16()
+    torch.testing.assert_close(convex_upsample(flow.detach(), mb), ref.convex_upsample(flow.detach(), mb.float()),
+                               rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gru_gates_and_blend(cuda, dtype):
+    torch.manual_seed(4)
+    from raft_ros_amd.ops import gru
+
+    B, C, H, W = 2, 128, 9, 11
+    cl = torch.channels_last
+    zr = torch.randn(B, 2 * C, H, W, device=cuda).to(dtype).contiguous(memory_format=cl).requires_grad_(True)
+    h = torch.randn(B, C, H, W, device=cuda).to(dtype).contiguous(memory_format=cl).requires_grad_(True)
+    q = torch.randn(B, C, H, W, device=cuda).to(dtype).contiguous(memory_format=cl).requires_grad_(True)
+    z, rh = gru.gates_zr(zr, h)
+    out = gru.blend(z, q, h)
+    zr32, h32, q32 = (t.detach().float().requires_grad_(True) for t in (zr, h, q))
+    zz = torch.sigmoid(zr32[:, :C])
+    rr = torch.sigmoid(zr32[:, C:]) * h32
+    want = (1 - zz) * h32 + zz * torch.tanh(q32)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(rh.float(), rr, **tol)
+    torch.testing.assert_close(out.float(), want, **tol)
+    g = torch.randn_like(want)
+    got = torch.autograd.grad(out, (zr, h, q), g.to(dtype))
+    exp = torch.autograd.grad(want, (zr32, h32, q32), g)
+    for a, b in zip(got, exp):
+        torch.testing.assert_close(a.float(), b, **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_local_corr_fwd_bwd(cuda, dtype):
+    torch.manual_seed(5)
+    from raft_ros_amd.ops.corr import _LocalCorr
+
+    B, C, H1, W1, H2, W2, r = 2, 64, 11, 13, 6, 7, 4
+    f1 = torch.randn(B, H1, W1, C, device=cuda).to(dtype).requires_grad_(True)
+    f2 = torch.randn(B, H2, W2, C, device=cuda).to(dtype).requires_grad_(True)
+    coords = (ref.coords_grid(B, H1, W1, cuda) / 2 + 2 * torch.randn(B, 2, H1, W1, device=cuda)).contiguous()
+    scale = 1 / math.sqrt(C)
+    out = _LocalCorr.apply(f1, f2, coords, r, scale)
+    f1r = f1.detach().float().permute(0, 3, 1, 2).requires_grad_(True)
+    f2r = f2.detach().float().permute(0, 3, 1, 2).requires_grad_(True)
+    want = ref.local_corr(f1r, f2r, coords, r).permute(0, 2, 3, 1) * scale
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(out, want, **tol)
+    g = torch.randn_like(want)
+    d1, d2 = torch.autograd.grad(out, (f1, f2), g)
+    r1, r2 = torch.autograd.grad(want, (f1r, f2r), g)
+    torch.testing.assert_close(d1.float(), r1.permute(0, 2, 3, 1), **tol)
+    torch.testing.assert_close(d2.float(), r2.permute(0, 2, 3, 1), **tol)
