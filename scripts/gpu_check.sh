@@ -19,13 +19,21 @@ run() {  # run <name> <timeout-seconds> <cmd...>
 }
 
 STEPS=${STEPS:-10}
-run pytest_gpu 900 python -m pytest tests -m gpu -x -q
-run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-run bench_native 600 python bench.py --steps "$STEPS" --warmup 3
+if [ "${TESTS:-1}" = "1" ]; then
+  run pytest_gpu 900 python -m pytest tests -m gpu -q -rf --tb=short
+  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [ "${BENCH:-1}" = "1" ]; then
+  run bench_native 600 python bench.py --steps "$STEPS" --warmup 3
+fi
 if [ "${SKIP_REF:-0}" != "1" ]; then
   run bench_reference 900 python bench.py --steps "$STEPS" --warmup 3 --impl reference
 fi
 if [ "${PROFILE:-1}" = "1" ]; then
-  run rocprof_native 900 rocprofv3 --kernel-trace --stats -d $OUT/prof_native -o run -- python3 bench.py --steps 3 --warmup 2
+  TAG=${TAG:-native}
+  run rocprof_$TAG 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 bench.py --steps 4 --warmup 3 ${PROF_ARGS:-}
+  python scripts/kernel_summary.py $OUT/prof_$TAG/run_kernel_trace.csv --boundary "${BOUNDARY:-pyramid_grad_combine}" --every "${EVERY:-1}" --skip 3 --out $OUT/prof_$TAG/steady_summary.csv > $OUT/prof_$TAG/steady_summary.txt 2>&1
+  # keep only the summaries (the per-dispatch trace is too large to ship back)
+  find $OUT/prof_$TAG -type f ! -name '*stats*' ! -name 'steady_summary*' -delete
 fi
 echo "done"

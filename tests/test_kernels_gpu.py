@@ -86,18 +86,17 @@ def test_corr_pyramid_autograd_matches_reference(cuda):
     gouts = [torch.randn(B, 4 * (2 * r + 1) ** 2, H, W, device=cuda) for _ in range(3)]
 
     cp = CorrPyramid(f1, f2, 4, r)
-    loss = sum((cp(c) * g).sum() for c, g in zip(coords_list, gouts))
-    loss.backward()
-    g1, g2 = f1.grad.clone(), f2.grad.clone()
-
+    outs_native = [cp(c) for c in coords_list]
     f1r = f1.detach().clone().requires_grad_(True)
     f2r = f2.detach().clone().requires_grad_(True)
     pyr = ref.build_pyramid(ref.corr_volume(f1r, f2r), 4)
     outs = [ref.pyramid_lookup(pyr, c, r) for c in coords_list]
-    with torch.no_grad():
-        for o, c in zip(outs, [cp(c) for c in coords_list]):
-            # bf16 MFMA volume vs fp32 reference
-            assert (o - c.float()).abs().max() < 0.05 * o.abs().max()
+    for o, c in zip(outs, outs_native):
+        # bf16 MFMA volume vs fp32 reference
+        assert (o.detach() - c.detach().float()).abs().max() < 0.05 * o.detach().abs().max()
+    loss = sum((o * g).sum() for o, g in zip(outs_native, gouts))
+    loss.backward()
+    g1, g2 = f1.grad.clone(), f2.grad.clone()
     lr = sum((o * g).sum() for o, g in zip(outs, gouts))
     lr.backward()
     for got, want in ((g1, f1r.grad), (g2, f2r.grad)):
