@@ -31,9 +31,19 @@ hipError_t launch_gemm_nt_bf16(const void* A, long lda, long strideA, const void
                                int N, int K, float alpha, int batch, hipStream_t stream);
 hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int W, hipStream_t s);
 hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void* out, int out_dtype,
-                                  int B, int H, int W, int r, hipStream_t s);
+                                  int B, int H, int W, int r, int out_ch, hipStream_t s);
 hipError_t launch_corr_lookup_bwd(const PyrDesc& dpyr, const float* coords, const void* gout,
-                                  int g_dtype, int B, int H, int W, int r, hipStream_t s);
+                                  int g_dtype, int B, int H, int W, int r, int gstride, hipStream_t s);
+hipError_t launch_gru_bwd_a(const float* dH, long sdh, const void* z, long sz, const void* q, long sq,
+                            const void* h, long sh, void* dq, long sdq, void* dz, long sdz, float* carry,
+                            long sc, long P, int C, hipStream_t s);
+hipError_t launch_gru_bwd_b(float* drh, long sd, const void* r, long sr, const void* h, long sh,
+                            const float* carry, long sc, void* dr, long sdr, long P, int C,
+                            hipStream_t s);
+hipError_t launch_masked_cast(const float* src, long ss, const void* mask, long sm, void* out, long so,
+                              long P, int C, int Cvalid, hipStream_t s);
+hipError_t launch_pack_flow(const float* flow, void* flow8, void* motion, long smo, int B, int HW,
+                            hipStream_t s);
 hipError_t launch_pyramid_grad_combine(const PyrDesc& dpyr, void* dC, void* dCt, int B, int H,
                                        int W, int ldp, float alpha, hipStream_t s);
 hipError_t launch_convex_up_fwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
@@ -56,6 +66,50 @@ hipError_t launch_gru_blend_fwd(int dtype, const void* z, const void* q, const v
                                 long numel, hipStream_t s);
 hipError_t launch_gru_blend_bwd(int dtype, const void* z, const void* q, const void* h, const void* g,
                                 void* dz, void* dq, void* dh, long numel, hipStream_t s);
+
+struct ConvSrc {
+  const void* ptr;
+  long stride;
+  int C;
+  int pad_;
+};
+struct ConvFwdArgs {
+  ConvSrc src[3];
+  int nsrc, Cin;
+  int B, H, W, KH, KW, PH, PW;
+  int K, Kpad;
+  const void* wt;
+  int N;
+  long P;
+  int epi, act, out_f32, acc_c0;
+  float alpha;
+  const float* bias;
+  void* out;
+  long out_stride;
+  const void* mask;
+  long mask_stride;
+  const void* h;
+  long h_stride;
+  const void* z;
+  long z_stride;
+  void* out2;
+  long out2_stride;
+};
+struct ConvWgradArgs {
+  ConvSrc src[3];
+  int nsrc, Cin;
+  int B, H, W, KH, KW, PH, PW;
+  int K, Kpad;
+  const void* dy;
+  long dy_stride;
+  int N;
+  long P;
+  long pix_per_split;
+  float* dw;
+  float* db;
+};
+hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s);
+hipError_t launch_conv_wgrad(ConvWgradArgs a, hipStream_t s);
 
 namespace {
 
@@ -147,16 +201,18 @@ void check_coords(const at::Tensor& coords) {
 }
 
 at::Tensor corr_lookup(at::TensorList pyramid, const at::Tensor& coords, int64_t radius,
-                       at::ScalarType out_dtype) {
+                       at::ScalarType out_dtype, int64_t out_channels) {
   check_coords(coords);
   const long B = coords.size(0), H = coords.size(2), W = coords.size(3);
   std::vector<at::Tensor> lv(pyramid.begin(), pyramid.end());
   PyrDesc d = make_desc(lv, B * H * W);
   const long win = (2 * radius + 1) * (2 * radius + 1);
   const c10::DeviceGuard guard(coords.device());
-  auto out = at::empty({B, H, W, d.levels * win}, coords.options().dtype(out_dtype));
+  const long och = out_channels > 0 ? out_channels : d.levels * win;
+  TORCH_CHECK(och >= d.levels * win, "raft_amd::corr_lookup: out_channels < L*(2r+1)^2");
+  auto out = at::empty({B, H, W, och}, coords.options().dtype(out_dtype));
   HIP_OK(launch_corr_lookup_fwd(d, coords.data_ptr<float>(), out.data_ptr(), dtype_code(out_dtype),
-                                B, H, W, static_cast<int>(radius), cur_stream()));
+                                B, H, W, static_cast<int>(radius), static_cast<int>(och), cur_stream()));
   return out;
 }
 
@@ -169,13 +225,13 @@ void corr_lookup_backward_(at::TensorList dpyr, const at::Tensor& coords, const 
   const long win = (2 * radius + 1) * (2 * radius + 1);
   check_gpu(grad, "grad");
   TORCH_CHECK(grad.dim() == 4 && grad.size(0) == B && grad.size(1) == H && grad.size(2) == W &&
-                  grad.size(3) == d.levels * win,
-              "raft_amd::corr_lookup_backward_: grad must be (B, H, W, L*(2r+1)^2)");
+                  grad.size(3) >= d.levels * win,
+              "raft_amd::corr_lookup_backward_: grad must be (B, H, W, >= L*(2r+1)^2)");
   auto g = grad.contiguous();
   const c10::DeviceGuard guard(coords.device());
   HIP_OK(launch_corr_lookup_bwd(d, coords.data_ptr<float>(), g.data_ptr(),
                                 dtype_code(g.scalar_type()), B, H, W, static_cast<int>(radius),
-                                cur_stream()));
+                                static_cast<int>(g.size(3)), cur_stream()));
 }
 
 std::tuple<at::Tensor, at::Tensor> pyramid_grad_combine(at::TensorList dpyr, int64_t B, int64_t H,
@@ -360,17 +416,216 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> gru_blend_backward(const at::Tens
   return {dz, dq, dh};
 }
 
+// ---------------------------------------------------------------- implicit-GEMM convs
+// Pixel-major operands are 2-D (P, C) views: stride(1) == 1, stride(0) = pixel stride.
+void check_pm(const at::Tensor& t, const char* name, long P) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1 && t.size(0) == P,
+              "raft_amd conv: ", name, " must be a (P, C) pixel-major view with unit channel stride");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              "raft_amd conv: ", name, " needs 16-byte aligned pixel rows");
+}
+
+int fill_srcs(at::TensorList srcs, long P, ConvSrc* out) {
+  TORCH_CHECK(srcs.size() >= 1 && srcs.size() <= 3, "raft_amd conv: 1..3 input sources");
+  int Cin = 0;
+  for (int i = 0; i < 3; ++i) out[i] = ConvSrc{nullptr, 0, 0, 0};
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    check_pm(srcs[i], "src", P);
+    TORCH_CHECK(srcs[i].scalar_type() == at::kBFloat16, "raft_amd conv: sources must be bf16");
+    TORCH_CHECK(srcs[i].size(1) % 8 == 0, "raft_amd conv: source channels must be multiples of 8");
+    out[i] = ConvSrc{srcs[i].data_ptr(), srcs[i].stride(0), static_cast<int>(srcs[i].size(1)), 0};
+    Cin += static_cast<int>(srcs[i].size(1));
+  }
+  return Cin;
+}
+
+void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, int64_t N, const c10::optional<at::Tensor>& bias,
+              int64_t epi, int64_t act, double alpha, const at::Tensor& out, int64_t acc_c0,
+              const c10::optional<at::Tensor>& mask, const c10::optional<at::Tensor>& h,
+              const c10::optional<at::Tensor>& z, const c10::optional<at::Tensor>& out2) {
+  TORCH_CHECK(geom.size() == 7, "raft_amd conv_fwd: geom = (B, H, W, KH, KW, PH, PW)");
+  ConvFwdArgs a{};
+  a.B = geom[0]; a.H = geom[1]; a.W = geom[2]; a.KH = geom[3]; a.KW = geom[4]; a.PH = geom[5]; a.PW = geom[6];
+  a.P = (long)a.B * a.H * a.W;
+  a.nsrc = static_cast<int>(srcs.size());
+  a.Cin = fill_srcs(srcs, a.P, a.src);
+  a.K = a.KH * a.KW * a.Cin;
+  check_gpu(wt, "wt");
+  TORCH_CHECK(wt.scalar_type() == at::kBFloat16 && wt.dim() == 2 && wt.is_contiguous() && wt.size(0) >= N &&
+                  wt.size(1) >= a.K && wt.size(1) % 64 == 0,
+              "raft_amd conv_fwd: wt must be contiguous bf16 [>=N][Kpad], Kpad % 64 == 0, Kpad >= K (", a.K, ")");
+  a.Kpad = static_cast<int>(wt.size(1));
+  a.wt = wt.data_ptr();
+  a.N = static_cast<int>(N);
+  a.epi = static_cast<int>(epi);
+  a.act = static_cast<int>(act);
+  a.alpha = static_cast<float>(alpha);
+  a.acc_c0 = static_cast<int>(acc_c0);
+  if (bias) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() >= N,
+                "raft_amd conv_fwd: bias must be contiguous fp32 [N]");
+    a.bias = bias->data_ptr<float>();
+  }
+  check_pm(out, "out", a.P);
+  TORCH_CHECK(out.size(1) >= N, "raft_amd conv_fwd: out has too few channels");
+  a.out = out.data_ptr();
+  a.out_stride = out.stride(0);
+  a.out_f32 = out.scalar_type() == at::kFloat;
+  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "raft_amd conv_fwd: out dtype");
+  if (epi >= 2) TORCH_CHECK(!a.out_f32, "raft_amd conv_fwd: GRU epilogues write bf16");
+  if (mask) {
+    check_pm(*mask, "mask", a.P);
+    a.mask = mask->data_ptr();
+    a.mask_stride = mask->stride(0);
+  }
+  if (h) {
+    check_pm(*h, "h", a.P);
+    a.h = h->data_ptr();
+    a.h_stride = h->stride(0);
+  }
+  if (z) {
+    check_pm(*z, "z", a.P);
+    a.z = z->data_ptr();
+    a.z_stride = z->stride(0);
+  }
+  if (out2) {
+    check_pm(*out2, "out2", a.P);
+    a.out2 = out2->data_ptr();
+    a.out2_stride = out2->stride(0);
+  }
+  if (epi == 2) TORCH_CHECK(h && out2 && N % 2 == 0, "raft_amd conv_fwd: GRU z||r epilogue needs h, out2");
+  if (epi == 3) TORCH_CHECK(h && z && out2, "raft_amd conv_fwd: GRU blend epilogue needs h, z, out2");
+  const c10::DeviceGuard guard(wt.device());
+  HIP_OK(launch_conv_fwd(a, cur_stream()));
+}
+
+void conv_wgrad(at::TensorList srcs, const at::Tensor& dy, at::IntArrayRef geom, int64_t N, const at::Tensor& dw,
+                const c10::optional<at::Tensor>& db) {
+  TORCH_CHECK(geom.size() == 7, "raft_amd conv_wgrad: geom = (B, H, W, KH, KW, PH, PW)");
+  ConvWgradArgs a{};
+  a.B = geom[0]; a.H = geom[1]; a.W = geom[2]; a.KH = geom[3]; a.KW = geom[4]; a.PH = geom[5]; a.PW = geom[6];
+  a.P = (long)a.B * a.H * a.W;
+  a.nsrc = static_cast<int>(srcs.size());
+  a.Cin = fill_srcs(srcs, a.P, a.src);
+  a.K = a.KH * a.KW * a.Cin;
+  check_pm(dy, "dy", a.P);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16, "raft_amd conv_wgrad: dy must be bf16");
+  TORCH_CHECK(dy.size(1) >= (N + 7) / 8 * 8, "raft_amd conv_wgrad: dy must hold N channels (rounded to 8)");
+  a.dy = dy.data_ptr();
+  a.dy_stride = dy.stride(0);
+  a.N = static_cast<int>(N);
+  check_gpu(dw, "dw");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.dim() == 2 && dw.is_contiguous() && dw.size(0) >= N &&
+                  dw.size(1) >= a.K,
+              "raft_amd conv_wgrad: dw must be contiguous fp32 [>=N][Kpad >= K]");
+  a.Kpad = static_cast<int>(dw.size(1));
+  a.dw = dw.data_ptr<float>();
+  if (db) {
+    TORCH_CHECK(db->scalar_type() == at::kFloat && db->is_contiguous() && db->numel() >= N,
+                "raft_amd conv_wgrad: db must be contiguous fp32 [N]");
+    a.db = db->data_ptr<float>();
+  }
+  const c10::DeviceGuard guard(dy.device());
+  HIP_OK(launch_conv_wgrad(a, cur_stream()));
+}
+
+// ---------------------------------------------------------------- update-block elementwise
+void pm_any(const at::Tensor& t, const char* name, long P, at::ScalarType dt) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1 && t.size(0) == P && t.scalar_type() == dt,
+              "raft_amd: ", name, " must be a (P, C) pixel-major view of dtype ", dt);
+}
+
+void gru_bwd_a(const at::Tensor& dH, const at::Tensor& z, const at::Tensor& q, const at::Tensor& h,
+               const at::Tensor& dq, const at::Tensor& dz, const at::Tensor& carry) {
+  const long P = dH.size(0), C = dH.size(1);
+  pm_any(dH, "dH", P, at::kFloat);
+  pm_any(z, "z", P, at::kBFloat16);
+  pm_any(q, "q", P, at::kBFloat16);
+  pm_any(h, "h", P, at::kBFloat16);
+  pm_any(dq, "dq", P, at::kBFloat16);
+  pm_any(dz, "dz", P, at::kBFloat16);
+  pm_any(carry, "carry", P, at::kFloat);
+  TORCH_CHECK(z.size(1) >= C && q.size(1) >= C && h.size(1) >= C && dq.size(1) >= C && dz.size(1) >= C &&
+                  carry.size(1) >= C, "raft_amd gru_bwd_a: channel mismatch");
+  const c10::DeviceGuard guard(dH.device());
+  HIP_OK(launch_gru_bwd_a(dH.data_ptr<float>(), dH.stride(0), z.data_ptr(), z.stride(0), q.data_ptr(),
+                          q.stride(0), h.data_ptr(), h.stride(0), dq.data_ptr(), dq.stride(0), dz.data_ptr(),
+                          dz.stride(0), carry.data_ptr<float>(), carry.stride(0), P, C, cur_stream()));
+}
+
+void gru_bwd_b(const at::Tensor& drh, const at::Tensor& r, const at::Tensor& h, const at::Tensor& carry,
+               const at::Tensor& dr) {
+  const long P = drh.size(0), C = drh.size(1);
+  pm_any(drh, "drh", P, at::kFloat);
+  pm_any(r, "r", P, at::kBFloat16);
+  pm_any(h, "h", P, at::kBFloat16);
+  pm_any(carry, "carry", P, at::kFloat);
+  pm_any(dr, "dr", P, at::kBFloat16);
+  const c10::DeviceGuard guard(drh.device());
+  HIP_OK(launch_gru_bwd_b(drh.data_ptr<float>(), drh.stride(0), r.data_ptr(), r.stride(0), h.data_ptr(),
+                          h.stride(0), carry.data_ptr<float>(), carry.stride(0), dr.data_ptr(), dr.stride(0), P,
+                          C, cur_stream()));
+}
+
+void masked_cast(const at::Tensor& src, const c10::optional<at::Tensor>& mask, const at::Tensor& out) {
+  const long P = out.size(0), C = out.size(1);
+  pm_any(src, "src", P, at::kFloat);
+  pm_any(out, "out", P, at::kBFloat16);
+  TORCH_CHECK(src.size(1) <= C, "raft_amd masked_cast: src wider than out");
+  const void* m = nullptr;
+  long sm = 0;
+  if (mask) {
+    pm_any(*mask, "mask", P, at::kBFloat16);
+    TORCH_CHECK(mask->size(1) >= C, "raft_amd masked_cast: mask too narrow");
+    m = mask->data_ptr();
+    sm = mask->stride(0);
+  }
+  const c10::DeviceGuard guard(src.device());
+  HIP_OK(launch_masked_cast(src.data_ptr<float>(), src.stride(0), m, sm, out.data_ptr(), out.stride(0), P, C,
+                            static_cast<int>(src.size(1)), cur_stream()));
+}
+
+void pack_flow(const at::Tensor& flow, const at::Tensor& flow8, const c10::optional<at::Tensor>& motion) {
+  check_gpu(flow, "flow");
+  TORCH_CHECK(flow.scalar_type() == at::kFloat && flow.is_contiguous() && flow.dim() == 4 && flow.size(1) == 2,
+              "raft_amd pack_flow: flow must be contiguous fp32 (B, 2, H, W)");
+  const long B = flow.size(0), HW = flow.size(2) * flow.size(3);
+  TORCH_CHECK(flow8.is_contiguous() && flow8.scalar_type() == at::kBFloat16 && flow8.numel() == B * HW * 8,
+              "raft_amd pack_flow: flow8 must be contiguous bf16 (P, 8)");
+  void* mo = nullptr;
+  long smo = 0;
+  if (motion) {
+    pm_any(*motion, "motion", B * HW, at::kBFloat16);
+    TORCH_CHECK(motion->size(1) >= 2, "raft_amd pack_flow: motion slice needs 2 channels");
+    mo = motion->data_ptr();
+    smo = motion->stride(0);
+  }
+  const c10::DeviceGuard guard(flow.device());
+  HIP_OK(launch_pack_flow(flow.data_ptr<float>(), flow8.data_ptr(), mo, smo, B, HW, cur_stream()));
+}
+
 }  // namespace
 }  // namespace raft_amd
 
 TORCH_LIBRARY(raft_amd, m) {
+  m.def(
+      "conv_fwd(Tensor[] srcs, Tensor wt, int[] geom, int N, Tensor? bias, int epi, int act, float alpha, "
+      "Tensor(a!) out, int acc_c0, Tensor? mask, Tensor? h, Tensor? z, Tensor(b!)? out2) -> ()");
+  m.def("conv_wgrad(Tensor[] srcs, Tensor dy, int[] geom, int N, Tensor(a!) dw, Tensor(b!)? db) -> ()");
   m.def("gru_gates(Tensor zr, Tensor h) -> (Tensor, Tensor)");
   m.def("gru_gates_backward(Tensor zr, Tensor h, Tensor gz, Tensor grh) -> (Tensor, Tensor)");
   m.def("gru_blend(Tensor z, Tensor q, Tensor h) -> Tensor");
   m.def("gru_blend_backward(Tensor z, Tensor q, Tensor h, Tensor g) -> (Tensor, Tensor, Tensor)");
   m.def("gemm_nt(Tensor A, Tensor B, float alpha, ScalarType out_dtype) -> Tensor");
   m.def("avgpool2x2(Tensor x) -> Tensor");
-  m.def("corr_lookup(Tensor[] pyramid, Tensor coords, int radius, ScalarType out_dtype) -> Tensor");
+  m.def("corr_lookup(Tensor[] pyramid, Tensor coords, int radius, ScalarType out_dtype, int out_channels=0) -> Tensor");
+  m.def(
+      "gru_bwd_a(Tensor dH, Tensor z, Tensor q, Tensor h, Tensor(a!) dq, Tensor(b!) dz, Tensor(c!) carry) -> ()");
+  m.def("gru_bwd_b(Tensor(a!) drh, Tensor r, Tensor h, Tensor carry, Tensor(b!) dr) -> ()");
+  m.def("masked_cast(Tensor src, Tensor? mask, Tensor(a!) out) -> ()");
+  m.def("pack_flow(Tensor flow, Tensor(a!) flow8, Tensor(b!)? motion) -> ()");
   m.def("corr_lookup_backward_(Tensor(a!)[] dpyramid, Tensor coords, Tensor grad, int radius) -> ()");
   m.def(
       "pyramid_grad_combine(Tensor[] dpyramid, int B, int H, int W, int ldp, float alpha) -> (Tensor, "
@@ -393,6 +648,12 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("convex_upsample_backward", &raft_amd::convex_upsample_backward);
   m.impl("local_corr", &raft_amd::local_corr);
   m.impl("local_corr_backward", &raft_amd::local_corr_backward);
+  m.impl("conv_fwd", &raft_amd::conv_fwd);
+  m.impl("gru_bwd_a", &raft_amd::gru_bwd_a);
+  m.impl("gru_bwd_b", &raft_amd::gru_bwd_b);
+  m.impl("masked_cast", &raft_amd::masked_cast);
+  m.impl("pack_flow", &raft_amd::pack_flow);
+  m.impl("conv_wgrad", &raft_amd::conv_wgrad);
   m.impl("gru_gates", &raft_amd::gru_gates);
   m.impl("gru_gates_backward", &raft_amd::gru_gates_backward);
   m.impl("gru_blend", &raft_amd::gru_blend);

@@ -1,0 +1,502 @@
+// Implicit-GEMM NHWC convolutions on gfx950 MFMA for the RAFT update block
+// (reference core/update.py:6-136: motion encoder, SepConvGRU/ConvGRU, flow and
+// mask heads), forward + both backward GEMMs, bf16 operands, fp32 accumulate.
+//
+// conv_fwd_kernel  Y[p][n] = epi( sum_{tap,c} X[p + d_tap][c] * W[n][tap][c] )
+//   * M = pixels (B*H*W), N = output channels, K = taps * Cin.
+//   * X may be the channel-concatenation of up to 3 NHWC sources (pointer +
+//     pixel stride each), so torch.cat of [h, inp, motion] etc. is never
+//     materialised; outputs may be written into a channel slice of a wider
+//     buffer (pixel stride != N), which fuses the concatenations on the output
+//     side too (e.g. motion features = [conv out (126) | flow (2)]).
+//   * fused epilogues: bias + ReLU / identity; GRU z||r gates (sigmoid, r*h);
+//     GRU candidate + blend ((1-z) h + z tanh(q)); gradient store with ReLU'
+//     mask of the conv input and partial (channel-range) accumulation.
+//   * the data-gradient of a stride-1 conv is the same kernel on dY with
+//     flipped/transposed packed weights and padding K-1-P.
+// conv_wgrad_kernel  dW[n][tap][c] += sum_p dY[p][n] * X[p + d_tap][c]   (fp32)
+//   * M = out channels, N = K = taps * Cin, reduction over pixels split across
+//     workgroups; both operands are staged transposed into LDS; fp32 atomics
+//     accumulate straight into the persistent weight-gradient buffer, so the
+//     12 refinement iterations never materialise per-iteration weight grads.
+//   * the bias gradient (column sums of dY) is fused into the same pass.
+//
+// Tiling: 256 threads = 4 wave64s in a 2x2 arrangement, v_mfma_f32_32x32x16_bf16,
+// BK = 32 per LDS stage with register double buffering, LDS rows padded to
+// 80 B (conflict-free 16-lane ds_read_b128 groups), XCD-aware tile order.
+#include "common.h"
+
+#include <cstdlib>
+
+namespace raft_amd {
+
+struct ConvSrc {
+  const __bf16* ptr;
+  long stride;  // elements between consecutive pixels
+  int C;        // channels taken from this source (multiple of 8)
+  int pad_;
+};
+
+struct ConvFwdArgs {
+  ConvSrc src[3];
+  int nsrc, Cin;
+  int B, H, W, KH, KW, PH, PW;
+  int K, Kpad;
+  const __bf16* wt;  // packed weights [N][Kpad], k = tap*Cin + c
+  int N;
+  long P;
+  // epilogue
+  int epi;      // 0: bias+act store, 1: grad store, 2: GRU z||r, 3: GRU q+blend
+  int act;      // 0: none, 1: relu
+  int out_f32;  // output element type (epi 0/1)
+  int acc_c0;   // epi 1: accumulate (+=) into out for channels n >= acc_c0
+  float alpha;
+  const float* bias;
+  void* out;
+  long out_stride;
+  const __bf16* mask;  // epi 1: multiply by (mask[p][n] > 0) (ReLU' of the conv input)
+  long mask_stride;
+  const __bf16* h;  // epi 2/3: hidden state
+  long h_stride;
+  const __bf16* z;  // epi 3: update gate
+  long z_stride;
+  __bf16* out2;  // epi 2: r*h, epi 3: tanh(q)
+  long out2_stride;
+};
+
+struct ConvWgradArgs {
+  ConvSrc src[3];
+  int nsrc, Cin;
+  int B, H, W, KH, KW, PH, PW;
+  int K, Kpad;
+  const __bf16* dy;  // [P][dy_stride], N channels used
+  long dy_stride;
+  int N;
+  long P;
+  long pix_per_split;
+  float* dw;  // [N][Kpad] fp32, accumulated
+  float* db;  // [N] fp32, accumulated (may be null)
+};
+
+namespace {
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float tanhf_(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
+
+struct SrcSel {
+  const __bf16* ptr;
+  long stride;
+  int c;
+};
+
+// Source segment holding concatenated channel c (segments are consecutive).
+__device__ __forceinline__ SrcSel select_src(const ConvSrc* src, int c) {
+  const int c0 = src[0].C, c1 = src[1].C;
+  if (c < c0) return {src[0].ptr, src[0].stride, c};
+  if (c < c0 + c1) return {src[1].ptr, src[1].stride, c - c0};
+  return {src[2].ptr, src[2].stride, c - c0 - c1};
+}
+
+// Generic 16-byte im2col chunk (per-thread tap decode): 8 consecutive k of pixel (b, py, px).
+__device__ __forceinline__ u32x4 im2col_chunk(const ConvSrc* src, int Cin, int K, int H, int W, int KW,
+                                              int PH, int PW, bool pvalid, int b, int py, int px, int k) {
+  u32x4 v = {0, 0, 0, 0};
+  if (!pvalid || k >= K) return v;
+  const int tap = k / Cin;
+  const int c = k - tap * Cin;
+  const int ky = tap / KW;
+  const int kx = tap - ky * KW;
+  const int y = py + ky - PH, x = px + kx - PW;
+  if (y < 0 || y >= H || x < 0 || x >= W) return v;
+  const SrcSel s = select_src(src, c);
+  return *reinterpret_cast<const u32x4*>(s.ptr + ((long)(b * H + y) * W + x) * s.stride + s.c);
+}
+
+// Per-thread pixel coordinates of the rows it stages.
+struct PixCoord {
+  long p;  // flat pixel index (or -1 when out of range)
+  int py, px;
+};
+
+__device__ __forceinline__ PixCoord decode_pix(long p, long P, int H, int W) {
+  PixCoord c{-1, 0, 0};
+  if (p < P) {
+    const int HW = H * W;
+    const long b = p / HW;
+    const int rem = (int)(p - b * HW);
+    c.p = p;
+    c.py = rem / W;
+    c.px = rem - c.py * W;
+  }
+  return c;
+}
+
+// ============================================================================ forward / dgrad
+// BM x BN output tile, BK = 64, 256 threads as 2x2 waves, each wave (BM/2)x(BN/2)
+// = TM x TN MFMA 32x32x16 tiles; two LDS stages, one barrier per K step.
+constexpr int FBK = 64, FLDK = FBK + 8;  // padded row: 144 B -> conflict-free ds_read_b128 groups
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvFwdArgs a) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int ACH = BM * FBK / 8 / 256, BCH = BN * FBK / 8 / 256;
+  constexpr int STAGE = (BM + BN) * FLDK;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+
+  const int tilesN = (a.N + BN - 1) / BN;
+  const int tilesM = (int)((a.P + BM - 1) / BM);
+  const int wg = xcd_remap(blockIdx.x, tilesM * tilesN);
+  const int tm = wg / tilesN, tn = wg - (wg / tilesN) * tilesN;
+  const long m0 = (long)tm * BM;
+  const int n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int kc = tid & 7;  // fixed 16-byte column of every chunk this thread stages
+
+  PixCoord pc[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) pc[i] = decode_pix(m0 + (tid >> 3) + 32 * i, a.P, a.H, a.W);
+
+  // the K step never straddles a tap / source segment when every segment is a multiple
+  // of FBK channels (or the conv is 1x1): tap + segment are then wave-uniform (scalar)
+  bool uniform = (a.KH * a.KW == 1) || (a.Cin % FBK == 0);
+  for (int i = 0; i < 3; ++i) uniform = uniform && (a.src[i].C % FBK == 0 || a.KH * a.KW == 1);
+  const int nk = a.Kpad / FBK;
+
+  u32x4 ra[ACH], rb[BCH];
+  auto load = [&](int k0) {
+    if (uniform) {
+      int tap = k0 / a.Cin;
+      int c0 = k0 - tap * a.Cin;
+      if (a.KH * a.KW == 1) { tap = 0; c0 = k0; }
+      const int ky = tap / a.KW, kx = tap - (tap / a.KW) * a.KW;
+      const int dy = ky - a.PH, dx = kx - a.PW;
+      const SrcSel s = select_src(a.src, c0);
+      const long doff = (long)dy * a.W + dx;
+#pragma unroll
+      for (int i = 0; i < ACH; ++i) {
+        const int y = pc[i].py + dy, x = pc[i].px + dx;
+        const bool ok = pc[i].p >= 0 && k0 + kc * 8 < a.K && y >= 0 && y < a.H && x >= 0 && x < a.W;
+        ra[i] = ok ? *reinterpret_cast<const u32x4*>(s.ptr + (pc[i].p + doff) * s.stride + s.c + kc * 8)
+                   : u32x4{0, 0, 0, 0};
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < ACH; ++i) {
+        const long p = pc[i].p;
+        const int b = p >= 0 ? (int)(p / ((long)a.H * a.W)) : 0;
+        ra[i] = im2col_chunk(a.src, a.Cin, a.K, a.H, a.W, a.KW, a.PH, a.PW, p >= 0, b, pc[i].py, pc[i].px,
+                             k0 + kc * 8);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int n = n0 + (tid >> 3) + 32 * i;
+      rb[i] = n < a.N ? *reinterpret_cast<const u32x4*>(a.wt + (long)n * a.Kpad + k0 + kc * 8)
+                      : u32x4{0, 0, 0, 0};
+    }
+  };
+  auto store = [&](int buf) {
+    __bf16* sA = smem + buf * STAGE;
+    __bf16* sB = sA + BM * FLDK;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i)
+      *reinterpret_cast<u32x4*>(sA + ((tid >> 3) + 32 * i) * FLDK + kc * 8) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BCH; ++i)
+      *reinterpret_cast<u32x4*>(sB + ((tid >> 3) + 32 * i) * FLDK + kc * 8) = rb[i];
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int fr = lane & 31, fk = (lane >> 5) * 8;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) load((t + 1) * FBK);
+    const __bf16* sA = smem + (t & 1) * STAGE;
+    const __bf16* sB = sA + BM * FLDK;
+#pragma unroll
+    for (int s = 0; s < FBK / 16; ++s) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(sA + (wm * (BM / 2) + i * 32 + fr) * FLDK + s * 16 + fk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(sB + (wn * (BN / 2) + j * 32 + fr) * FLDK + s * 16 + fk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nk) store((t + 1) & 1);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------------ epilogue
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
+    if (n >= a.N) continue;
+    const float bias = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row >= a.P) continue;
+        float v = acc[i][j][r] * a.alpha + bias;
+        if (a.epi == 0) {
+          if (a.act == 1) v = fmaxf(v, 0.f);
+          if (a.out_f32)
+            static_cast<float*>(a.out)[row * a.out_stride + n] = v;
+          else
+            static_cast<__bf16*>(a.out)[row * a.out_stride + n] = static_cast<__bf16>(v);
+        } else if (a.epi == 1) {
+          if (a.mask && !(static_cast<float>(a.mask[row * a.mask_stride + n]) > 0.f)) v = 0.f;
+          if (a.out_f32) {
+            float* o = static_cast<float*>(a.out) + row * a.out_stride + n;
+            *o = n >= a.acc_c0 ? *o + v : v;
+          } else {
+            __bf16* o = static_cast<__bf16*>(a.out) + row * a.out_stride + n;
+            *o = static_cast<__bf16>(n >= a.acc_c0 ? static_cast<float>(*o) + v : v);
+          }
+        } else if (a.epi == 2) {
+          // z||r gates: out = sigmoid(zr) (2C channels), out2 = r * h
+          const int C = a.N >> 1;
+          const float sg = sigmoidf_(v);
+          static_cast<__bf16*>(a.out)[row * a.out_stride + n] = static_cast<__bf16>(sg);
+          if (n >= C) {
+            const float hv = static_cast<float>(a.h[row * a.h_stride + (n - C)]);
+            a.out2[row * a.out2_stride + (n - C)] = static_cast<__bf16>(sg * hv);
+          }
+        } else {
+          // candidate + blend: out = (1-z) h + z tanh(q), out2 = tanh(q)
+          const float q = tanhf_(v);
+          const float zv = static_cast<float>(a.z[row * a.z_stride + n]);
+          const float hv = static_cast<float>(a.h[row * a.h_stride + n]);
+          static_cast<__bf16*>(a.out)[row * a.out_stride + n] =
+              static_cast<__bf16>((1.f - zv) * hv + zv * q);
+          a.out2[row * a.out2_stride + n] = static_cast<__bf16>(q);
+        }
+      }
+  }
+}
+
+// ============================================================================ wgrad
+// dW tile BM (out channels) x BN (k = tap*Cin + c), reduction over 64-pixel stages.
+// Both operands are staged in their natural [pixel][column] layout with 16-byte
+// writes and read as MFMA operands with ds_read_b64_tr_b16 (gfx950 transposed LDS
+// read: per 16-lane group a 4-row x 16-column block lands column-major in VGPRs).
+// Row pitch = columns + 32 bf16 so the 4 rows of a block hit disjoint 16-bank ranges.
+constexpr int WBK = 64;
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ s16x4 tr_read(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s16x4*)(reinterpret_cast<uintptr_t>(p) & 0xffffffffu));
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(const ConvWgradArgs a) {
+  constexpr int LDA = BM + 32, LDB = BN + 32;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int ACPR = BM / 8, BCPR = BN / 8;  // 16-byte chunks per pixel row
+  constexpr int ACH = WBK * ACPR / 256, BCH = WBK * BCPR / 256;
+  constexpr int STAGE = WBK * (LDA + LDB);
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+  __shared__ float sdb[BM];
+
+  const int tilesM = (a.N + BM - 1) / BM;
+  const int tilesN = (a.K + BN - 1) / BN;
+  const int tiles = tilesM * tilesN;
+  const int split = blockIdx.x / tiles;
+  const int t0 = blockIdx.x - split * tiles;
+  const int tm = t0 / tilesN, tn = t0 - (t0 / tilesN) * tilesN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const long pbeg = (long)split * a.pix_per_split;
+  const long pend = pbeg + a.pix_per_split < a.P ? pbeg + a.pix_per_split : a.P;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const bool do_db = a.db != nullptr && tn == 0;
+  if (tid < BM) sdb[tid] = 0.f;
+
+  const int acc_col = tid % ACPR, arow0 = tid / ACPR;  // A: chunk column fixed per thread
+  const int bcc = tid % BCPR, brow0 = tid / BCPR;
+  constexpr int AROWS = 256 / ACPR, BROWS = 256 / BCPR;
+  float dbacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dbacc[j] = 0.f;
+
+  u32x4 ra[ACH], rb[BCH];
+  auto load = [&](long p0) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const long p = p0 + arow0 + AROWS * i;
+      const int n = m0 + acc_col * 8;
+      ra[i] = (p < pend && n < a.N) ? *reinterpret_cast<const u32x4*>(a.dy + p * a.dy_stride + n)
+                                     : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const long p = p0 + brow0 + BROWS * i;
+      const bool pv = p < pend;
+      int b = 0, py = 0, px = 0;
+      if (pv) {
+        const int HW = a.H * a.W;
+        b = p / HW;
+        const int rem = p - (long)b * HW;
+        py = rem / a.W;
+        px = rem - py * a.W;
+      }
+      rb[i] = im2col_chunk(a.src, a.Cin, a.K, a.H, a.W, a.KW, a.PH, a.PW, pv, b, py, px, n0 + bcc * 8);
+    }
+  };
+  auto store = [&](int buf) {
+    __bf16* sA = smem + buf * STAGE;
+    __bf16* sB = sA + WBK * LDA;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      *reinterpret_cast<u32x4*>(sA + (arow0 + AROWS * i) * LDA + acc_col * 8) = ra[i];
+      if (do_db) {
+        const __bf16* v = reinterpret_cast<const __bf16*>(&ra[i]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dbacc[j] += static_cast<float>(v[j]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) *reinterpret_cast<u32x4*>(sB + (brow0 + BROWS * i) * LDB + bcc * 8) = rb[i];
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // transposed-read lane geometry: half h = lane>>5 picks rows +8, gi = (lane>>4)&1 the
+  // 16-column block, q = row within the 4-row block, pq = 4-column group
+  const int h = lane >> 5, gi = (lane >> 4) & 1, q = (lane & 15) >> 2, pq = lane & 3;
+  const int nsteps = pend > pbeg ? (int)((pend - pbeg + WBK - 1) / WBK) : 0;
+  if (nsteps > 0) {
+    load(pbeg);
+    store(0);
+  }
+  __syncthreads();
+  for (int t = 0; t < nsteps; ++t) {
+    if (t + 1 < nsteps) load(pbeg + (long)(t + 1) * WBK);
+    const __bf16* sA = smem + (t & 1) * STAGE;
+    const __bf16* sB = sA + WBK * LDA;
+#pragma unroll
+    for (int s = 0; s < WBK / 16; ++s) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int col = wm * (BM / 2) + i * 32 + gi * 16 + 4 * pq;
+        const s16x4 lo = tr_read(sA + (s * 16 + h * 8 + q) * LDA + col);
+        const s16x4 hi = tr_read(sA + (s * 16 + h * 8 + 4 + q) * LDA + col);
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * (BN / 2) + j * 32 + gi * 16 + 4 * pq;
+        const s16x4 lo = tr_read(sB + (s * 16 + h * 8 + q) * LDB + col);
+        const s16x4 hi = tr_read(sB + (s * 16 + h * 8 + 4 + q) * LDB + col);
+        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nsteps) store((t + 1) & 1);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
+    if (col >= a.K) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < a.N) atomicAdd(a.dw + (long)row * a.Kpad + col, acc[i][j][r]);
+      }
+  }
+  if (do_db) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(&sdb[acc_col * 8 + j], dbacc[j]);
+    __syncthreads();
+    if (tid < BM && m0 + tid < a.N) atomicAdd(a.db + m0 + tid, sdb[tid]);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
+  if (a.P == 0 || a.N == 0) return hipSuccess;
+  if (a.Kpad % FBK != 0) return hipErrorInvalidValue;
+  auto tiles = [&](int bm, int bn) { return (long)((a.P + bm - 1) / bm) * ((a.N + bn - 1) / bn); };
+  // largest tile that still gives >= 2 workgroups per CU (256 CUs); small-N convs use 64-wide N
+  // measured on MI355X (scripts/bench_convs.py): 64x64 tiles win for every update-block
+  // shape at B=8 (occupancy beats operand reuse at these M=22.8k GEMMs)
+  int cfg = 2;  // 0: 128x128, 1: 64x128, 2: 64x64, 3: 128x64
+  if (const char* e = getenv("RAFT_CONV_FWD_CFG")) cfg = atoi(e);
+  switch (cfg) {
+    case 0:
+      hipLaunchKernelGGL((conv_fwd_kernel<128, 128>), dim3(tiles(128, 128)), dim3(256), 0, s, a);
+      break;
+    case 1:
+      hipLaunchKernelGGL((conv_fwd_kernel<64, 128>), dim3(tiles(64, 128)), dim3(256), 0, s, a);
+      break;
+    case 3:
+      hipLaunchKernelGGL((conv_fwd_kernel<128, 64>), dim3(tiles(128, 64)), dim3(256), 0, s, a);
+      break;
+    default:
+      hipLaunchKernelGGL((conv_fwd_kernel<64, 64>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_wgrad(ConvWgradArgs a, hipStream_t s) {
+  if (a.P == 0 || a.N == 0) return hipSuccess;
+  const bool big = a.N > 64;
+  const int BM = big ? 128 : 64, BN = 128;
+  const long tiles = (long)((a.N + BM - 1) / BM) * ((a.K + BN - 1) / BN);
+  // split the pixel reduction so the grid covers the chip, but keep >= 1024 pixels per
+  // split: every split adds one fp32 atomic pass over the dW tile
+  long splits = (768 + tiles - 1) / tiles;
+  const long max_splits = (a.P + 1023) / 1024;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  long per = (a.P + splits - 1) / splits;
+  per = (per + WBK - 1) / WBK * WBK;
+  splits = (a.P + per - 1) / per;
+  a.pix_per_split = per;
+  const dim3 grid((unsigned)(tiles * splits));
+  if (big)
+    hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace raft_amd

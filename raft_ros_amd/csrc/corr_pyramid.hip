@@ -60,16 +60,20 @@ template <typename OutT>
 __global__ __launch_bounds__(256) void corr_lookup_fwd_kernel(PyrDesc pyr,
                                                               const float* __restrict__ coords,
                                                               OutT* __restrict__ out, int B, int H,
-                                                              int W, int r) {
+                                                              int W, int r, int out_ch) {
   const int rd = 2 * r + 1;
   const int win = rd * rd;
   const int Ch = pyr.levels * win;
   const int HW = H * W;
-  const long total = (long)B * HW * Ch;
+  const long total = (long)B * HW * out_ch;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    const int ch = i % Ch;
-    const long pix = i / Ch;
+    const int ch = i % out_ch;
+    const long pix = i / out_ch;
+    if (ch >= Ch) {  // zero padding channels (K padding of the consuming conv)
+      out[i] = from_f32<OutT>(0.f);
+      continue;
+    }
     const int b = pix / HW;
     const int p = pix - (long)b * HW;
     const int l = ch / win;
@@ -107,7 +111,7 @@ template <typename GT>
 __global__ __launch_bounds__(256) void corr_lookup_bwd_kernel(PyrDesc dpyr,
                                                               const float* __restrict__ coords,
                                                               const GT* __restrict__ gout, int B,
-                                                              int H, int W, int r) {
+                                                              int H, int W, int r, int gstride) {
   const int rd = 2 * r + 1;
   const int nb = rd + 1;
   const int win = rd * rd;
@@ -134,7 +138,7 @@ __global__ __launch_bounds__(256) void corr_lookup_bwd_kernel(PyrDesc dpyr,
     const int yy = (int)fy0 - r + a, xx = (int)fx0 - r + c;
     const int Hl = dpyr.H[l], Wl = dpyr.W[l];
     if (yy < 0 || yy >= Hl || xx < 0 || xx >= Wl) continue;
-    const GT* g = gout + pix * Ch + l * win;
+    const GT* g = gout + pix * gstride + l * win;
     float v = 0.f;
     // tap (ix, iy) touches (iy + {0,1}, ix + {0,1}); this element is corner
     //   (0,0) of tap (c, a), (0,1) of tap (c-1, a), (1,0) of (c, a-1), (1,1) of (c-1, a-1)
@@ -214,36 +218,36 @@ hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int 
 }
 
 hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void* out, int out_dtype,
-                                  int B, int H, int W, int r, hipStream_t s) {
-  const long total = (long)B * H * W * pyr.levels * (2 * r + 1) * (2 * r + 1);
+                                  int B, int H, int W, int r, int out_ch, hipStream_t s) {
+  const long total = (long)B * H * W * out_ch;
   if (total == 0) return hipSuccess;
   const dim3 g(grid_for(total)), blk(256);
   if (out_dtype == kBF16)
     hipLaunchKernelGGL(corr_lookup_fwd_kernel<__bf16>, g, blk, 0, s, pyr, coords,
-                       static_cast<__bf16*>(out), B, H, W, r);
+                       static_cast<__bf16*>(out), B, H, W, r, out_ch);
   else if (out_dtype == kF16)
     hipLaunchKernelGGL(corr_lookup_fwd_kernel<_Float16>, g, blk, 0, s, pyr, coords,
-                       static_cast<_Float16*>(out), B, H, W, r);
+                       static_cast<_Float16*>(out), B, H, W, r, out_ch);
   else
     hipLaunchKernelGGL(corr_lookup_fwd_kernel<float>, g, blk, 0, s, pyr, coords,
-                       static_cast<float*>(out), B, H, W, r);
+                       static_cast<float*>(out), B, H, W, r, out_ch);
   return hipGetLastError();
 }
 
 hipError_t launch_corr_lookup_bwd(const PyrDesc& dpyr, const float* coords, const void* gout,
-                                  int g_dtype, int B, int H, int W, int r, hipStream_t s) {
+                                  int g_dtype, int B, int H, int W, int r, int gstride, hipStream_t s) {
   const long total = (long)B * H * W * dpyr.levels * (2 * r + 2) * (2 * r + 2);
   if (total == 0) return hipSuccess;
   const dim3 g(grid_for(total)), blk(256);
   if (g_dtype == kBF16)
     hipLaunchKernelGGL(corr_lookup_bwd_kernel<__bf16>, g, blk, 0, s, dpyr, coords,
-                       static_cast<const __bf16*>(gout), B, H, W, r);
+                       static_cast<const __bf16*>(gout), B, H, W, r, gstride);
   else if (g_dtype == kF16)
     hipLaunchKernelGGL(corr_lookup_bwd_kernel<_Float16>, g, blk, 0, s, dpyr, coords,
-                       static_cast<const _Float16*>(gout), B, H, W, r);
+                       static_cast<const _Float16*>(gout), B, H, W, r, gstride);
   else
     hipLaunchKernelGGL(corr_lookup_bwd_kernel<float>, g, blk, 0, s, dpyr, coords,
-                       static_cast<const float*>(gout), B, H, W, r);
+                       static_cast<const float*>(gout), B, H, W, r, gstride);
   return hipGetLastError();
 }
 

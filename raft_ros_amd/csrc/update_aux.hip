@@ -1,0 +1,133 @@
+// Small fused elementwise kernels around the implicit-GEMM convs of the fused
+// RAFT update block (raft_ros_amd/ops/update_fused.py).  All tensors are
+// pixel-major (P, C) views with a pixel stride; one thread per (pixel, channel).
+//
+//   gru_bwd_a:  from dH (fp32), z, q, h of a GRU stage (core/update.py:43-58)
+//               dq_pre = dH * z * (1 - q^2)        -> bf16 (dy of the q conv)
+//               dz_pre = dH * (q - h) * z (1 - z)  -> bf16 (first half of the z||r dy)
+//               carry  = dH * (1 - z)              -> fp32
+//   gru_bwd_b:  from d(rh) (fp32, in place), r, h, carry
+//               dr_pre = d(rh) * h * r (1 - r)     -> bf16 (second half of the z||r dy)
+//               dh     = carry + d(rh) * r         -> fp32, written over d(rh)
+//   masked_cast: out_bf16 = src_fp32 * (mask > 0)   (ReLU' + cast for the next dy)
+//   pack_flow:  (B, 2, H, W) fp32 flow -> (P, 8) bf16 [u, v, 0...] and the two
+//               flow channels of the motion-feature buffer (torch.cat in
+//               BasicMotionEncoder.forward, core/update.py:96)
+#include "common.h"
+
+namespace raft_amd {
+namespace {
+
+__global__ __launch_bounds__(256) void gru_bwd_a_kernel(const float* __restrict__ dH, long sdh,
+                                                        const __bf16* __restrict__ z, long sz,
+                                                        const __bf16* __restrict__ q, long sq,
+                                                        const __bf16* __restrict__ h, long sh,
+                                                        __bf16* __restrict__ dq, long sdq,
+                                                        __bf16* __restrict__ dz, long sdz,
+                                                        float* __restrict__ carry, long sc, long P,
+                                                        int C) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= P * C) return;
+  const long p = i / C;
+  const int c = i - p * C;
+  const float g = dH[p * sdh + c];
+  const float zv = static_cast<float>(z[p * sz + c]);
+  const float qv = static_cast<float>(q[p * sq + c]);
+  const float hv = static_cast<float>(h[p * sh + c]);
+  dq[p * sdq + c] = static_cast<__bf16>(g * zv * (1.f - qv * qv));
+  dz[p * sdz + c] = static_cast<__bf16>(g * (qv - hv) * zv * (1.f - zv));
+  carry[p * sc + c] = g * (1.f - zv);
+}
+
+__global__ __launch_bounds__(256) void gru_bwd_b_kernel(float* __restrict__ drh, long sd,
+                                                        const __bf16* __restrict__ r, long sr,
+                                                        const __bf16* __restrict__ h, long sh,
+                                                        const float* __restrict__ carry, long sc,
+                                                        __bf16* __restrict__ dr, long sdr, long P,
+                                                        int C) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= P * C) return;
+  const long p = i / C;
+  const int c = i - p * C;
+  const float g = drh[p * sd + c];
+  const float rv = static_cast<float>(r[p * sr + c]);
+  const float hv = static_cast<float>(h[p * sh + c]);
+  dr[p * sdr + c] = static_cast<__bf16>(g * hv * rv * (1.f - rv));
+  drh[p * sd + c] = carry[p * sc + c] + g * rv;
+}
+
+__global__ __launch_bounds__(256) void masked_cast_kernel(const float* __restrict__ src, long ss,
+                                                          const __bf16* __restrict__ mask, long sm,
+                                                          __bf16* __restrict__ out, long so, long P,
+                                                          int C, int Cvalid) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= P * C) return;
+  const long p = i / C;
+  const int c = i - p * C;
+  float v = c < Cvalid ? src[p * ss + c] : 0.f;
+  if (mask && !(static_cast<float>(mask[p * sm + c]) > 0.f)) v = 0.f;
+  out[p * so + c] = static_cast<__bf16>(v);
+}
+
+__global__ __launch_bounds__(256) void pack_flow_kernel(const float* __restrict__ flow,
+                                                        __bf16* __restrict__ flow8,
+                                                        __bf16* __restrict__ motion, long smo, int B,
+                                                        int HW) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (long)B * HW) return;
+  const int b = p / HW;
+  const int s = p - (long)b * HW;
+  const float u = flow[(long)b * 2 * HW + s], v = flow[(long)b * 2 * HW + HW + s];
+  bf16x8 o;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = static_cast<__bf16>(0.f);
+  o[0] = static_cast<__bf16>(u);
+  o[1] = static_cast<__bf16>(v);
+  *reinterpret_cast<bf16x8*>(flow8 + p * 8) = o;
+  if (motion) {
+    motion[p * smo] = o[0];
+    motion[p * smo + 1] = o[1];
+  }
+}
+
+inline dim3 grid1(long n) { return dim3((unsigned)((n + 255) / 256)); }
+
+}  // namespace
+
+hipError_t launch_gru_bwd_a(const float* dH, long sdh, const void* z, long sz, const void* q, long sq,
+                            const void* h, long sh, void* dq, long sdq, void* dz, long sdz, float* carry,
+                            long sc, long P, int C, hipStream_t s) {
+  if (P * C == 0) return hipSuccess;
+  hipLaunchKernelGGL(gru_bwd_a_kernel, grid1(P * C), dim3(256), 0, s, dH, sdh, (const __bf16*)z, sz,
+                     (const __bf16*)q, sq, (const __bf16*)h, sh, (__bf16*)dq, sdq, (__bf16*)dz, sdz, carry,
+                     sc, P, C);
+  return hipGetLastError();
+}
+
+hipError_t launch_gru_bwd_b(float* drh, long sd, const void* r, long sr, const void* h, long sh,
+                            const float* carry, long sc, void* dr, long sdr, long P, int C,
+                            hipStream_t s) {
+  if (P * C == 0) return hipSuccess;
+  hipLaunchKernelGGL(gru_bwd_b_kernel, grid1(P * C), dim3(256), 0, s, drh, sd, (const __bf16*)r, sr,
+                     (const __bf16*)h, sh, carry, sc, (__bf16*)dr, sdr, P, C);
+  return hipGetLastError();
+}
+
+hipError_t launch_masked_cast(const float* src, long ss, const void* mask, long sm, void* out, long so,
+                              long P, int C, int Cvalid, hipStream_t s) {
+  if (P * C == 0) return hipSuccess;
+  hipLaunchKernelGGL(masked_cast_kernel, grid1(P * C), dim3(256), 0, s, src, ss, (const __bf16*)mask, sm,
+                     (__bf16*)out, so, P, C, Cvalid);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_flow(const float* flow, void* flow8, void* motion, long smo, int B, int HW,
+                            hipStream_t s) {
+  const long P = (long)B * HW;
+  if (!P) return hipSuccess;
+  hipLaunchKernelGGL(pack_flow_kernel, grid1(P), dim3(256), 0, s, flow, (__bf16*)flow8, (__bf16*)motion,
+                     smo, B, HW);
+  return hipGetLastError();
+}
+
+}  // namespace raft_amd

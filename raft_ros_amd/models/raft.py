@@ -27,6 +27,8 @@ import torch
 import torch.nn as nn
 
 from ..ops import CorrPyramid, LocalCorrPyramid, convex_upsample, upflow8
+from ..ops import update_fused
+from ..ops._ext import use_native
 from ..ops.reference import coords_grid
 from .extractor import BasicEncoder, SmallEncoder
 from .update import BasicUpdateBlock, SmallUpdateBlock
@@ -135,6 +137,8 @@ class RAFT(nn.Module):
         corr_dtype = self.amp_dtype if (amp and dev == "cuda") else None
         flow_predictions = []
         flow_up = None
+        if self._use_fused(image1, amp):
+            return self._forward_fused(corr_fn, net, inp, coords0, coords1, iters, test_mode)
         for _ in range(iters):
             coords1 = coords1.detach()
             corr = corr_fn(coords1, out_dtype=corr_dtype)
@@ -150,6 +154,32 @@ class RAFT(nn.Module):
                 flow_up = self.upsample_flow(coords1 - coords0, up_mask)
             flow_predictions.append(flow_up)
 
+        if test_mode:
+            return coords1 - coords0, flow_up
+        return flow_predictions
+
+    # ------------------------------------------------------------------ fused (HIP) update path
+    def _use_fused(self, image1, amp: bool) -> bool:
+        return (amp and self.amp_dtype == torch.bfloat16 and _arg(self.args, "fused_update", True)
+                and update_fused.supported(self.update_block) and use_native(image1))
+
+    def _forward_fused(self, corr_fn, net, inp, coords0, coords1, iters: int, test_mode: bool):
+        """Refinement loop with the update block on fused HIP implicit-GEMM kernels
+        (raft_ros_amd/ops/update_fused.py); same math as the loop above."""
+        upd = update_fused.FusedBasicUpdate(self.update_block, inp)
+        flow_predictions = []
+        flow_up = None
+        for _ in range(iters):
+            coords1 = coords1.detach()
+            if isinstance(corr_fn, CorrPyramid):
+                corr = corr_fn.lookup_padded(coords1, update_fused.CORR_PAD)
+            else:
+                c = corr_fn(coords1, out_dtype=torch.bfloat16).permute(0, 2, 3, 1)
+                corr = torch.nn.functional.pad(c, (0, update_fused.CORR_PAD - c.shape[-1])).contiguous()
+            net, up_mask, delta_flow = upd(net, corr, coords1 - coords0)
+            coords1 = coords1 + delta_flow
+            flow_up = self.upsample_flow(coords1 - coords0, up_mask)
+            flow_predictions.append(flow_up)
         if test_mode:
             return coords1 - coords0, flow_up
         return flow_predictions

@@ -1,0 +1,105 @@
+"""Host side of the implicit-GEMM NHWC conv kernels (``csrc/conv_igemm.hip``).
+
+Activations are *pixel-major* 2-D views ``(P, C)`` (P = B*H*W, unit channel
+stride, pixel stride = the row pitch of the buffer they live in), so a conv can
+read a channel slice of a wider buffer and write into one.  Weights are packed
+once per forward into the GEMM layout the kernels read:
+
+* forward  ``[Cout][Kpad]`` with ``k = tap*Cin_pad + c`` (``pack_fwd``);
+* data-grad ``[Cin_pad][Kpad']`` with flipped taps and ``k = tap*Cout_pad + n``
+  (``pack_dgrad``) -- the data-gradient of a stride-1 conv is itself a conv.
+
+``segments`` describe how the kernel's input channels map onto (possibly
+padded) source channels: a list of ``(real, padded)`` pairs, e.g. the motion
+encoder's flow input is ``[(2, 8)]`` (2 real channels stored in an 8-channel
+buffer) and the corr features ``[(324, 328)]``.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from ._ext import ops
+
+KBLK = 64  # K granularity of the kernels (BK)
+
+
+def _round(n: int, m: int) -> int:
+    return (n + m - 1) // m * m
+
+
+def _expand_cin(w: torch.Tensor, segments: Sequence[Tuple[int, int]]) -> torch.Tensor:
+    """(Cout, Cin, kh, kw) -> (Cout, Cin_pad, kh, kw) with zeros in padded slots."""
+    real = sum(r for r, _ in segments)
+    assert real == w.shape[1], (real, w.shape)
+    if all(r == p for r, p in segments):
+        return w
+    parts, c = [], 0
+    for r, p in segments:
+        parts.append(w[:, c:c + r])
+        if p > r:
+            parts.append(w.new_zeros(w.shape[0], p - r, w.shape[2], w.shape[3]))
+        c += r
+    return torch.cat(parts, dim=1)
+
+
+def pack_fwd(w: torch.Tensor, segments: Optional[Sequence[Tuple[int, int]]] = None, scale: float = 1.0):
+    """(Cout, Cin, kh, kw) fp32 -> bf16 [Cout][Kpad] (k = tap*Cin_pad + c)."""
+    cout, cin, kh, kw = w.shape
+    segments = segments or [(cin, cin)]
+    we = _expand_cin(w.detach(), segments)
+    cin_p = we.shape[1]
+    k = kh * kw * cin_p
+    out = torch.zeros(cout, _round(k, KBLK), device=w.device, dtype=torch.bfloat16)
+    out[:, :k] = (we * scale).permute(0, 2, 3, 1).reshape(cout, k).to(torch.bfloat16)
+    return out
+
+
+def pack_dgrad(w: torch.Tensor, segments: Optional[Sequence[Tuple[int, int]]] = None, cout_pad: Optional[int] = None,
+               scale: float = 1.0):
+    """bf16 [Cin_pad][Kpad] for dX = conv(dY, W flipped/transposed), k = tap*Cout_pad + n."""
+    cout, cin, kh, kw = w.shape
+    segments = segments or [(cin, cin)]
+    we = _expand_cin(w.detach(), segments) * scale  # (Cout, Cin_pad, kh, kw)
+    cout_p = cout_pad or _round(cout, 8)
+    if cout_p > cout:
+        we = torch.cat([we, we.new_zeros(cout_p - cout, *we.shape[1:])], dim=0)
+    wt = we.flip(2, 3).permute(1, 2, 3, 0)  # (Cin_pad, kh, kw, Cout_pad)
+    cin_p = wt.shape[0]
+    k = kh * kw * cout_p
+    out = torch.zeros(cin_p, _round(k, KBLK), device=w.device, dtype=torch.bfloat16)
+    out[:, :k] = wt.reshape(cin_p, k).to(torch.bfloat16)
+    return out
+
+
+def unpack_grad(dw: torch.Tensor, shape, segments: Optional[Sequence[Tuple[int, int]]] = None) -> torch.Tensor:
+    """fp32 [Cout][Kpad] accumulated weight gradient -> (Cout, Cin, kh, kw)."""
+    cout, cin, kh, kw = shape
+    segments = segments or [(cin, cin)]
+    cin_p = sum(p for _, p in segments)
+    g = dw[:cout, : kh * kw * cin_p].reshape(cout, kh, kw, cin_p).permute(0, 3, 1, 2)
+    if cin_p != cin:
+        parts, c = [], 0
+        for r, p in segments:
+            parts.append(g[:, c:c + r])
+            c += p
+        g = torch.cat(parts, dim=1)
+    return g.contiguous()
+
+
+def geom(B: int, H: int, W: int, kh: int, kw: int, ph: int, pw: int) -> List[int]:
+    return [B, H, W, kh, kw, ph, pw]
+
+
+EPI_STORE, EPI_GRAD, EPI_GRU_ZR, EPI_GRU_Q = 0, 1, 2, 3
+
+
+def conv_fwd(srcs, wt, g, N, out, bias=None, act=0, alpha=1.0, epi=EPI_STORE, acc_c0=1 << 30, mask=None,
+             h=None, z=None, out2=None):
+    ops().conv_fwd(list(srcs), wt, g, N, bias, epi, act, alpha, out, acc_c0, mask, h, z, out2)
+    return out
+
+
+def conv_wgrad(srcs, dy, g, N, dw, db=None):
+    ops().conv_wgrad(list(srcs), dy, g, N, dw, db)

@@ -107,9 +107,9 @@ class _BuildPyramid(torch.autograd.Function):
 
 class _Lookup(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, token, coords, state: _PyramidState, out_dtype):
+    def forward(ctx, token, coords, state: _PyramidState, out_dtype, out_channels=0):
         coords = coords.detach().float().contiguous()
-        out = ops().corr_lookup(state.levels, coords, state.radius, out_dtype)
+        out = ops().corr_lookup(state.levels, coords, state.radius, out_dtype, out_channels)
         ctx.state = state
         ctx.save_for_backward(coords)
         return out
@@ -120,7 +120,7 @@ class _Lookup(torch.autograd.Function):
         state: _PyramidState = ctx.state
         if state.levels:
             ops().corr_lookup_backward_(state.grad_buffers(), coords, gout.contiguous(), state.radius)
-        return torch.zeros((), device=gout.device), None, None, None
+        return torch.zeros((), device=gout.device), None, None, None, None
 
 
 class CorrPyramid:
@@ -142,10 +142,15 @@ class CorrPyramid:
             corr = ref.corr_volume(fmap1.float(), fmap2.float())
             self.pyramid = ref.build_pyramid(corr, num_levels)
 
+    def lookup_padded(self, coords: torch.Tensor, out_channels: int, out_dtype=torch.bfloat16) -> torch.Tensor:
+        """Native only: (B, H, W, out_channels) NHWC features, zero beyond L*(2r+1)^2
+        (the K padding the fused motion encoder's 1x1 conv expects)."""
+        return _Lookup.apply(self.token, coords, self.state, out_dtype, out_channels)
+
     def __call__(self, coords: torch.Tensor, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
         if self.native:
             dt = out_dtype or torch.float32
-            out = _Lookup.apply(self.token, coords, self.state, dt)
+            out = _Lookup.apply(self.token, coords, self.state, dt, 0)
             return out.permute(0, 3, 1, 2)  # channels-last view (B, Ch, H, W)
         out = ref.pyramid_lookup(self.pyramid, coords, self.radius)
         return out if out_dtype is None else out.to(out_dtype)

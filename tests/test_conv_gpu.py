@@ -1,0 +1,143 @@
+"""Implicit-GEMM NHWC conv kernels vs torch.nn.functional.conv2d in fp32."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from raft_ros_amd.ops import conv as C
+
+pytestmark = pytest.mark.gpu
+
+
+def _pm(t):
+    """(B, C, H, W) -> bf16 pixel-major (P, C) contiguous."""
+    B, Ch, H, W = t.shape
+    return t.permute(0, 2, 3, 1).reshape(B * H * W, Ch).to(torch.bfloat16).contiguous()
+
+
+def _from_pm(t, B, H, W):
+    return t.reshape(B, H, W, -1).permute(0, 3, 1, 2).float()
+
+
+def _rel(a, b):
+    return ((a - b).norm() / b.norm().clamp_min(1e-6)).item()
+
+
+CASES = [
+    # (Cin segments (real, padded), Cout, kh, kw, act)
+    ([(256, 256)], 192, 3, 3, 1),
+    ([(128, 128), (128, 128), (128, 128)], 256, 1, 5, 0),
+    ([(128, 128), (256, 256)], 128, 5, 1, 0),
+    ([(2, 8)], 128, 7, 7, 1),
+    ([(324, 328)], 256, 1, 1, 1),
+    ([(256, 256)], 2, 3, 3, 0),
+    ([(256, 256)], 576, 1, 1, 0),
+]
+
+
+@pytest.mark.parametrize("segs,cout,kh,kw,act", CASES)
+def test_conv_fwd_dgrad_wgrad(cuda, segs, cout, kh, kw, act):
+    torch.manual_seed(0)
+    B, H, W = 2, 13, 19
+    ph, pw = kh // 2, kw // 2
+    cin = sum(r for r, _ in segs)
+    x_parts = [torch.randn(B, r, H, W, device=cuda) for r, _ in segs]
+    w = torch.randn(cout, cin, kh, kw, device=cuda) / (cin * kh * kw) ** 0.5
+    bias = torch.randn(cout, device=cuda)
+    # bf16-rounded operands for the fp32 reference
+    xr = torch.cat([p.bfloat16().float() for p in x_parts], dim=1).requires_grad_(True)
+    wr = w.bfloat16().float().requires_grad_(True)
+    br = bias.clone().requires_grad_(True)
+    y = F.conv2d(xr, wr, br, padding=(ph, pw))
+    if act:
+        y = F.relu(y)
+
+    P = B * H * W
+    srcs = []
+    for (r, pd), part in zip(segs, x_parts):
+        buf = torch.zeros(P, pd, device=cuda, dtype=torch.bfloat16)
+        buf[:, :r] = _pm(part)
+        srcs.append(buf)
+    g = C.geom(B, H, W, kh, kw, ph, pw)
+    wt = C.pack_fwd(w, segs)
+    # forward, written into a channel slice of a wider buffer
+    outbuf = torch.zeros(P, (cout + 7) // 8 * 8 + 8, device=cuda, dtype=torch.bfloat16)
+    C.conv_fwd(srcs, wt, g, cout, outbuf[:, :cout], bias=bias, act=act)
+    got = _from_pm(outbuf[:, :cout], B, H, W)
+    assert _rel(got, y) < 1e-2, _rel(got, y)
+    assert (outbuf[:, cout:] == 0).all()
+
+    # backward
+    gy = torch.randn_like(y)
+    if act:
+        gy = gy * (y > 0)
+    y.backward(gy)
+    cout_p = (cout + 7) // 8 * 8
+    dy = torch.zeros(P, cout_p, device=cuda, dtype=torch.bfloat16)
+    dy[:, :cout] = _pm(gy)
+    # data grad
+    cin_p = sum(p for _, p in segs)
+    wtd = C.pack_dgrad(w, segs, cout_p)
+    dx = torch.zeros(P, cin_p, device=cuda, dtype=torch.float32)
+    C.conv_fwd([dy], wtd, C.geom(B, H, W, kh, kw, kh - 1 - ph, kw - 1 - pw), cin_p, dx, epi=C.EPI_GRAD)
+    dx_real = torch.cat([dx[:, o:o + r] for o, (r, _) in zip(
+        [sum(p for _, p in segs[:i]) for i in range(len(segs))], segs)], dim=1)
+    assert _rel(_from_pm(dx_real, B, H, W), xr.grad) < 1e-2
+    # weight + bias grad (accumulated twice -> 2x)
+    dw = torch.zeros(cout, wt.shape[1], device=cuda)
+    db = torch.zeros(cout, device=cuda)
+    C.conv_wgrad(srcs, dy, g, cout, dw, db)
+    C.conv_wgrad(srcs, dy, g, cout, dw, db)
+    gw = C.unpack_grad(dw, w.shape, segs)
+    assert _rel(gw, 2 * wr.grad) < 1e-2, _rel(gw, 2 * wr.grad)
+    assert _rel(db, 2 * dy.float().sum(0)[:cout]) < 1e-4
+
+
+def test_dgrad_relu_mask_and_partial_accumulate(cuda):
+    torch.manual_seed(1)
+    B, H, W, cin, cout = 1, 9, 10, 64, 32
+    P = B * H * W
+    x = torch.randn(P, cin, device=cuda).bfloat16()
+    w = torch.randn(cout, cin, 3, 3, device=cuda) * 0.1
+    dy = torch.randn(P, cout, device=cuda).bfloat16()
+    base = torch.randn(P, cin, device=cuda)
+    out = base.clone()
+    C.conv_fwd([dy], C.pack_dgrad(w), C.geom(B, H, W, 3, 3, 1, 1), cin, out, epi=C.EPI_GRAD, acc_c0=32, mask=x)
+    xr = _from_pm(x, B, H, W).requires_grad_(True)
+    y = F.conv2d(xr, w.bfloat16().float(), padding=1)
+    y.backward(_from_pm(dy, B, H, W))
+    ref = xr.grad.permute(0, 2, 3, 1).reshape(P, cin) * (x.float() > 0)
+    ref[:, 32:] += base[:, 32:]
+    assert _rel(out, ref) < 1e-2
+
+
+def test_gru_epilogues(cuda):
+    torch.manual_seed(2)
+    B, H, W, Ch = 2, 7, 11, 128
+    P = B * H * W
+    hx = torch.randn(P, 3 * Ch, device=cuda).bfloat16()  # [h | x]
+    h = hx[:, :Ch]
+    wzr = torch.randn(2 * Ch, 3 * Ch, 1, 5, device=cuda) * 0.05
+    bzr = torch.randn(2 * Ch, device=cuda) * 0.1
+    g = C.geom(B, H, W, 1, 5, 0, 2)
+    zr = torch.empty(P, 2 * Ch, device=cuda, dtype=torch.bfloat16)
+    rh = torch.empty(P, Ch, device=cuda, dtype=torch.bfloat16)
+    C.conv_fwd([hx], C.pack_fwd(wzr), g, 2 * Ch, zr, bias=bzr, epi=C.EPI_GRU_ZR, h=h, out2=rh)
+    hxf = _from_pm(hx, B, H, W)
+    pre = F.conv2d(hxf, wzr.bfloat16().float(), bzr, padding=(0, 2))
+    sig = torch.sigmoid(pre)
+    assert _rel(_from_pm(zr, B, H, W), sig) < 1e-2
+    rh_ref = sig[:, Ch:] * hxf[:, :Ch]
+    assert _rel(_from_pm(rh, B, H, W), rh_ref) < 1e-2
+    # candidate + blend: sources [rh | x]
+    wq = torch.randn(Ch, 3 * Ch, 1, 5, device=cuda) * 0.05
+    bq = torch.randn(Ch, device=cuda) * 0.1
+    hn = torch.empty(P, Ch, device=cuda, dtype=torch.bfloat16)
+    q = torch.empty(P, Ch, device=cuda, dtype=torch.bfloat16)
+    z = zr[:, :Ch]
+    C.conv_fwd([rh, hx[:, Ch:]], C.pack_fwd(wq), g, Ch, hn, bias=bq, epi=C.EPI_GRU_Q, h=h, z=z, out2=q)
+    rx = torch.cat([_from_pm(rh, B, H, W), hxf[:, Ch:]], dim=1)
+    qr = torch.tanh(F.conv2d(rx, wq.bfloat16().float(), bq, padding=(0, 2)))
+    zf = _from_pm(z, B, H, W)
+    hn_ref = (1 - zf) * hxf[:, :Ch] + zf * qr
+    assert _rel(_from_pm(q, B, H, W), qr) < 1e-2
+    assert _rel(_from_pm(hn, B, H, W), hn_ref) < 1e-2
