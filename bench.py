@@ -31,7 +31,7 @@ import torch.distributed as dist
 
 METRIC = "image-pairs/sec training + Sintel-clean EPE, RAFT base at 1/2/4/8 MI355X"
 # Eager PyTorch baseline of the reference algorithm on 1x MI355X (pairs/s), see BASELINE.md
-BASELINE_PAIRS_PER_SEC = None
+BASELINE_PAIRS_PER_SEC = 94.932  # measured r1: bench.py --impl reference, bf16, batch 8
 
 
 def parse():
@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--amp_dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--lr", type=float, default=4e-4)
     ap.add_argument("--bucket_mb", type=float, default=32.0)
+    ap.add_argument("--no_fused", action="store_true", help="update block on PyTorch/MIOpen convs")
     return ap.parse_args()
 
 
@@ -71,7 +72,8 @@ def main():
     torch.backends.cudnn.benchmark = True
     torch.manual_seed(1234 + rank)
     margs = Namespace(small=args.small, mixed_precision=True, amp_dtype=args.amp_dtype, alternate_corr=False,
-                      dropout=0.0, channels_last=args.impl == "native")
+                      dropout=0.0, channels_last=args.impl == "native",
+                      fused_update=not args.no_fused)
     model = RAFT(margs).to(device)
     if args.impl == "native":
         model = model.to(memory_format=torch.channels_last)
@@ -144,6 +146,7 @@ def main():
                 "iters": args.iters,
                 "parallelism": f"dp{world}",
                 "impl": args.impl,
+                "fused_update": (args.impl == "native" and not args.no_fused),
             },
             "final_loss": round(float(loss.item()), 4),
             "epe_synthetic": round(float(metrics["epe"].item()), 4),

@@ -293,6 +293,241 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvFwdArgs a) {
   }
 }
 
+// ============================================================================ forward v3
+// Direct-to-LDS pipeline: every 16-byte chunk of the A (im2col) and B (packed weight)
+// tiles is fetched with global_load_lds_dwordx4 into an S-stage LDS ring, so S-1
+// K steps are in flight with no staging registers.  LDS rows are 128 B (64 bf16)
+// with the chunk index XOR-swizzled by (row>>1)&7: the lane-linear DMA image stays
+// contiguous (the swizzle is applied to the per-lane SOURCE address) and every
+// 16-lane ds_read_b128 group of the MFMA fragment reads hits 16 distinct bank slots.
+// Padding / out-of-image taps are redirected to a zero page.  Waits are counted
+// (s_waitcnt vmcnt(N)) and barriers are raw s_barrier so the DMA stays in flight
+// across them (cdna_hip_programming.md "Pipelining across barriers").
+__device__ __attribute__((aligned(64))) uint32_t g_zero_page[64];
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void glds16(const void* g, __bf16* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void*)(reinterpret_cast<uintptr_t>(lds_wave_base) & 0xffffffffu),
+                                   16, 0, 0);
+}
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+template <int BM, int BN, int S>
+__global__ __launch_bounds__(256) void conv_fwd3_kernel(const ConvFwdArgs a) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int AI = BM / 32, BI = BN / 32;  // wave-instructions (8 rows each) per wave per step
+  constexpr int G = AI + BI;                 // glds per thread per step
+  constexpr int STAGE = (BM + BN) * 64;      // bf16 elements
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[S * STAGE];
+
+  // kernel arguments used in the loop, as plain scalars (taking the address of the
+  // by-value argument struct inside a lambda turns its reads into VMEM loads that
+  // hipcc then waits for with vmcnt(0), draining the DMA pipeline)
+  const __bf16* const sp0 = a.src[0].ptr;
+  const __bf16* const sp1 = a.src[1].ptr;
+  const __bf16* const sp2 = a.src[2].ptr;
+  const long ss0 = a.src[0].stride, ss1 = a.src[1].stride, ss2 = a.src[2].stride;
+  const int sc0 = a.src[0].C, sc1 = a.src[1].C;
+  const int Cin = a.Cin, K = a.K, Kpad = a.Kpad, H = a.H, W = a.W, KW = a.KW, PH = a.PH, PW = a.PW;
+  const int ntaps = a.KH * a.KW;
+  const long P = a.P;
+  const int Nn = a.N;
+
+  const int tilesN = (Nn + BN - 1) / BN;
+  const int tilesM = (int)((P + BM - 1) / BM);
+  const int wg = xcd_remap(blockIdx.x, tilesM * tilesN);
+  const int tm = wg / tilesN, tn = wg - (wg / tilesN) * tilesN;
+  const long m0 = (long)tm * BM;
+  const int n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lrow = lane >> 3, lpc = lane & 7;  // row within an 8-row DMA block, physical chunk
+
+  PixCoord pc[AI];
+  int achunk[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = (wave * AI + i) * 8 + lrow;
+    pc[i] = decode_pix(m0 + row, P, H, W);
+    achunk[i] = swz(row, lpc);
+  }
+  int bchunk[BI];
+  const __bf16* bsrc[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int row = (wave * BI + i) * 8 + lrow;
+    bchunk[i] = swz(row, lpc);
+    bsrc[i] = (n0 + row < Nn) ? a.wt + (long)(n0 + row) * Kpad : nullptr;
+  }
+  bool uniform = (ntaps == 1) || (Cin % 64 == 0);
+  uniform = uniform && (ntaps == 1 || ((sc0 % 64 == 0) && (sc1 % 64 == 0)));
+  const int nk = Kpad / 64;
+  const void* zero = g_zero_page;
+
+  auto pick = [&](int c, const __bf16*& ptr, long& stride, int& cc) {
+    if (c < sc0) { ptr = sp0; stride = ss0; cc = c; }
+    else if (c < sc0 + sc1) { ptr = sp1; stride = ss1; cc = c - sc0; }
+    else { ptr = sp2; stride = ss2; cc = c - sc0 - sc1; }
+  };
+
+  auto issue = [&](int step, int stage) {
+    const int k0 = step * 64;
+    __bf16* sA = smem + stage * STAGE;
+    __bf16* sB = sA + BM * 64;
+    if (uniform) {
+      int tap = 0, c0 = k0;
+      if (ntaps != 1) {
+        tap = k0 / Cin;
+        c0 = k0 - tap * Cin;
+      }
+      const int ky = tap / KW, kx = tap - (tap / KW) * KW;
+      const int dy = ky - PH, dx = kx - PW;
+      const __bf16* ptr;
+      long stride;
+      int cc;
+      pick(c0, ptr, stride, cc);
+      const long doff = (long)dy * W + dx;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int y = pc[i].py + dy, x = pc[i].px + dx;
+        const int k = k0 + achunk[i] * 8;
+        const bool ok = pc[i].p >= 0 && k < K && y >= 0 && y < H && x >= 0 && x < W;
+        const void* g = ok ? (const void*)(ptr + (pc[i].p + doff) * stride + cc + achunk[i] * 8) : zero;
+        glds16(g, sA + (wave * AI + i) * 512);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int k = k0 + achunk[i] * 8;
+        const void* g = zero;
+        if (pc[i].p >= 0 && k < K) {
+          const int tap = k / Cin;
+          const int c = k - tap * Cin;
+          const int ky = tap / KW, kx = tap - (tap / KW) * KW;
+          const int y = pc[i].py + ky - PH, x = pc[i].px + kx - PW;
+          if (y >= 0 && y < H && x >= 0 && x < W) {
+            const __bf16* ptr;
+            long stride;
+            int cc;
+            pick(c, ptr, stride, cc);
+            g = ptr + (pc[i].p + (long)(ky - PH) * W + (kx - PW)) * stride + cc;
+          }
+        }
+        glds16(g, sA + (wave * AI + i) * 512);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const void* g = bsrc[i] ? (const void*)(bsrc[i] + k0 + bchunk[i] * 8) : zero;
+      glds16(g, sB + (wave * BI + i) * 512);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int fr = lane & 31, fh = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < nk) issue(i, i);
+
+  for (int t = 0; t < nk; ++t) {
+    // retire step t: leave the younger steps (up to S-2) in flight
+    const int ahead = (nk - 1 - t) < (S - 2) ? (nk - 1 - t) : (S - 2);
+    if (ahead >= S - 2) wait_vmcnt<(S - 2) * G>();
+    else if (ahead == 2) wait_vmcnt<2 * G>();
+    else if (ahead == 1) wait_vmcnt<G>();
+    else wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + S - 1 < nk) issue(t + S - 1, (t + S - 1) % S);
+    const __bf16* sA = smem + (t % S) * STAGE;
+    const __bf16* sB = sA + BM * 64;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c = 2 * s + fh;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * (BM / 2) + i * 32 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(sA + row * 64 + swz(row, c) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * (BN / 2) + j * 32 + fr;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(sB + row * 64 + swz(row, c) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  wait_vmcnt<0>();
+
+  // ------------------------------------------------------------------ epilogue
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
+    if (n >= a.N) continue;
+    const float bias = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row >= a.P) continue;
+        float v = acc[i][j][r] * a.alpha + bias;
+        if (a.epi == 0) {
+          if (a.act == 1) v = fmaxf(v, 0.f);
+          if (a.out_f32)
+            static_cast<float*>(a.out)[row * a.out_stride + n] = v;
+          else
+            static_cast<__bf16*>(a.out)[row * a.out_stride + n] = static_cast<__bf16>(v);
+        } else if (a.epi == 1) {
+          if (a.mask && !(static_cast<float>(a.mask[row * a.mask_stride + n]) > 0.f)) v = 0.f;
+          if (a.out_f32) {
+            float* o = static_cast<float*>(a.out) + row * a.out_stride + n;
+            *o = n >= a.acc_c0 ? *o + v : v;
+          } else {
+            __bf16* o = static_cast<__bf16*>(a.out) + row * a.out_stride + n;
+            *o = static_cast<__bf16>(n >= a.acc_c0 ? static_cast<float>(*o) + v : v);
+          }
+        } else if (a.epi == 2) {
+          const int C = a.N >> 1;
+          const float sg = sigmoidf_(v);
+          static_cast<__bf16*>(a.out)[row * a.out_stride + n] = static_cast<__bf16>(sg);
+          if (n >= C) {
+            const float hv = static_cast<float>(a.h[row * a.h_stride + (n - C)]);
+            a.out2[row * a.out2_stride + (n - C)] = static_cast<__bf16>(sg * hv);
+          }
+        } else {
+          const float q = tanhf_(v);
+          const float zv = static_cast<float>(a.z[row * a.z_stride + n]);
+          const float hv = static_cast<float>(a.h[row * a.h_stride + n]);
+          static_cast<__bf16*>(a.out)[row * a.out_stride + n] =
+              static_cast<__bf16>((1.f - zv) * hv + zv * q);
+          a.out2[row * a.out2_stride + n] = static_cast<__bf16>(q);
+        }
+      }
+  }
+}
+
 // ============================================================================ wgrad
 // dW tile BM (out channels) x BN (k = tap*Cin + c), reduction over 64-pixel stages.
 // Both operands are staged in their natural [pixel][column] layout with 16-byte
@@ -461,6 +696,18 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   int cfg = 2;  // 0: 128x128, 1: 64x128, 2: 64x64, 3: 128x64
   if (const char* e = getenv("RAFT_CONV_FWD_CFG")) cfg = atoi(e);
   switch (cfg) {
+    case 4:
+      hipLaunchKernelGGL((conv_fwd3_kernel<64, 64, 4>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
+      break;
+    case 5:
+      hipLaunchKernelGGL((conv_fwd3_kernel<128, 64, 3>), dim3(tiles(128, 64)), dim3(256), 0, s, a);
+      break;
+    case 6:
+      hipLaunchKernelGGL((conv_fwd3_kernel<64, 128, 3>), dim3(tiles(64, 128)), dim3(256), 0, s, a);
+      break;
+    case 7:
+      hipLaunchKernelGGL((conv_fwd3_kernel<128, 128, 2>), dim3(tiles(128, 128)), dim3(256), 0, s, a);
+      break;
     case 0:
       hipLaunchKernelGGL((conv_fwd_kernel<128, 128>), dim3(tiles(128, 128)), dim3(256), 0, s, a);
       break;
