@@ -111,6 +111,11 @@ struct ConvWgradArgs {
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s);
 hipError_t launch_conv_wgrad(ConvWgradArgs a, hipStream_t s);
 
+hipError_t launch_instance_norm_fwd(int dtype, const void* x, void* y, float* stats, int N, int HW, int C,
+                                    int relu, float eps, hipStream_t s);
+hipError_t launch_instance_norm_bwd(int dtype, const void* x, const void* dy, const float* stats, float* gsum,
+                                    void* dx, int N, int HW, int C, int relu, hipStream_t s);
+
 namespace {
 
 #define HIP_OK(expr)                                                                     \
@@ -606,10 +611,45 @@ void pack_flow(const at::Tensor& flow, const at::Tensor& flow8, const c10::optio
   HIP_OK(launch_pack_flow(flow.data_ptr<float>(), flow8.data_ptr(), mo, smo, B, HW, cur_stream()));
 }
 
+// ---------------------------------------------------------------- NHWC instance norm
+void check_in(const at::Tensor& x, const char* name) {
+  check_gpu(x, name);
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat) && x.size(1) % 8 == 0 &&
+                  x.size(1) <= 512,
+              "raft_amd instance_norm: ", name, " must be channels-last bf16/fp32 (N, C%8==0, H, W)");
+}
+
+std::tuple<at::Tensor, at::Tensor> instance_norm_fwd(const at::Tensor& x, bool relu, double eps) {
+  check_in(x, "x");
+  const long N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  const c10::DeviceGuard guard(x.device());
+  auto y = at::empty(x.sizes(), x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto stats = at::empty({N, C, 2}, x.options().dtype(at::kFloat));
+  HIP_OK(launch_instance_norm_fwd(dtype_code(x.scalar_type()), x.data_ptr(), y.data_ptr(), stats.data_ptr<float>(),
+                                  N, HW, C, relu, static_cast<float>(eps), cur_stream()));
+  return {y, stats};
+}
+
+at::Tensor instance_norm_bwd(const at::Tensor& x, const at::Tensor& dy, const at::Tensor& stats, bool relu) {
+  check_in(x, "x");
+  auto g = dy.to(x.scalar_type()).contiguous(at::MemoryFormat::ChannelsLast);
+  const long N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  TORCH_CHECK(stats.is_contiguous() && stats.numel() == N * C * 2, "raft_amd instance_norm_bwd: bad stats");
+  const c10::DeviceGuard guard(x.device());
+  auto dx = at::empty(x.sizes(), x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto gsum = at::empty({N, C, 2}, x.options().dtype(at::kFloat));
+  HIP_OK(launch_instance_norm_bwd(dtype_code(x.scalar_type()), x.data_ptr(), g.data_ptr(), stats.data_ptr<float>(),
+                                  gsum.data_ptr<float>(), dx.data_ptr(), N, HW, C, relu, cur_stream()));
+  return dx;
+}
+
 }  // namespace
 }  // namespace raft_amd
 
 TORCH_LIBRARY(raft_amd, m) {
+  m.def("instance_norm_fwd(Tensor x, bool relu, float eps) -> (Tensor, Tensor)");
+  m.def("instance_norm_bwd(Tensor x, Tensor dy, Tensor stats, bool relu) -> Tensor");
   m.def(
       "conv_fwd(Tensor[] srcs, Tensor wt, int[] geom, int N, Tensor? bias, int epi, int act, float alpha, "
       "Tensor(a!) out, int acc_c0, Tensor? mask, Tensor? h, Tensor? z, Tensor(b!)? out2) -> ()");
@@ -649,6 +689,8 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("local_corr", &raft_amd::local_corr);
   m.impl("local_corr_backward", &raft_amd::local_corr_backward);
   m.impl("conv_fwd", &raft_amd::conv_fwd);
+  m.impl("instance_norm_fwd", &raft_amd::instance_norm_fwd);
+  m.impl("instance_norm_bwd", &raft_amd::instance_norm_bwd);
   m.impl("gru_bwd_a", &raft_amd::gru_bwd_a);
   m.impl("gru_bwd_b", &raft_amd::gru_bwd_b);
   m.impl("masked_cast", &raft_amd::masked_cast);

@@ -26,6 +26,7 @@
 // 80 B (conflict-free 16-lane ds_read_b128 groups), XCD-aware tile order.
 #include "common.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace raft_amd {
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvFwdArgs a) {
   const int nk = a.Kpad / FBK;
 
   u32x4 ra[ACH], rb[BCH];
-  auto load = [&](int k0) {
+  auto load = [&](int k0) __attribute__((always_inline)) {
     if (uniform) {
       int tap = k0 / a.Cin;
       int c0 = k0 - tap * a.Cin;
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvFwdArgs a) {
                       : u32x4{0, 0, 0, 0};
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf) __attribute__((always_inline)) {
     __bf16* sA = smem + buf * STAGE;
     __bf16* sB = sA + BM * FLDK;
 #pragma unroll
@@ -378,7 +379,7 @@ __global__ __launch_bounds__(256) void conv_fwd3_kernel(const ConvFwdArgs a) {
     else { ptr = sp2; stride = ss2; cc = c - sc0 - sc1; }
   };
 
-  auto issue = [&](int step, int stage) {
+  auto issue = [&](int step, int stage) __attribute__((always_inline)) {
     const int k0 = step * 64;
     __bf16* sA = smem + stage * STAGE;
     __bf16* sB = sA + BM * 64;
@@ -528,6 +529,337 @@ __global__ __launch_bounds__(256) void conv_fwd3_kernel(const ConvFwdArgs a) {
   }
 }
 
+// ============================================================================ forward v4
+// Same direct-to-LDS ring as v3, but every load is a bounds-checked raw buffer load
+// (buffer_load_dwordx4 ... lds): the per-lane byte offset is one v_mad_u32_u24 of a
+// precomputed pixel index, padding taps / rows past P / N use an out-of-range offset
+// (the hardware returns zeros), the weight tile needs no per-step VALU at all
+// (its K offset rides in the scalar soffset), and the epilogue is staged through
+// LDS so each thread finishes 8 consecutive output channels with 16-byte accesses.
+// (rocprofv3 PMC on v2/v3: ~15 VALU instructions per MFMA from 64-bit address math
+// and per-element epilogues -- the kernels were VALU-issue bound.)
+constexpr unsigned kOOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void bload16(__amdgpu_buffer_rsrc_t r, __bf16* lds_wave_base, unsigned voff,
+                                        unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      r, (lds_void*)(reinterpret_cast<uintptr_t>(lds_wave_base) & 0xffffffffu), 16, voff, soff, 0, 0);
+}
+
+struct Fwd4Src {
+  __amdgpu_buffer_rsrc_t r0, r1, r2;
+  unsigned st0, st1, st2;
+  int sc0, sc1;
+};
+struct Fwd4Geo {
+  int Cin, K, H, W, KW, PH, PW, ntaps;
+  bool uniform;
+};
+
+// Issue one K step (64 columns) of A (im2col) and B (weights) into an LDS stage.
+template <int BM, int BN, int AI, int BI>
+__device__ __forceinline__ void fwd4_issue(const Fwd4Src& src, const __amdgpu_buffer_rsrc_t rw, const Fwd4Geo& g,
+                                           __bf16* sA, int wave, int k0, const int (&pix)[AI],
+                                           const int (&py)[AI], const int (&px)[AI], const int (&achunk)[AI],
+                                           const unsigned (&bvoff)[BI]) {
+  __bf16* sB = sA + BM * 64;
+  if (g.uniform) {
+    int tap = 0, c0 = k0;
+    if (g.ntaps != 1) {
+      tap = k0 / g.Cin;
+      c0 = k0 - tap * g.Cin;
+    }
+    const int ky = tap / g.KW;
+    const int dy = ky - g.PH, dx = tap - ky * g.KW - g.PW;
+    const int doff = dy * g.W + dx;
+    const bool kin = k0 < g.K;
+    if (c0 < src.sc0) {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const bool ok = kin && (unsigned)(py[i] + dy) < (unsigned)g.H && (unsigned)(px[i] + dx) < (unsigned)g.W;
+        const unsigned voff = ok ? (unsigned)(pix[i] + doff) * src.st0 + (unsigned)(achunk[i] * 16) : kOOB;
+        bload16(src.r0, sA + (wave * AI + i) * 512, voff, (unsigned)c0 * 2);
+      }
+    } else if (c0 < src.sc0 + src.sc1) {
+      const int cc = c0 - src.sc0;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const bool ok = kin && (unsigned)(py[i] + dy) < (unsigned)g.H && (unsigned)(px[i] + dx) < (unsigned)g.W;
+        const unsigned voff = ok ? (unsigned)(pix[i] + doff) * src.st1 + (unsigned)(achunk[i] * 16) : kOOB;
+        bload16(src.r1, sA + (wave * AI + i) * 512, voff, (unsigned)cc * 2);
+      }
+    } else {
+      const int cc = c0 - src.sc0 - src.sc1;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const bool ok = kin && (unsigned)(py[i] + dy) < (unsigned)g.H && (unsigned)(px[i] + dx) < (unsigned)g.W;
+        const unsigned voff = ok ? (unsigned)(pix[i] + doff) * src.st2 + (unsigned)(achunk[i] * 16) : kOOB;
+        bload16(src.r2, sA + (wave * AI + i) * 512, voff, (unsigned)cc * 2);
+      }
+    }
+  } else {
+    // non-uniform K steps: single source segment only (host check)
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int k = k0 + achunk[i] * 8;
+      unsigned voff = kOOB;
+      if (pix[i] >= 0 && k < g.K) {
+        const int tap = k / g.Cin;
+        const int c = k - tap * g.Cin;
+        const int ky = tap / g.KW;
+        const int kx = tap - ky * g.KW;
+        const int y = py[i] + ky - g.PH, x = px[i] + kx - g.PW;
+        if ((unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W)
+          voff = (unsigned)(pix[i] + (ky - g.PH) * g.W + (kx - g.PW)) * src.st0 + (unsigned)c * 2;
+      }
+      bload16(src.r0, sA + (wave * AI + i) * 512, voff, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < BI; ++i) bload16(rw, sB + (wave * BI + i) * 512, bvoff[i], (unsigned)k0 * 2);
+}
+
+template <int BM, int BN, int S>
+__global__ __launch_bounds__(256) void conv_fwd4_kernel(const ConvFwdArgs a) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int AI = BM / 32, BI = BN / 32;
+  constexpr int G = AI + BI;
+  constexpr int STAGE = (BM + BN) * 64;
+  constexpr int EPI_LD = BN + 4;  // fp32 epilogue tile row pitch
+  static_assert(S * STAGE * 2 >= BM * EPI_LD * 4, "epilogue tile must fit in the ring");
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[S * STAGE];
+
+  const int Cin = a.Cin, K = a.K, Kpad = a.Kpad, H = a.H, W = a.W, KW = a.KW, PH = a.PH, PW = a.PW;
+  const int ntaps = a.KH * a.KW;
+  const int P = (int)a.P;
+  const int Nn = a.N;
+  const int sc0 = a.src[0].C, sc1 = a.src[1].C;
+  const int nsrc = a.nsrc;
+  // one buffer resource per source segment (+ the weights)
+  const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.src[0].ptr, (unsigned)(a.P * a.src[0].stride * 2));
+  const __amdgpu_buffer_rsrc_t r1 =
+      make_rsrc(nsrc > 1 ? a.src[1].ptr : a.src[0].ptr, nsrc > 1 ? (unsigned)(a.P * a.src[1].stride * 2) : 0u);
+  const __amdgpu_buffer_rsrc_t r2 =
+      make_rsrc(nsrc > 2 ? a.src[2].ptr : a.src[0].ptr, nsrc > 2 ? (unsigned)(a.P * a.src[2].stride * 2) : 0u);
+  const unsigned st0 = (unsigned)a.src[0].stride * 2, st1 = (unsigned)a.src[1].stride * 2,
+                 st2 = (unsigned)a.src[2].stride * 2;
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.wt, (unsigned)((long)Nn * Kpad * 2));
+
+  const int tilesN = (Nn + BN - 1) / BN;
+  const int tilesM = (P + BM - 1) / BM;
+  const int wg = xcd_remap(blockIdx.x, tilesM * tilesN);
+  const int tm = wg / tilesN, tn = wg - (wg / tilesN) * tilesN;
+  const int m0 = tm * BM;
+  const int n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lrow = lane >> 3, lpc = lane & 7;
+
+  int pix[AI], py[AI], px[AI], achunk[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = (wave * AI + i) * 8 + lrow;
+    const int p = m0 + row;
+    achunk[i] = swz(row, lpc);
+    if (p < P) {
+      const int HW = H * W;
+      const int rem = p % HW;
+      pix[i] = p;
+      py[i] = rem / W;
+      px[i] = rem - py[i] * W;
+    } else {
+      pix[i] = -1;
+      py[i] = px[i] = -(1 << 20);
+    }
+  }
+  unsigned bvoff[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int row = (wave * BI + i) * 8 + lrow;
+    bvoff[i] = (n0 + row < Nn) ? (unsigned)((n0 + row) * Kpad * 2 + swz(row, lpc) * 16) : kOOB;
+  }
+  const bool uniform = (ntaps == 1) || (Cin % 64 == 0 && sc0 % 64 == 0 && sc1 % 64 == 0);
+  const int nk = Kpad / 64;
+
+  Fwd4Src src{r0, r1, r2, st0, st1, st2, sc0, sc1};
+  Fwd4Geo geo{Cin, K, H, W, KW, PH, PW, ntaps, uniform};
+#define RAFT_FWD4_ISSUE(step, stage) \
+  fwd4_issue<BM, BN, AI, BI>(src, rw, geo, smem + (stage) * STAGE, wave, (step) * 64, pix, py, px, achunk, bvoff)
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int fr = lane & 31, fh = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < nk) RAFT_FWD4_ISSUE(i, i);
+
+  for (int t = 0; t < nk; ++t) {
+    const int ahead = (nk - 1 - t) < (S - 2) ? (nk - 1 - t) : (S - 2);
+    if (ahead >= S - 2) wait_vmcnt<(S - 2) * G>();
+    else if (ahead == 2) wait_vmcnt<2 * G>();
+    else if (ahead == 1) wait_vmcnt<G>();
+    else wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + S - 1 < nk) RAFT_FWD4_ISSUE(t + S - 1, (t + S - 1) % S);
+    const __bf16* sA = smem + (t % S) * STAGE;
+    const __bf16* sB = sA + BM * 64;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c = 2 * s + fh;
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * (BM / 2) + i * 32 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(sA + row * 64 + swz(row, c) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * (BN / 2) + j * 32 + fr;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(sB + row * 64 + swz(row, c) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#undef RAFT_FWD4_ISSUE
+  wait_vmcnt<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // ------------------------------------------------------------------ epilogue via LDS
+  float* et = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = wn * (BN / 2) + j * 32 + (lane & 31);
+        et[row * EPI_LD + col] = acc[i][j][r];
+      }
+  __syncthreads();
+  constexpr int CPR = BN / 8;  // 8-channel chunks per tile row
+  for (int e = tid; e < BM * CPR; e += 256) {
+    const int row = e / CPR, ch = e - row * CPR;
+    const long p = m0 + row;
+    const int n = n0 + ch * 8;
+    if (p >= P || n >= Nn) continue;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8 + 4);
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    const int nv = Nn - n < 8 ? Nn - n : 8;  // valid channels in this chunk
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = v[q] * a.alpha + ((a.bias && q < nv) ? a.bias[n + q] : 0.f);
+    if (a.epi == 0) {
+      if (a.act == 1)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+      if (a.out_f32) {
+        float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
+        if (nv == 8 && (a.out_stride & 3) == 0) {
+          *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (q < nv) o[q] = v[q];
+        }
+      } else {
+        __bf16* o = static_cast<__bf16*>(a.out) + p * a.out_stride + n;
+        if (nv == 8) {
+          bf16x8 w;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(v[q]);
+          *reinterpret_cast<bf16x8*>(o) = w;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (q < nv) o[q] = static_cast<__bf16>(v[q]);
+        }
+      }
+    } else if (a.epi == 1) {
+      if (a.mask) {
+        const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.mask + p * a.mask_stride + n);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (!(static_cast<float>(m[q]) > 0.f)) v[q] = 0.f;
+      }
+      const bool accum = n >= a.acc_c0;  // acc_c0 is a multiple of 8
+      if (a.out_f32) {
+        float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
+        if (nv == 8) {
+          f32x4 x0 = {v[0], v[1], v[2], v[3]}, x1 = {v[4], v[5], v[6], v[7]};
+          if (accum) {
+            x0 += *reinterpret_cast<const f32x4*>(o);
+            x1 += *reinterpret_cast<const f32x4*>(o + 4);
+          }
+          *reinterpret_cast<f32x4*>(o) = x0;
+          *reinterpret_cast<f32x4*>(o + 4) = x1;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (q < nv) o[q] = accum ? o[q] + v[q] : v[q];
+        }
+      } else {
+        __bf16* o = static_cast<__bf16*>(a.out) + p * a.out_stride + n;
+        if (nv == 8) {
+          bf16x8 w;
+          const bf16x8 old = accum ? *reinterpret_cast<const bf16x8*>(o) : bf16x8{};
+#pragma unroll
+          for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(accum ? static_cast<float>(old[q]) + v[q] : v[q]);
+          *reinterpret_cast<bf16x8*>(o) = w;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (q < nv) o[q] = static_cast<__bf16>(accum ? static_cast<float>(o[q]) + v[q] : v[q]);
+        }
+      }
+    } else if (a.epi == 2) {
+      const int C = Nn >> 1;
+      bf16x8 sg;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) sg[q] = static_cast<__bf16>(sigmoidf_(v[q]));
+      *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = sg;
+      if (n >= C) {
+        const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + (n - C));
+        bf16x8 rh;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) rh[q] = static_cast<__bf16>(static_cast<float>(sg[q]) * static_cast<float>(hv[q]));
+        *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + (n - C)) = rh;
+      }
+    } else {
+      const bf16x8 zv = *reinterpret_cast<const bf16x8*>(a.z + p * a.z_stride + n);
+      const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + n);
+      bf16x8 hn, qo;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float qq = tanhf_(v[q]);
+        const float z = static_cast<float>(zv[q]);
+        hn[q] = static_cast<__bf16>((1.f - z) * static_cast<float>(hv[q]) + z * qq);
+        qo[q] = static_cast<__bf16>(qq);
+      }
+      *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = hn;
+      *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + n) = qo;
+    }
+  }
+}
+
 // ============================================================================ wgrad
 // dW tile BM (out channels) x BN (k = tap*Cin + c), reduction over 64-pixel stages.
 // Both operands are staged in their natural [pixel][column] layout with 16-byte
@@ -577,7 +909,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const ConvWgradArgs a) 
   for (int j = 0; j < 8; ++j) dbacc[j] = 0.f;
 
   u32x4 ra[ACH], rb[BCH];
-  auto load = [&](long p0) {
+  auto load = [&](long p0) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const long p = p0 + arow0 + AROWS * i;
@@ -600,7 +932,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const ConvWgradArgs a) 
       rb[i] = im2col_chunk(a.src, a.Cin, a.K, a.H, a.W, a.KW, a.PH, a.PW, pv, b, py, px, n0 + bcc * 8);
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf) __attribute__((always_inline)) {
     __bf16* sA = smem + buf * STAGE;
     __bf16* sB = sA + WBK * LDA;
 #pragma unroll
@@ -686,6 +1018,201 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const ConvWgradArgs a) 
 
 }  // namespace
 
+namespace {
+// ============================================================================ wgrad v2
+// dW[n][k] += sum_p dY[p][n] * im2col(X)[p][k], reduction over 64-pixel K steps.
+// Both operands are DMA'd by bounds-checked buffer_load ... lds into an S-stage ring
+// in their natural [pixel][column] layout and consumed with ds_read_b64_tr_b16
+// transposed reads.  The lane -> (row, 16-byte chunk) map of the DMA image fixes each
+// lane's column chunk for the whole reduction, so its k -> (tap, channel) decode is done
+// once; pixel rows advance incrementally.  Chunks are XOR-swizzled inside 64-byte groups
+// so the 4 rows one transposed read touches fall on disjoint banks.
+template <int COLS>
+__device__ __forceinline__ int wswz(int row, int chunk) {
+  return COLS == 128 ? (chunk ^ ((row & 3) << 2)) : (chunk ^ (((row >> 1) & 1) << 2));
+}
+
+template <int BM, int BN, int S>
+__global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int ACPR = BM / 8, BCPR = BN / 8;      // chunks per row
+  constexpr int ARPI = 64 / ACPR, BRPI = 64 / BCPR;  // rows per wave-instruction
+  constexpr int AI = 64 / (4 * ARPI), BI = 64 / (4 * BRPI);
+  constexpr int G = AI + BI;
+  constexpr int STAGE = 64 * (BM + BN);
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[S * STAGE];
+
+  const int tilesM = (a.N + BM - 1) / BM;
+  const int tilesN = (a.K + BN - 1) / BN;
+  const int tiles = tilesM * tilesN;
+  const int split = blockIdx.x / tiles;
+  const int t0 = blockIdx.x - split * tiles;
+  const int tm = t0 / tilesN, tn = t0 - (t0 / tilesN) * tilesN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int P = (int)a.P;
+  const int pbeg = (int)(split * a.pix_per_split);
+  const int pend = min(pbeg + (int)a.pix_per_split, P);
+  const int H = a.H, W = a.W;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // ---- A = dY rows: lane's logical chunk (fixed), byte offsets of its rows
+  const int arl = lane / ACPR;  // row within the instruction's row block
+  const int achunk = wswz<BM>(arl, lane % ACPR);
+  const bool a_ok = m0 + achunk * 8 < a.N;
+  const unsigned dyst = (unsigned)a.dy_stride * 2;
+  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(a.dy, (unsigned)(a.P * a.dy_stride * 2));
+
+  // ---- B = im2col(X) rows: lane's k chunk -> tap / channel, once
+  const int brl = lane / BCPR;
+  const int bchunk = wswz<BN>(brl, lane % BCPR);
+  const int kb = n0 + bchunk * 8;
+  const bool b_ok = kb < a.K;
+  int tap = 0, c = 0;
+  if (b_ok) {
+    tap = kb / a.Cin;
+    c = kb - tap * a.Cin;
+  }
+  const int ky = tap / a.KW;
+  const int dyy = ky - a.PH, dxx = tap - ky * a.KW - a.PW;
+  // the whole k tile lies in one source segment (host check) -> uniform resource
+  const int kt0 = n0 % a.Cin;
+  int seg = 0, cseg = c;
+  if (kt0 >= a.src[0].C) {
+    seg = 1;
+    if (kt0 >= a.src[0].C + a.src[1].C) seg = 2;
+  }
+  if (seg >= 1) cseg -= a.src[0].C;
+  if (seg == 2) cseg -= a.src[1].C;
+  const __bf16* xptr = seg == 0 ? a.src[0].ptr : (seg == 1 ? a.src[1].ptr : a.src[2].ptr);
+  const long xstride = seg == 0 ? a.src[0].stride : (seg == 1 ? a.src[1].stride : a.src[2].stride);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(xptr, (unsigned)(a.P * xstride * 2));
+  const unsigned xst = (unsigned)xstride * 2;
+  const int doff = dyy * W + dxx;
+
+  // pixel walkers for this lane's B rows
+  int bp[BI], bpy[BI], bpx[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int p = pbeg + (wave * BI + i) * BRPI + brl;
+    bp[i] = p;
+    const int rem = p % (H * W);
+    bpy[i] = rem / W;
+    bpx[i] = rem - bpy[i] * W;
+  }
+
+  const int nsteps = pend > pbeg ? (pend - pbeg + 63) / 64 : 0;
+
+#define RAFT_WG_ISSUE(step, stage)                                                                         \
+  do {                                                                                                     \
+    __bf16* sA_ = smem + (stage) * STAGE;                                                                  \
+    __bf16* sB_ = sA_ + 64 * BM;                                                                           \
+    const int p0_ = pbeg + (step) * 64;                                                                    \
+    _Pragma("unroll") for (int i = 0; i < AI; ++i) {                                                       \
+      const int p = p0_ + (wave * AI + i) * ARPI + arl;                                                    \
+      const unsigned voff = (a_ok && p < pend) ? (unsigned)p * dyst + (unsigned)(achunk * 16) : kOOB;      \
+      bload16(rdy, sA_ + (wave * AI + i) * 512, voff, (unsigned)m0 * 2);                                   \
+    }                                                                                                      \
+    _Pragma("unroll") for (int i = 0; i < BI; ++i) {                                                       \
+      const bool ok = b_ok && bp[i] < pend && (unsigned)(bpy[i] + dyy) < (unsigned)H &&                    \
+                      (unsigned)(bpx[i] + dxx) < (unsigned)W;                                              \
+      const unsigned voff = ok ? (unsigned)(bp[i] + doff) * xst + (unsigned)cseg * 2 : kOOB;              \
+      bload16(rx, sB_ + (wave * BI + i) * 512, voff, 0);                                                   \
+      bp[i] += 64;                                                                                         \
+      bpx[i] += 64;                                                                                        \
+      while (bpx[i] >= W) {                                                                                \
+        bpx[i] -= W;                                                                                       \
+        if (++bpy[i] >= H) bpy[i] = 0;                                                                     \
+      }                                                                                                    \
+    }                                                                                                      \
+  } while (0)
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // transposed-read lane geometry
+  const int hh = lane >> 5, gi = (lane >> 4) & 1, q = (lane & 15) >> 2, pq = lane & 3;
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < nsteps) RAFT_WG_ISSUE(i, i);
+
+  for (int t = 0; t < nsteps; ++t) {
+    const int ahead = (nsteps - 1 - t) < (S - 2) ? (nsteps - 1 - t) : (S - 2);
+    if (ahead >= S - 2) wait_vmcnt<(S - 2) * G>();
+    else if (ahead == 1) wait_vmcnt<G>();
+    else wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + S - 1 < nsteps) RAFT_WG_ISSUE(t + S - 1, (t + S - 1) % S);
+    const __bf16* sA = smem + (t % S) * STAGE;
+    const __bf16* sB = sA + 64 * BM;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int col = wm * (BM / 2) + i * 32 + gi * 16 + 4 * pq;  // logical column
+        const int r0 = s * 16 + hh * 8 + q, r1 = r0 + 4;
+        const s16x4 lo = tr_read(sA + r0 * BM + wswz<BM>(r0, col >> 3) * 8 + (col & 7));
+        const s16x4 hi = tr_read(sA + r1 * BM + wswz<BM>(r1, col >> 3) * 8 + (col & 7));
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * (BN / 2) + j * 32 + gi * 16 + 4 * pq;
+        const int r0 = s * 16 + hh * 8 + q, r1 = r0 + 4;
+        const s16x4 lo = tr_read(sB + r0 * BN + wswz<BN>(r0, col >> 3) * 8 + (col & 7));
+        const s16x4 hi = tr_read(sB + r1 * BN + wswz<BN>(r1, col >> 3) * 8 + (col & 7));
+        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#undef RAFT_WG_ISSUE
+  wait_vmcnt<0>();
+
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
+    if (col >= a.K) continue;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < a.N) atomicAdd(a.dw + (long)row * a.Kpad + col, acc[i][j][r]);
+      }
+  }
+}
+
+// column sums of dY accumulated into db (bias gradient): block = 64 channels x 4 pixel lanes
+__global__ __launch_bounds__(256) void colsum_kernel(const __bf16* __restrict__ dy, long stride, int N, long P,
+                                                     long ppb, float* __restrict__ db) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int pl = threadIdx.x >> 6;
+  const long p0 = (long)blockIdx.x * ppb;
+  const long p1 = p0 + ppb < P ? p0 + ppb : P;
+  float s = 0.f;
+  if (c < N)
+    for (long p = p0 + pl; p < p1; p += 4) s += static_cast<float>(dy[p * stride + c]);
+  red[pl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (pl == 0 && c < N) atomicAdd(db + c, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+}  // namespace
+
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   if (a.P == 0 || a.N == 0) return hipSuccess;
   if (a.Kpad % FBK != 0) return hipErrorInvalidValue;
@@ -693,9 +1220,26 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   // largest tile that still gives >= 2 workgroups per CU (256 CUs); small-N convs use 64-wide N
   // measured on MI355X (scripts/bench_convs.py): 64x64 tiles win for every update-block
   // shape at B=8 (occupancy beats operand reuse at these M=22.8k GEMMs)
-  int cfg = 2;  // 0: 128x128, 1: 64x128, 2: 64x64, 3: 128x64
+  // v4 kernels (scripts/bench_convs.py on MI355X): 64x128 tiles for 64 < N <= 512, 64x64 otherwise
+  int cfg = (a.N > 64 && a.N <= 512) ? 8 : 9;
+  {
+    // v4 needs either 64-aligned K steps or a single source segment, and 32-bit offsets
+    bool uniform = (a.KH * a.KW == 1) || (a.Cin % 64 == 0 && a.src[0].C % 64 == 0 && a.src[1].C % 64 == 0);
+    long maxbytes = 0;
+    for (int i = 0; i < a.nsrc; ++i) maxbytes = std::max(maxbytes, a.P * a.src[i].stride * 2);
+    if ((!uniform && a.nsrc > 1) || maxbytes >= (1L << 31) || (long)a.N * a.Kpad * 2 >= (1L << 31)) cfg = 2;
+  }
   if (const char* e = getenv("RAFT_CONV_FWD_CFG")) cfg = atoi(e);
   switch (cfg) {
+    case 8:
+      hipLaunchKernelGGL((conv_fwd4_kernel<64, 128, 3>), dim3(tiles(64, 128)), dim3(256), 0, s, a);
+      break;
+    case 9:
+      hipLaunchKernelGGL((conv_fwd4_kernel<64, 64, 4>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
+      break;
+    case 10:
+      hipLaunchKernelGGL((conv_fwd4_kernel<128, 64, 3>), dim3(tiles(128, 64)), dim3(256), 0, s, a);
+      break;
     case 4:
       hipLaunchKernelGGL((conv_fwd3_kernel<64, 64, 4>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
       break;
@@ -725,11 +1269,20 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
 
 hipError_t launch_conv_wgrad(ConvWgradArgs a, hipStream_t s) {
   if (a.P == 0 || a.N == 0) return hipSuccess;
+  bool seg_ok = a.nsrc == 1;
+  if (!seg_ok) {
+    seg_ok = a.Cin % 128 == 0;
+    for (int i = 0; i < a.nsrc; ++i) seg_ok = seg_ok && a.src[i].C % 128 == 0;
+  }
+  long maxbytes = 0;
+  for (int i = 0; i < a.nsrc; ++i) maxbytes = std::max(maxbytes, a.P * a.src[i].stride * 2);
+  const bool v2 = seg_ok && maxbytes < (1L << 31) && a.P * a.dy_stride * 2 < (1L << 31) &&
+                  getenv("RAFT_WGRAD_V1") == nullptr;
   const bool big = a.N > 64;
   const int BM = big ? 128 : 64, BN = 128;
   const long tiles = (long)((a.N + BM - 1) / BM) * ((a.K + BN - 1) / BN);
-  // split the pixel reduction so the grid covers the chip, but keep >= 1024 pixels per
-  // split: every split adds one fp32 atomic pass over the dW tile
+  // split the pixel reduction so the grid covers the chip; every split adds one fp32
+  // atomic pass over the dW tile, so keep >= 1024 pixels per split
   long splits = (768 + tiles - 1) / tiles;
   const long max_splits = (a.P + 1023) / 1024;
   if (splits > max_splits) splits = max_splits;
@@ -739,6 +1292,19 @@ hipError_t launch_conv_wgrad(ConvWgradArgs a, hipStream_t s) {
   splits = (a.P + per - 1) / per;
   a.pix_per_split = per;
   const dim3 grid((unsigned)(tiles * splits));
+  if (v2) {
+    if (big)
+      hipLaunchKernelGGL((conv_wgrad2_kernel<128, 128, 3>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_wgrad2_kernel<64, 128, 3>), grid, dim3(256), 0, s, a);
+    RAFT_HIP_CHECK(hipGetLastError());
+    if (a.db) {
+      const long ppb = 512;
+      const dim3 g2((unsigned)((a.P + ppb - 1) / ppb), (unsigned)((a.N + 63) / 64));
+      hipLaunchKernelGGL(colsum_kernel, g2, dim3(256), 0, s, a.dy, a.dy_stride, a.N, a.P, ppb, a.db);
+    }
+    return hipGetLastError();
+  }
   if (big)
     hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, s, a);
   else

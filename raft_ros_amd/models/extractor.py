@@ -16,6 +16,8 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from ..ops.norm import InstanceNorm2dNHWC
+
 
 def make_norm(kind: str, channels: int, groups: int):
     if kind == "group":
@@ -23,10 +25,18 @@ def make_norm(kind: str, channels: int, groups: int):
     if kind == "batch":
         return nn.BatchNorm2d(channels)
     if kind == "instance":
-        return nn.InstanceNorm2d(channels)
+        # parameter-free like nn.InstanceNorm2d(channels); NHWC HIP kernels with fused ReLU on GPU
+        return InstanceNorm2dNHWC(channels)
     if kind == "none":
         return nn.Sequential()
     raise ValueError(f"unknown norm_fn {kind!r}")
+
+
+def norm_relu(norm: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """relu(norm(x)), fusing the ReLU into the NHWC instance-norm kernel when possible."""
+    if isinstance(norm, InstanceNorm2dNHWC):
+        return norm(x, relu=True)
+    return torch.relu(norm(x))
 
 
 class ResidualBlock(nn.Module):
@@ -45,8 +55,8 @@ class ResidualBlock(nn.Module):
             self.downsample = None
 
     def forward(self, x):
-        y = self.relu(self.norm1(self.conv1(x)))
-        y = self.relu(self.norm2(self.conv2(y)))
+        y = norm_relu(self.norm1, self.conv1(x))
+        y = norm_relu(self.norm2, self.conv2(y))
         if self.downsample is not None:
             x = self.downsample(x)
         return self.relu(x + y)
@@ -71,9 +81,9 @@ class BottleneckBlock(nn.Module):
             self.downsample = None
 
     def forward(self, x):
-        y = self.relu(self.norm1(self.conv1(x)))
-        y = self.relu(self.norm2(self.conv2(y)))
-        y = self.relu(self.norm3(self.conv3(y)))
+        y = norm_relu(self.norm1, self.conv1(x))
+        y = norm_relu(self.norm2, self.conv2(y))
+        y = norm_relu(self.norm3, self.conv3(y))
         if self.downsample is not None:
             x = self.downsample(x)
         return self.relu(x + y)
@@ -102,7 +112,7 @@ class _Encoder(nn.Module):
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
-            elif isinstance(m, (nn.BatchNorm2d, nn.InstanceNorm2d, nn.GroupNorm)):
+            elif isinstance(m, (nn.BatchNorm2d, nn.GroupNorm)):
                 if m.weight is not None:
                     nn.init.constant_(m.weight, 1)
                 if m.bias is not None:
@@ -119,7 +129,7 @@ class _Encoder(nn.Module):
         if paired:
             n = x[0].shape[0]
             x = torch.cat(x, dim=0)
-        x = self.relu1(self.norm1(self.conv1(x)))
+        x = norm_relu(self.norm1, self.conv1(x))
         x = self.layer3(self.layer2(self.layer1(x)))
         x = self.conv2(x)
         if self.training and self.dropout is not None:

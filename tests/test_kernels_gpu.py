@@ -172,3 +172,23 @@ def test_local_corr_fwd_bwd(cuda, dtype):
     r1, r2 = torch.autograd.grad(want, (f1r, f2r), g)
     torch.testing.assert_close(d1.float(), r1.permute(0, 2, 3, 1), **tol)
     torch.testing.assert_close(d2.float(), r2.permute(0, 2, 3, 1), **tol)
+
+
+@pytest.mark.parametrize("C,relu,dtype", [(64, True, torch.bfloat16), (96, False, torch.float32), (128, True, torch.float32)])
+def test_instance_norm_nhwc(cuda, C, relu, dtype):
+    torch.manual_seed(6)
+    from raft_ros_amd.ops.norm import InstanceNorm2dNHWC
+
+    x = (torch.randn(3, C, 37, 29, device=cuda) * 2 + 0.5).to(dtype).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = InstanceNorm2dNHWC(C)(x, relu=relu)
+    xr = x.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.instance_norm(xr)
+    if relu:
+        yr = torch.relu(yr)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    g = torch.randn_like(yr)
+    (dx,) = torch.autograd.grad(y, x, g.to(dtype))
+    (dxr,) = torch.autograd.grad(yr, xr, g)
+    torch.testing.assert_close(dx.float(), dxr, **tol)

@@ -52,6 +52,9 @@ def test_fused_update_matches_torch_path(cuda, shape):
         scale = max(torch.stack([gr[n].float().norm() for n in names]).max().item(), 1e-12)
         for n in names:
             err = (gf[n].float() - gr[n].float()).norm().item()
-            if err > 0.1 * max(gr[n].float().norm().item(), 1e-2 * scale):
+            # encoder grads pass through the bf16 corr GEMM backward and 10+ bf16 layers in both
+            # paths; the update block itself is held to 10 %
+            tol = 0.1 if grp == "update_block" else 0.25
+            if err > tol * max(gr[n].float().norm().item(), 1e-2 * scale):
                 bad[n] = (err, gr[n].float().norm().item())
     assert not bad, bad
