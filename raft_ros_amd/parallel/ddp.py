@@ -1,0 +1,110 @@
+"""Multi-GPU data parallelism: one process per GPU, DDP over RCCL (xGMI).
+
+Replaces the reference's single-process ``nn.DataParallel`` (train.py:138), which
+broadcasts all 5.26 M parameters to every replica, scatters inputs and gathers
+all 12 full-resolution flow predictions to GPU 0 *every step* (SURVEY.md 2.5).
+Here each rank keeps its own replica; the only per-step collective is the
+bucketed fp32 gradient all-reduce (~21 MB for RAFT-base), overlapped with the
+backward pass by DistributedDataParallel.  On ROCm the ``"nccl"`` backend is
+RCCL.  CPU runs (tests) use ``gloo``.
+
+Rendezvous always uses 127.0.0.1 unless MASTER_ADDR says otherwise.
+"""
+from __future__ import annotations
+
+import os
+import socket
+from dataclasses import dataclass
+from typing import Dict
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def init_distributed(backend: str | None = None, device_type: str | None = None) -> DistInfo:
+    """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = (device_type or ("cuda" if torch.cuda.is_available() else "cpu")) == "cuda"
+    device = torch.device("cuda", local) if use_cuda else torch.device("cpu")
+    if use_cuda:
+        torch.cuda.set_device(local)
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = backend or ("nccl" if use_cuda else "gloo")
+        kw = {"device_id": device} if use_cuda else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    return DistInfo(rank, world, local, device)
+
+
+def wrap_model(model: torch.nn.Module, info: DistInfo, bucket_cap_mb: float = 32.0, static_graph: bool = True):
+    """DDP wrapper sized for xGMI: the whole RAFT-base gradient (21 MB fp32) fits in one
+    32 MB bucket, i.e. one ring all-reduce per step, launched as soon as backward has
+    produced it (earlier buckets overlap with the rest of backward)."""
+    if not info.distributed:
+        return model
+    kw = dict(bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True, static_graph=static_graph)
+    if info.device.type == "cuda":
+        kw["device_ids"] = [info.device.index]
+    return torch.nn.parallel.DistributedDataParallel(model, **kw)
+
+
+def all_reduce_mean(values: Dict[str, float], info: DistInfo) -> Dict[str, float]:
+    if not info.distributed or not values:
+        return values
+    keys = sorted(values)
+    t = torch.tensor([float(values[k]) for k in keys], dtype=torch.float64, device=info.device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    t /= info.world_size
+    return dict(zip(keys, t.tolist()))
+
+
+def barrier(info: DistInfo) -> None:
+    if info.distributed:
+        if info.device.type == "cuda":
+            dist.barrier(device_ids=[info.device.index])
+        else:
+            dist.barrier()
+
+
+def cleanup() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def _spawn_entry(rank, fn, nprocs, port, args):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(nprocs),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    fn(rank, *args)
+
+
+def spawn(fn, nprocs: int, *args) -> None:
+    """Run ``fn(rank, *args)`` in ``nprocs`` processes with torchrun-style env vars set
+    (used when train.py is started without torchrun but with several --gpus).
+    ``fn`` must be a module-level (picklable) function."""
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_spawn_entry, args=(fn, nprocs, free_port(), args), nprocs=nprocs, start_method="spawn")

@@ -1,0 +1,151 @@
+"""RAFT training loop (reference train.py:136-214), MI355X / multi-GPU edition.
+
+Same schedule semantics as the reference: AdamW + OneCycle (``fetch_optimizer``),
+sequence loss with ``args.gamma``, optional Gaussian input noise
+(``--add_noise``, sigma ~ U(0, 5)), gradient clipping to ``args.clip``, BatchNorm
+frozen for every stage except chairs (re-applied after validation), a weights
+checkpoint every ``VAL_FREQ`` steps followed by validation, and a final
+``checkpoints/<name>.pth`` -- in the reference's ``module.``-prefixed format.
+
+MI355X-specific:
+
+* one process per GPU with DDP over RCCL (torchrun, or ``--gpus 0 1 ...``
+  which spawns the ranks itself); ``--batch_size`` stays the GLOBAL batch;
+* bf16 autocast by default for ``--mixed_precision`` (``--amp_dtype fp16``
+  restores the reference's fp16 + GradScaler);
+* channels-last model, fused AdamW, loss metrics kept on the device;
+* non-finite-loss guard (the step is skipped and counted) and an exact-resume
+  sidecar ``<name>.state.pt`` next to every checkpoint.
+"""
+from __future__ import annotations
+
+import os
+import time
+from argparse import Namespace
+
+import numpy as np
+import torch
+
+from ..data.datasets import fetch_dataloader
+from ..eval.validate import run_validation
+from ..models import RAFT
+from ..parallel import ddp
+from ..utils import checkpoint
+from .logger import Logger
+from .loss import sequence_loss
+from .optim import count_parameters, fetch_optimizer
+
+VAL_FREQ = 5000
+
+
+def _infinite(loader, sampler_epoch=None):
+    epoch = 0
+    while True:
+        if sampler_epoch is not None:
+            sampler_epoch(epoch)
+        for batch in loader:
+            yield batch
+        epoch += 1
+
+
+def train(args: Namespace) -> str:
+    info = ddp.init_distributed()
+    args.rank, args.world_size = info.rank, info.world_size
+    dev = info.device
+    if args.batch_size % info.world_size != 0 and info.is_main:
+        print(f"warning: global batch {args.batch_size} not divisible by {info.world_size} ranks; "
+              f"using {args.batch_size // info.world_size} per rank")
+
+    model = RAFT(args)
+    if info.is_main:
+        print("Parameter Count: %d" % count_parameters(model))
+    if args.restore_ckpt is not None:
+        checkpoint.load_weights(model, args.restore_ckpt, strict=False)
+    model = model.to(dev)
+    if dev.type == "cuda" and getattr(args, "channels_last", True):
+        model = model.to(memory_format=torch.channels_last)
+    model.train()
+    if args.stage != "chairs":
+        model.freeze_bn()
+    net = ddp.wrap_model(model, info, bucket_cap_mb=getattr(args, "bucket_mb", 32.0))
+
+    train_loader = fetch_dataloader(args)
+    optimizer, scheduler = fetch_optimizer(args, model)
+    use_scaler = bool(args.mixed_precision) and getattr(args, "amp_dtype", "bf16") == "fp16" and dev.type == "cuda"
+    scaler = torch.amp.GradScaler("cuda", enabled=use_scaler)
+    per_rank = max(1, args.batch_size // info.world_size)
+    logger = Logger(model, scheduler, log_dir=os.path.join(args.log_dir, args.name), enabled=info.is_main,
+                    pairs_per_step=per_rank * info.world_size)
+
+    total_steps = 0
+    if getattr(args, "resume", False) and args.restore_ckpt is not None:
+        st = checkpoint.load_state(checkpoint.state_path(args.restore_ckpt), optimizer, scheduler, scaler)
+        if st is not None:
+            total_steps = st
+            logger.total_steps = st
+            if info.is_main:
+                print(f"resumed at step {st}")
+
+    sampler = getattr(train_loader, "sampler", None)
+    set_epoch = sampler.set_epoch if hasattr(sampler, "set_epoch") else None
+    skipped = torch.zeros((), device=dev)
+    fused_opt = bool(optimizer.defaults.get("fused"))
+    t0 = time.perf_counter()
+    for data_blob in _infinite(train_loader, set_epoch):
+        optimizer.zero_grad(set_to_none=True)
+        image1, image2, flow, valid = [x.to(dev, non_blocking=True) for x in data_blob]
+        if args.add_noise:
+            stdv = np.random.uniform(0.0, 5.0)
+            image1 = (image1 + stdv * torch.randn_like(image1)).clamp(0.0, 255.0)
+            image2 = (image2 + stdv * torch.randn_like(image2)).clamp(0.0, 255.0)
+
+        flow_predictions = net(image1, image2, iters=args.iters)
+        loss, metrics = sequence_loss(flow_predictions, flow, valid, args.gamma)
+        scaler.scale(loss).backward()
+        scaler.unscale_(optimizer)
+        gnorm = torch.nn.utils.clip_grad_norm_(model.parameters(), args.clip)
+        if use_scaler:
+            scaler.step(optimizer)  # GradScaler already skips non-finite steps
+            scaler.update()
+        else:
+            # failure guard without a host sync: a non-finite gradient norm (identical on all
+            # ranks after the all-reduce) turns the fused AdamW update into a no-op on device
+            bad = (~torch.isfinite(gnorm)).float()
+            skipped += bad
+            if fused_opt:
+                optimizer.found_inf = bad
+                optimizer.step()
+                optimizer.found_inf = None
+            elif not bool(bad):
+                optimizer.step()
+        scheduler.step()
+        logger.push(metrics)
+
+        if total_steps % VAL_FREQ == VAL_FREQ - 1:
+            path = os.path.join(args.ckpt_dir, "%d_%s.pth" % (total_steps + 1, args.name))
+            if info.is_main:
+                checkpoint.save_weights(model, path)
+                checkpoint.save_state(checkpoint.state_path(path), optimizer, scheduler, scaler, total_steps + 1)
+            results = run_validation(model, args.validation, rank=info.rank, world=info.world_size)
+            logger.write_dict(results)
+            model.train()
+            if args.stage != "chairs":
+                model.freeze_bn()
+            ddp.barrier(info)
+
+        total_steps += 1
+        if total_steps > args.num_steps:
+            break
+
+    if info.is_main:
+        dt = time.perf_counter() - t0
+        print(f"trained {total_steps} steps in {dt:.1f}s ({per_rank * info.world_size * total_steps / dt:.2f} "
+              f"pairs/s, {int(skipped.item())} non-finite steps skipped)")
+    logger.close()
+    path = os.path.join(args.ckpt_dir, "%s.pth" % args.name)
+    if info.is_main:
+        checkpoint.save_weights(model, path)
+        checkpoint.save_state(checkpoint.state_path(path), optimizer, scheduler, scaler, total_steps)
+    ddp.barrier(info)
+    ddp.cleanup()
+    return path

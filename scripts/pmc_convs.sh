@@ -5,7 +5,8 @@ export TMPDIR=/tmp
 OUT=gpurun_out/pmc
 mkdir -p $OUT
 timeout -k 10 120 rocprofv3 --list-avail > $OUT/avail.txt 2>&1 || true
-for spec in "zr fwd 2" "zr fwd 6" "zr wgrad" "heads fwd 6"; do
+IFS=, read -ra SPEC_LIST <<< "${SPECS:-zr fwd 8,zr wgrad,mask2 wgrad}"
+for spec in "${SPEC_LIST[@]}"; do
   tag=$(echo $spec | tr ' ' '_')
   for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS" "SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE"; do
     g=$(echo $grp | cut -d' ' -f1)

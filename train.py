@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Train RAFT -- same command line as the reference train.py (train.py:217-247).
+
+Single GPU:        python train.py --stage chairs --gpus 0 --batch_size 8 --mixed_precision ...
+Multi-GPU (DDP):   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 train.py --stage chairs ...
+                   or  python train.py --gpus 0 1 ...   (spawns one process per listed GPU)
+``--batch_size`` is the global batch, split evenly over the GPUs like the
+reference's DataParallel.  Extra flags (all optional) are listed under
+"MI355X options".
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser()
+    p.add_argument("--name", default="raft", help="name your experiment")
+    p.add_argument("--stage", help="determines which dataset to use for training")
+    p.add_argument("--restore_ckpt", help="restore checkpoint")
+    p.add_argument("--small", action="store_true", help="use small model")
+    p.add_argument("--validation", type=str, nargs="+")
+    p.add_argument("--lr", type=float, default=0.00002)
+    p.add_argument("--num_steps", type=int, default=100000)
+    p.add_argument("--batch_size", type=int, default=6)
+    p.add_argument("--image_size", type=int, nargs="+", default=[384, 512])
+    p.add_argument("--gpus", type=int, nargs="+", default=[0, 1])
+    p.add_argument("--mixed_precision", action="store_true", help="use mixed precision")
+    p.add_argument("--iters", type=int, default=12)
+    p.add_argument("--wdecay", type=float, default=0.00005)
+    p.add_argument("--epsilon", type=float, default=1e-8)
+    p.add_argument("--clip", type=float, default=1.0)
+    p.add_argument("--dropout", type=float, default=0.0)
+    p.add_argument("--gamma", type=float, default=0.8, help="exponential weighting")
+    p.add_argument("--add_noise", action="store_true")
+    g = p.add_argument_group("MI355X options")
+    g.add_argument("--amp_dtype", default="bf16", choices=["bf16", "fp16"], help="autocast dtype for --mixed_precision")
+    g.add_argument("--alternate_corr", action="store_true", help="memory-efficient local correlation (trainable)")
+    g.add_argument("--no_channels_last", dest="channels_last", action="store_false")
+    g.add_argument("--no_fused_update", dest="fused_update", action="store_false",
+                   help="run the update block on PyTorch convs instead of the fused HIP kernels")
+    g.add_argument("--resume", action="store_true", help="also restore optimizer/scheduler/step from <ckpt>.state.pt")
+    g.add_argument("--num_workers", type=int, default=4)
+    g.add_argument("--ckpt_dir", default="checkpoints")
+    g.add_argument("--log_dir", default="runs")
+    g.add_argument("--dataset_root", default=None, help="directory holding Sintel/, KITTI/, ... (default ./datasets)")
+    g.add_argument("--bucket_mb", type=float, default=32.0, help="DDP gradient bucket size")
+    g.add_argument("--seed", type=int, default=1234)
+    return p
+
+
+def _main(args) -> str:
+    from raft_ros_amd.train.trainer import train
+
+    rank = int(os.environ.get("RANK", "0"))
+    torch.manual_seed(args.seed + rank)
+    np.random.seed(args.seed + rank)
+    os.makedirs(args.ckpt_dir, exist_ok=True)
+    return train(args)
+
+
+def _spawned(rank: int, args) -> None:
+    os.environ["LOCAL_RANK"] = str(args.gpus[rank])
+    _main(args)
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    if args.dataset_root:
+        os.environ["RAFT_DATASET_ROOT"] = args.dataset_root
+    if "WORLD_SIZE" not in os.environ and len(args.gpus) > 1 and torch.cuda.is_available():
+        from raft_ros_amd.parallel.ddp import spawn
+
+        spawn(_spawned, len(args.gpus), args)
+        return None
+    if "LOCAL_RANK" not in os.environ and torch.cuda.is_available():
+        os.environ["LOCAL_RANK"] = str(args.gpus[0])
+    return _main(args)
+
+
+if __name__ == "__main__":
+    main()
