@@ -1281,10 +1281,13 @@ hipError_t launch_conv_wgrad(ConvWgradArgs a, hipStream_t s) {
   const bool big = a.N > 64;
   const int BM = big ? 128 : 64, BN = 128;
   const long tiles = (long)((a.N + BM - 1) / BM) * ((a.K + BN - 1) / BN);
-  // split the pixel reduction so the grid covers the chip; every split adds one fp32
-  // atomic pass over the dW tile, so keep >= 1024 pixels per split
-  long splits = (768 + tiles - 1) / tiles;
-  const long max_splits = (a.P + 1023) / 1024;
+  // split the pixel reduction so ~one round of workgroups covers the 256 CUs.  Every split
+  // adds one fp32-atomic pass over its dW tile (64 KB per 128x128 tile at ~1.3 TB/s
+  // chip-wide, i.e. ~12 us of atomics per wave of 256 workgroups), so more splits than
+  // CUs cost more in atomics than they win in parallelism.
+  long splits = std::max(1L, (256 + tiles / 2) / tiles);
+  if (const char* e = getenv("RAFT_WGRAD_SPLITS")) splits = atol(e);
+  const long max_splits = (a.P + 255) / 256;
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   long per = (a.P + splits - 1) / splits;

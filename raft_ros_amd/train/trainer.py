@@ -31,6 +31,7 @@ from ..eval.validate import run_validation
 from ..models import RAFT
 from ..parallel import ddp
 from ..utils import checkpoint
+from ..utils.profiling import maybe_profiler, trace_range
 from .logger import Logger
 from .loss import sequence_loss
 from .optim import count_parameters, fetch_optimizer
@@ -91,6 +92,8 @@ def train(args: Namespace) -> str:
     skipped = torch.zeros((), device=dev)
     fused_opt = bool(optimizer.defaults.get("fused"))
     t0 = time.perf_counter()
+    prof = maybe_profiler(getattr(args, "profile_dir", None))
+    profiler = prof.__enter__()
     for data_blob in _infinite(train_loader, set_epoch):
         optimizer.zero_grad(set_to_none=True)
         image1, image2, flow, valid = [x.to(dev, non_blocking=True) for x in data_blob]
@@ -99,9 +102,11 @@ def train(args: Namespace) -> str:
             image1 = (image1 + stdv * torch.randn_like(image1)).clamp(0.0, 255.0)
             image2 = (image2 + stdv * torch.randn_like(image2)).clamp(0.0, 255.0)
 
-        flow_predictions = net(image1, image2, iters=args.iters)
-        loss, metrics = sequence_loss(flow_predictions, flow, valid, args.gamma)
-        scaler.scale(loss).backward()
+        with trace_range("forward"):
+            flow_predictions = net(image1, image2, iters=args.iters)
+            loss, metrics = sequence_loss(flow_predictions, flow, valid, args.gamma)
+        with trace_range("backward"):
+            scaler.scale(loss).backward()
         scaler.unscale_(optimizer)
         gnorm = torch.nn.utils.clip_grad_norm_(model.parameters(), args.clip)
         if use_scaler:
@@ -120,6 +125,8 @@ def train(args: Namespace) -> str:
                 optimizer.step()
         scheduler.step()
         logger.push(metrics)
+        if profiler is not None:
+            profiler.step()
 
         if total_steps % VAL_FREQ == VAL_FREQ - 1:
             path = os.path.join(args.ckpt_dir, "%d_%s.pth" % (total_steps + 1, args.name))
@@ -137,6 +144,7 @@ def train(args: Namespace) -> str:
         if total_steps > args.num_steps:
             break
 
+    prof.__exit__(None, None, None)
     if info.is_main:
         dt = time.perf_counter() - t0
         print(f"trained {total_steps} steps in {dt:.1f}s ({per_rank * info.world_size * total_steps / dt:.2f} "

@@ -53,6 +53,7 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--dataset_root", default=None, help="directory holding Sintel/, KITTI/, ... (default ./datasets)")
     g.add_argument("--bucket_mb", type=float, default=32.0, help="DDP gradient bucket size")
     g.add_argument("--seed", type=int, default=1234)
+    g.add_argument("--profile_dir", default=None, help="capture a torch.profiler trace of steps 5-7 here")
     return p
 
 
