@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--mode", choices=["train", "infer"], default="train",
                     help="infer: forward-only test_mode passes (BASELINE config #5: --image_size 1080 1920 --iters 32)")
     ap.add_argument("--alternate_corr", action="store_true", help="memory-efficient local correlation (config #4)")
+    ap.add_argument("--graph", action="store_true", help="infer mode: replay the forward as a captured HIP graph")
     return ap.parse_args()
 
 
@@ -95,12 +96,15 @@ def main():
     pool = [synthetic_batch(args.batch, H, W, seed=rank * 97 + i, device=device) for i in range(2 if H * W > 1e6 else 4)]
 
     if args.mode == "infer":
+        from raft_ros_amd.runtime import GraphedRAFT
+
         model.eval()
+        runner = GraphedRAFT(model, iters=args.iters, enabled=args.graph)
 
         @torch.inference_mode()
         def step(i):
             i1, i2, flow, valid = pool[i % len(pool)]
-            _, flow_up = model(i1, i2, iters=args.iters, test_mode=True)
+            _, flow_up = runner(i1, i2)
             return flow_up.new_zeros(()), {"epe": (flow_up - flow).norm(dim=1).mean()}
     else:
         step = None
@@ -167,6 +171,7 @@ def main():
                 "fused_update": (args.impl == "native" and not args.no_fused),
                 "mode": args.mode,
                 "alternate_corr": args.alternate_corr,
+                "hip_graph": bool(args.graph and args.mode == "infer"),
             },
             "final_loss": round(float(loss.item()), 4),
             "epe_synthetic": round(float(metrics["epe"].item()), 4),

@@ -107,6 +107,7 @@ struct ConvWgradArgs {
   long pix_per_split;
   float* dw;
   float* db;
+  int xcd_g;  // layout must match conv_igemm.hip
 };
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s);
 hipError_t launch_conv_wgrad(ConvWgradArgs a, hipStream_t s);

@@ -77,6 +77,7 @@ struct ConvWgradArgs {
   long pix_per_split;
   float* dw;  // [N][Kpad] fp32, accumulated
   float* db;  // [N] fp32, accumulated (may be null)
+  int xcd_g;  // >0: XCD-grouped split mapping with xcd_g splits per XCD (set by the launcher)
 };
 
 namespace {
@@ -889,8 +890,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const ConvWgradArgs a) 
   const int tilesM = (a.N + BM - 1) / BM;
   const int tilesN = (a.K + BN - 1) / BN;
   const int tiles = tilesM * tilesN;
-  const int split = blockIdx.x / tiles;
-  const int t0 = blockIdx.x - split * tiles;
+  int split, t0;
+  if (a.xcd_g > 0) {
+    // workgroups are dealt round-robin to the 8 XCDs: keep every tile of a pixel split on
+    // one XCD so the split's dY / X rows are fetched into that XCD's L2 once
+    const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
+    const int si = local / tiles;
+    t0 = local - si * tiles;
+    split = xcd * a.xcd_g + si;
+  } else {
+    split = blockIdx.x / tiles;
+    t0 = blockIdx.x - split * tiles;
+  }
   const int tm = t0 / tilesN, tn = t0 - (t0 / tilesN) * tilesN;
   const int m0 = tm * BM, n0 = tn * BN;
   const long pbeg = (long)split * a.pix_per_split;
@@ -1045,8 +1056,18 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
   const int tilesM = (a.N + BM - 1) / BM;
   const int tilesN = (a.K + BN - 1) / BN;
   const int tiles = tilesM * tilesN;
-  const int split = blockIdx.x / tiles;
-  const int t0 = blockIdx.x - split * tiles;
+  int split, t0;
+  if (a.xcd_g > 0) {
+    // workgroups are dealt round-robin to the 8 XCDs: keep every tile of a pixel split on
+    // one XCD so the split's dY / X rows are fetched into that XCD's L2 once
+    const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
+    const int si = local / tiles;
+    t0 = local - si * tiles;
+    split = xcd * a.xcd_g + si;
+  } else {
+    split = blockIdx.x / tiles;
+    t0 = blockIdx.x - split * tiles;
+  }
   const int tm = t0 / tilesN, tn = t0 - (t0 / tilesN) * tilesN;
   const int m0 = tm * BM, n0 = tn * BN;
   const int P = (int)a.P;
@@ -1135,6 +1156,19 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // bias gradient: dY fragments are also multiplied by a ones B-operand, so every output
+  // column of accb holds the pixel sum of dY rows.  The 64-pixel steps are dealt to the
+  // (column tile, wave column) pairs round-robin -- step t goes to tn == t % tilesN,
+  // wn == (t / tilesN) & 1 -- so the extra MFMAs are spread over the whole grid.
+  const bool do_db = a.db != nullptr;
+  f32x16 accb[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accb[i][r] = 0.f;
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = static_cast<__bf16>(1.0f);
 
   // transposed-read lane geometry
   const int hh = lane >> 5, gi = (lane >> 4) & 1, q = (lane & 15) >> 2, pq = lane & 3;
@@ -1153,6 +1187,8 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
     if (t + S - 1 < nsteps) RAFT_WG_ISSUE(t + S - 1, (t + S - 1) % S);
     const __bf16* sA = smem + (t % S) * STAGE;
     const __bf16* sB = sA + 64 * BM;
+    const int tq = t / tilesN;
+    const bool db_step = do_db && (t - tq * tilesN) == tn && (tq & 1) == wn;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       bf16x8 af[TM], bfr[TN];
@@ -1177,10 +1213,30 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if (db_step) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) accb[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], ones, accb[i], 0, 0, 0);
+      }
     }
   }
 #undef RAFT_WG_ISSUE
   wait_vmcnt<0>();
+  if (do_db && nsteps > tn) {
+    // every column of accb holds the row sums: stage column 0 of both wave columns in LDS
+    // (the ring is free now), then add BM contiguous floats per workgroup -- 256-byte
+    // atomic wave-instructions instead of one scattered dword per lane
+    float* sdb = reinterpret_cast<float*>(smem);
+    __syncthreads();
+    if ((lane & 31) == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          sdb[wn * BM + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)] = accb[i][r];
+    }
+    __syncthreads();
+    if (tid < BM && m0 + tid < a.N) atomicAdd(a.db + m0 + tid, sdb[tid] + sdb[BM + tid]);
+  }
 
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -1196,21 +1252,6 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
   }
 }
 
-// column sums of dY accumulated into db (bias gradient): block = 64 channels x 4 pixel lanes
-__global__ __launch_bounds__(256) void colsum_kernel(const __bf16* __restrict__ dy, long stride, int N, long P,
-                                                     long ppb, float* __restrict__ db) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
-  const int pl = threadIdx.x >> 6;
-  const long p0 = (long)blockIdx.x * ppb;
-  const long p1 = p0 + ppb < P ? p0 + ppb : P;
-  float s = 0.f;
-  if (c < N)
-    for (long p = p0 + pl; p < p1; p += 4) s += static_cast<float>(dy[p * stride + c]);
-  red[pl][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (pl == 0 && c < N) atomicAdd(db + c, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
-}
 }  // namespace
 
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
@@ -1285,27 +1326,33 @@ hipError_t launch_conv_wgrad(ConvWgradArgs a, hipStream_t s) {
   // adds one fp32-atomic pass over its dW tile (64 KB per 128x128 tile at ~1.3 TB/s
   // chip-wide, i.e. ~12 us of atomics per wave of 256 workgroups), so more splits than
   // CUs cost more in atomics than they win in parallelism.
-  long splits = std::max(1L, (256 + tiles / 2) / tiles);
-  if (const char* e = getenv("RAFT_WGRAD_SPLITS")) splits = atol(e);
+  // One workgroup per CU (the 3-stage ring uses 96 KB of LDS).  The pixel reduction is
+  // split 8*g ways, g splits per XCD, each XCD running all tiles of its splits (<= 32 CUs),
+  // so the split's rows stay in that XCD's L2 and the grid is one round of workgroups.
+  // Measured on MI355X: a 270-workgroup grid (two rounds) with splits interleaved over the
+  // XCDs ran at ~1.8 us per 64-pixel step with 70% L2 misses.
+  // When the tiles fill less than 3/4 of an XCD that way (or exceed it), interleaved
+  // splits sized to ~one round over the chip win instead.
+  long g = 32 / tiles;
+  if (4 * g * tiles < 3 * 32) g = 0;
+  if (const char* e = getenv("RAFT_WGRAD_XCDG")) g = atol(e);
+  long splits = g > 0 ? 8 * g : std::max(1L, (256 + tiles / 2) / tiles);
+  if (const char* e = getenv("RAFT_WGRAD_SPLITS")) splits = atol(e), g = 0;
   const long max_splits = (a.P + 255) / 256;
-  if (splits > max_splits) splits = max_splits;
+  if (splits > max_splits) splits = max_splits, g = 0;
   if (splits < 1) splits = 1;
   long per = (a.P + splits - 1) / splits;
   per = (per + WBK - 1) / WBK * WBK;
+  if ((a.P + per - 1) / per != splits) g = 0;  // rounding dropped a split: plain mapping
   splits = (a.P + per - 1) / per;
   a.pix_per_split = per;
+  a.xcd_g = (int)g;
   const dim3 grid((unsigned)(tiles * splits));
   if (v2) {
     if (big)
       hipLaunchKernelGGL((conv_wgrad2_kernel<128, 128, 3>), grid, dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL((conv_wgrad2_kernel<64, 128, 3>), grid, dim3(256), 0, s, a);
-    RAFT_HIP_CHECK(hipGetLastError());
-    if (a.db) {
-      const long ppb = 512;
-      const dim3 g2((unsigned)((a.P + ppb - 1) / ppb), (unsigned)((a.N + 63) / 64));
-      hipLaunchKernelGGL(colsum_kernel, g2, dim3(256), 0, s, a.dy, a.dy_stride, a.N, a.P, ppb, a.db);
-    }
     return hipGetLastError();
   }
   if (big)

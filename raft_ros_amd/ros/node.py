@@ -32,6 +32,7 @@ import numpy as np
 import torch
 
 from ..models import RAFT
+from ..runtime import GraphedRAFT
 from ..utils import checkpoint, flow_viz
 from ..utils.utils import InputPadder
 
@@ -95,7 +96,7 @@ class FlowInference:
     """RAFT inference on numpy HxWx3 uint8 frames -> BGR uint8 flow visualisation."""
 
     def __init__(self, weight_path: Optional[str], small: bool = False, device: str = "cuda", iters: int = 20,
-                 mixed_precision: bool = False):
+                 mixed_precision: bool = False, hip_graph: bool = True):
         if device.startswith("cuda") and not torch.cuda.is_available():
             device = "cpu"
         self.device = torch.device(device)
@@ -105,6 +106,8 @@ class FlowInference:
         if weight_path:
             checkpoint.load_weights(self.model, weight_path, map_location="cpu")
         self.model.to(self.device).eval()
+        # camera streams have a fixed frame size: capture the forward once, replay per pair
+        self.runner = GraphedRAFT(self.model, iters=iters, enabled=hip_graph)
 
     @torch.inference_mode()
     def flow(self, prev: np.ndarray, curr: np.ndarray) -> torch.Tensor:
@@ -113,7 +116,7 @@ class FlowInference:
         image1, image2 = image1.to(self.device), image2.to(self.device)
         padder = InputPadder(image1.shape)
         image1, image2 = padder.pad(image1, image2)
-        _, flow_up = self.model(image1, image2, iters=self.iters, test_mode=True)
+        _, flow_up = self.runner(image1, image2)
         return flow_up
 
     def visualize(self, prev: np.ndarray, curr: np.ndarray) -> np.ndarray:
@@ -145,7 +148,8 @@ class RaftRosNode:
             print("Initialize RAFT...")
             inference = FlowInference(rospy.get_param("/RAFT/weight_path"), bool(rospy.get_param("/RAFT/is_small")),
                                       str(rospy.get_param("/RAFT/device")),
-                                      mixed_precision=bool(_get_param(rospy, "/RAFT/mixed_precision", False)))
+                                      mixed_precision=bool(_get_param(rospy, "/RAFT/mixed_precision", False)),
+                                      hip_graph=bool(_get_param(rospy, "/RAFT/hip_graph", True)))
             print("Initialize RAFT finish!")
         self.inference = inference
         self._thread: Optional[threading.Thread] = None

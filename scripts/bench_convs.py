@@ -85,7 +85,8 @@ def main():
                         f"({2 * macs / td / 1e6:5.0f}TF)")
         os.environ.pop("RAFT_CONV_FWD_CFG", None)
         tw = timeit(lambda: C.conv_wgrad([x], dy, g, cout, dw, db))
-        line.append(f"wgrad {tw:7.1f}us ({2 * macs / tw / 1e6:5.0f}TF)")
+        tw0 = timeit(lambda: C.conv_wgrad([x], dy, g, cout, dw, None))
+        line.append(f"wgrad {tw:7.1f}us (no db {tw0:6.1f}us {2 * macs / tw0 / 1e6:5.0f}TF)")
         # MIOpen reference
         xt = x[:, :cin].float().reshape(B, H, W, cin).permute(0, 3, 1, 2).bfloat16().contiguous(
             memory_format=torch.channels_last).requires_grad_(True)

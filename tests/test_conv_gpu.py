@@ -92,6 +92,31 @@ def test_conv_fwd_dgrad_wgrad(cuda, segs, cout, kh, kw, act):
     assert _rel(db, 2 * dy.float().sum(0)[:cout]) < 1e-4
 
 
+@pytest.mark.parametrize("segs,cout,kh,kw", [([(128, 128), (128, 128), (128, 128)], 256, 1, 5),
+                                              ([(324, 328)], 256, 1, 1), ([(128, 128)], 64, 3, 3)])
+def test_wgrad_full_size_split_paths(cuda, segs, cout, kh, kw):
+    """RAFT-sized pixel counts take the XCD-grouped split-K mapping and the fused bias sum."""
+    torch.manual_seed(3)
+    B, H, W = 8, 46, 62
+    P = B * H * W
+    cin = sum(r for r, _ in segs)
+    srcs = [torch.zeros(P, pd, device=cuda, dtype=torch.bfloat16) for _, pd in segs]
+    for (r, _), buf in zip(segs, srcs):
+        buf[:, :r] = torch.randn(P, r, device=cuda).bfloat16()
+    dy = torch.randn(P, cout, device=cuda).bfloat16()
+    w = torch.zeros(cout, cin, kh, kw, device=cuda)
+    wt = C.pack_fwd(w, segs)
+    dw = torch.zeros(cout, wt.shape[1], device=cuda)
+    db = torch.zeros(cout, device=cuda)
+    C.conv_wgrad(srcs, dy, C.geom(B, H, W, kh, kw, kh // 2, kw // 2), cout, dw, db)
+    x = torch.cat([_from_pm(buf[:, :r], B, H, W) for (r, _), buf in zip(segs, srcs)], dim=1)
+    wr = torch.zeros(cout, cin, kh, kw, device=cuda, requires_grad=True)
+    y = F.conv2d(x, wr, padding=(kh // 2, kw // 2))
+    y.backward(_from_pm(dy, B, H, W))
+    assert _rel(C.unpack_grad(dw, w.shape, segs), wr.grad) < 1e-3
+    assert _rel(db, dy.float().sum(0)) < 1e-4
+
+
 def test_dgrad_relu_mask_and_partial_accumulate(cuda):
     torch.manual_seed(1)
     B, H, W, cin, cout = 1, 9, 10, 64, 32

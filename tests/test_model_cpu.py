@@ -121,3 +121,18 @@ def test_freeze_bn():
     m.freeze_bn()
     bns = [x for x in m.modules() if isinstance(x, torch.nn.BatchNorm2d)]
     assert bns and all(not x.training for x in bns)
+
+
+def test_graphed_runner_falls_back_to_eager_on_cpu():
+    from argparse import Namespace
+
+    from raft_ros_amd.data.synthetic import synthetic_batch
+    from raft_ros_amd.models import RAFT
+    from raft_ros_amd.runtime import GraphedRAFT
+
+    model = RAFT(Namespace(small=True, mixed_precision=False)).eval()
+    i1, i2, _, _ = synthetic_batch(1, 128, 128, seed=0)
+    with torch.no_grad():
+        ref = model(i1, i2, iters=2, test_mode=True)[1]
+    out = GraphedRAFT(model, iters=2)(i1, i2)[1]
+    torch.testing.assert_close(out, ref)

@@ -64,3 +64,26 @@ def test_alternate_corr_inference(cuda):
         _, up = model(i1, i2, iters=3, test_mode=True)
         _, up_alt = alt(i1, i2, iters=3, test_mode=True)
     assert (up - up_alt).norm(dim=1).mean().item() < 0.05 * max(1.0, up.norm(dim=1).mean().item())
+
+
+@pytest.mark.parametrize("small,amp", [(True, False), (False, True)])
+def test_graphed_inference_matches_eager(cuda, small, amp):
+    from raft_ros_amd.data.synthetic import synthetic_batch
+    from raft_ros_amd.runtime import GraphedRAFT
+
+    torch.manual_seed(0)
+    model = RAFT(Namespace(small=small, mixed_precision=amp, alternate_corr=False)).to(cuda).eval()
+    runner = GraphedRAFT(model, iters=4)
+    for seed in (1, 2):  # second pair replays the captured graph on new inputs
+        i1, i2, _, _ = synthetic_batch(2, 128, 192, seed=seed, device=cuda)
+        with torch.no_grad():
+            ref_low, ref_up = model(i1, i2, iters=4, test_mode=True)
+        low, up = runner(i1, i2)
+        if amp:  # bf16: MIOpen may pick other solvers under capture -> rounding-level differences
+            for a, b in ((up, ref_up), (low, ref_low)):
+                rel = ((a - b).abs().mean() / b.abs().mean()).item()
+                assert rel < 2e-2, (rel, b.abs().mean().item())
+        else:
+            torch.testing.assert_close(up, ref_up, rtol=1e-3, atol=1e-3)
+            torch.testing.assert_close(low, ref_low, rtol=1e-3, atol=1e-3)
+    assert runner.num_graphs == 1
