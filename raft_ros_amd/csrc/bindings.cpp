@@ -112,10 +112,11 @@ struct ConvWgradArgs {
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s);
 hipError_t launch_conv_wgrad(ConvWgradArgs a, hipStream_t s);
 
-hipError_t launch_instance_norm_fwd(int dtype, const void* x, void* y, float* stats, int N, int HW, int C,
-                                    int relu, float eps, hipStream_t s);
+int instance_norm_chunks(int HW);
+hipError_t launch_instance_norm_fwd(int dtype, const void* x, void* y, float* stats, float* part, int N, int HW,
+                                    int C, int relu, float eps, hipStream_t s);
 hipError_t launch_instance_norm_bwd(int dtype, const void* x, const void* dy, const float* stats, float* gsum,
-                                    void* dx, int N, int HW, int C, int relu, hipStream_t s);
+                                    float* part, void* dx, int N, int HW, int C, int relu, hipStream_t s);
 
 namespace {
 
@@ -627,8 +628,9 @@ std::tuple<at::Tensor, at::Tensor> instance_norm_fwd(const at::Tensor& x, bool r
   const c10::DeviceGuard guard(x.device());
   auto y = at::empty(x.sizes(), x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto stats = at::empty({N, C, 2}, x.options().dtype(at::kFloat));
+  auto part = at::empty({instance_norm_chunks(HW), N, C, 2}, x.options().dtype(at::kFloat));
   HIP_OK(launch_instance_norm_fwd(dtype_code(x.scalar_type()), x.data_ptr(), y.data_ptr(), stats.data_ptr<float>(),
-                                  N, HW, C, relu, static_cast<float>(eps), cur_stream()));
+                                  part.data_ptr<float>(), N, HW, C, relu, static_cast<float>(eps), cur_stream()));
   return {y, stats};
 }
 
@@ -640,8 +642,10 @@ at::Tensor instance_norm_bwd(const at::Tensor& x, const at::Tensor& dy, const at
   const c10::DeviceGuard guard(x.device());
   auto dx = at::empty(x.sizes(), x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto gsum = at::empty({N, C, 2}, x.options().dtype(at::kFloat));
+  auto part = at::empty({instance_norm_chunks(HW), N, C, 2}, x.options().dtype(at::kFloat));
   HIP_OK(launch_instance_norm_bwd(dtype_code(x.scalar_type()), x.data_ptr(), g.data_ptr(), stats.data_ptr<float>(),
-                                  gsum.data_ptr<float>(), dx.data_ptr(), N, HW, C, relu, cur_stream()));
+                                  gsum.data_ptr<float>(), part.data_ptr<float>(), dx.data_ptr(), N, HW, C, relu,
+                                  cur_stream()));
   return dx;
 }
 

@@ -624,6 +624,141 @@ __device__ __forceinline__ void fwd4_issue(const Fwd4Src& src, const __amdgpu_bu
   for (int i = 0; i < BI; ++i) bload16(rw, sB + (wave * BI + i) * 512, bvoff[i], (unsigned)k0 * 2);
 }
 
+// Shared epilogue of the forward kernels: the fp32 accumulators go through an LDS tile
+// (et, BM x (BN+4) floats) so each thread finishes 8 consecutive output channels of one
+// pixel with 16-byte accesses; applies alpha/bias and the fused epilogue selected by a.epi.
+template <int BM, int BN, int TM, int TN>
+__device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f32x16 (&acc)[TM][TN], int m0,
+                                             int n0, int P, int Nn) {
+  constexpr int EPI_LD = BN + 4;  // fp32 epilogue tile row pitch
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = wn * (BN / 2) + j * 32 + (lane & 31);
+        et[row * EPI_LD + col] = acc[i][j][r];
+      }
+  __syncthreads();
+  constexpr int CPR = BN / 8;  // 8-channel chunks per tile row
+  static_assert(256 % CPR == 0, "a thread keeps one channel chunk across rows");
+  // every thread owns the same 8-channel chunk in all of its rows (256 % CPR == 0): the
+  // bias is loaded once, before the row loop, instead of as a dependent load per row
+  const int ch = tid % CPR;
+  const int n = n0 + ch * 8;
+  if (n >= Nn) return;
+  const int nv = Nn - n < 8 ? Nn - n : 8;  // valid channels in this chunk
+  float bia[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) bia[q] = (a.bias && q < nv) ? a.bias[n + q] : 0.f;
+  const float alpha = a.alpha;
+#pragma unroll 2
+  for (int row = tid / CPR; row < BM; row += 256 / CPR) {
+    const long p = m0 + row;
+    if (p >= P) break;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8 + 4);
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = v[q] * alpha + bia[q];
+    if (a.epi == 0) {
+      if (a.act == 1)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+      if (a.out_f32) {
+        float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
+        if (nv == 8 && (a.out_stride & 3) == 0) {
+          *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (q < nv) o[q] = v[q];
+        }
+      } else {
+        __bf16* o = static_cast<__bf16*>(a.out) + p * a.out_stride + n;
+        if (nv == 8) {
+          bf16x8 w;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(v[q]);
+          *reinterpret_cast<bf16x8*>(o) = w;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (q < nv) o[q] = static_cast<__bf16>(v[q]);
+        }
+      }
+    } else if (a.epi == 1) {
+      if (a.mask) {
+        const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.mask + p * a.mask_stride + n);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (!(static_cast<float>(m[q]) > 0.f)) v[q] = 0.f;
+      }
+      const bool accum = n >= a.acc_c0;  // acc_c0 is a multiple of 8
+      if (a.out_f32) {
+        float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
+        if (nv == 8) {
+          f32x4 x0 = {v[0], v[1], v[2], v[3]}, x1 = {v[4], v[5], v[6], v[7]};
+          if (accum) {
+            x0 += *reinterpret_cast<const f32x4*>(o);
+            x1 += *reinterpret_cast<const f32x4*>(o + 4);
+          }
+          *reinterpret_cast<f32x4*>(o) = x0;
+          *reinterpret_cast<f32x4*>(o + 4) = x1;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (q < nv) o[q] = accum ? o[q] + v[q] : v[q];
+        }
+      } else {
+        __bf16* o = static_cast<__bf16*>(a.out) + p * a.out_stride + n;
+        if (nv == 8) {
+          bf16x8 w;
+          const bf16x8 old = accum ? *reinterpret_cast<const bf16x8*>(o) : bf16x8{};
+#pragma unroll
+          for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(accum ? static_cast<float>(old[q]) + v[q] : v[q]);
+          *reinterpret_cast<bf16x8*>(o) = w;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (q < nv) o[q] = static_cast<__bf16>(accum ? static_cast<float>(o[q]) + v[q] : v[q]);
+        }
+      }
+    } else if (a.epi == 2) {
+      const int C = Nn >> 1;
+      bf16x8 sg;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) sg[q] = static_cast<__bf16>(sigmoidf_(v[q]));
+      *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = sg;
+      if (n >= C) {
+        const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + (n - C));
+        bf16x8 rh;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) rh[q] = static_cast<__bf16>(static_cast<float>(sg[q]) * static_cast<float>(hv[q]));
+        *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + (n - C)) = rh;
+      }
+    } else {
+      const bf16x8 zv = *reinterpret_cast<const bf16x8*>(a.z + p * a.z_stride + n);
+      const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + n);
+      bf16x8 hn, qo;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float qq = tanhf_(v[q]);
+        const float z = static_cast<float>(zv[q]);
+        hn[q] = static_cast<__bf16>((1.f - z) * static_cast<float>(hv[q]) + z * qq);
+        qo[q] = static_cast<__bf16>(qq);
+      }
+      *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = hn;
+      *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + n) = qo;
+    }
+  }
+}
+
 template <int BM, int BN, int S>
 __global__ __launch_bounds__(256) void conv_fwd4_kernel(const ConvFwdArgs a) {
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -742,123 +877,241 @@ __global__ __launch_bounds__(256) void conv_fwd4_kernel(const ConvFwdArgs a) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
-  // ------------------------------------------------------------------ epilogue via LDS
-  float* et = reinterpret_cast<float*>(smem);
+  fwd_epilogue<BM, BN, TM, TN>(a, reinterpret_cast<float*>(smem), acc, m0, n0, P, Nn);
+}
+
+// ============================================================================ forward v5 (halo strip)
+// Implicit GEMM with operand reuse across taps.  v4 re-fetches the im2col A tile for
+// every tap (9x the activation bytes for a 3x3 conv) and a BM=64 tile re-reads the
+// whole weight slice for every 64 pixels; on MI355X those L2->CU fills (~70 GB/s per
+// CU) bound the update-block convs, not the MFMA.  v5 stages, per 64-channel chunk,
+// ONE contiguous strip of input pixels covering the tile plus its halo
+//     rows [m0 - (PH*W+PW), m0 + BM + (KH-1)*W + KW-1 - (PH*W+PW))
+// (flat NHWC pixel order, so a tap is a constant row shift of the strip) and then
+// runs every tap of the chunk from it: only the BN x 64 weight tile is fetched per
+// tap.  Pixels outside the image (row ends, image borders, batch borders) are
+// zeroed at the A-fragment read by a per-lane (py, px) bounds test.
+//   steps t = chunk * ntaps + tap;  3-stage weight ring, 2 strip buffers; the strip of
+//   chunk c+1 is fetched with the weights two steps ahead (same counted-vmcnt DMA
+//   pipeline as v4).  Dynamic LDS: 2 strips + 3 weight stages (<= 160 KB).
+typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8;
+
+// 16-byte LDS read at a 32-bit LDS byte address
+__device__ __forceinline__ bf16x8 lds_read16(unsigned addr) { return *(const lds_bf16x8*)(uintptr_t)addr; }
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void conv_fwd5_kernel(const ConvFwdArgs a, int strip_rows) {
+  extern __shared__ __attribute__((aligned(1024))) __bf16 dsm[];
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int BI = BN / 32;  // weight wave-instructions (8 rows each) per wave per step
+  constexpr int BSTAGE = BN * 64;
+  const int strip_elems = strip_rows * 64;
+  __bf16* const strips = dsm;
+  __bf16* const bring = dsm + 2 * strip_elems;
+  __bf16* const zrow = bring + 3 * BSTAGE;  // 64 zero bf16: the A row of out-of-image taps
+
+  const int Cin = a.Cin, Kpad = a.Kpad, H = a.H, W = a.W, KW = a.KW, PH = a.PH, PW = a.PW;
+  const int ntaps = a.KH * a.KW;
+  const int P = (int)a.P;
+  const int Nn = a.N;
+  const int sc0 = a.src[0].C, sc1 = a.src[1].C;
+  const int nsrc = a.nsrc;
+  const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.src[0].ptr, (unsigned)(a.P * a.src[0].stride * 2));
+  const __amdgpu_buffer_rsrc_t r1 =
+      make_rsrc(nsrc > 1 ? a.src[1].ptr : a.src[0].ptr, nsrc > 1 ? (unsigned)(a.P * a.src[1].stride * 2) : 0u);
+  const __amdgpu_buffer_rsrc_t r2 =
+      make_rsrc(nsrc > 2 ? a.src[2].ptr : a.src[0].ptr, nsrc > 2 ? (unsigned)(a.P * a.src[2].stride * 2) : 0u);
+  const unsigned st0 = (unsigned)a.src[0].stride * 2, st1 = (unsigned)a.src[1].stride * 2,
+                 st2 = (unsigned)a.src[2].stride * 2;
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.wt, (unsigned)((long)Nn * Kpad * 2));
+
+  const int tilesN = (Nn + BN - 1) / BN;
+  const int tilesM = (P + BM - 1) / BM;
+  const int wg = xcd_remap(blockIdx.x, tilesM * tilesN);
+  const int tm = wg / tilesN, tn = wg - (wg / tilesN) * tilesN;
+  const int m0 = tm * BM;
+  const int n0 = tn * BN;
+  const int halo_lo = PH * W + PW;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lrow = lane >> 3, lpc = lane & 7;
+  const int fr = lane & 31, fh = lane >> 5;
+  if (tid < 8) reinterpret_cast<u32x4*>(zrow)[tid] = u32x4{0, 0, 0, 0};
+
+  // A-fragment rows of this lane: tile row and image coordinates
+  int frow[TM], fpy[TM], fpx[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    frow[i] = wm * (BM / 2) + i * 32 + fr;
+    const int p = m0 + frow[i];
+    if (p < P) {
+      const int rem = p % (H * W);
+      fpy[i] = rem / W;
+      fpx[i] = rem - fpy[i] * W;
+    } else {
+      fpy[i] = fpx[i] = -(1 << 20);
+    }
+  }
+  // B-fragment LDS byte offsets (within a stage) of this lane, per sub-step; fragment j adds
+  // j*32 rows (a multiple of 16 rows leaves the swizzle unchanged -> immediate offset)
+  unsigned boff[4];
+  {
+    const int row = wn * (BN / 2) + fr;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) boff[s] = (unsigned)(row * 128 + swz(row, 2 * s + fh) * 16);
+  }
+  unsigned bvoff[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int row = (wave * BI + i) * 8 + lrow;
+    bvoff[i] = (n0 + row < Nn) ? (unsigned)((n0 + row) * Kpad * 2 + swz(row, lpc) * 16) : kOOB;
+  }
+  const int nchunks = Cin / 64;
+  const int nsteps = nchunks * ntaps;
+  const int strip_instr = strip_rows / 8;  // 8 rows (1 KB) per wave-instruction
+  const unsigned lds_strips = (unsigned)(reinterpret_cast<uintptr_t>(strips) & 0xffffffffu);
+  const unsigned lds_bring = (unsigned)(reinterpret_cast<uintptr_t>(bring) & 0xffffffffu);
+  const unsigned lds_zero = (unsigned)(reinterpret_cast<uintptr_t>(zrow) & 0xffffffffu);
+
+  // ---- DMA issue state (step `is_t`): chunk, tap, weight k offset, stage
+  int is_t = 0, is_cc = 0, is_tap = 0, is_stage = 0;
+  auto issue_next = [&]() __attribute__((always_inline)) {
+    if (is_tap == 0) {
+      const int c0 = is_cc * 64;
+      __amdgpu_buffer_rsrc_t rs = r0;
+      unsigned st = st0, soff = (unsigned)c0 * 2;
+      if (c0 >= sc0 + sc1) {
+        rs = r2; st = st2; soff = (unsigned)(c0 - sc0 - sc1) * 2;
+      } else if (c0 >= sc0) {
+        rs = r1; st = st1; soff = (unsigned)(c0 - sc0) * 2;
+      }
+      __bf16* sbuf = strips + (is_cc & 1) * strip_elems;
+      for (int q = wave; q < strip_instr; q += 4) {
+        const int row = q * 8 + lrow;
+        const int p = m0 - halo_lo + row;
+        const unsigned voff = (p >= 0 && p < P) ? (unsigned)p * st + (unsigned)(swz(row, lpc) * 16) : kOOB;
+        bload16(rs, sbuf + q * 512, voff, soff);
+      }
+    }
+    __bf16* sB = bring + is_stage * BSTAGE;
+    const unsigned k0 = (unsigned)(is_tap * Cin + is_cc * 64);
+#pragma unroll
+    for (int i = 0; i < BI; ++i) bload16(rw, sB + (wave * BI + i) * 512, bvoff[i], k0 * 2);
+    ++is_t;
+    is_stage = is_stage == 2 ? 0 : is_stage + 1;
+    if (++is_tap == ntaps) {
+      is_tap = 0;
+      ++is_cc;
+    }
+  };
+
+  // ---- fragment-read state (step `rd_t`)
+  int rd_cc = 0, rd_ky = 0, rd_kx = 0, rd_stage = 0;
+  auto read_frags = [&](bf16x8 (&fa)[TM][4], bf16x8 (&fb)[TN][4]) __attribute__((always_inline)) {
+    const int shift = rd_ky * W + rd_kx;
+    const int dy = rd_ky - PH, dx = rd_kx - PW;
+    const unsigned sbase = lds_strips + (unsigned)((rd_cc & 1) * strip_elems * 2);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = frow[i] + shift;
+      const bool ok = (unsigned)(fpy[i] + dy) < (unsigned)H && (unsigned)(fpx[i] + dx) < (unsigned)W;
+      const unsigned base = ok ? sbase + (unsigned)row * 128u : lds_zero;
+      const unsigned x = (unsigned)((((row >> 1) & 7) ^ fh) << 4);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        fa[i][s] = lds_read16(base + (x ^ (unsigned)(s << 5)));
+    }
+    const unsigned bbase = lds_bring + (unsigned)(rd_stage * BSTAGE * 2);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        fb[j][s] = lds_read16(bbase + boff[s] + (unsigned)(j * 32 * 128));
+    rd_stage = rd_stage == 2 ? 0 : rd_stage + 1;
+    if (++rd_kx == KW) {
+      rd_kx = 0;
+      if (++rd_ky == a.KH) {
+        rd_ky = 0;
+        ++rd_cc;
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int col = wn * (BN / 2) + j * 32 + (lane & 31);
-        et[row * EPI_LD + col] = acc[i][j][r];
-      }
-  __syncthreads();
-  constexpr int CPR = BN / 8;  // 8-channel chunks per tile row
-  for (int e = tid; e < BM * CPR; e += 256) {
-    const int row = e / CPR, ch = e - row * CPR;
-    const long p = m0 + row;
-    const int n = n0 + ch * 8;
-    if (p >= P || n >= Nn) continue;
-    const f32x4 lo = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8);
-    const f32x4 hi = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8 + 4);
-    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    const int nv = Nn - n < 8 ? Nn - n : 8;  // valid channels in this chunk
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto mfma_sub = [&](bf16x8 (&fa)[TM][4], bf16x8 (&fb)[TN][4], int s) __attribute__((always_inline)) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = v[q] * a.alpha + ((a.bias && q < nv) ? a.bias[n + q] : 0.f);
-    if (a.epi == 0) {
-      if (a.act == 1)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
-      if (a.out_f32) {
-        float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
-        if (nv == 8 && (a.out_stride & 3) == 0) {
-          *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
-          *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
-        } else {
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (q < nv) o[q] = v[q];
-        }
-      } else {
-        __bf16* o = static_cast<__bf16*>(a.out) + p * a.out_stride + n;
-        if (nv == 8) {
-          bf16x8 w;
-#pragma unroll
-          for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(v[q]);
-          *reinterpret_cast<bf16x8*>(o) = w;
-        } else {
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (q < nv) o[q] = static_cast<__bf16>(v[q]);
-        }
-      }
-    } else if (a.epi == 1) {
-      if (a.mask) {
-        const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.mask + p * a.mask_stride + n);
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (!(static_cast<float>(m[q]) > 0.f)) v[q] = 0.f;
-      }
-      const bool accum = n >= a.acc_c0;  // acc_c0 is a multiple of 8
-      if (a.out_f32) {
-        float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
-        if (nv == 8) {
-          f32x4 x0 = {v[0], v[1], v[2], v[3]}, x1 = {v[4], v[5], v[6], v[7]};
-          if (accum) {
-            x0 += *reinterpret_cast<const f32x4*>(o);
-            x1 += *reinterpret_cast<const f32x4*>(o + 4);
-          }
-          *reinterpret_cast<f32x4*>(o) = x0;
-          *reinterpret_cast<f32x4*>(o + 4) = x1;
-        } else {
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (q < nv) o[q] = accum ? o[q] + v[q] : v[q];
-        }
-      } else {
-        __bf16* o = static_cast<__bf16*>(a.out) + p * a.out_stride + n;
-        if (nv == 8) {
-          bf16x8 w;
-          const bf16x8 old = accum ? *reinterpret_cast<const bf16x8*>(o) : bf16x8{};
-#pragma unroll
-          for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(accum ? static_cast<float>(old[q]) + v[q] : v[q]);
-          *reinterpret_cast<bf16x8*>(o) = w;
-        } else {
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (q < nv) o[q] = static_cast<__bf16>(accum ? static_cast<float>(o[q]) + v[q] : v[q]);
-        }
-      }
-    } else if (a.epi == 2) {
-      const int C = Nn >> 1;
-      bf16x8 sg;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) sg[q] = static_cast<__bf16>(sigmoidf_(v[q]));
-      *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = sg;
-      if (n >= C) {
-        const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + (n - C));
-        bf16x8 rh;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) rh[q] = static_cast<__bf16>(static_cast<float>(sg[q]) * static_cast<float>(hv[q]));
-        *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + (n - C)) = rh;
-      }
-    } else {
-      const bf16x8 zv = *reinterpret_cast<const bf16x8*>(a.z + p * a.z_stride + n);
-      const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + n);
-      bf16x8 hn, qo;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float qq = tanhf_(v[q]);
-        const float z = static_cast<float>(zv[q]);
-        hn[q] = static_cast<__bf16>((1.f - z) * static_cast<float>(hv[q]) + z * qq);
-        qo[q] = static_cast<__bf16>(qq);
-      }
-      *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = hn;
-      *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + n) = qo;
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+  };
+
+  bf16x8 fa0[TM][4], fb0[TN][4], fa1[TM][4], fb1[TN][4];
+  // prologue: three steps in flight, fragments of step 0 in registers
+  issue_next();
+  if (nsteps > 1) issue_next();
+  if (nsteps > 2) issue_next();
+  if (nsteps > 2) wait_vmcnt<2 * BI>();
+  else wait_vmcnt<0>();
+  __syncthreads();  // also publishes the zero row
+  read_frags(fa0, fb0);
+
+  // one step: MFMAs of step t from (ca, cb) with the next step's LDS reads (into na, nb)
+  // in the middle, after the wait + barrier that make step t+1 (and the strip) visible
+  auto step = [&](bf16x8 (&ca)[TM][4], bf16x8 (&cb)[TN][4], bf16x8 (&na)[TM][4], bf16x8 (&nb)[TN][4],
+                  int t) __attribute__((always_inline)) {
+    mfma_sub(ca, cb, 0);
+    mfma_sub(ca, cb, 1);
+    if (t + 1 < nsteps) {
+      if (t + 2 < nsteps) wait_vmcnt<BI>();
+      else wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (is_t < nsteps) issue_next();
+      read_frags(na, nb);
     }
+    mfma_sub(ca, cb, 2);
+    mfma_sub(ca, cb, 3);
+  };
+  for (int t = 0; t < nsteps; t += 2) {
+    step(fa0, fb0, fa1, fb1, t);
+    if (t + 1 < nsteps) step(fa1, fb1, fa0, fb0, t + 1);
   }
+  wait_vmcnt<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  fwd_epilogue<BM, BN, TM, TN>(a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn);
+}
+
+// raise a kernel's dynamic-LDS limit once (it only ever grows)
+inline void set_lds_limit(const void* fn, int bytes) {
+  static thread_local const void* last_fn[8] = {};
+  static thread_local int last_bytes[8] = {};
+  for (int i = 0; i < 8; ++i)
+    if (last_fn[i] == fn && last_bytes[i] >= bytes) return;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  for (int i = 0; i < 8; ++i)
+    if (last_fn[i] == nullptr || last_fn[i] == fn) {
+      last_fn[i] = fn;
+      last_bytes[i] = 160 * 1024;
+      return;
+    }
+}
+
+// LDS bytes of conv_fwd5<BM, BN> for a given strip (0 if it does not fit in 160 KB)
+inline long fwd5_lds_bytes(int BM, int BN, int strip_rows) {
+  const long ring = 2L * strip_rows * 64 * 2 + 3L * BN * 64 * 2 + 128;
+  const long epi = (long)BM * (BN + 4) * 4;
+  const long need = ring > epi ? ring : epi;
+  return need <= 160 * 1024 ? need : 0;
 }
 
 // ============================================================================ wgrad
@@ -1252,11 +1505,142 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
   }
 }
 
+// ============================================================================ narrow output (N <= 2)
+// flow_head.conv2 (3x3, 256 -> 2) is a pair of 2,304-long dot products per pixel: a
+// bandwidth problem, not a GEMM (a 64-wide MFMA tile would be 97% padding).  LPP lanes
+// own one pixel, each lane 8 channels (one 16-byte load per tap); the weights live in
+// registers; lanes combine with a butterfly.  Single source, bf16 in, epilogue 0
+// (bias, optional ReLU) with fp32 or bf16 output.
+template <int LPP>
+__global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
+  constexpr int PPW = 64 / LPP;  // pixels per wave per pass
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane / LPP, cl = lane - sub * LPP;
+  const int ntaps = a.KH * a.KW;
+  const int Cin = a.Cin;
+  float w[2][9][8];
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      bf16x8 v{};
+      if (n < a.N && t < ntaps) v = *reinterpret_cast<const bf16x8*>(a.wt + (long)n * a.Kpad + t * Cin + cl * 8);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) w[n][t][q] = static_cast<float>(v[q]);
+    }
+  const float b0 = a.bias ? a.bias[0] : 0.f, b1 = (a.bias && a.N > 1) ? a.bias[1] : 0.f;
+  const int HW = a.H * a.W;
+  const long stride = a.src[0].stride;
+  const long step = (long)gridDim.x * 4 * PPW;
+  for (long p = ((long)blockIdx.x * 4 + wave) * PPW + sub; p < a.P + sub; p += step) {
+    float s0 = 0.f, s1 = 0.f;
+    if (p < a.P) {
+      const int rem = (int)(p % HW);
+      const int py = rem / a.W, px = rem - (rem / a.W) * a.W;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (t >= ntaps) break;
+        const int ky = t / a.KW, kx = t - (t / a.KW) * a.KW;
+        const int y = py + ky - a.PH, x = px + kx - a.PW;
+        if ((unsigned)y >= (unsigned)a.H || (unsigned)x >= (unsigned)a.W) continue;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(
+            a.src[0].ptr + (p + (long)(ky - a.PH) * a.W + (kx - a.PW)) * stride + cl * 8);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float xv = static_cast<float>(v[q]);
+          s0 += xv * w[0][t][q];
+          s1 += xv * w[1][t][q];
+        }
+      }
+    }
+#pragma unroll
+    for (int off = LPP / 2; off > 0; off >>= 1) {
+      s0 += __shfl_xor(s0, off, 64);
+      s1 += __shfl_xor(s1, off, 64);
+    }
+    if (cl == 0 && p < a.P) {
+      float v0 = s0 * a.alpha + b0, v1 = s1 * a.alpha + b1;
+      if (a.act == 1) {
+        v0 = fmaxf(v0, 0.f);
+        v1 = fmaxf(v1, 0.f);
+      }
+      if (a.out_f32) {
+        float* o = static_cast<float*>(a.out) + p * a.out_stride;
+        o[0] = v0;
+        if (a.N > 1) o[1] = v1;
+      } else {
+        __bf16* o = static_cast<__bf16*>(a.out) + p * a.out_stride;
+        o[0] = static_cast<__bf16>(v0);
+        if (a.N > 1) o[1] = static_cast<__bf16>(v1);
+      }
+    }
+  }
+}
+
+// dW[n][tap][c] += sum_p dY[p][n] X[p + d_tap][c] for N <= 2: thread (tap, 8-channel chunk)
+// sweeps a pixel range (16-byte loads, coalesced across the chunks of one tap), partial
+// sums go out with one fp32 atomic per weight per workgroup; two extra lanes sum db.
+constexpr int N2_PIX = 128;
+__global__ __launch_bounds__(320) void conv_n2_wgrad_kernel(const ConvWgradArgs a) {
+  const int tid = threadIdx.x;
+  const int chunks = a.Cin / 8;
+  const int ntaps = a.KH * a.KW;
+  const long p0 = (long)blockIdx.x * N2_PIX;
+  const long p1 = p0 + N2_PIX < a.P ? p0 + N2_PIX : a.P;
+  const int HW = a.H * a.W;
+  if (tid < ntaps * chunks) {
+    const int t = tid / chunks, cl = tid - t * chunks;
+    const int ky = t / a.KW, kx = t - (t / a.KW) * a.KW;
+    const long shift = (long)(ky - a.PH) * a.W + (kx - a.PW);
+    const long stride = a.src[0].stride;
+    float s0[8], s1[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s0[q] = s1[q] = 0.f;
+#pragma unroll 4
+    for (long p = p0; p < p1; ++p) {
+      const int rem = (int)(p % HW);
+      const int py = rem / a.W, px = rem - (rem / a.W) * a.W;
+      const int y = py + ky - a.PH, x = px + kx - a.PW;
+      if ((unsigned)y >= (unsigned)a.H || (unsigned)x >= (unsigned)a.W) continue;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(a.src[0].ptr + (p + shift) * stride + cl * 8);
+      const float g0 = static_cast<float>(a.dy[p * a.dy_stride]);
+      const float g1 = a.N > 1 ? static_cast<float>(a.dy[p * a.dy_stride + 1]) : 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float xv = static_cast<float>(v[q]);
+        s0[q] += g0 * xv;
+        s1[q] += g1 * xv;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      atomicAdd(a.dw + t * a.Cin + cl * 8 + q, s0[q]);
+      if (a.N > 1) atomicAdd(a.dw + a.Kpad + t * a.Cin + cl * 8 + q, s1[q]);
+    }
+  } else if (a.db && tid < ntaps * chunks + a.N) {
+    const int n = tid - ntaps * chunks;
+    float s = 0.f;
+    for (long p = p0; p < p1; ++p) s += static_cast<float>(a.dy[p * a.dy_stride + n]);
+    atomicAdd(a.db + n, s);
+  }
+}
+
 }  // namespace
 
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   if (a.P == 0 || a.N == 0) return hipSuccess;
   if (a.Kpad % FBK != 0) return hipErrorInvalidValue;
+  if (a.N <= 2 && a.epi == 0 && a.nsrc == 1 && a.KH * a.KW <= 9 && a.src[0].C == a.Cin &&
+      (a.Cin == 64 || a.Cin == 128 || a.Cin == 256 || a.Cin == 512) && getenv("RAFT_CONV_NO_N2") == nullptr) {
+    const int lpp = a.Cin / 8;
+    const int ppb = 4 * (64 / lpp);
+    const long blocks = std::min<long>((a.P + ppb - 1) / ppb, 2048);
+    if (lpp == 8) hipLaunchKernelGGL(conv_n2_fwd_kernel<8>, dim3(blocks), dim3(256), 0, s, a);
+    else if (lpp == 16) hipLaunchKernelGGL(conv_n2_fwd_kernel<16>, dim3(blocks), dim3(256), 0, s, a);
+    else if (lpp == 32) hipLaunchKernelGGL(conv_n2_fwd_kernel<32>, dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(conv_n2_fwd_kernel<64>, dim3(blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   auto tiles = [&](int bm, int bn) { return (long)((a.P + bm - 1) / bm) * ((a.N + bn - 1) / bn); };
   // largest tile that still gives >= 2 workgroups per CU (256 CUs); small-N convs use 64-wide N
   // measured on MI355X (scripts/bench_convs.py): 64x64 tiles win for every update-block
@@ -1271,6 +1655,61 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
     if ((!uniform && a.nsrc > 1) || maxbytes >= (1L << 31) || (long)a.N * a.Kpad * 2 >= (1L << 31)) cfg = 2;
   }
   if (const char* e = getenv("RAFT_CONV_FWD_CFG")) cfg = atoi(e);
+  if (cfg == 8 || cfg == 9 || cfg >= 20) {
+    // v5 (halo strip): multi-tap convs whose 64-channel chunks never straddle a source
+    // segment, 32-bit offsets; tile chosen by N, falling back to v4 when the strip does
+    // not fit the LDS budget
+    bool ok5 = a.KH * a.KW > 1 && a.Cin % 64 == 0 && a.N >= 64 && getenv("RAFT_CONV_NO_V5") == nullptr;
+    for (int i = 0; i < a.nsrc; ++i) ok5 = ok5 && a.src[i].C % 64 == 0;
+    for (int i = 0; i < a.nsrc; ++i) ok5 = ok5 && a.P * a.src[i].stride * 2 < (1L << 31);
+    ok5 = ok5 && (long)a.N * a.Kpad * 2 < (1L << 31) && a.P < (1L << 30);
+    // tile per shape, from scripts/bench_convs.py on MI355X (B=8, 46x62): 256x128 for wide
+    // 3x3 convs, 128x128 for 3x3 with ~128 outputs, 128x256 for the 384-channel 1x5 z||r
+    // conv; every other shape measured faster on v4
+    int v5 = cfg >= 20 ? cfg : 0;
+    if (ok5 && v5 == 0) {
+      const int taps = a.KH * a.KW;
+      if (taps == 9 && a.N >= 192) v5 = 23;
+      else if (taps == 9 && a.N > 64) v5 = 21;
+      else if (a.KH == 1 && a.KW == 5 && a.Cin >= 384 && a.N >= 256) v5 = 22;
+      else ok5 = false;
+    }
+    if (ok5) {
+      auto bm_of = [](int v) { return v == 20 ? 64 : v == 23 ? 256 : 128; };
+      auto bn_of = [](int v) { return v == 22 ? 256 : 128; };
+      auto rows_of = [&](int v) { return (bm_of(v) + (a.KH - 1) * a.W + a.KW - 1 + 7) / 8 * 8; };
+      long lds = fwd5_lds_bytes(bm_of(v5), bn_of(v5), rows_of(v5));
+      if (lds == 0 && v5 != 21) {
+        v5 = 21;
+        lds = fwd5_lds_bytes(128, 128, rows_of(v5));
+      }
+      const int rows = rows_of(v5);
+      if (lds > 0) {
+        const dim3 grid(tiles(bm_of(v5), bn_of(v5)));
+        switch (v5) {
+          case 23:
+            set_lds_limit((const void*)conv_fwd5_kernel<256, 128>, (int)lds);
+            hipLaunchKernelGGL((conv_fwd5_kernel<256, 128>), grid, dim3(256), lds, s, a, rows);
+            break;
+          case 20:
+            set_lds_limit((const void*)conv_fwd5_kernel<64, 128>, (int)lds);
+            hipLaunchKernelGGL((conv_fwd5_kernel<64, 128>), grid, dim3(256), lds, s, a, rows);
+            break;
+          case 22:
+            set_lds_limit((const void*)conv_fwd5_kernel<128, 256>,
+(int)lds);
+            hipLaunchKernelGGL((conv_fwd5_kernel<128, 256>), grid, dim3(256), lds, s, a, rows);
+            break;
+          default:
+            set_lds_limit((const void*)conv_fwd5_kernel<128, 128>,
+(int)lds);
+            hipLaunchKernelGGL((conv_fwd5_kernel<128, 128>), grid, dim3(256), lds, s, a, rows);
+        }
+        return hipGetLastError();
+      }
+    }
+    if (cfg >= 20) cfg = (a.N > 64 && a.N <= 512) ? 8 : 9;
+  }
   switch (cfg) {
     case 8:
       hipLaunchKernelGGL((conv_fwd4_kernel<64, 128, 3>), dim3(tiles(64, 128)), dim3(256), 0, s, a);

@@ -7,7 +7,8 @@
 // and backward) -- ~70 full-resolution copies per training step.  These kernels
 // work on the NHWC layout directly:
 //   stats:  per (n, c) sum / sum of squares, 16-byte loads of 8 channels per
-//           thread, LDS reduction, one fp32 atomic per channel per block;
+//           thread, fixed-order LDS reduction to one partial per 1024-pixel chunk,
+//           then a fixed-order sum of the partials (deterministic, no atomics);
 //   apply:  y = relu?((x - mean) * rstd), vectorised;
 //   bwd:    dxhat = dy * [xhat > 0 if relu]; per (n, c) sums of dxhat and
 //           dxhat*xhat; dx = rstd * (dxhat - mean(dxhat) - xhat * mean(dxhat*xhat)).
@@ -58,27 +59,27 @@ struct Vec8IO<float> {
 
 constexpr int PIX_PER_BLOCK = 1024;
 
+// Per-(image, channel) partial sums over one PIX_PER_BLOCK pixel chunk.
 // mode 0: sums of x and x^2.  mode 1: sums of dxhat and dxhat*xhat (needs stats + dy).
+// Every block writes its own partial (no atomics, no memset): the reduction order is
+// fixed, so the statistics are bit-reproducible run to run and graph replays need no
+// zero-initialised accumulator.
 template <typename T, int MODE>
-__global__ __launch_bounds__(256) void in_stats_kernel(const T* __restrict__ x, const T* __restrict__ dy,
-                                                       const float* __restrict__ mr, float* __restrict__ acc,
-                                                       int HW, int C, int relu) {
-  __shared__ float s1[512], s2[512];
+__global__ __launch_bounds__(256) void in_partial_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                         const float* __restrict__ mr, float* __restrict__ part,
+                                                         int N, int HW, int C, int relu) {
+  __shared__ float r1[2048], r2[2048];  // [R][C], R * C <= 256 * 8
   const int n = blockIdx.y;
   const int G = C / 8;
   const int R = 256 / G;
   const int tid = threadIdx.x;
-  for (int c = tid; c < C; c += 256) {
-    s1[c] = 0.f;
-    s2[c] = 0.f;
-  }
-  __syncthreads();
   const int cg = tid % G, pr = tid / G;
   float a1[8], a2[8], mean[8], rstd[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     a1[j] = a2[j] = 0.f;
-    if (MODE == 1) {
+    mean[j] = rstd[j] = 0.f;
+    if (MODE == 1 && pr < R) {
       mean[j] = mr[((long)n * C + cg * 8 + j) * 2];
       rstd[j] = mr[((long)n * C + cg * 8 + j) * 2 + 1];
     }
@@ -110,25 +111,42 @@ __global__ __launch_bounds__(256) void in_stats_kernel(const T* __restrict__ x, 
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      atomicAdd(&s1[cg * 8 + j], a1[j]);
-      atomicAdd(&s2[cg * 8 + j], a2[j]);
+      r1[pr * C + cg * 8 + j] = a1[j];
+      r2[pr * C + cg * 8 + j] = a2[j];
     }
   }
   __syncthreads();
   for (int c = tid; c < C; c += 256) {
-    atomicAdd(&acc[((long)n * C + c) * 2], s1[c]);
-    atomicAdd(&acc[((long)n * C + c) * 2 + 1], s2[c]);
+    float s1 = 0.f, s2 = 0.f;
+    for (int r = 0; r < R; ++r) {
+      s1 += r1[r * C + c];
+      s2 += r2[r * C + c];
+    }
+    const long o = (((long)blockIdx.x * N + n) * C + c) * 2;
+    part[o] = s1;
+    part[o + 1] = s2;
   }
 }
 
-// sums -> (mean, rstd) in place
-__global__ void in_finalize_kernel(float* __restrict__ acc, long NC, int HW, float eps) {
+// Sum the per-chunk partials in a fixed order.  mode 0 -> (mean, rstd); mode 1 -> raw sums.
+__global__ void in_reduce_kernel(const float* __restrict__ part, float* __restrict__ out, int chunks, long NC,
+                                 int HW, float eps, int mode) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= NC) return;
-  const float m = acc[2 * i] / HW;
-  const float var = fmaxf(acc[2 * i + 1] / HW - m * m, 0.f);
-  acc[2 * i] = m;
-  acc[2 * i + 1] = rsqrtf(var + eps);
+  float s1 = 0.f, s2 = 0.f;
+  for (int k = 0; k < chunks; ++k) {
+    s1 += part[(k * NC + i) * 2];
+    s2 += part[(k * NC + i) * 2 + 1];
+  }
+  if (mode == 0) {
+    const float m = s1 / HW;
+    const float var = fmaxf(s2 / HW - m * m, 0.f);
+    out[2 * i] = m;
+    out[2 * i + 1] = rsqrtf(var + eps);
+  } else {
+    out[2 * i] = s1;
+    out[2 * i + 1] = s2;
+  }
 }
 
 template <typename T>
@@ -180,22 +198,25 @@ __global__ __launch_bounds__(256) void in_bwd_apply_kernel(const T* __restrict__
 
 }  // namespace
 
-hipError_t launch_instance_norm_fwd(int dtype, const void* x, void* y, float* stats, int N, int HW, int C,
-                                    int relu, float eps, hipStream_t s) {
+int instance_norm_chunks(int HW) { return (HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK; }
+
+hipError_t launch_instance_norm_fwd(int dtype, const void* x, void* y, float* stats, float* part, int N, int HW,
+                                    int C, int relu, float eps, hipStream_t s) {
   if (C % 8 || C > 512) return hipErrorInvalidValue;
-  RAFT_HIP_CHECK(hipMemsetAsync(stats, 0, sizeof(float) * 2 * N * C, s));
-  const dim3 g((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, N);
+  const int chunks = instance_norm_chunks(HW);
+  const dim3 g(chunks, N);
   const long total8 = (long)N * HW * C / 8;
   const dim3 ga((total8 + 255) / 256);
   if (dtype == kBF16) {
-    hipLaunchKernelGGL((in_stats_kernel<__bf16, 0>), g, dim3(256), 0, s, (const __bf16*)x, nullptr, nullptr,
-                       stats, HW, C, relu);
+    hipLaunchKernelGGL((in_partial_kernel<__bf16, 0>), g, dim3(256), 0, s, (const __bf16*)x, nullptr, nullptr,
+                       part, N, HW, C, relu);
   } else {
-    hipLaunchKernelGGL((in_stats_kernel<float, 0>), g, dim3(256), 0, s, (const float*)x, nullptr, nullptr,
-                       stats, HW, C, relu);
+    hipLaunchKernelGGL((in_partial_kernel<float, 0>), g, dim3(256), 0, s, (const float*)x, nullptr, nullptr,
+                       part, N, HW, C, relu);
   }
   RAFT_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(in_finalize_kernel, dim3((N * C + 255) / 256), dim3(256), 0, s, stats, (long)N * C, HW, eps);
+  hipLaunchKernelGGL(in_reduce_kernel, dim3((N * C + 255) / 256), dim3(256), 0, s, part, stats, chunks,
+                     (long)N * C, HW, eps, 0);
   RAFT_HIP_CHECK(hipGetLastError());
   if (dtype == kBF16)
     hipLaunchKernelGGL(in_apply_kernel<__bf16>, ga, dim3(256), 0, s, (const __bf16*)x, stats, (__bf16*)y,
@@ -207,25 +228,28 @@ hipError_t launch_instance_norm_fwd(int dtype, const void* x, void* y, float* st
 }
 
 hipError_t launch_instance_norm_bwd(int dtype, const void* x, const void* dy, const float* stats, float* gsum,
-                                    void* dx, int N, int HW, int C, int relu, hipStream_t s) {
+                                    float* part, void* dx, int N, int HW, int C, int relu, hipStream_t s) {
   if (C % 8 || C > 512) return hipErrorInvalidValue;
-  RAFT_HIP_CHECK(hipMemsetAsync(gsum, 0, sizeof(float) * 2 * N * C, s));
-  const dim3 g((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, N);
+  const int chunks = instance_norm_chunks(HW);
+  const dim3 g(chunks, N);
   const long total8 = (long)N * HW * C / 8;
   const dim3 ga((total8 + 255) / 256);
-  if (dtype == kBF16) {
-    hipLaunchKernelGGL((in_stats_kernel<__bf16, 1>), g, dim3(256), 0, s, (const __bf16*)x, (const __bf16*)dy,
-                       stats, gsum, HW, C, relu);
-    RAFT_HIP_CHECK(hipGetLastError());
+  if (dtype == kBF16)
+    hipLaunchKernelGGL((in_partial_kernel<__bf16, 1>), g, dim3(256), 0, s, (const __bf16*)x, (const __bf16*)dy,
+                       stats, part, N, HW, C, relu);
+  else
+    hipLaunchKernelGGL((in_partial_kernel<float, 1>), g, dim3(256), 0, s, (const float*)x, (const float*)dy,
+                       stats, part, N, HW, C, relu);
+  RAFT_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(in_reduce_kernel, dim3((N * C + 255) / 256), dim3(256), 0, s, part, gsum, chunks,
+                     (long)N * C, HW, 0.f, 1);
+  RAFT_HIP_CHECK(hipGetLastError());
+  if (dtype == kBF16)
     hipLaunchKernelGGL(in_bwd_apply_kernel<__bf16>, ga, dim3(256), 0, s, (const __bf16*)x, (const __bf16*)dy,
                        stats, gsum, (__bf16*)dx, total8, HW, C, relu);
-  } else {
-    hipLaunchKernelGGL((in_stats_kernel<float, 1>), g, dim3(256), 0, s, (const float*)x, (const float*)dy, stats,
-                       gsum, HW, C, relu);
-    RAFT_HIP_CHECK(hipGetLastError());
+  else
     hipLaunchKernelGGL(in_bwd_apply_kernel<float>, ga, dim3(256), 0, s, (const float*)x, (const float*)dy, stats,
                        gsum, (float*)dx, total8, HW, C, relu);
-  }
   return hipGetLastError();
 }
 

@@ -97,7 +97,11 @@ class RAFT(nn.Module):
         enabled = bool(self.args.mixed_precision)
         if device_type == "cpu" and self.amp_dtype == torch.float16:
             enabled = False  # fp16 autocast is a GPU feature
-        return torch.autocast(device_type=device_type, dtype=self.amp_dtype, enabled=enabled)
+        # the cast cache reuses a weight's bf16 copy across the refinement iterations; a
+        # HIP-graph capture turns it off (runtime/train_graph.py) so that casts made outside
+        # the capture cannot leak into it
+        cache = getattr(self, "autocast_cache", True)
+        return torch.autocast(device_type=device_type, dtype=self.amp_dtype, enabled=enabled, cache_enabled=cache)
 
     # ------------------------------------------------------------------ forward
     def forward(self, image1, image2, iters: int = 12, flow_init=None, upsample: bool = True,

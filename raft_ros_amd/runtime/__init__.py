@@ -1,4 +1,5 @@
-"""Execution runtime helpers: HIP-graph inference replay."""
+"""Execution runtime helpers: HIP-graph replay of inference and of the whole training step."""
 from .graphs import GraphedRAFT
+from .train_graph import GraphedTrainStep
 
-__all__ = ["GraphedRAFT"]
+__all__ = ["GraphedRAFT", "GraphedTrainStep"]

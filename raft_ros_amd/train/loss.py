@@ -25,7 +25,8 @@ def sequence_loss(flow_preds: List[torch.Tensor], flow_gt: torch.Tensor, valid: 
     for i, pred in enumerate(flow_preds):
         w = gamma ** (n - i - 1)
         loss = loss + w * (vmask * (pred - flow_gt).abs()).mean()
-    epe = torch.sum((flow_preds[-1] - flow_gt) ** 2, dim=1).sqrt()
+    # metrics carry no autograd graph (a live graph would pin the AccumulateGrad nodes)
+    epe = torch.sum((flow_preds[-1].detach() - flow_gt) ** 2, dim=1).sqrt()
     vf = valid.to(epe.dtype)
     cnt = vf.sum().clamp_min(1.0)
     metrics = {

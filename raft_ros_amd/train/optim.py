@@ -14,10 +14,17 @@ def count_parameters(model) -> int:
     return sum(p.numel() for p in model.parameters() if p.requires_grad)
 
 
-def fetch_optimizer(args, model):
+def fetch_optimizer(args, model, capturable: bool = False):
+    """``capturable=True`` (GPU): lr lives in a device tensor and the step counter on the
+    device, so the optimizer step can be captured in a HIP graph
+    (``runtime.GraphedTrainStep``); the scheduler updates the lr tensor in place."""
     params = [p for p in model.parameters() if p.requires_grad]
-    kw = dict(lr=args.lr, weight_decay=args.wdecay, eps=args.epsilon)
     fused = bool(params) and params[0].is_cuda
+    capturable = capturable and fused
+    lr = torch.tensor(float(args.lr), device=params[0].device) if capturable else args.lr
+    kw = dict(lr=lr, weight_decay=args.wdecay, eps=args.epsilon)
+    if capturable:
+        kw["capturable"] = True
     try:
         optimizer = optim.AdamW(params, fused=fused, **kw)
     except (RuntimeError, TypeError):  # pragma: no cover - fused unsupported

@@ -166,3 +166,28 @@ def test_gru_epilogues(cuda):
     hn_ref = (1 - zf) * hxf[:, :Ch] + zf * qr
     assert _rel(_from_pm(q, B, H, W), qr) < 1e-2
     assert _rel(_from_pm(hn, B, H, W), hn_ref) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", ["20", "21", "22"])
+@pytest.mark.parametrize("segs,cout,kh,kw,hw", [
+    ([(256, 256)], 192, 3, 3, (46, 62)),
+    ([(128, 128), (128, 128), (128, 128)], 256, 1, 5, (46, 62)),
+    ([(128, 128), (128, 128), (128, 128)], 128, 5, 1, (46, 62)),
+    ([(128, 128)], 512, 3, 3, (23, 31)),
+    ([(64, 64)], 128, 3, 3, (17, 21)),
+])
+def test_fwd_halo_strip_full_size(cuda, monkeypatch, cfg, segs, cout, kh, kw, hw):
+    """v5 (halo-strip) forward at RAFT sizes vs an fp32 conv2d, every tile config."""
+    monkeypatch.setenv("RAFT_CONV_FWD_CFG", cfg)
+    torch.manual_seed(4)
+    B, (H, W) = 8, hw
+    P = B * H * W
+    cin = sum(r for r, _ in segs)
+    srcs = [torch.randn(P, pd, device=cuda).bfloat16() for _, pd in segs]
+    w = torch.randn(cout, cin, kh, kw, device=cuda) / (cin * kh * kw) ** 0.5
+    bias = torch.randn(cout, device=cuda)
+    out = torch.full((P, cout), float("nan"), device=cuda, dtype=torch.bfloat16)
+    C.conv_fwd(srcs, C.pack_fwd(w, segs), C.geom(B, H, W, kh, kw, kh // 2, kw // 2), cout, out, bias=bias, act=1)
+    x = torch.cat([_from_pm(s, B, H, W) for s in srcs], dim=1)
+    ref = F.relu(F.conv2d(x, w.bfloat16().float(), bias, padding=(kh // 2, kw // 2)))
+    assert _rel(_from_pm(out, B, H, W), ref) < 1e-2
