@@ -1537,14 +1537,18 @@ __global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
     if (p < a.P) {
       const int rem = (int)(p % HW);
       const int py = rem / a.W, px = rem - (rem / a.W) * a.W;
+      // no break/continue: the tap loop must fully unroll so that w[][t][] stays in
+      // registers (a data-dependent exit demotes w to scratch -- 6x slower); out-of-range
+      // taps load zeros under the exec mask instead
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        if (t >= ntaps) break;
         const int ky = t / a.KW, kx = t - (t / a.KW) * a.KW;
         const int y = py + ky - a.PH, x = px + kx - a.PW;
-        if ((unsigned)y >= (unsigned)a.H || (unsigned)x >= (unsigned)a.W) continue;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(
-            a.src[0].ptr + (p + (long)(ky - a.PH) * a.W + (kx - a.PW)) * stride + cl * 8);
+        const bool ok = t < ntaps && (unsigned)y < (unsigned)a.H && (unsigned)x < (unsigned)a.W;
+        bf16x8 v{};
+        if (ok)
+          v = *reinterpret_cast<const bf16x8*>(a.src[0].ptr + (p + (long)(ky - a.PH) * a.W + (kx - a.PW)) * stride +
+                                               cl * 8);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const float xv = static_cast<float>(v[q]);
