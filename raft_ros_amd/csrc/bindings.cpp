@@ -51,6 +51,20 @@ hipError_t launch_convex_up_fwd(const float* flow, const void* mask, int m_dtype
 hipError_t launch_convex_up_bwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
                                 long msH, long msW, const float* gout, void* dmask, float* part,
                                 float* dflow, int B, int H, int W, hipStream_t s);
+constexpr int kMaxPreds = 32;
+struct SeqPreds {
+  const float* p[kMaxPreds];
+};
+struct SeqGrads {
+  float* g[kMaxPreds];
+};
+int seq_loss_num_blocks(long P);
+hipError_t launch_seq_loss_fwd(const SeqPreds& preds, int n, const float* gt, const float* valid,
+                               float gamma, float max_flow, long B, long HW, float* partial,
+                               hipStream_t s);
+hipError_t launch_seq_loss_bwd(const SeqPreds& preds, const SeqGrads& grads, int n, const float* gt,
+                               const float* valid, const float* dloss, float gamma, float max_flow,
+                               long B, long HW, hipStream_t s);
 hipError_t launch_local_corr_fwd(const void* f1, const void* f2, int dtype, const float* coords,
                                  float* out, int B, int H1, int W1, int H2, int W2, int C, int r,
                                  float scale, hipStream_t s);
@@ -297,6 +311,63 @@ std::tuple<at::Tensor, at::Tensor> convex_upsample_backward(const at::Tensor& fl
                               g.data_ptr<float>(), dmask.data_ptr(), part.data_ptr<float>(),
                               dflow.data_ptr<float>(), B, H, W, cur_stream()));
   return {dflow, dmask};
+}
+
+// ---------------------------------------------------------------- fused sequence loss
+SeqPreds check_seq_inputs(const std::vector<at::Tensor>& preds, const at::Tensor& gt,
+                          const at::Tensor& valid) {
+  TORCH_CHECK(!preds.empty() && preds.size() <= (size_t)kMaxPreds,
+              "raft_amd::seq_loss: 1..32 predictions supported");
+  check_gpu(gt, "flow_gt");
+  check_gpu(valid, "valid");
+  TORCH_CHECK(gt.scalar_type() == at::kFloat && gt.is_contiguous() && gt.dim() == 4 && gt.size(1) == 2,
+              "raft_amd::seq_loss: flow_gt must be contiguous fp32 (B, 2, H, W)");
+  TORCH_CHECK(valid.scalar_type() == at::kFloat && valid.is_contiguous() && valid.dim() == 3 &&
+                  valid.size(0) == gt.size(0) && valid.size(1) == gt.size(2) &&
+                  valid.size(2) == gt.size(3),
+              "raft_amd::seq_loss: valid must be contiguous fp32 (B, H, W)");
+  SeqPreds d{};
+  for (size_t i = 0; i < preds.size(); ++i) {
+    const auto& p = preds[i];
+    check_gpu(p, "flow prediction");
+    TORCH_CHECK(p.scalar_type() == at::kFloat && p.is_contiguous() && p.sizes() == gt.sizes(),
+                "raft_amd::seq_loss: predictions must be contiguous fp32 shaped like flow_gt");
+    d.p[i] = p.data_ptr<float>();
+  }
+  return d;
+}
+
+// -> (6,) fp32: {sum_i w_i * sum(vmask*|p_i-gt|), sum epe, #<1px, #<3px, #<5px, #valid}
+at::Tensor seq_loss(const std::vector<at::Tensor>& preds, const at::Tensor& gt, const at::Tensor& valid,
+                    double gamma, double max_flow) {
+  SeqPreds d = check_seq_inputs(preds, gt, valid);
+  const c10::DeviceGuard guard(gt.device());
+  const long B = gt.size(0), HW = gt.size(2) * gt.size(3);
+  auto partial = at::empty({seq_loss_num_blocks(B * HW), 6}, gt.options());
+  HIP_OK(launch_seq_loss_fwd(d, (int)preds.size(), gt.data_ptr<float>(), valid.data_ptr<float>(),
+                             (float)gamma, (float)max_flow, B, HW, partial.data_ptr<float>(),
+                             cur_stream()));
+  return partial.sum(0);
+}
+
+std::vector<at::Tensor> seq_loss_backward(const std::vector<at::Tensor>& preds, const at::Tensor& gt,
+                                          const at::Tensor& valid, const at::Tensor& dloss, double gamma,
+                                          double max_flow) {
+  SeqPreds d = check_seq_inputs(preds, gt, valid);
+  TORCH_CHECK(dloss.is_cuda() && dloss.scalar_type() == at::kFloat && dloss.numel() == 1,
+              "raft_amd::seq_loss_backward: dloss must be a one-element fp32 GPU tensor");
+  const c10::DeviceGuard guard(gt.device());
+  const long B = gt.size(0), HW = gt.size(2) * gt.size(3);
+  auto dl = dloss.contiguous();
+  std::vector<at::Tensor> grads;
+  SeqGrads g{};
+  for (size_t i = 0; i < preds.size(); ++i) {
+    grads.push_back(at::empty_like(gt));
+    g.g[i] = grads.back().data_ptr<float>();
+  }
+  HIP_OK(launch_seq_loss_bwd(d, g, (int)preds.size(), gt.data_ptr<float>(), valid.data_ptr<float>(),
+                             dl.data_ptr<float>(), (float)gamma, (float)max_flow, B, HW, cur_stream()));
+  return grads;
 }
 
 // ---------------------------------------------------------------- local (alternate) correlation
@@ -677,6 +748,10 @@ TORCH_LIBRARY(raft_amd, m) {
       "Tensor)");
   m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");
   m.def("convex_upsample_backward(Tensor flow, Tensor mask, Tensor grad) -> (Tensor, Tensor)");
+  m.def("seq_loss(Tensor[] preds, Tensor gt, Tensor valid, float gamma, float max_flow) -> Tensor");
+  m.def(
+      "seq_loss_backward(Tensor[] preds, Tensor gt, Tensor valid, Tensor dloss, float gamma, float "
+      "max_flow) -> Tensor[]");
   m.def("local_corr(Tensor fmap1, Tensor fmap2, Tensor coords, int radius, float scale) -> Tensor");
   m.def(
       "local_corr_backward(Tensor fmap1, Tensor fmap2, Tensor coords, Tensor grad, int radius, float "
@@ -691,6 +766,8 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("pyramid_grad_combine", &raft_amd::pyramid_grad_combine);
   m.impl("convex_upsample", &raft_amd::convex_upsample);
   m.impl("convex_upsample_backward", &raft_amd::convex_upsample_backward);
+  m.impl("seq_loss", &raft_amd::seq_loss);
+  m.impl("seq_loss_backward", &raft_amd::seq_loss_backward);
   m.impl("local_corr", &raft_amd::local_corr);
   m.impl("local_corr_backward", &raft_amd::local_corr_backward);
   m.impl("conv_fwd", &raft_amd::conv_fwd);

@@ -12,11 +12,45 @@ from typing import Dict, List
 
 import torch
 
+from ..ops._ext import ops, use_native
+
 MAX_FLOW = 400.0
+
+
+class _FusedSeqLoss(torch.autograd.Function):
+    """One HIP pass forward (loss + metric sums), one pass backward (all n
+    prediction gradients); raft_ros_amd/csrc/seq_loss.hip."""
+
+    @staticmethod
+    def forward(ctx, flow_gt, valid, gamma, max_flow, *preds):
+        sums = ops().seq_loss(list(preds), flow_gt, valid, gamma, max_flow)
+        ctx.save_for_backward(flow_gt, valid, *preds)
+        ctx.gamma, ctx.max_flow = gamma, max_flow
+        ctx.mark_non_differentiable(sums)
+        loss = sums[0] / float(2 * valid.numel())
+        return loss, sums
+
+    @staticmethod
+    def backward(ctx, gloss, _gsums):
+        flow_gt, valid, *preds = ctx.saved_tensors
+        grads = ops().seq_loss_backward(preds, flow_gt, valid, gloss.float().reshape(1), ctx.gamma,
+                                        ctx.max_flow)
+        return (None, None, None, None, *grads)
+
+
+def _fused_ok(flow_preds, flow_gt) -> bool:
+    return (use_native(flow_gt) and 1 <= len(flow_preds) <= 32 and flow_gt.dtype == torch.float32
+            and all(p.dtype == torch.float32 and p.shape == flow_gt.shape for p in flow_preds))
 
 
 def sequence_loss(flow_preds: List[torch.Tensor], flow_gt: torch.Tensor, valid: torch.Tensor,
                   gamma: float = 0.8, max_flow: float = MAX_FLOW):
+    if _fused_ok(flow_preds, flow_gt):
+        preds = [p.contiguous() for p in flow_preds]
+        loss, s = _FusedSeqLoss.apply(flow_gt.contiguous(), valid.float().contiguous(), float(gamma),
+                                      float(max_flow), *preds)
+        cnt = s[5].clamp_min(1.0)
+        return loss, {"epe": s[1] / cnt, "1px": s[2] / cnt, "3px": s[3] / cnt, "5px": s[4] / cnt}
     n = len(flow_preds)
     mag = torch.sum(flow_gt ** 2, dim=1).sqrt()
     valid = (valid >= 0.5) & (mag < max_flow)
