@@ -15,7 +15,14 @@ PyTorch baseline of the reference algorithm measured on the same MI355X
 
     python bench.py                      # 1 GPU, defaults
     python bench.py --impl reference     # the reference's eager op sequence (baseline)
+    python bench.py --gpus 8             # spawns 8 rank processes itself (no torchrun needed)
     torchrun --nproc-per-node 8 bench.py --gpus 8
+
+Launch contract: under torchrun (WORLD_SIZE set) every process is one rank and
+``--gpus`` must equal WORLD_SIZE.  Without WORLD_SIZE and ``--gpus N > 1`` the
+parent process starts N rank processes with ``torch.multiprocessing`` (spawn)
+BEFORE touching the GPU, and exits with the first non-zero rank exit code.
+``n_gpus`` in the JSON is always the real world size.
 """
 from __future__ import annotations
 
@@ -55,19 +62,79 @@ def parse():
                     help="replay the step as captured HIP graph(s) (train: fwd+loss+bwd+clip+AdamW, grads "
                          "all-reduced between two graphs when N>1; infer: the forward). Default: on for infer; "
                          "off for train, where the step is GPU-bound (graph 223 vs eager 224 pairs/s on MI355X)")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: gloo-backend plumbing check of the launch path only (tests), never a measurement")
     return ap.parse_args()
+
+
+def _sync(device):
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+def _rank_entry(rank, nprocs, port, argv):
+    """Child process of ``python bench.py --gpus N`` (no torchrun): one rank per GPU."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(nprocs),
+                      LOCAL_WORLD_SIZE=str(nprocs), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.argv = [sys.argv[0]] + list(argv)
+    run(parse())
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # spawn the ranks before anything initialises HIP in this process
+        # (torch.cuda.device_count() does not initialise the runtime)
+        ndev = torch.cuda.device_count() if args.device == "cuda" else args.gpus
+        if ndev < args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but only {ndev} GPU(s) visible")
+        import torch.multiprocessing as mp
+
+        from raft_ros_amd.parallel.ddp import free_port
+
+        mp.start_processes(_rank_entry, args=(args.gpus, free_port(), sys.argv[1:]), nprocs=args.gpus,
+                           start_method="spawn")
+        return 0
+    return run(args)
+
+
+def _allreduce_ms(model, device, world, reps: int = 10) -> float:
+    """Time of one all-reduce of a gradient-sized fp32 buffer (what DDP moves per step)."""
+    if world <= 1:
+        return 0.0
+    n = sum(p.numel() for p in model.parameters() if p.requires_grad)
+    buf = torch.ones(n, device=device, dtype=torch.float32)
+    for _ in range(3):
+        dist.all_reduce(buf)
+    _sync(device)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_reduce(buf)
+    _sync(device)
+    t = torch.tensor([(time.perf_counter() - t0) / reps], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return 1000.0 * float(t.item())
+
+
+def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
-    if distributed:
-        dist.init_process_group("nccl", device_id=device)
+    if "WORLD_SIZE" in os.environ and args.gpus != world and rank == 0:
+        print(f"bench.py: warning: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the real world size",
+              file=sys.stderr, flush=True)
+    if args.device == "cuda":
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+        if distributed:
+            dist.init_process_group("nccl", device_id=device)
+    else:
+        device = torch.device("cpu")
+        torch.set_num_threads(max(1, (os.cpu_count() or 2) // max(world, 1)))
+        if distributed:
+            dist.init_process_group("gloo")
 
     from raft_ros_amd.data.synthetic import synthetic_batch
     from raft_ros_amd.models import RAFT
@@ -89,12 +156,13 @@ def main():
     oargs = Namespace(lr=args.lr, wdecay=1e-4, epsilon=1e-8, num_steps=100000)
     train_graph = bool(args.graph) and args.mode == "train" and args.impl == "native" and args.amp_dtype == "bf16"
     if distributed and not train_graph:
-        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=args.bucket_mb,
+        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local] if device.type == "cuda" else None,
+                                                        bucket_cap_mb=args.bucket_mb,
                                                         gradient_as_bucket_view=True, static_graph=True)
     else:
         ddp = model
     optimizer, scheduler = fetch_optimizer(oargs, model, capturable=train_graph)
-    scaler = torch.amp.GradScaler("cuda", enabled=args.amp_dtype == "fp16")
+    scaler = torch.amp.GradScaler("cuda", enabled=args.amp_dtype == "fp16" and device.type == "cuda")
 
     H, W = args.image_size
     pool = [synthetic_batch(args.batch, H, W, seed=rank * 97 + i, device=device) for i in range(2 if H * W > 1e6 else 4)]
@@ -141,22 +209,23 @@ def main():
     step = step or train_step
     for i in range(args.warmup):
         loss, metrics = step(i)
-    torch.cuda.synchronize()
+    _sync(device)
     if distributed:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(device)
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss, metrics = step(args.warmup + i)
-    torch.cuda.synchronize()
+    _sync(device)
     if distributed:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(device)
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], device=device, dtype=torch.float64)
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    ar_ms = _allreduce_ms(model, device, world)
     pairs = args.batch * world * args.steps
     value = pairs / elapsed
     if rank == 0:
@@ -174,7 +243,7 @@ def main():
                             if BASELINE_PAIRS_PER_SEC and args.impl == "native" and args.mode == "train"
                             and not args.small and not args.alternate_corr and (H, W) == (368, 496)
                             and args.iters == 12 and args.batch == 8 else None),
-            "dtype": args.amp_dtype,
+            "dtype": args.amp_dtype if device.type == "cuda" else "fp32",
             "data": "synthetic (textured pairs warped by known smooth flow; random-init weights)",
             "config": {
                 "model": "RAFT-small" if args.small else "RAFT-base",
@@ -191,11 +260,14 @@ def main():
             },
             "final_loss": round(float(loss.item()), 4),
             "epe_synthetic": round(float(metrics["epe"].item()), 4),
-            "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2),
+            "peak_mem_gb": (round(torch.cuda.max_memory_allocated(device) / 2**30, 2)
+                            if device.type == "cuda" else None),
+            "allreduce_ms": round(ar_ms, 3),
         }
         print(json.dumps(out), flush=True)
     if distributed:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":

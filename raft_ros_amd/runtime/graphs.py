@@ -13,7 +13,9 @@ Usage::
     flow_low, flow_up = runner(image1, image2)      # same as model(..., test_mode=True)
 
 Outputs are views of the graph's static buffers: they are overwritten by the
-next call with the same shape (``clone()`` them to keep them).  Weight updates
+next call with the same shape (``clone()`` them to keep them).  Every shape has
+its own memory pool, so replaying one shape never clobbers the outputs another
+shape returned earlier.  Weight updates
 in place (``load_state_dict``, optimizer steps) are picked up by the replay;
 call :meth:`reset` after replacing parameter tensors.  On CPU (or with
 ``enabled=False``) the runner simply calls the model.
@@ -39,11 +41,9 @@ class GraphedRAFT:
         self.enabled = enabled
         self.warmup = warmup
         self._graphs: "OrderedDict[tuple, _Entry]" = OrderedDict()
-        self._pool = None
 
     def reset(self) -> None:
         self._graphs.clear()
-        self._pool = None
 
     @property
     def num_graphs(self) -> int:
@@ -85,9 +85,9 @@ class GraphedRAFT:
             for _ in range(self.warmup):  # allocator / lazy-init warm-up outside the capture
                 self._eager(e.in1, e.in2, e.init)
         torch.cuda.current_stream(image1.device).wait_stream(side)
-        if self._pool is None:
-            self._pool = torch.cuda.graph_pool_handle()
+        # a private pool per shape: a later capture must not place its temporaries in
+        # memory that holds the outputs of an earlier shape's graph
         e.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(e.graph, pool=self._pool):
+        with torch.cuda.graph(e.graph, pool=torch.cuda.graph_pool_handle()):
             e.out = self._eager(e.in1, e.in2, e.init)
         return e

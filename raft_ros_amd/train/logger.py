@@ -5,7 +5,9 @@ Keeps the reference's console format -- every ``SUM_FREQ`` steps
 by name -- and adds a JSONL log (one record per print and per validation) and
 pairs/s throughput.  TensorBoard is used when ``torch.utils.tensorboard`` is
 importable (it is optional; the package is not installed in this image).
-Only rank 0 writes.
+Only rank 0 writes, but with several ranks the window averages are all-reduced
+first (``reduce_fn``, a collective every rank enters at the same step), so the
+printed metrics are over the whole global batch, not rank 0's shard.
 """
 from __future__ import annotations
 
@@ -19,7 +21,7 @@ SUM_FREQ = 100
 
 class Logger:
     def __init__(self, model=None, scheduler=None, log_dir: str = "runs", enabled: bool = True,
-                 sum_freq: int = SUM_FREQ, pairs_per_step: int = 0):
+                 sum_freq: int = SUM_FREQ, pairs_per_step: int = 0, reduce_fn=None):
         self.model = model
         self.scheduler = scheduler
         self.total_steps = 0
@@ -27,6 +29,7 @@ class Logger:
         self.enabled = enabled
         self.sum_freq = sum_freq
         self.pairs_per_step = pairs_per_step
+        self.reduce_fn = reduce_fn  # {name: value} -> {name: mean over ranks}; called on every rank
         self.writer = None
         self.log_dir = log_dir
         self.jsonl = None
@@ -50,7 +53,10 @@ class Logger:
 
     def _print_training_status(self):
         keys = sorted(self.running_loss)
-        vals = [float(self.running_loss[k]) / self.sum_freq for k in keys]
+        means = {k: float(self.running_loss[k]) / self.sum_freq for k in keys}
+        if self.reduce_fn is not None:
+            means = self.reduce_fn(means)
+        vals = [means[k] for k in keys]
         now = time.perf_counter()
         rate = self.pairs_per_step * self.sum_freq / max(now - self._t, 1e-9) if self.pairs_per_step else 0.0
         self._t = now

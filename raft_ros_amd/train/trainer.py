@@ -76,7 +76,8 @@ def train(args: Namespace) -> str:
     scaler = torch.amp.GradScaler("cuda", enabled=use_scaler)
     per_rank = max(1, args.batch_size // info.world_size)
     logger = Logger(model, scheduler, log_dir=os.path.join(args.log_dir, args.name), enabled=info.is_main,
-                    pairs_per_step=per_rank * info.world_size)
+                    pairs_per_step=per_rank * info.world_size,
+                    reduce_fn=(lambda m: ddp.all_reduce_mean(m, info)) if info.distributed else None)
 
     total_steps = 0
     if getattr(args, "resume", False) and args.restore_ckpt is not None:

@@ -61,6 +61,19 @@ def state_path(weights_path: str) -> str:
     return root + ".state.pt"
 
 
+def _py_rng_state():
+    """``random.getstate()`` as tensors/ints only, so ``torch.load(weights_only=True)`` can read it."""
+    version, internal, gauss = random.getstate()
+    return {"version": int(version), "internal": torch.tensor(internal, dtype=torch.int64),
+            "gauss": None if gauss is None else float(gauss)}
+
+
+def _set_py_rng_state(st) -> None:
+    if not isinstance(st, dict):  # older sidecars stored an unusable repr string
+        return
+    random.setstate((st["version"], tuple(int(x) for x in st["internal"].tolist()), st["gauss"]))
+
+
 def save_state(path: str, optimizer, scheduler, scaler, step: int) -> None:
     np_state = np.random.get_state()
     state = {
@@ -72,7 +85,7 @@ def save_state(path: str, optimizer, scheduler, scaler, step: int) -> None:
         "cuda_rng": torch.cuda.get_rng_state_all() if torch.cuda.is_available() else [],
         "numpy_rng": {"name": np_state[0], "keys": torch.from_numpy(np_state[1].astype(np.int64)),
                       "pos": int(np_state[2]), "has_gauss": int(np_state[3]), "cached": float(np_state[4])},
-        "python_rng": repr(random.getstate()),
+        "python_rng": _py_rng_state(),
     }
     tmp = path + ".tmp"
     torch.save(state, tmp)
@@ -94,4 +107,5 @@ def load_state(path: str, optimizer, scheduler, scaler, map_location="cpu") -> O
     n = st.get("numpy_rng")
     if n:
         np.random.set_state((n["name"], n["keys"].numpy().astype(np.uint32), n["pos"], n["has_gauss"], n["cached"]))
+    _set_py_rng_state(st.get("python_rng"))
     return int(st["step"])

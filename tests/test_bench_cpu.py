@@ -1,0 +1,42 @@
+"""bench.py launch contract on CPU (gloo): ``--gpus N`` without torchrun spawns N ranks
+itself and reports the real world size; the JSON line carries every required key."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config", "allreduce_ms"}
+
+
+def _bench(*extra, env=None):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--small", "--image_size", "128",
+           "128", "--batch", "1", "--steps", "1", "--warmup", "0", "--iters", "2", *extra]
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=500, cwd=ROOT, env=e)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 only
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(600)
+def test_bench_spawns_ranks_for_gpus_flag():
+    r = _bench("--gpus", "2")
+    assert KEYS <= set(r), set(KEYS) - set(r)
+    assert r["n_gpus"] == 2
+    assert r["config"]["parallelism"] == "dp2"
+    assert r["config"]["global_batch"] == 2
+    assert r["allreduce_ms"] > 0
+
+
+@pytest.mark.timeout(600)
+def test_bench_single_process_default():
+    r = _bench()
+    assert r["n_gpus"] == 1 and r["allreduce_ms"] == 0.0
+    assert r["steps"] == 1 and r["warmup"] == 0

@@ -100,3 +100,37 @@ def test_train_cli_runs_on_cpu(tmp_path, monkeypatch):
                         "--restore_ckpt", path, "--resume"])
     assert os.path.exists(path2)
     assert os.path.exists(os.path.join("runs", "t", "metrics.jsonl"))
+
+
+def test_resume_restores_python_and_numpy_rng(tmp_path):
+    import random
+
+    import numpy as np
+
+    m = RAFT(Namespace(small=True))
+    opt, sch = fetch_optimizer(Namespace(lr=1e-4, wdecay=1e-5, epsilon=1e-8, num_steps=10), m)
+    random.seed(123)
+    np.random.seed(321)
+    p = str(tmp_path / "s.state.pt")
+    checkpoint.save_state(p, opt, sch, None, 5)
+    expect = (random.random(), float(np.random.rand()))
+    random.seed(999)
+    np.random.seed(999)
+    assert checkpoint.load_state(p, opt, sch, None) == 5
+    assert (random.random(), float(np.random.rand())) == expect
+
+
+def test_logger_reduces_metrics_before_printing(tmp_path, capsys):
+    from raft_ros_amd.train.logger import Logger
+
+    calls = []
+
+    def reduce_fn(m):
+        calls.append(dict(m))
+        return {k: 2 * v for k, v in m.items()}
+
+    lg = Logger(log_dir=str(tmp_path), sum_freq=2, reduce_fn=reduce_fn)
+    lg.push({"epe": torch.tensor(1.0)})
+    out = capsys.readouterr().out
+    assert calls == [{"epe": 0.5}] and "1.0000" in out  # window of 2 -> mean 0.5, reduced x2
+    lg.close()
