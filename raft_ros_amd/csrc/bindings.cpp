@@ -42,15 +42,18 @@ hipError_t launch_gru_bwd_b(float* drh, long sd, const void* r, long sr, const v
                             hipStream_t s);
 hipError_t launch_masked_cast(const float* src, long ss, const void* mask, long sm, void* out, long so,
                               long P, int C, int Cvalid, hipStream_t s);
-hipError_t launch_pack_flow(const float* flow, void* flow8, void* motion, long smo, int B, int HW,
-                            hipStream_t s);
+hipError_t launch_pack_flow(const float* flow, void* flow8, void* motion, long smo, int B, int HW, int W,
+                            int from_coords, hipStream_t s);
+hipError_t launch_apply_delta(const float* coords1, const float* delta, long sd, float* coords_out,
+                              float* flow_out, int B, int HW, int W, hipStream_t s);
 hipError_t launch_pyramid_grad_combine(const PyrDesc& dpyr, void* dC, void* dCt, int B, int H,
                                        int W, int ldp, float alpha, hipStream_t s);
 hipError_t launch_convex_up_fwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
                                 long msH, long msW, float* out, int B, int H, int W, hipStream_t s);
 hipError_t launch_convex_up_bwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
-                                long msH, long msW, const float* gout, void* dmask, float* part,
-                                float* dflow, int B, int H, int W, hipStream_t s);
+                                long msH, long msW, const float* gout, void* dmask, long dsN, long dsC,
+                                long dsH, long dsW, float* part, float* dflow, void* rows, int rows_ld, int B,
+                                int H, int W, hipStream_t s);
 constexpr int kMaxPreds = 32;
 struct SeqPreds {
   const float* p[kMaxPreds];
@@ -85,7 +88,7 @@ struct ConvSrc {
   const void* ptr;
   long stride;
   int C;
-  int pad_;
+  int period;
 };
 struct ConvFwdArgs {
   ConvSrc src[3];
@@ -108,6 +111,7 @@ struct ConvFwdArgs {
   long z_stride;
   void* out2;
   long out2_stride;
+  int cfg;
 };
 struct ConvWgradArgs {
   ConvSrc src[3];
@@ -119,12 +123,36 @@ struct ConvWgradArgs {
   int N;
   long P;
   long pix_per_split;
-  float* dw;
-  float* db;
-  int xcd_g;  // layout must match conv_igemm.hip
+  float* slab;
+  float* dbslab;
+  int Npad;
+  int xcd_g;  // layouts must match conv_igemm.hip
+};
+struct WgradPlan {
+  int BM, BN, tilesM, tilesN, nsplit, Npad, xcd_g;
+  long pix_per_split;
+  int kind;
+};
+struct ConvParamDesc {
+  float* w[2];
+  long ws[2][4];
+  float* b[2];
+  int rows[2];
+  int nseg;
+  int seg_real[3], seg_pad[3];
+  int Cin, Cin_pad, KH, KW;
+  float scale;
 };
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s);
-hipError_t launch_conv_wgrad(ConvWgradArgs a, hipStream_t s);
+bool wgrad_supported(const ConvWgradArgs& a);
+WgradPlan plan_conv_wgrad(const ConvWgradArgs& a);
+hipError_t launch_conv_wgrad(ConvWgradArgs a, const WgradPlan& pl, hipStream_t s);
+hipError_t launch_pack_conv_weights(const ConvParamDesc& d, int N, void* wf, int Kf, void* wd, int Kd, int Cout_pad,
+                                    float* bias, hipStream_t s);
+hipError_t launch_wgrad_reduce_params(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, int ndb,
+                                      const ConvParamDesc& d, int N, int accumulate, hipStream_t s);
+hipError_t launch_wgrad_reduce_packed(const float* slab, int nsplit, int Npad, int Kpad, int K, const float* dbslab,
+                                      int ndb, float* dw, long ldw, float* db, int N, int accumulate, hipStream_t s);
 
 int instance_norm_chunks(int HW);
 hipError_t launch_instance_norm_fwd(int dtype, const void* x, void* y, float* stats, float* part, int N, int HW,
@@ -142,6 +170,7 @@ namespace {
   } while (0)
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+void pm_any(const at::Tensor& t, const char* name, long P, at::ScalarType dt);
 
 int dtype_code(at::ScalarType t) {
   switch (t) {
@@ -308,9 +337,33 @@ std::tuple<at::Tensor, at::Tensor> convex_upsample_backward(const at::Tensor& fl
   auto dflow = at::empty_like(flow);
   HIP_OK(launch_convex_up_bwd(flow.data_ptr<float>(), mask.data_ptr(), dtype_code(mask.scalar_type()),
                               mask.stride(0), mask.stride(1), mask.stride(2), mask.stride(3),
-                              g.data_ptr<float>(), dmask.data_ptr(), part.data_ptr<float>(),
-                              dflow.data_ptr<float>(), B, H, W, cur_stream()));
+                              g.data_ptr<float>(), dmask.data_ptr(), dmask.stride(0), dmask.stride(1),
+                              dmask.stride(2), dmask.stride(3), part.data_ptr<float>(), dflow.data_ptr<float>(),
+                              nullptr, 0, B, H, W, cur_stream()));
   return {dflow, dmask};
+}
+
+// Fused update block: dmask into a caller buffer (any strides, mask dtype) and the low-res
+// flow gradient as bf16 rows [du, dv, 0..] of a (P, ld) buffer (the flow head's dY).
+void convex_upsample_backward_into(const at::Tensor& flow, const at::Tensor& mask, const at::Tensor& grad,
+                                   const at::Tensor& dmask, const at::Tensor& rows) {
+  check_up_inputs(flow, mask);
+  const long B = flow.size(0), H = flow.size(2), W = flow.size(3);
+  TORCH_CHECK(grad.dim() == 4 && grad.size(0) == B && grad.size(1) == 2 && grad.size(2) == 8 * H &&
+                  grad.size(3) == 8 * W,
+              "raft_amd::convex_upsample_backward_into: bad grad shape");
+  TORCH_CHECK(dmask.sizes() == mask.sizes() && dmask.scalar_type() == mask.scalar_type(),
+              "raft_amd::convex_upsample_backward_into: dmask must match mask");
+  pm_any(rows, "rows", B * H * W, at::kBFloat16);
+  TORCH_CHECK(rows.size(1) >= 2, "raft_amd::convex_upsample_backward_into: rows need >= 2 channels");
+  auto g = grad.to(at::kFloat).contiguous();
+  const c10::DeviceGuard guard(flow.device());
+  auto part = at::empty({B, 18, H, W}, flow.options());
+  HIP_OK(launch_convex_up_bwd(flow.data_ptr<float>(), mask.data_ptr(), dtype_code(mask.scalar_type()),
+                              mask.stride(0), mask.stride(1), mask.stride(2), mask.stride(3),
+                              g.data_ptr<float>(), dmask.data_ptr(), dmask.stride(0), dmask.stride(1),
+                              dmask.stride(2), dmask.stride(3), part.data_ptr<float>(), nullptr, rows.data_ptr(),
+                              (int)rows.stride(0), B, H, W, cur_stream()));
 }
 
 // ---------------------------------------------------------------- fused sequence loss
@@ -504,15 +557,20 @@ void check_pm(const at::Tensor& t, const char* name, long P) {
               "raft_amd conv: ", name, " needs 16-byte aligned pixel rows");
 }
 
-int fill_srcs(at::TensorList srcs, long P, ConvSrc* out) {
+// Sources of a conv: (rows, C) pixel-major views.  rows == P, or (weight gradient only) a
+// divisor of P: a periodic source whose row p % rows is read for pixel p.
+int fill_srcs(at::TensorList srcs, long P, ConvSrc* out, bool allow_period) {
   TORCH_CHECK(srcs.size() >= 1 && srcs.size() <= 3, "raft_amd conv: 1..3 input sources");
   int Cin = 0;
   for (int i = 0; i < 3; ++i) out[i] = ConvSrc{nullptr, 0, 0, 0};
   for (size_t i = 0; i < srcs.size(); ++i) {
-    check_pm(srcs[i], "src", P);
+    const long rows = srcs[i].size(0);
+    const bool periodic = allow_period && rows != P && rows > 0 && P % rows == 0;
+    check_pm(srcs[i], "src", periodic ? rows : P);
     TORCH_CHECK(srcs[i].scalar_type() == at::kBFloat16, "raft_amd conv: sources must be bf16");
     TORCH_CHECK(srcs[i].size(1) % 8 == 0, "raft_amd conv: source channels must be multiples of 8");
-    out[i] = ConvSrc{srcs[i].data_ptr(), srcs[i].stride(0), static_cast<int>(srcs[i].size(1)), 0};
+    out[i] = ConvSrc{srcs[i].data_ptr(), srcs[i].stride(0), static_cast<int>(srcs[i].size(1)),
+                     periodic ? static_cast<int>(rows) : 0};
     Cin += static_cast<int>(srcs[i].size(1));
   }
   return Cin;
@@ -521,14 +579,15 @@ int fill_srcs(at::TensorList srcs, long P, ConvSrc* out) {
 void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, int64_t N, const c10::optional<at::Tensor>& bias,
               int64_t epi, int64_t act, double alpha, const at::Tensor& out, int64_t acc_c0,
               const c10::optional<at::Tensor>& mask, const c10::optional<at::Tensor>& h,
-              const c10::optional<at::Tensor>& z, const c10::optional<at::Tensor>& out2) {
+              const c10::optional<at::Tensor>& z, const c10::optional<at::Tensor>& out2, int64_t cfg) {
   TORCH_CHECK(geom.size() == 7, "raft_amd conv_fwd: geom = (B, H, W, KH, KW, PH, PW)");
   ConvFwdArgs a{};
   a.B = geom[0]; a.H = geom[1]; a.W = geom[2]; a.KH = geom[3]; a.KW = geom[4]; a.PH = geom[5]; a.PW = geom[6];
   a.P = (long)a.B * a.H * a.W;
   a.nsrc = static_cast<int>(srcs.size());
-  a.Cin = fill_srcs(srcs, a.P, a.src);
+  a.Cin = fill_srcs(srcs, a.P, a.src, false);
   a.K = a.KH * a.KW * a.Cin;
+  a.cfg = static_cast<int>(cfg);
   check_gpu(wt, "wt");
   TORCH_CHECK(wt.scalar_type() == at::kBFloat16 && wt.dim() == 2 && wt.is_contiguous() && wt.size(0) >= N &&
                   wt.size(1) >= a.K && wt.size(1) % 64 == 0,
@@ -578,34 +637,142 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
   HIP_OK(launch_conv_fwd(a, cur_stream()));
 }
 
-void conv_wgrad(at::TensorList srcs, const at::Tensor& dy, at::IntArrayRef geom, int64_t N, const at::Tensor& dw,
-                const c10::optional<at::Tensor>& db) {
+ConvWgradArgs wgrad_args(at::TensorList srcs, const at::Tensor& dy, at::IntArrayRef geom, int64_t N) {
   TORCH_CHECK(geom.size() == 7, "raft_amd conv_wgrad: geom = (B, H, W, KH, KW, PH, PW)");
   ConvWgradArgs a{};
   a.B = geom[0]; a.H = geom[1]; a.W = geom[2]; a.KH = geom[3]; a.KW = geom[4]; a.PH = geom[5]; a.PW = geom[6];
   a.P = (long)a.B * a.H * a.W;
   a.nsrc = static_cast<int>(srcs.size());
-  a.Cin = fill_srcs(srcs, a.P, a.src);
+  a.Cin = fill_srcs(srcs, a.P, a.src, true);
   a.K = a.KH * a.KW * a.Cin;
+  a.Kpad = (a.K + 63) / 64 * 64;
   check_pm(dy, "dy", a.P);
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16, "raft_amd conv_wgrad: dy must be bf16");
   TORCH_CHECK(dy.size(1) >= (N + 7) / 8 * 8, "raft_amd conv_wgrad: dy must hold N channels (rounded to 8)");
   a.dy = dy.data_ptr();
   a.dy_stride = dy.stride(0);
   a.N = static_cast<int>(N);
+  TORCH_CHECK(wgrad_supported(a), "raft_amd conv_wgrad: unsupported source layout (multi-source convs need "
+              "128-channel segments; every operand must stay below 2 GiB)");
+  return a;
+}
+
+// Runs the split weight-gradient GEMM into fresh partial slabs; returns (slab, dbslab, plan).
+std::tuple<at::Tensor, at::Tensor, WgradPlan> run_wgrad(ConvWgradArgs& a, bool with_bias, const at::Tensor& like) {
+  const WgradPlan pl = plan_conv_wgrad(a);
+  auto opts = like.options().dtype(at::kFloat);
+  auto slab = at::empty({(long)pl.nsplit * pl.Npad * a.Kpad}, opts);
+  at::Tensor dbslab;
+  if (with_bias) dbslab = at::empty({(long)pl.nsplit * pl.tilesN * pl.Npad}, opts);
+  a.slab = slab.data_ptr<float>();
+  a.dbslab = with_bias ? dbslab.data_ptr<float>() : nullptr;
+  HIP_OK(launch_conv_wgrad(a, pl, cur_stream()));
+  return {slab, dbslab, pl};
+}
+
+// dw[N][Kpad] (+)= dW in the packed GEMM layout (tests, microbenchmarks); deterministic.
+void conv_wgrad(at::TensorList srcs, const at::Tensor& dy, at::IntArrayRef geom, int64_t N, const at::Tensor& dw,
+                const c10::optional<at::Tensor>& db, bool accumulate) {
+  ConvWgradArgs a = wgrad_args(srcs, dy, geom, N);
   check_gpu(dw, "dw");
-  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.dim() == 2 && dw.is_contiguous() && dw.size(0) >= N &&
-                  dw.size(1) >= a.K,
-              "raft_amd conv_wgrad: dw must be contiguous fp32 [>=N][Kpad >= K]");
-  a.Kpad = static_cast<int>(dw.size(1));
-  a.dw = dw.data_ptr<float>();
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.dim() == 2 && dw.stride(1) == 1 && dw.size(0) >= N &&
+                  dw.size(1) >= a.Kpad,
+              "raft_amd conv_wgrad: dw must be fp32 [>=N][>=Kpad] with unit column stride");
   if (db) {
     TORCH_CHECK(db->scalar_type() == at::kFloat && db->is_contiguous() && db->numel() >= N,
                 "raft_amd conv_wgrad: db must be contiguous fp32 [N]");
-    a.db = db->data_ptr<float>();
   }
+  if (a.P == 0 || N == 0) return;
   const c10::DeviceGuard guard(dy.device());
-  HIP_OK(launch_conv_wgrad(a, cur_stream()));
+  auto [slab, dbslab, pl] = run_wgrad(a, db.has_value(), dy);
+  HIP_OK(launch_wgrad_reduce_packed(slab.data_ptr<float>(), pl.nsplit, pl.Npad, a.Kpad, a.K,
+                                    db ? dbslab.data_ptr<float>() : nullptr, pl.nsplit * pl.tilesN,
+                                    dw.data_ptr<float>(), dw.stride(0), db ? db->data_ptr<float>() : nullptr,
+                                    (int)N, accumulate ? 1 : 0, cur_stream()));
+}
+
+// Parameter descriptor: 1..2 stacked (Cout_i, Cin, KH, KW) fp32 tensors + optional biases, input
+// channel segments [real0, pad0, real1, pad1, ...].
+ConvParamDesc param_desc(at::TensorList w, const c10::List<c10::optional<at::Tensor>>& b, at::IntArrayRef segs,
+                         double scale, const char* what) {
+  TORCH_CHECK(w.size() >= 1 && w.size() <= 2, "raft_amd ", what, ": 1..2 stacked weights");
+  TORCH_CHECK(b.size() == w.size(), "raft_amd ", what, ": one bias entry per weight");
+  TORCH_CHECK(segs.size() % 2 == 0 && segs.size() >= 2 && segs.size() <= 6, "raft_amd ", what, ": bad segments");
+  ConvParamDesc d{};
+  for (size_t i = 0; i < w.size(); ++i) {
+    const auto& t = w[i];
+    check_gpu(t, "weight");
+    TORCH_CHECK(t.scalar_type() == at::kFloat && t.dim() == 4, "raft_amd ", what, ": weights must be fp32 4-D");
+    TORCH_CHECK(t.size(1) == w[0].size(1) && t.size(2) == w[0].size(2) && t.size(3) == w[0].size(3),
+                "raft_amd ", what, ": stacked weights must agree in (Cin, kh, kw)");
+    d.w[i] = t.data_ptr<float>();
+    for (int j = 0; j < 4; ++j) d.ws[i][j] = t.stride(j);
+    d.rows[i] = static_cast<int>(t.size(0));
+    const auto& bi = b.get(i);
+    if (bi.has_value()) {
+      TORCH_CHECK(bi->scalar_type() == at::kFloat && bi->is_contiguous() && bi->numel() == t.size(0),
+                  "raft_amd ", what, ": bias must be contiguous fp32 [Cout]");
+      d.b[i] = bi->data_ptr<float>();
+    }
+  }
+  d.nseg = static_cast<int>(segs.size() / 2);
+  int real = 0, pad = 0;
+  for (int i = 0; i < d.nseg; ++i) {
+    d.seg_real[i] = static_cast<int>(segs[2 * i]);
+    d.seg_pad[i] = static_cast<int>(segs[2 * i + 1]);
+    TORCH_CHECK(d.seg_real[i] <= d.seg_pad[i], "raft_amd ", what, ": segment real > padded");
+    real += d.seg_real[i];
+    pad += d.seg_pad[i];
+  }
+  TORCH_CHECK(real == w[0].size(1), "raft_amd ", what, ": segments do not cover Cin");
+  d.Cin = real;
+  d.Cin_pad = pad;
+  d.KH = static_cast<int>(w[0].size(2));
+  d.KW = static_cast<int>(w[0].size(3));
+  d.scale = static_cast<float>(scale);
+  return d;
+}
+
+// Weight gradient of all stacked parameters of one conv, written (or accumulated) into the
+// parameter gradients themselves: split GEMM -> fixed-order slab reduce (deterministic).
+void conv_wgrad_params(at::TensorList srcs, const at::Tensor& dy, at::IntArrayRef geom, at::TensorList wgrad,
+                       const c10::List<c10::optional<at::Tensor>>& bgrad, at::IntArrayRef segs, double scale,
+                       bool accumulate) {
+  ConvParamDesc d = param_desc(wgrad, bgrad, segs, scale, "conv_wgrad_params");
+  const int N = d.rows[0] + d.rows[1];
+  ConvWgradArgs a = wgrad_args(srcs, dy, geom, N);
+  TORCH_CHECK(a.Cin == d.Cin_pad && a.KH == d.KH && a.KW == d.KW,
+              "raft_amd conv_wgrad_params: sources / geometry do not match the parameter layout");
+  bool with_bias = false;
+  for (size_t i = 0; i < bgrad.size(); ++i) with_bias = with_bias || bgrad.get(i).has_value();
+  if (a.P == 0 || N == 0) return;
+  const c10::DeviceGuard guard(dy.device());
+  auto [slab, dbslab, pl] = run_wgrad(a, with_bias, dy);
+  HIP_OK(launch_wgrad_reduce_params(slab.data_ptr<float>(), pl.nsplit, pl.Npad, a.Kpad,
+                                    with_bias ? dbslab.data_ptr<float>() : nullptr, pl.nsplit * pl.tilesN, d, N,
+                                    accumulate ? 1 : 0, cur_stream()));
+}
+
+// fp32 parameters -> bf16 forward operand [N][Kf], optional data-gradient operand
+// [Cin_pad][Kd] (flipped taps, Cout padded to cout_pad), fp32 scaled bias [N].
+std::tuple<at::Tensor, c10::optional<at::Tensor>, at::Tensor> pack_conv_weights(
+    at::TensorList w, const c10::List<c10::optional<at::Tensor>>& b, at::IntArrayRef segs, double scale, int64_t Kf,
+    int64_t Kd, int64_t cout_pad) {
+  ConvParamDesc d = param_desc(w, b, segs, scale, "pack_conv_weights");
+  const int N = d.rows[0] + d.rows[1];
+  const int taps = d.KH * d.KW;
+  TORCH_CHECK(Kf >= taps * d.Cin_pad && Kf % 64 == 0, "raft_amd pack_conv_weights: Kf too small / not % 64");
+  TORCH_CHECK(Kd == 0 || (cout_pad >= N && Kd >= taps * cout_pad && Kd % 64 == 0),
+              "raft_amd pack_conv_weights: bad dgrad layout");
+  const c10::DeviceGuard guard(w[0].device());
+  auto bopt = w[0].options().dtype(at::kBFloat16);
+  auto wf = at::empty({N, Kf}, bopt);
+  c10::optional<at::Tensor> wd;
+  if (Kd > 0) wd = at::empty({d.Cin_pad, Kd}, bopt);
+  auto bias = at::empty({N}, w[0].options());
+  HIP_OK(launch_pack_conv_weights(d, N, wf.data_ptr(), (int)Kf, Kd > 0 ? wd->data_ptr() : nullptr, (int)Kd,
+                                  (int)cout_pad, bias.data_ptr<float>(), cur_stream()));
+  return {wf, wd, bias};
 }
 
 // ---------------------------------------------------------------- update-block elementwise
@@ -665,7 +832,8 @@ void masked_cast(const at::Tensor& src, const c10::optional<at::Tensor>& mask, c
                             static_cast<int>(src.size(1)), cur_stream()));
 }
 
-void pack_flow(const at::Tensor& flow, const at::Tensor& flow8, const c10::optional<at::Tensor>& motion) {
+void pack_flow(const at::Tensor& flow, const at::Tensor& flow8, const c10::optional<at::Tensor>& motion,
+               bool from_coords) {
   check_gpu(flow, "flow");
   TORCH_CHECK(flow.scalar_type() == at::kFloat && flow.is_contiguous() && flow.dim() == 4 && flow.size(1) == 2,
               "raft_amd pack_flow: flow must be contiguous fp32 (B, 2, H, W)");
@@ -681,7 +849,41 @@ void pack_flow(const at::Tensor& flow, const at::Tensor& flow8, const c10::optio
     smo = motion->stride(0);
   }
   const c10::DeviceGuard guard(flow.device());
-  HIP_OK(launch_pack_flow(flow.data_ptr<float>(), flow8.data_ptr(), mo, smo, B, HW, cur_stream()));
+  HIP_OK(launch_pack_flow(flow.data_ptr<float>(), flow8.data_ptr(), mo, smo, B, HW, (int)flow.size(3),
+                          from_coords ? 1 : 0, cur_stream()));
+}
+
+// coords_out = coords1 + delta[:, :2] (delta: (P, >=2) fp32 rows), flow_out = coords_out - grid
+void apply_delta(const at::Tensor& coords1, const at::Tensor& delta, const at::Tensor& coords_out,
+                 const at::Tensor& flow_out) {
+  check_coords(coords1);
+  check_coords(coords_out);
+  check_coords(flow_out);
+  TORCH_CHECK(coords_out.sizes() == coords1.sizes() && flow_out.sizes() == coords1.sizes(),
+              "raft_amd apply_delta: shape mismatch");
+  const long B = coords1.size(0), HW = coords1.size(2) * coords1.size(3);
+  pm_any(delta, "delta", B * HW, at::kFloat);
+  TORCH_CHECK(delta.size(1) >= 2, "raft_amd apply_delta: delta needs 2 channels");
+  const c10::DeviceGuard guard(coords1.device());
+  HIP_OK(launch_apply_delta(coords1.data_ptr<float>(), delta.data_ptr<float>(), delta.stride(0),
+                            coords_out.data_ptr<float>(), flow_out.data_ptr<float>(), B, HW, (int)coords1.size(3),
+                            cur_stream()));
+}
+
+// corr_lookup into a caller buffer (B, H, W, och) with och >= L*(2r+1)^2 (zero padded)
+void corr_lookup_into(at::TensorList pyramid, const at::Tensor& coords, int64_t radius, const at::Tensor& out) {
+  check_coords(coords);
+  const long B = coords.size(0), H = coords.size(2), W = coords.size(3);
+  std::vector<at::Tensor> lv(pyramid.begin(), pyramid.end());
+  PyrDesc d = make_desc(lv, B * H * W);
+  const long win = (2 * radius + 1) * (2 * radius + 1);
+  check_gpu(out, "out");
+  TORCH_CHECK(out.dim() == 4 && out.is_contiguous() && out.size(0) == B && out.size(1) == H && out.size(2) == W &&
+                  out.size(3) >= d.levels * win,
+              "raft_amd::corr_lookup_into: out must be contiguous (B, H, W, >= L*(2r+1)^2)");
+  const c10::DeviceGuard guard(coords.device());
+  HIP_OK(launch_corr_lookup_fwd(d, coords.data_ptr<float>(), out.data_ptr(), dtype_code(out.scalar_type()), B, H, W,
+                                static_cast<int>(radius), static_cast<int>(out.size(3)), cur_stream()));
 }
 
 // ---------------------------------------------------------------- NHWC instance norm
@@ -728,8 +930,13 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("instance_norm_bwd(Tensor x, Tensor dy, Tensor stats, bool relu) -> Tensor");
   m.def(
       "conv_fwd(Tensor[] srcs, Tensor wt, int[] geom, int N, Tensor? bias, int epi, int act, float alpha, "
-      "Tensor(a!) out, int acc_c0, Tensor? mask, Tensor? h, Tensor? z, Tensor(b!)? out2) -> ()");
-  m.def("conv_wgrad(Tensor[] srcs, Tensor dy, int[] geom, int N, Tensor(a!) dw, Tensor(b!)? db) -> ()");
+      "Tensor(a!) out, int acc_c0, Tensor? mask, Tensor? h, Tensor? z, Tensor(b!)? out2, int cfg=0) -> ()");
+  m.def("conv_wgrad(Tensor[] srcs, Tensor dy, int[] geom, int N, Tensor(a!) dw, Tensor(b!)? db, "
+        "bool accumulate=True) -> ()");
+  m.def("conv_wgrad_params(Tensor[] srcs, Tensor dy, int[] geom, Tensor(a!)[] wgrad, Tensor?[] bgrad, int[] segs, "
+        "float scale, bool accumulate) -> ()");
+  m.def("pack_conv_weights(Tensor[] w, Tensor?[] b, int[] segs, float scale, int Kf, int Kd, int cout_pad) -> "
+        "(Tensor, Tensor?, Tensor)");
   m.def("gru_gates(Tensor zr, Tensor h) -> (Tensor, Tensor)");
   m.def("gru_gates_backward(Tensor zr, Tensor h, Tensor gz, Tensor grh) -> (Tensor, Tensor)");
   m.def("gru_blend(Tensor z, Tensor q, Tensor h) -> Tensor");
@@ -741,7 +948,10 @@ TORCH_LIBRARY(raft_amd, m) {
       "gru_bwd_a(Tensor dH, Tensor z, Tensor q, Tensor h, Tensor(a!) dq, Tensor(b!) dz, Tensor(c!) carry) -> ()");
   m.def("gru_bwd_b(Tensor(a!) drh, Tensor r, Tensor h, Tensor carry, Tensor(b!) dr) -> ()");
   m.def("masked_cast(Tensor src, Tensor? mask, Tensor(a!) out) -> ()");
-  m.def("pack_flow(Tensor flow, Tensor(a!) flow8, Tensor(b!)? motion) -> ()");
+  m.def("pack_flow(Tensor flow, Tensor(a!) flow8, Tensor(b!)? motion, bool from_coords=False) -> ()");
+  m.def("apply_delta(Tensor coords1, Tensor delta, Tensor(a!) coords_out, Tensor(b!) flow_out) -> ()");
+  m.def("corr_lookup_into(Tensor[] pyramid, Tensor coords, int radius, Tensor(a!) out) -> ()");
+  m.def("convex_upsample_backward_into(Tensor flow, Tensor mask, Tensor grad, Tensor(a!) dmask, Tensor(b!) rows) -> ()");
   m.def("corr_lookup_backward_(Tensor(a!)[] dpyramid, Tensor coords, Tensor grad, int radius) -> ()");
   m.def(
       "pyramid_grad_combine(Tensor[] dpyramid, int B, int H, int W, int ldp, float alpha) -> (Tensor, "
@@ -777,7 +987,12 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("gru_bwd_b", &raft_amd::gru_bwd_b);
   m.impl("masked_cast", &raft_amd::masked_cast);
   m.impl("pack_flow", &raft_amd::pack_flow);
+  m.impl("apply_delta", &raft_amd::apply_delta);
+  m.impl("corr_lookup_into", &raft_amd::corr_lookup_into);
+  m.impl("convex_upsample_backward_into", &raft_amd::convex_upsample_backward_into);
   m.impl("conv_wgrad", &raft_amd::conv_wgrad);
+  m.impl("conv_wgrad_params", &raft_amd::conv_wgrad_params);
+  m.impl("pack_conv_weights", &raft_amd::pack_conv_weights);
   m.impl("gru_gates", &raft_amd::gru_gates);
   m.impl("gru_gates_backward", &raft_amd::gru_gates_backward);
   m.impl("gru_blend", &raft_amd::gru_blend);

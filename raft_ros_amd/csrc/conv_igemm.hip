@@ -2,7 +2,7 @@
 // (reference core/update.py:6-136: motion encoder, SepConvGRU/ConvGRU, flow and
 // mask heads), forward + both backward GEMMs, bf16 operands, fp32 accumulate.
 //
-// conv_fwd_kernel  Y[p][n] = epi( sum_{tap,c} X[p + d_tap][c] * W[n][tap][c] )
+// Forward / data-gradient:  Y[p][n] = epi( sum_{tap,c} X[p + d_tap][c] * W[n][tap][c] )
 //   * M = pixels (B*H*W), N = output channels, K = taps * Cin.
 //   * X may be the channel-concatenation of up to 3 NHWC sources (pointer +
 //     pixel stride each), so torch.cat of [h, inp, motion] etc. is never
@@ -14,20 +14,25 @@
 //     mask of the conv input and partial (channel-range) accumulation.
 //   * the data-gradient of a stride-1 conv is the same kernel on dY with
 //     flipped/transposed packed weights and padding K-1-P.
-// conv_wgrad_kernel  dW[n][tap][c] += sum_p dY[p][n] * X[p + d_tap][c]   (fp32)
-//   * M = out channels, N = K = taps * Cin, reduction over pixels split across
-//     workgroups; both operands are staged transposed into LDS; fp32 atomics
-//     accumulate straight into the persistent weight-gradient buffer, so the
-//     12 refinement iterations never materialise per-iteration weight grads.
-//   * the bias gradient (column sums of dY) is fused into the same pass.
+//   * kernels: v4 (DMA ring, 64x128 / 64x64 tiles) for 1x1 convs and as the
+//     default, v5 (halo strip: one LDS strip per 64-channel chunk serves every
+//     tap) for the multi-tap update-block convs, an N<=2 register kernel for
+//     the flow-head output, and a generic register-staged kernel for the odd
+//     shapes the DMA kernels do not take.
+// Weight gradient:  dW[n][tap][c] = sum_p dY[p][n] * X[p + d_tap][c]
+//   * M = out channels, N = K = taps * Cin, reduction over pixels split over
+//     workgroups (one fp32 partial slab per split, summed in a fixed order by
+//     csrc/weights.hip: deterministic, no atomics).  A source may be
+//     "periodic" (period = pixel count of one refinement iteration): the
+//     update block's context features are shared by every iteration, so the
+//     weight gradient of all iterations is one reduction over iters*P pixels
+//     that re-reads the same context rows (ops/update_fused.py).
 //
 // Tiling: 256 threads = 4 wave64s in a 2x2 arrangement, v_mfma_f32_32x32x16_bf16,
-// BK = 32 per LDS stage with register double buffering, LDS rows padded to
-// 80 B (conflict-free 16-lane ds_read_b128 groups), XCD-aware tile order.
+// BK = 64 per LDS stage, XCD-aware tile order.
 #include "common.h"
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace raft_amd {
 
@@ -35,7 +40,7 @@ struct ConvSrc {
   const __bf16* ptr;
   long stride;  // elements between consecutive pixels
   int C;        // channels taken from this source (multiple of 8)
-  int pad_;
+  int period;   // wgrad only: >0 -> pixel p reads row p % period (0: no wrap)
 };
 
 struct ConvFwdArgs {
@@ -63,6 +68,7 @@ struct ConvFwdArgs {
   long z_stride;
   __bf16* out2;  // epi 2: r*h, epi 3: tanh(q)
   long out2_stride;
+  int cfg;  // kernel variant: 0 = automatic, otherwise forced (tests / microbenchmarks)
 };
 
 struct ConvWgradArgs {
@@ -75,9 +81,20 @@ struct ConvWgradArgs {
   int N;
   long P;
   long pix_per_split;
-  float* dw;  // [N][Kpad] fp32, accumulated
-  float* db;  // [N] fp32, accumulated (may be null)
-  int xcd_g;  // >0: XCD-grouped split mapping with xcd_g splits per XCD (set by the launcher)
+  float* slab;    // [nsplit][Npad][Kpad] fp32: the split's partial dW (written, not accumulated)
+  float* dbslab;  // [nsplit][tilesN][Npad] fp32 bias partials (may be null)
+  int Npad;       // slab rows (N rounded up to the row tile)
+  int xcd_g;      // >0: XCD-grouped split mapping with xcd_g splits per XCD (set by the launcher)
+};
+
+// Plan of one weight-gradient launch (the caller sizes the slabs from it).
+//   kind 2: wgrad v2, tilesN = column tiles, pix_per_split = pixels per split
+//   kind 3: wgrad v3 (tap-batched), tilesN = 64-channel chunks, pix_per_split = pixel TILES per split
+// Bias partials: nsplit * tilesN rows of Npad floats.
+struct WgradPlan {
+  int BM, BN, tilesM, tilesN, nsplit, Npad, xcd_g;
+  long pix_per_split;
+  int kind;
 };
 
 namespace {
@@ -295,7 +312,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvFwdArgs a) {
   }
 }
 
-// ============================================================================ forward v3
+// ============================================================================ DMA helpers
 // Direct-to-LDS pipeline: every 16-byte chunk of the A (im2col) and B (packed weight)
 // tiles is fetched with global_load_lds_dwordx4 into an S-stage LDS ring, so S-1
 // K steps are in flight with no staging registers.  LDS rows are 128 B (64 bf16)
@@ -320,215 +337,6 @@ __device__ __forceinline__ void glds16(const void* g, __bf16* lds_wave_base) {
 }
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
-
-template <int BM, int BN, int S>
-__global__ __launch_bounds__(256) void conv_fwd3_kernel(const ConvFwdArgs a) {
-  constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int AI = BM / 32, BI = BN / 32;  // wave-instructions (8 rows each) per wave per step
-  constexpr int G = AI + BI;                 // glds per thread per step
-  constexpr int STAGE = (BM + BN) * 64;      // bf16 elements
-  __shared__ __attribute__((aligned(1024))) __bf16 smem[S * STAGE];
-
-  // kernel arguments used in the loop, as plain scalars (taking the address of the
-  // by-value argument struct inside a lambda turns its reads into VMEM loads that
-  // hipcc then waits for with vmcnt(0), draining the DMA pipeline)
-  const __bf16* const sp0 = a.src[0].ptr;
-  const __bf16* const sp1 = a.src[1].ptr;
-  const __bf16* const sp2 = a.src[2].ptr;
-  const long ss0 = a.src[0].stride, ss1 = a.src[1].stride, ss2 = a.src[2].stride;
-  const int sc0 = a.src[0].C, sc1 = a.src[1].C;
-  const int Cin = a.Cin, K = a.K, Kpad = a.Kpad, H = a.H, W = a.W, KW = a.KW, PH = a.PH, PW = a.PW;
-  const int ntaps = a.KH * a.KW;
-  const long P = a.P;
-  const int Nn = a.N;
-
-  const int tilesN = (Nn + BN - 1) / BN;
-  const int tilesM = (int)((P + BM - 1) / BM);
-  const int wg = xcd_remap(blockIdx.x, tilesM * tilesN);
-  const int tm = wg / tilesN, tn = wg - (wg / tilesN) * tilesN;
-  const long m0 = (long)tm * BM;
-  const int n0 = tn * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int lrow = lane >> 3, lpc = lane & 7;  // row within an 8-row DMA block, physical chunk
-
-  PixCoord pc[AI];
-  int achunk[AI];
-#pragma unroll
-  for (int i = 0; i < AI; ++i) {
-    const int row = (wave * AI + i) * 8 + lrow;
-    pc[i] = decode_pix(m0 + row, P, H, W);
-    achunk[i] = swz(row, lpc);
-  }
-  int bchunk[BI];
-  const __bf16* bsrc[BI];
-#pragma unroll
-  for (int i = 0; i < BI; ++i) {
-    const int row = (wave * BI + i) * 8 + lrow;
-    bchunk[i] = swz(row, lpc);
-    bsrc[i] = (n0 + row < Nn) ? a.wt + (long)(n0 + row) * Kpad : nullptr;
-  }
-  bool uniform = (ntaps == 1) || (Cin % 64 == 0);
-  uniform = uniform && (ntaps == 1 || ((sc0 % 64 == 0) && (sc1 % 64 == 0)));
-  const int nk = Kpad / 64;
-  const void* zero = g_zero_page;
-
-  auto pick = [&](int c, const __bf16*& ptr, long& stride, int& cc) {
-    if (c < sc0) { ptr = sp0; stride = ss0; cc = c; }
-    else if (c < sc0 + sc1) { ptr = sp1; stride = ss1; cc = c - sc0; }
-    else { ptr = sp2; stride = ss2; cc = c - sc0 - sc1; }
-  };
-
-  auto issue = [&](int step, int stage) __attribute__((always_inline)) {
-    const int k0 = step * 64;
-    __bf16* sA = smem + stage * STAGE;
-    __bf16* sB = sA + BM * 64;
-    if (uniform) {
-      int tap = 0, c0 = k0;
-      if (ntaps != 1) {
-        tap = k0 / Cin;
-        c0 = k0 - tap * Cin;
-      }
-      const int ky = tap / KW, kx = tap - (tap / KW) * KW;
-      const int dy = ky - PH, dx = kx - PW;
-      const __bf16* ptr;
-      long stride;
-      int cc;
-      pick(c0, ptr, stride, cc);
-      const long doff = (long)dy * W + dx;
-#pragma unroll
-      for (int i = 0; i < AI; ++i) {
-        const int y = pc[i].py + dy, x = pc[i].px + dx;
-        const int k = k0 + achunk[i] * 8;
-        const bool ok = pc[i].p >= 0 && k < K && y >= 0 && y < H && x >= 0 && x < W;
-        const void* g = ok ? (const void*)(ptr + (pc[i].p + doff) * stride + cc + achunk[i] * 8) : zero;
-        glds16(g, sA + (wave * AI + i) * 512);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < AI; ++i) {
-        const int k = k0 + achunk[i] * 8;
-        const void* g = zero;
-        if (pc[i].p >= 0 && k < K) {
-          const int tap = k / Cin;
-          const int c = k - tap * Cin;
-          const int ky = tap / KW, kx = tap - (tap / KW) * KW;
-          const int y = pc[i].py + ky - PH, x = pc[i].px + kx - PW;
-          if (y >= 0 && y < H && x >= 0 && x < W) {
-            const __bf16* ptr;
-            long stride;
-            int cc;
-            pick(c, ptr, stride, cc);
-            g = ptr + (pc[i].p + (long)(ky - PH) * W + (kx - PW)) * stride + cc;
-          }
-        }
-        glds16(g, sA + (wave * AI + i) * 512);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < BI; ++i) {
-      const void* g = bsrc[i] ? (const void*)(bsrc[i] + k0 + bchunk[i] * 8) : zero;
-      glds16(g, sB + (wave * BI + i) * 512);
-    }
-  };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int fr = lane & 31, fh = lane >> 5;
-#pragma unroll
-  for (int i = 0; i < S - 1; ++i)
-    if (i < nk) issue(i, i);
-
-  for (int t = 0; t < nk; ++t) {
-    // retire step t: leave the younger steps (up to S-2) in flight
-    const int ahead = (nk - 1 - t) < (S - 2) ? (nk - 1 - t) : (S - 2);
-    if (ahead >= S - 2) wait_vmcnt<(S - 2) * G>();
-    else if (ahead == 2) wait_vmcnt<2 * G>();
-    else if (ahead == 1) wait_vmcnt<G>();
-    else wait_vmcnt<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + S - 1 < nk) issue(t + S - 1, (t + S - 1) % S);
-    const __bf16* sA = smem + (t % S) * STAGE;
-    const __bf16* sB = sA + BM * 64;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int c = 2 * s + fh;
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * (BM / 2) + i * 32 + fr;
-        af[i] = *reinterpret_cast<const bf16x8*>(sA + row * 64 + swz(row, c) * 8);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * (BN / 2) + j * 32 + fr;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(sB + row * 64 + swz(row, c) * 8);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-  }
-  wait_vmcnt<0>();
-
-  // ------------------------------------------------------------------ epilogue
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
-    if (n >= a.N) continue;
-    const float bias = a.bias ? a.bias[n] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row >= a.P) continue;
-        float v = acc[i][j][r] * a.alpha + bias;
-        if (a.epi == 0) {
-          if (a.act == 1) v = fmaxf(v, 0.f);
-          if (a.out_f32)
-            static_cast<float*>(a.out)[row * a.out_stride + n] = v;
-          else
-            static_cast<__bf16*>(a.out)[row * a.out_stride + n] = static_cast<__bf16>(v);
-        } else if (a.epi == 1) {
-          if (a.mask && !(static_cast<float>(a.mask[row * a.mask_stride + n]) > 0.f)) v = 0.f;
-          if (a.out_f32) {
-            float* o = static_cast<float*>(a.out) + row * a.out_stride + n;
-            *o = n >= a.acc_c0 ? *o + v : v;
-          } else {
-            __bf16* o = static_cast<__bf16*>(a.out) + row * a.out_stride + n;
-            *o = static_cast<__bf16>(n >= a.acc_c0 ? static_cast<float>(*o) + v : v);
-          }
-        } else if (a.epi == 2) {
-          const int C = a.N >> 1;
-          const float sg = sigmoidf_(v);
-          static_cast<__bf16*>(a.out)[row * a.out_stride + n] = static_cast<__bf16>(sg);
-          if (n >= C) {
-            const float hv = static_cast<float>(a.h[row * a.h_stride + (n - C)]);
-            a.out2[row * a.out2_stride + (n - C)] = static_cast<__bf16>(sg * hv);
-          }
-        } else {
-          const float q = tanhf_(v);
-          const float zv = static_cast<float>(a.z[row * a.z_stride + n]);
-          const float hv = static_cast<float>(a.h[row * a.h_stride + n]);
-          static_cast<__bf16*>(a.out)[row * a.out_stride + n] =
-              static_cast<__bf16>((1.f - zv) * hv + zv * q);
-          a.out2[row * a.out2_stride + n] = static_cast<__bf16>(q);
-        }
-      }
-  }
-}
 
 // ============================================================================ forward v4
 // Same direct-to-LDS ring as v3, but every load is a bounds-checked raw buffer load
@@ -1114,12 +922,7 @@ inline long fwd5_lds_bytes(int BM, int BN, int strip_rows) {
   return need <= 160 * 1024 ? need : 0;
 }
 
-// ============================================================================ wgrad
-// dW tile BM (out channels) x BN (k = tap*Cin + c), reduction over 64-pixel stages.
-// Both operands are staged in their natural [pixel][column] layout with 16-byte
-// writes and read as MFMA operands with ds_read_b64_tr_b16 (gfx950 transposed LDS
-// read: per 16-lane group a 4-row x 16-column block lands column-major in VGPRs).
-// Row pitch = columns + 32 bf16 so the 4 rows of a block hit disjoint 16-bank ranges.
+// ============================================================================ wgrad helpers
 constexpr int WBK = 64;
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -1128,156 +931,6 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 __device__ __forceinline__ s16x4 tr_read(const __bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       (lds_s16x4*)(reinterpret_cast<uintptr_t>(p) & 0xffffffffu));
-}
-
-template <int BM, int BN>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(const ConvWgradArgs a) {
-  constexpr int LDA = BM + 32, LDB = BN + 32;
-  constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int ACPR = BM / 8, BCPR = BN / 8;  // 16-byte chunks per pixel row
-  constexpr int ACH = WBK * ACPR / 256, BCH = WBK * BCPR / 256;
-  constexpr int STAGE = WBK * (LDA + LDB);
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
-  __shared__ float sdb[BM];
-
-  const int tilesM = (a.N + BM - 1) / BM;
-  const int tilesN = (a.K + BN - 1) / BN;
-  const int tiles = tilesM * tilesN;
-  int split, t0;
-  if (a.xcd_g > 0) {
-    // workgroups are dealt round-robin to the 8 XCDs: keep every tile of a pixel split on
-    // one XCD so the split's dY / X rows are fetched into that XCD's L2 once
-    const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
-    const int si = local / tiles;
-    t0 = local - si * tiles;
-    split = xcd * a.xcd_g + si;
-  } else {
-    split = blockIdx.x / tiles;
-    t0 = blockIdx.x - split * tiles;
-  }
-  const int tm = t0 / tilesN, tn = t0 - (t0 / tilesN) * tilesN;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const long pbeg = (long)split * a.pix_per_split;
-  const long pend = pbeg + a.pix_per_split < a.P ? pbeg + a.pix_per_split : a.P;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const bool do_db = a.db != nullptr && tn == 0;
-  if (tid < BM) sdb[tid] = 0.f;
-
-  const int acc_col = tid % ACPR, arow0 = tid / ACPR;  // A: chunk column fixed per thread
-  const int bcc = tid % BCPR, brow0 = tid / BCPR;
-  constexpr int AROWS = 256 / ACPR, BROWS = 256 / BCPR;
-  float dbacc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) dbacc[j] = 0.f;
-
-  u32x4 ra[ACH], rb[BCH];
-  auto load = [&](long p0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < ACH; ++i) {
-      const long p = p0 + arow0 + AROWS * i;
-      const int n = m0 + acc_col * 8;
-      ra[i] = (p < pend && n < a.N) ? *reinterpret_cast<const u32x4*>(a.dy + p * a.dy_stride + n)
-                                     : u32x4{0, 0, 0, 0};
-    }
-#pragma unroll
-    for (int i = 0; i < BCH; ++i) {
-      const long p = p0 + brow0 + BROWS * i;
-      const bool pv = p < pend;
-      int b = 0, py = 0, px = 0;
-      if (pv) {
-        const int HW = a.H * a.W;
-        b = p / HW;
-        const int rem = p - (long)b * HW;
-        py = rem / a.W;
-        px = rem - py * a.W;
-      }
-      rb[i] = im2col_chunk(a.src, a.Cin, a.K, a.H, a.W, a.KW, a.PH, a.PW, pv, b, py, px, n0 + bcc * 8);
-    }
-  };
-  auto store = [&](int buf) __attribute__((always_inline)) {
-    __bf16* sA = smem + buf * STAGE;
-    __bf16* sB = sA + WBK * LDA;
-#pragma unroll
-    for (int i = 0; i < ACH; ++i) {
-      *reinterpret_cast<u32x4*>(sA + (arow0 + AROWS * i) * LDA + acc_col * 8) = ra[i];
-      if (do_db) {
-        const __bf16* v = reinterpret_cast<const __bf16*>(&ra[i]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) dbacc[j] += static_cast<float>(v[j]);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < BCH; ++i) *reinterpret_cast<u32x4*>(sB + (brow0 + BROWS * i) * LDB + bcc * 8) = rb[i];
-  };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  // transposed-read lane geometry: half h = lane>>5 picks rows +8, gi = (lane>>4)&1 the
-  // 16-column block, q = row within the 4-row block, pq = 4-column group
-  const int h = lane >> 5, gi = (lane >> 4) & 1, q = (lane & 15) >> 2, pq = lane & 3;
-  const int nsteps = pend > pbeg ? (int)((pend - pbeg + WBK - 1) / WBK) : 0;
-  if (nsteps > 0) {
-    load(pbeg);
-    store(0);
-  }
-  __syncthreads();
-  for (int t = 0; t < nsteps; ++t) {
-    if (t + 1 < nsteps) load(pbeg + (long)(t + 1) * WBK);
-    const __bf16* sA = smem + (t & 1) * STAGE;
-    const __bf16* sB = sA + WBK * LDA;
-#pragma unroll
-    for (int s = 0; s < WBK / 16; ++s) {
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int col = wm * (BM / 2) + i * 32 + gi * 16 + 4 * pq;
-        const s16x4 lo = tr_read(sA + (s * 16 + h * 8 + q) * LDA + col);
-        const s16x4 hi = tr_read(sA + (s * 16 + h * 8 + 4 + q) * LDA + col);
-        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = wn * (BN / 2) + j * 32 + gi * 16 + 4 * pq;
-        const s16x4 lo = tr_read(sB + (s * 16 + h * 8 + q) * LDB + col);
-        const s16x4 hi = tr_read(sB + (s * 16 + h * 8 + 4 + q) * LDB + col);
-        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    if (t + 1 < nsteps) store((t + 1) & 1);
-    __syncthreads();
-  }
-
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
-    if (col >= a.K) continue;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row < a.N) atomicAdd(a.dw + (long)row * a.Kpad + col, acc[i][j][r]);
-      }
-  }
-  if (do_db) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(&sdb[acc_col * 8 + j], dbacc[j]);
-    __syncthreads();
-    if (tid < BM && m0 + tid < a.N) atomicAdd(a.db + m0 + tid, sdb[tid]);
-  }
 }
 
 }  // namespace
@@ -1361,16 +1014,19 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
   if (seg == 2) cseg -= a.src[1].C;
   const __bf16* xptr = seg == 0 ? a.src[0].ptr : (seg == 1 ? a.src[1].ptr : a.src[2].ptr);
   const long xstride = seg == 0 ? a.src[0].stride : (seg == 1 ? a.src[1].stride : a.src[2].stride);
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(xptr, (unsigned)(a.P * xstride * 2));
+  const int xper0 = seg == 0 ? a.src[0].period : (seg == 1 ? a.src[1].period : a.src[2].period);
+  const int xper = xper0 > 0 ? xper0 : P;  // rows of this source (pixel p reads row p % xper)
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(xptr, (unsigned)((long)xper * xstride * 2));
   const unsigned xst = (unsigned)xstride * 2;
   const int doff = dyy * W + dxx;
 
-  // pixel walkers for this lane's B rows
-  int bp[BI], bpy[BI], bpx[BI];
+  // pixel walkers for this lane's B rows: flat pixel (bounds), source row (address), image coords
+  int bp[BI], bw[BI], bpy[BI], bpx[BI];
 #pragma unroll
   for (int i = 0; i < BI; ++i) {
     const int p = pbeg + (wave * BI + i) * BRPI + brl;
     bp[i] = p;
+    bw[i] = p % xper;
     const int rem = p % (H * W);
     bpy[i] = rem / W;
     bpx[i] = rem - bpy[i] * W;
@@ -1391,9 +1047,11 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
     _Pragma("unroll") for (int i = 0; i < BI; ++i) {                                                       \
       const bool ok = b_ok && bp[i] < pend && (unsigned)(bpy[i] + dyy) < (unsigned)H &&                    \
                       (unsigned)(bpx[i] + dxx) < (unsigned)W;                                              \
-      const unsigned voff = ok ? (unsigned)(bp[i] + doff) * xst + (unsigned)cseg * 2 : kOOB;              \
+      const unsigned voff = ok ? (unsigned)(bw[i] + doff) * xst + (unsigned)cseg * 2 : kOOB;              \
       bload16(rx, sB_ + (wave * BI + i) * 512, voff, 0);                                                   \
       bp[i] += 64;                                                                                         \
+      bw[i] += 64;                                                                                         \
+      while (bw[i] >= xper) bw[i] -= xper;                                                                 \
       bpx[i] += 64;                                                                                        \
       while (bpx[i] >= W) {                                                                                \
         bpx[i] -= W;                                                                                       \
@@ -1413,7 +1071,7 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
   // column of accb holds the pixel sum of dY rows.  The 64-pixel steps are dealt to the
   // (column tile, wave column) pairs round-robin -- step t goes to tn == t % tilesN,
   // wn == (t / tilesN) & 1 -- so the extra MFMAs are spread over the whole grid.
-  const bool do_db = a.db != nullptr;
+  const bool do_db = a.dbslab != nullptr;
   f32x16 accb[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -1474,11 +1132,12 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
   }
 #undef RAFT_WG_ISSUE
   wait_vmcnt<0>();
-  if (do_db && nsteps > tn) {
+  if (a.dbslab) {
     // every column of accb holds the row sums: stage column 0 of both wave columns in LDS
-    // (the ring is free now), then add BM contiguous floats per workgroup -- 256-byte
-    // atomic wave-instructions instead of one scattered dword per lane
+    // (the ring is free now) and write this workgroup's BM partial bias sums (zeros if it
+    // took no bias steps) -- the reduce kernel sums them in a fixed order
     float* sdb = reinterpret_cast<float*>(smem);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
     if ((lane & 31) == 0) {
 #pragma unroll
@@ -1488,19 +1147,264 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
           sdb[wn * BM + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)] = accb[i][r];
     }
     __syncthreads();
-    if (tid < BM && m0 + tid < a.N) atomicAdd(a.db + m0 + tid, sdb[tid] + sdb[BM + tid]);
+    if (tid < BM) a.dbslab[((long)split * tilesN + tn) * a.Npad + m0 + tid] = sdb[tid] + sdb[BM + tid];
   }
 
+  // partial dW tile of this split: plain stores (32 consecutive floats per 32 lanes)
+  float* slab = a.slab + (long)split * a.Npad * a.Kpad;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
-    if (col >= a.K) continue;
+    if (col >= a.Kpad) continue;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row < a.N) atomicAdd(a.dw + (long)row * a.Kpad + col, acc[i][j][r]);
+        slab[(long)row * a.Kpad + col] = acc[i][j][r];
+      }
+  }
+}
+
+// ============================================================================ wgrad v3 (tap-batched)
+// dW[n][tap][c] = sum_p dY[p][n] X[p + d_tap][c] for every tap of a KHxKW conv at once.
+// wgrad v2 re-fetches im2col(X) per tap (5-9x the activation bytes) and its 128x128 tile
+// does 32 MAC per operand byte, so on MI355X it is bound by the L2->LDS fills, not the MFMA.
+// v3 gives a workgroup BM output channels x one 64-channel input chunk x ALL taps
+// (columns tap*64 + c), and per step a 2-D tile of TH x TW = 64 pixels:
+//   * dY tile [64 px][BM] and the tile's halo block [(TH+KH-1) x (TW+KW-1) px][64 ch] are
+//     DMA'd (buffer_load ... lds) into an S-stage ring; out-of-image rows load as zeros, so
+//     the conv padding needs no masking at all;
+//   * every tap reads its B fragments from the SAME halo block at a per-lane row shift
+//     (ds_read_b64_tr_b16, rows = pixels), the A fragments (dY^T) are shared by all taps;
+//   * ~110 MAC per operand byte (3.5x v2).
+// Pixel tiles never cross an image; the (T*B, H, W) image stack is tiled, the tile list is
+// split over workgroups (XCD-grouped like v2) and each split writes its own fp32 slab.
+// Periodic sources: image i reads source image i % (period / HW).
+template <int KH, int KW, int TH, int TW>
+struct WG3Geo {
+  static constexpr int BH = TH + KH - 1, BW = TW + KW - 1;
+  static constexpr int ROWS = (BH * BW + 31) / 32 * 32;  // halo-block rows, a multiple of 4 waves x 8
+  static constexpr int TAPS = KH * KW;
+};
+
+template <int KH, int KW, int TH, int TW, int MT, int S>
+__global__ __launch_bounds__(256) void conv_wgrad3_kernel(const ConvWgradArgs a) {
+  using G3 = WG3Geo<KH, KW, TH, TW>;
+  static_assert(TH * TW == 64, "64-pixel tiles");
+  static_assert(TW % 4 == 0, "4 consecutive tile pixels share a tile row (transposed-read rows)");
+  constexpr int BM = 64 * MT;          // 2 wave rows x MT 32-row tiles
+  constexpr int NT = G3::TAPS;         // 32-column tiles per wave: 2 wave columns x NT = TAPS x 64
+  constexpr int ACPR = BM / 8;         // dY chunks per row
+  constexpr int ARPI = 64 / ACPR;      // dY rows per wave-instruction
+  constexpr int AI = 64 / (4 * ARPI);  // dY wave-instructions per wave per step
+  constexpr int SI = G3::ROWS / 32;    // halo-block wave-instructions per wave per step
+  constexpr int G = AI + SI;
+  constexpr int STAGE = 64 * BM + G3::ROWS * 64;  // bf16 elements
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[S * STAGE];
+
+  const int H = a.H, W = a.W;
+  const int tilesY = (H + TH - 1) / TH, tilesX = (W + TW - 1) / TW;
+  const int tiles_img = tilesY * tilesX;
+  const int nimg = a.B;
+  const int ntiles = nimg * tiles_img;
+  const int nchunk = a.Cin / 64;
+  const int tilesM = (a.N + BM - 1) / BM;
+  const int wtiles = tilesM * nchunk;
+  int split, t0;
+  if (a.xcd_g > 0) {
+    const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
+    const int si = local / wtiles;
+    t0 = local - si * wtiles;
+    split = xcd * a.xcd_g + si;
+  } else {
+    split = blockIdx.x / wtiles;
+    t0 = blockIdx.x - split * wtiles;
+  }
+  const int tm = t0 / nchunk, cc = t0 - tm * nchunk;
+  const int m0 = tm * BM;
+  const int tbeg = split * (int)a.pix_per_split;  // pix_per_split counts pixel TILES here
+  const int tend = min(tbeg + (int)a.pix_per_split, ntiles);
+  const int nsteps = tend > tbeg ? tend - tbeg : 0;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int HW = H * W;
+
+  // ---- dY (A operand) DMA geometry: lane -> (tile pixel row of its instruction, chunk)
+  const int arl = lane / ACPR;
+  const int achunk = wswz<BM>(arl, lane % ACPR);
+  const bool a_ok = m0 + achunk * 8 < a.N;
+  const unsigned dyst = (unsigned)a.dy_stride * 2;
+  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(a.dy, (unsigned)(a.P * a.dy_stride * 2));
+  int aty[AI], atx[AI];  // tile-local pixel of each of this lane's dY rows
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int k = (wave * AI + i) * ARPI + arl;
+    aty[i] = k / TW;
+    atx[i] = k - aty[i] * TW;
+  }
+
+  // ---- X (B operand) source: the chunk's segment (64-channel chunks never straddle one)
+  const int c0 = cc * 64;
+  int seg = 0, cseg = c0;
+  if (c0 >= a.src[0].C) {
+    seg = 1;
+    cseg -= a.src[0].C;
+    if (cseg >= a.src[1].C) {
+      seg = 2;
+      cseg -= a.src[1].C;
+    }
+  }
+  const __bf16* xptr = seg == 0 ? a.src[0].ptr : (seg == 1 ? a.src[1].ptr : a.src[2].ptr);
+  const long xstride = seg == 0 ? a.src[0].stride : (seg == 1 ? a.src[1].stride : a.src[2].stride);
+  const int xper = seg == 0 ? a.src[0].period : (seg == 1 ? a.src[1].period : a.src[2].period);
+  const int ximgs = xper > 0 ? xper / HW : nimg;  // images held by the source
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(xptr, (unsigned)((long)ximgs * HW * xstride * 2));
+  const unsigned xst = (unsigned)xstride * 2;
+  const int lrow = lane >> 3;
+  int bby[SI], bbx[SI], bchk[SI];  // halo-block position of each of this lane's block rows
+#pragma unroll
+  for (int i = 0; i < SI; ++i) {
+    const int r = (wave * SI + i) * 8 + lrow;
+    bby[i] = r < G3::BH * G3::BW ? r / G3::BW : (1 << 20);  // padding rows: never in the image
+    bbx[i] = r - (r / G3::BW) * G3::BW;
+    bchk[i] = wswz<64>(lrow, lane & 7);
+  }
+
+  auto issue = [&](int step, int stage) __attribute__((always_inline)) {
+    __bf16* sA = smem + stage * STAGE;
+    __bf16* sB = sA + 64 * BM;
+    const int tile = tbeg + step;
+    const int img = tile / tiles_img;
+    const int trem = tile - img * tiles_img;
+    const int ty0 = (trem / tilesX) * TH, tx0 = (trem - (trem / tilesX) * tilesX) * TW;
+    const int pimg = img * HW;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int y = ty0 + aty[i], x = tx0 + atx[i];
+      const bool ok = a_ok && y < H && x < W;
+      const unsigned voff = ok ? (unsigned)(pimg + y * W + x) * dyst + (unsigned)(achunk * 16) : kOOB;
+      bload16(rdy, sA + (wave * AI + i) * 512, voff, (unsigned)m0 * 2);
+    }
+    const int ximg = img % ximgs;
+    const int by0 = ty0 - (KH / 2), bx0 = tx0 - (KW / 2);
+#pragma unroll
+    for (int i = 0; i < SI; ++i) {
+      const int y = by0 + bby[i], x = bx0 + bbx[i];
+      const bool ok = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+      const unsigned voff = ok ? (unsigned)((ximg * H + y) * W + x) * xst + (unsigned)(bchk[i] * 16) : kOOB;
+      bload16(rx, sB + (wave * SI + i) * 512, voff, (unsigned)cseg * 2);
+    }
+  };
+
+  f32x16 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // bias gradient via a ones B operand; step t goes to chunk t % nchunk, wave column
+  // (t / nchunk) & 1, so the extra MFMAs are spread over the grid
+  const bool do_db = a.dbslab != nullptr;
+  f32x16 accb[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accb[i][r] = 0.f;
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = static_cast<__bf16>(1.0f);
+
+  // transposed-read lane geometry: 16-lane group gi, row q within a 4-row block, column group pq
+  const int hh = lane >> 5, gi = (lane >> 4) & 1, q = (lane & 15) >> 2, pq = lane & 3;
+  // halo-block row of tile pixel k for tap (0, 0): (k / TW) * BW + k % TW; tap (ky, kx) adds ky*BW + kx
+  int brow[4][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = s * 16 + hh * 8 + q + 4 * u;
+      brow[s][u] = (k / TW) * G3::BW + (k - (k / TW) * TW);
+    }
+
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i)
+    if (i < nsteps) issue(i, i);
+
+  for (int t = 0; t < nsteps; ++t) {
+    const int ahead = (nsteps - 1 - t) < (S - 2) ? (nsteps - 1 - t) : (S - 2);
+    if (ahead >= S - 2) wait_vmcnt<(S - 2) * G>();
+    else if (ahead == 1) wait_vmcnt<G>();
+    else wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + S - 1 < nsteps) issue(t + S - 1, (t + S - 1) % S);
+    const __bf16* sA = smem + (t % S) * STAGE;
+    const __bf16* sB = sA + 64 * BM;
+    const int tq = t / nchunk;
+    const bool db_step = do_db && (t - tq * nchunk) == cc && (tq & 1) == wn;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 af[MT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int col = wm * (BM / 2) + i * 32 + gi * 16 + 4 * pq;
+        const int r0 = s * 16 + hh * 8 + q, r1 = r0 + 4;
+        const s16x4 lo = tr_read(sA + r0 * BM + wswz<BM>(r0, col >> 3) * 8 + (col & 7));
+        const s16x4 hi = tr_read(sA + r1 * BM + wswz<BM>(r1, col >> 3) * 8 + (col & 7));
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        // global 32-column tile jj = wn * NT + j  ->  tap jj / 2, channels (jj & 1) * 32 + ...
+        const int jj = wn * NT + j;
+        const int tap = jj >> 1;
+        const int ky = tap / KW, kx = tap - (tap / KW) * KW;
+        const int col = (jj & 1) * 32 + gi * 16 + 4 * pq;
+        const int r0 = brow[s][0] + ky * G3::BW + kx, r1 = brow[s][1] + ky * G3::BW + kx;
+        const s16x4 lo = tr_read(sB + r0 * 64 + wswz<64>(r0, col >> 3) * 8 + (col & 7));
+        const s16x4 hi = tr_read(sB + r1 * 64 + wswz<64>(r1, col >> 3) * 8 + (col & 7));
+        const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+      }
+      if (db_step) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) accb[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], ones, accb[i], 0, 0, 0);
+      }
+    }
+  }
+  wait_vmcnt<0>();
+  if (a.dbslab) {
+    float* sdb = reinterpret_cast<float*>(smem);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if ((lane & 31) == 0) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          sdb[wn * BM + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)] = accb[i][r];
+    }
+    __syncthreads();
+    if (tid < BM) a.dbslab[((long)split * nchunk + cc) * a.Npad + m0 + tid] = sdb[tid] + sdb[BM + tid];
+  }
+  // partial dW of this split, packed columns k = tap * Cin + c0 + c
+  float* slab = a.slab + (long)split * a.Npad * a.Kpad;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int jj = wn * NT + j;
+    const int col = (jj >> 1) * a.Cin + c0 + (jj & 1) * 32 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        slab[(long)row * a.Kpad + col] = acc[i][j][r];
       }
   }
 }
@@ -1581,61 +1485,15 @@ __global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
   }
 }
 
-// dW[n][tap][c] += sum_p dY[p][n] X[p + d_tap][c] for N <= 2: thread (tap, 8-channel chunk)
-// sweeps a pixel range (16-byte loads, coalesced across the chunks of one tap), partial
-// sums go out with one fp32 atomic per weight per workgroup; two extra lanes sum db.
-constexpr int N2_PIX = 128;
-__global__ __launch_bounds__(320) void conv_n2_wgrad_kernel(const ConvWgradArgs a) {
-  const int tid = threadIdx.x;
-  const int chunks = a.Cin / 8;
-  const int ntaps = a.KH * a.KW;
-  const long p0 = (long)blockIdx.x * N2_PIX;
-  const long p1 = p0 + N2_PIX < a.P ? p0 + N2_PIX : a.P;
-  const int HW = a.H * a.W;
-  if (tid < ntaps * chunks) {
-    const int t = tid / chunks, cl = tid - t * chunks;
-    const int ky = t / a.KW, kx = t - (t / a.KW) * a.KW;
-    const long shift = (long)(ky - a.PH) * a.W + (kx - a.PW);
-    const long stride = a.src[0].stride;
-    float s0[8], s1[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) s0[q] = s1[q] = 0.f;
-#pragma unroll 4
-    for (long p = p0; p < p1; ++p) {
-      const int rem = (int)(p % HW);
-      const int py = rem / a.W, px = rem - (rem / a.W) * a.W;
-      const int y = py + ky - a.PH, x = px + kx - a.PW;
-      if ((unsigned)y >= (unsigned)a.H || (unsigned)x >= (unsigned)a.W) continue;
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(a.src[0].ptr + (p + shift) * stride + cl * 8);
-      const float g0 = static_cast<float>(a.dy[p * a.dy_stride]);
-      const float g1 = a.N > 1 ? static_cast<float>(a.dy[p * a.dy_stride + 1]) : 0.f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float xv = static_cast<float>(v[q]);
-        s0[q] += g0 * xv;
-        s1[q] += g1 * xv;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      atomicAdd(a.dw + t * a.Cin + cl * 8 + q, s0[q]);
-      if (a.N > 1) atomicAdd(a.dw + a.Kpad + t * a.Cin + cl * 8 + q, s1[q]);
-    }
-  } else if (a.db && tid < ntaps * chunks + a.N) {
-    const int n = tid - ntaps * chunks;
-    float s = 0.f;
-    for (long p = p0; p < p1; ++p) s += static_cast<float>(a.dy[p * a.dy_stride + n]);
-    atomicAdd(a.db + n, s);
-  }
-}
-
 }  // namespace
 
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   if (a.P == 0 || a.N == 0) return hipSuccess;
   if (a.Kpad % FBK != 0) return hipErrorInvalidValue;
-  if (a.N <= 2 && a.epi == 0 && a.nsrc == 1 && a.KH * a.KW <= 9 && a.src[0].C == a.Cin &&
-      (a.Cin == 64 || a.Cin == 128 || a.Cin == 256 || a.Cin == 512) && getenv("RAFT_CONV_NO_N2") == nullptr) {
+  const int cfg = a.cfg;
+  if (cfg == 0 && a.N <= 2 && a.epi == 0 && a.nsrc == 1 && a.KH * a.KW <= 9 && a.src[0].C == a.Cin &&
+      (a.Cin == 64 || a.Cin == 128 || a.Cin == 256 || a.Cin == 512)) {
+    // narrow output (flow-head conv2): register dot products, not a GEMM
     const int lpp = a.Cin / 8;
     const int ppb = 4 * (64 / lpp);
     const long blocks = std::min<long>((a.P + ppb - 1) / ppb, 2048);
@@ -1646,162 +1504,168 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
     return hipGetLastError();
   }
   auto tiles = [&](int bm, int bn) { return (long)((a.P + bm - 1) / bm) * ((a.N + bn - 1) / bn); };
-  // largest tile that still gives >= 2 workgroups per CU (256 CUs); small-N convs use 64-wide N
-  // measured on MI355X (scripts/bench_convs.py): 64x64 tiles win for every update-block
-  // shape at B=8 (occupancy beats operand reuse at these M=22.8k GEMMs)
-  // v4 kernels (scripts/bench_convs.py on MI355X): 64x128 tiles for 64 < N <= 512, 64x64 otherwise
-  int cfg = (a.N > 64 && a.N <= 512) ? 8 : 9;
-  {
-    // v4 needs either 64-aligned K steps or a single source segment, and 32-bit offsets
-    bool uniform = (a.KH * a.KW == 1) || (a.Cin % 64 == 0 && a.src[0].C % 64 == 0 && a.src[1].C % 64 == 0);
-    long maxbytes = 0;
-    for (int i = 0; i < a.nsrc; ++i) maxbytes = std::max(maxbytes, a.P * a.src[i].stride * 2);
-    if ((!uniform && a.nsrc > 1) || maxbytes >= (1L << 31) || (long)a.N * a.Kpad * 2 >= (1L << 31)) cfg = 2;
+  // DMA kernels (v4/v5) need either 64-aligned K steps or a single source segment, and
+  // 32-bit buffer offsets; everything else takes the generic register-staged kernel
+  const bool uniform = (a.KH * a.KW == 1) || (a.Cin % 64 == 0 && a.src[0].C % 64 == 0 && a.src[1].C % 64 == 0);
+  long maxbytes = 0;
+  for (int i = 0; i < a.nsrc; ++i) maxbytes = std::max(maxbytes, a.P * a.src[i].stride * 2);
+  const bool dma_ok = (uniform || a.nsrc == 1) && maxbytes < (1L << 31) && (long)a.N * a.Kpad * 2 < (1L << 31);
+  if (!dma_ok || cfg == 1) {
+    hipLaunchKernelGGL((conv_fwd_kernel<64, 64>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
+    return hipGetLastError();
   }
-  if (const char* e = getenv("RAFT_CONV_FWD_CFG")) cfg = atoi(e);
-  if (cfg == 8 || cfg == 9 || cfg >= 20) {
-    // v5 (halo strip): multi-tap convs whose 64-channel chunks never straddle a source
-    // segment, 32-bit offsets; tile chosen by N, falling back to v4 when the strip does
-    // not fit the LDS budget
-    bool ok5 = a.KH * a.KW > 1 && a.Cin % 64 == 0 && a.N >= 64 && getenv("RAFT_CONV_NO_V5") == nullptr;
-    for (int i = 0; i < a.nsrc; ++i) ok5 = ok5 && a.src[i].C % 64 == 0;
-    for (int i = 0; i < a.nsrc; ++i) ok5 = ok5 && a.P * a.src[i].stride * 2 < (1L << 31);
-    ok5 = ok5 && (long)a.N * a.Kpad * 2 < (1L << 31) && a.P < (1L << 30);
-    // tile per shape, from scripts/bench_convs.py on MI355X (B=8, 46x62): 256x128 for wide
-    // 3x3 convs, 128x128 for 3x3 with ~128 outputs, 128x256 for the 384-channel 1x5 z||r
-    // conv; every other shape measured faster on v4
-    int v5 = cfg >= 20 ? cfg : 0;
-    if (ok5 && v5 == 0) {
-      const int taps = a.KH * a.KW;
-      if (taps == 9 && a.N >= 192) v5 = 23;
-      else if (taps == 9 && a.N > 64) v5 = 21;
-      else if (a.KH == 1 && a.KW == 5 && a.Cin >= 384 && a.N >= 256) v5 = 22;
-      else ok5 = false;
+  // v5 (halo strip): multi-tap convs whose 64-channel chunks never straddle a source segment.
+  // Tile per shape, from scripts/bench_convs.py on MI355X (B=8, 46x62): 256x128 for wide 3x3
+  // convs, 128x128 for 3x3 with ~128 outputs, 128x256 for the 384-channel 1x5 z||r conv;
+  // every other shape measured faster on v4.
+  bool ok5 = a.KH * a.KW > 1 && a.Cin % 64 == 0 && a.N >= 64 && a.P < (1L << 30);
+  for (int i = 0; i < a.nsrc; ++i) ok5 = ok5 && a.src[i].C % 64 == 0;
+  int v5 = cfg >= 20 ? cfg : 0;
+  if (ok5 && v5 == 0 && cfg == 0) {
+    const int taps = a.KH * a.KW;
+    if (taps == 9 && a.N >= 192) v5 = 23;
+    else if (taps == 9 && a.N > 64) v5 = 21;
+    else if (a.KH == 1 && a.KW == 5 && a.Cin >= 384 && a.N >= 256) v5 = 22;
+  }
+  if (ok5 && v5 >= 20) {
+    auto bm_of = [](int v) { return v == 20 ? 64 : v == 23 ? 256 : 128; };
+    auto bn_of = [](int v) { return v == 22 ? 256 : 128; };
+    auto rows_of = [&](int v) { return (bm_of(v) + (a.KH - 1) * a.W + a.KW - 1 + 7) / 8 * 8; };
+    long lds = fwd5_lds_bytes(bm_of(v5), bn_of(v5), rows_of(v5));
+    if (lds == 0 && v5 != 21) {
+      v5 = 21;
+      lds = fwd5_lds_bytes(128, 128, rows_of(v5));
     }
-    if (ok5) {
-      auto bm_of = [](int v) { return v == 20 ? 64 : v == 23 ? 256 : 128; };
-      auto bn_of = [](int v) { return v == 22 ? 256 : 128; };
-      auto rows_of = [&](int v) { return (bm_of(v) + (a.KH - 1) * a.W + a.KW - 1 + 7) / 8 * 8; };
-      long lds = fwd5_lds_bytes(bm_of(v5), bn_of(v5), rows_of(v5));
-      if (lds == 0 && v5 != 21) {
-        v5 = 21;
-        lds = fwd5_lds_bytes(128, 128, rows_of(v5));
+    const int rows = rows_of(v5);
+    if (lds > 0) {
+      const dim3 grid(tiles(bm_of(v5), bn_of(v5)));
+      switch (v5) {
+        case 23:
+          set_lds_limit((const void*)conv_fwd5_kernel<256, 128>, (int)lds);
+          hipLaunchKernelGGL((conv_fwd5_kernel<256, 128>), grid, dim3(256), lds, s, a, rows);
+          break;
+        case 20:
+          set_lds_limit((const void*)conv_fwd5_kernel<64, 128>, (int)lds);
+          hipLaunchKernelGGL((conv_fwd5_kernel<64, 128>), grid, dim3(256), lds, s, a, rows);
+          break;
+        case 22:
+          set_lds_limit((const void*)conv_fwd5_kernel<128, 256>, (int)lds);
+          hipLaunchKernelGGL((conv_fwd5_kernel<128, 256>), grid, dim3(256), lds, s, a, rows);
+          break;
+        default:
+          set_lds_limit((const void*)conv_fwd5_kernel<128, 128>, (int)lds);
+          hipLaunchKernelGGL((conv_fwd5_kernel<128, 128>), grid, dim3(256), lds, s, a, rows);
       }
-      const int rows = rows_of(v5);
-      if (lds > 0) {
-        const dim3 grid(tiles(bm_of(v5), bn_of(v5)));
-        switch (v5) {
-          case 23:
-            set_lds_limit((const void*)conv_fwd5_kernel<256, 128>, (int)lds);
-            hipLaunchKernelGGL((conv_fwd5_kernel<256, 128>), grid, dim3(256), lds, s, a, rows);
-            break;
-          case 20:
-            set_lds_limit((const void*)conv_fwd5_kernel<64, 128>, (int)lds);
-            hipLaunchKernelGGL((conv_fwd5_kernel<64, 128>), grid, dim3(256), lds, s, a, rows);
-            break;
-          case 22:
-            set_lds_limit((const void*)conv_fwd5_kernel<128, 256>,
-(int)lds);
-            hipLaunchKernelGGL((conv_fwd5_kernel<128, 256>), grid, dim3(256), lds, s, a, rows);
-            break;
-          default:
-            set_lds_limit((const void*)conv_fwd5_kernel<128, 128>,
-(int)lds);
-            hipLaunchKernelGGL((conv_fwd5_kernel<128, 128>), grid, dim3(256), lds, s, a, rows);
-        }
-        return hipGetLastError();
-      }
+      return hipGetLastError();
     }
-    if (cfg >= 20) cfg = (a.N > 64 && a.N <= 512) ? 8 : 9;
   }
-  switch (cfg) {
-    case 8:
-      hipLaunchKernelGGL((conv_fwd4_kernel<64, 128, 3>), dim3(tiles(64, 128)), dim3(256), 0, s, a);
-      break;
-    case 9:
-      hipLaunchKernelGGL((conv_fwd4_kernel<64, 64, 4>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
-      break;
-    case 10:
-      hipLaunchKernelGGL((conv_fwd4_kernel<128, 64, 3>), dim3(tiles(128, 64)), dim3(256), 0, s, a);
-      break;
-    case 4:
-      hipLaunchKernelGGL((conv_fwd3_kernel<64, 64, 4>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
-      break;
-    case 5:
-      hipLaunchKernelGGL((conv_fwd3_kernel<128, 64, 3>), dim3(tiles(128, 64)), dim3(256), 0, s, a);
-      break;
-    case 6:
-      hipLaunchKernelGGL((conv_fwd3_kernel<64, 128, 3>), dim3(tiles(64, 128)), dim3(256), 0, s, a);
-      break;
-    case 7:
-      hipLaunchKernelGGL((conv_fwd3_kernel<128, 128, 2>), dim3(tiles(128, 128)), dim3(256), 0, s, a);
-      break;
-    case 0:
-      hipLaunchKernelGGL((conv_fwd_kernel<128, 128>), dim3(tiles(128, 128)), dim3(256), 0, s, a);
-      break;
-    case 1:
-      hipLaunchKernelGGL((conv_fwd_kernel<64, 128>), dim3(tiles(64, 128)), dim3(256), 0, s, a);
-      break;
-    case 3:
-      hipLaunchKernelGGL((conv_fwd_kernel<128, 64>), dim3(tiles(128, 64)), dim3(256), 0, s, a);
-      break;
-    default:
-      hipLaunchKernelGGL((conv_fwd_kernel<64, 64>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
-  }
+  // v4 (scripts/bench_convs.py on MI355X): 64x128 tiles for 64 < N <= 512, 64x64 otherwise
+  const bool wide = cfg == 8 || (cfg != 9 && a.N > 64 && a.N <= 512);
+  if (wide)
+    hipLaunchKernelGGL((conv_fwd4_kernel<64, 128, 3>), dim3(tiles(64, 128)), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_fwd4_kernel<64, 64, 4>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_conv_wgrad(ConvWgradArgs a, hipStream_t s) {
-  if (a.P == 0 || a.N == 0) return hipSuccess;
+bool wgrad_supported(const ConvWgradArgs& a) {
   bool seg_ok = a.nsrc == 1;
   if (!seg_ok) {
     seg_ok = a.Cin % 128 == 0;
     for (int i = 0; i < a.nsrc; ++i) seg_ok = seg_ok && a.src[i].C % 128 == 0;
   }
   long maxbytes = 0;
-  for (int i = 0; i < a.nsrc; ++i) maxbytes = std::max(maxbytes, a.P * a.src[i].stride * 2);
-  const bool v2 = seg_ok && maxbytes < (1L << 31) && a.P * a.dy_stride * 2 < (1L << 31) &&
-                  getenv("RAFT_WGRAD_V1") == nullptr;
-  const bool big = a.N > 64;
-  const int BM = big ? 128 : 64, BN = 128;
-  const long tiles = (long)((a.N + BM - 1) / BM) * ((a.K + BN - 1) / BN);
-  // split the pixel reduction so ~one round of workgroups covers the 256 CUs.  Every split
-  // adds one fp32-atomic pass over its dW tile (64 KB per 128x128 tile at ~1.3 TB/s
-  // chip-wide, i.e. ~12 us of atomics per wave of 256 workgroups), so more splits than
-  // CUs cost more in atomics than they win in parallelism.
-  // One workgroup per CU (the 3-stage ring uses 96 KB of LDS).  The pixel reduction is
-  // split 8*g ways, g splits per XCD, each XCD running all tiles of its splits (<= 32 CUs),
-  // so the split's rows stay in that XCD's L2 and the grid is one round of workgroups.
-  // Measured on MI355X: a 270-workgroup grid (two rounds) with splits interleaved over the
-  // XCDs ran at ~1.8 us per 64-pixel step with 70% L2 misses.
-  // When the tiles fill less than 3/4 of an XCD that way (or exceed it), interleaved
-  // splits sized to ~one round over the chip win instead.
-  long g = 32 / tiles;
-  if (4 * g * tiles < 3 * 32) g = 0;
-  if (const char* e = getenv("RAFT_WGRAD_XCDG")) g = atol(e);
-  long splits = g > 0 ? 8 * g : std::max(1L, (256 + tiles / 2) / tiles);
-  if (const char* e = getenv("RAFT_WGRAD_SPLITS")) splits = atol(e), g = 0;
-  const long max_splits = (a.P + 255) / 256;
-  if (splits > max_splits) splits = max_splits, g = 0;
+  for (int i = 0; i < a.nsrc; ++i) {
+    const long rows = a.src[i].period > 0 ? a.src[i].period : a.P;
+    maxbytes = std::max(maxbytes, rows * a.src[i].stride * 2);
+  }
+  return seg_ok && maxbytes < (1L << 31) && a.P * a.dy_stride * 2 < (1L << 31) && a.P < (1L << 30);
+}
+
+// wgrad v3 shapes: (KH, KW) -> pixel tile (TH x TW)
+inline bool wgrad3_shape(int KH, int KW) {
+  return (KH == 1 && KW == 5) || (KH == 5 && KW == 1) || (KH == 3 && KW == 3);
+}
+
+// Split count: ~one round of workgroups over the 256 CUs.  When a whole number of splits per
+// XCD fills >= 7/8 of its 32 CUs, every tile of a split runs on one XCD (its rows are fetched
+// into that XCD's L2 once); otherwise splits are interleaved over the chip.
+inline void choose_splits(long tiles, long work_units, long& splits, long& g) {
+  g = 32 / tiles;
+  if (g * tiles < 28) g = 0;
+  splits = g > 0 ? 8 * g : std::max(1L, (256 + tiles / 2) / tiles);
+  if (splits > work_units) splits = work_units, g = 0;
   if (splits < 1) splits = 1;
+}
+
+WgradPlan plan_conv_wgrad3(const ConvWgradArgs& a) {
+  WgradPlan pl{};
+  pl.kind = 3;
+  const bool sq = a.KH == 3;
+  pl.BM = sq ? 64 : (a.N > 64 ? 128 : 64);
+  pl.BN = 64 * a.KH * a.KW;
+  pl.tilesM = (a.N + pl.BM - 1) / pl.BM;
+  pl.tilesN = a.Cin / 64;
+  pl.Npad = pl.tilesM * pl.BM;
+  const int TH = sq ? 8 : (a.KH == 5 ? 16 : 1), TW = 64 / TH;
+  const long ntiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
+  long splits, g;
+  choose_splits((long)pl.tilesM * pl.tilesN, ntiles, splits, g);
+  long per = (ntiles + splits - 1) / splits;
+  if ((ntiles + per - 1) / per != splits) g = 0;
+  pl.nsplit = (int)((ntiles + per - 1) / per);
+  pl.pix_per_split = per;
+  pl.xcd_g = (int)g;
+  return pl;
+}
+
+WgradPlan plan_conv_wgrad(const ConvWgradArgs& a) {
+  bool v3 = wgrad3_shape(a.KH, a.KW) && a.Cin % 64 == 0;
+  for (int i = 0; i < a.nsrc; ++i) v3 = v3 && a.src[i].C % 64 == 0;
+  if (v3) return plan_conv_wgrad3(a);
+  WgradPlan pl{};
+  pl.kind = 2;
+  const bool big = a.N > 64;
+  pl.BM = big ? 128 : 64;
+  pl.BN = 128;
+  pl.tilesM = (a.N + pl.BM - 1) / pl.BM;
+  pl.tilesN = (a.K + pl.BN - 1) / pl.BN;
+  pl.Npad = pl.tilesM * pl.BM;
+  long splits, g;
+  choose_splits((long)pl.tilesM * pl.tilesN, (a.P + 255) / 256, splits, g);
   long per = (a.P + splits - 1) / splits;
   per = (per + WBK - 1) / WBK * WBK;
   if ((a.P + per - 1) / per != splits) g = 0;  // rounding dropped a split: plain mapping
-  splits = (a.P + per - 1) / per;
-  a.pix_per_split = per;
-  a.xcd_g = (int)g;
-  const dim3 grid((unsigned)(tiles * splits));
-  if (v2) {
-    if (big)
-      hipLaunchKernelGGL((conv_wgrad2_kernel<128, 128, 3>), grid, dim3(256), 0, s, a);
+  pl.nsplit = (int)((a.P + per - 1) / per);
+  pl.pix_per_split = per;
+  pl.xcd_g = (int)g;
+  return pl;
+}
+
+hipError_t launch_conv_wgrad(ConvWgradArgs a, const WgradPlan& pl, hipStream_t s) {
+  if (a.P == 0 || a.N == 0) return hipSuccess;
+  if (!wgrad_supported(a)) return hipErrorInvalidValue;
+  a.pix_per_split = pl.pix_per_split;
+  a.xcd_g = pl.xcd_g;
+  a.Npad = pl.Npad;
+  const dim3 grid((unsigned)((long)pl.tilesM * pl.tilesN * pl.nsplit));
+  if (pl.kind == 3) {
+    if (a.KH == 3)
+      hipLaunchKernelGGL((conv_wgrad3_kernel<3, 3, 8, 8, 1, 3>), grid, dim3(256), 0, s, a);
+    else if (a.KH == 5 && pl.BM == 128)
+      hipLaunchKernelGGL((conv_wgrad3_kernel<5, 1, 16, 4, 2, 3>), grid, dim3(256), 0, s, a);
+    else if (a.KH == 5)
+      hipLaunchKernelGGL((conv_wgrad3_kernel<5, 1, 16, 4, 1, 3>), grid, dim3(256), 0, s, a);
+    else if (pl.BM == 128)
+      hipLaunchKernelGGL((conv_wgrad3_kernel<1, 5, 1, 64, 2, 3>), grid, dim3(256), 0, s, a);
     else
-      hipLaunchKernelGGL((conv_wgrad2_kernel<64, 128, 3>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((conv_wgrad3_kernel<1, 5, 1, 64, 1, 3>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
   }
-  if (big)
-    hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, s, a);
+  if (pl.BM == 128)
+    hipLaunchKernelGGL((conv_wgrad2_kernel<128, 128, 3>), grid, dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_wgrad2_kernel<64, 128, 3>), grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

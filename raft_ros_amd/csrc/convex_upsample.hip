@@ -63,8 +63,8 @@ __global__ __launch_bounds__(256) void convex_up_fwd_kernel(const float* __restr
 template <typename MT>
 __global__ __launch_bounds__(256) void convex_up_bwd_kernel(
     const float* __restrict__ flow, const MT* __restrict__ mask, long msN, long msC, long msH,
-    long msW, const float* __restrict__ gout, MT* __restrict__ dmask, float* __restrict__ part,
-    int B, int H, int W) {
+    long msW, const float* __restrict__ gout, MT* __restrict__ dmask, long dsN, long dsC, long dsH, long dsW,
+    float* __restrict__ part, int B, int H, int W) {
   const int lane = threadIdx.x & 63;
   const long pix = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (pix >= (long)B * H * W) return;
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void convex_up_bwd_kernel(
   }
 #pragma unroll
   for (int k = 0; k < 9; ++k)
-    dmask[moff + (long)(k * 64 + lane) * msC] = from_f32<MT>(p[k] * (gv[k] - dot));
+    dmask[b * dsN + y * dsH + x * dsW + (long)(k * 64 + lane) * dsC] = from_f32<MT>(p[k] * (gv[k] - dot));
   // d flow(neighbour k, c) = sum over the 64 sub-pixels of 8 * p_k * g_c
   float* pt = part + (long)b * 18 * HW + (long)y * W + x;
 #pragma unroll
@@ -143,6 +143,38 @@ __global__ __launch_bounds__(256) void convex_up_gather_kernel(const float* __re
   dflow[idx] = s;
 }
 
+// Per low-res pixel: both flow-gradient channels, written as (P, ld) bf16 rows [du, dv, 0..0]
+// (the dY operand of the flow head's last conv in the fused update block) and optionally fp32.
+__global__ __launch_bounds__(256) void convex_up_gather_rows_kernel(const float* __restrict__ part,
+                                                                    __bf16* __restrict__ rows, int ld,
+                                                                    float* __restrict__ dflow, int B, int H,
+                                                                    int W) {
+  const long HW = (long)H * W;
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (long)B * HW) return;
+  const int x = p % W;
+  const int y = (p / W) % H;
+  const int b = p / HW;
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int yy = y - (k / 3) + 1, xx = x - (k % 3) + 1;
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+      const long o = ((long)b * 18 + k * 2) * HW + yy * W + xx;
+      s0 += part[o];
+      s1 += part[o + HW];
+    }
+  }
+  __bf16* r = rows + p * ld;
+  r[0] = static_cast<__bf16>(s0);
+  r[1] = static_cast<__bf16>(s1);
+  for (int c = 2; c < ld; ++c) r[c] = static_cast<__bf16>(0.f);
+  if (dflow) {
+    dflow[(long)b * 2 * HW + y * W + x] = s0;
+    dflow[(long)b * 2 * HW + HW + y * W + x] = s1;
+  }
+}
+
 }  // namespace
 
 hipError_t launch_convex_up_fwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
@@ -163,24 +195,30 @@ hipError_t launch_convex_up_fwd(const float* flow, const void* mask, int m_dtype
 }
 
 hipError_t launch_convex_up_bwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
-                                long msH, long msW, const float* gout, void* dmask, float* part,
-                                float* dflow, int B, int H, int W, hipStream_t s) {
+                                long msH, long msW, const float* gout, void* dmask, long dsN, long dsC,
+                                long dsH, long dsW, float* part, float* dflow, void* rows, int rows_ld, int B,
+                                int H, int W, hipStream_t s) {
   const long npix = (long)B * H * W;
   if (npix == 0) return hipSuccess;
   const dim3 g((npix + 3) / 4), blk(256);
   if (m_dtype == kBF16)
     hipLaunchKernelGGL(convex_up_bwd_kernel<__bf16>, g, blk, 0, s, flow,
                        static_cast<const __bf16*>(mask), msN, msC, msH, msW, gout,
-                       static_cast<__bf16*>(dmask), part, B, H, W);
+                       static_cast<__bf16*>(dmask), dsN, dsC, dsH, dsW, part, B, H, W);
   else if (m_dtype == kF16)
     hipLaunchKernelGGL(convex_up_bwd_kernel<_Float16>, g, blk, 0, s, flow,
                        static_cast<const _Float16*>(mask), msN, msC, msH, msW, gout,
-                       static_cast<_Float16*>(dmask), part, B, H, W);
+                       static_cast<_Float16*>(dmask), dsN, dsC, dsH, dsW, part, B, H, W);
   else
     hipLaunchKernelGGL(convex_up_bwd_kernel<float>, g, blk, 0, s, flow,
                        static_cast<const float*>(mask), msN, msC, msH, msW, gout,
-                       static_cast<float*>(dmask), part, B, H, W);
+                       static_cast<float*>(dmask), dsN, dsC, dsH, dsW, part, B, H, W);
   RAFT_HIP_CHECK(hipGetLastError());
+  if (rows) {
+    hipLaunchKernelGGL(convex_up_gather_rows_kernel, dim3((npix + 255) / 256), blk, 0, s, part,
+                       static_cast<__bf16*>(rows), rows_ld, dflow, B, H, W);
+    return hipGetLastError();
+  }
   const long tot = (long)B * 2 * H * W;
   hipLaunchKernelGGL(convex_up_gather_kernel, dim3((tot + 255) / 256), blk, 0, s, part, dflow, B, H,
                      W);

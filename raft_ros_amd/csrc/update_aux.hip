@@ -12,7 +12,11 @@
 //   masked_cast: out_bf16 = src_fp32 * (mask > 0)   (ReLU' + cast for the next dy)
 //   pack_flow:  (B, 2, H, W) fp32 flow -> (P, 8) bf16 [u, v, 0...] and the two
 //               flow channels of the motion-feature buffer (torch.cat in
-//               BasicMotionEncoder.forward, core/update.py:96)
+//               BasicMotionEncoder.forward, core/update.py:96); with from_coords
+//               the input is coords1 and flow = coords1 - coords0 is formed here
+//               (coords0 = the pixel grid, core/raft.py:63-70,126)
+//   apply_delta: coords1 += delta (the flow head output, core/raft.py:131) and the
+//               new low-resolution flow = coords1 - coords0 for the upsampler
 #include "common.h"
 
 namespace raft_amd {
@@ -72,12 +76,17 @@ __global__ __launch_bounds__(256) void masked_cast_kernel(const float* __restric
 __global__ __launch_bounds__(256) void pack_flow_kernel(const float* __restrict__ flow,
                                                         __bf16* __restrict__ flow8,
                                                         __bf16* __restrict__ motion, long smo, int B,
-                                                        int HW) {
+                                                        int HW, int W, int from_coords) {
   const long p = (long)blockIdx.x * 256 + threadIdx.x;
   if (p >= (long)B * HW) return;
   const int b = p / HW;
   const int s = p - (long)b * HW;
-  const float u = flow[(long)b * 2 * HW + s], v = flow[(long)b * 2 * HW + HW + s];
+  float u = flow[(long)b * 2 * HW + s], v = flow[(long)b * 2 * HW + HW + s];
+  if (from_coords) {
+    const int y = s / W;
+    u -= (float)(s - y * W);
+    v -= (float)y;
+  }
   bf16x8 o;
 #pragma unroll
   for (int k = 0; k < 8; ++k) o[k] = static_cast<__bf16>(0.f);
@@ -88,6 +97,24 @@ __global__ __launch_bounds__(256) void pack_flow_kernel(const float* __restrict_
     motion[p * smo] = o[0];
     motion[p * smo + 1] = o[1];
   }
+}
+
+// coords_out = coords1 + delta[:, :2]; flow_out = coords_out - grid  (both (B, 2, H, W) fp32)
+__global__ __launch_bounds__(256) void apply_delta_kernel(const float* __restrict__ coords1,
+                                                          const float* __restrict__ delta, long sd,
+                                                          float* __restrict__ coords_out,
+                                                          float* __restrict__ flow_out, int B, int HW, int W) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (long)B * HW) return;
+  const int b = p / HW;
+  const int s = p - (long)b * HW;
+  const int y = s / W;
+  const long i0 = (long)b * 2 * HW + s, i1 = i0 + HW;
+  const float cx = coords1[i0] + delta[p * sd], cy = coords1[i1] + delta[p * sd + 1];
+  coords_out[i0] = cx;
+  coords_out[i1] = cy;
+  flow_out[i0] = cx - (float)(s - y * W);
+  flow_out[i1] = cy - (float)y;
 }
 
 inline dim3 grid1(long n) { return dim3((unsigned)((n + 255) / 256)); }
@@ -121,12 +148,21 @@ hipError_t launch_masked_cast(const float* src, long ss, const void* mask, long 
   return hipGetLastError();
 }
 
-hipError_t launch_pack_flow(const float* flow, void* flow8, void* motion, long smo, int B, int HW,
-                            hipStream_t s) {
+hipError_t launch_pack_flow(const float* flow, void* flow8, void* motion, long smo, int B, int HW, int W,
+                            int from_coords, hipStream_t s) {
   const long P = (long)B * HW;
   if (!P) return hipSuccess;
   hipLaunchKernelGGL(pack_flow_kernel, grid1(P), dim3(256), 0, s, flow, (__bf16*)flow8, (__bf16*)motion,
-                     smo, B, HW);
+                     smo, B, HW, W, from_coords);
+  return hipGetLastError();
+}
+
+hipError_t launch_apply_delta(const float* coords1, const float* delta, long sd, float* coords_out,
+                              float* flow_out, int B, int HW, int W, hipStream_t s) {
+  const long P = (long)B * HW;
+  if (!P) return hipSuccess;
+  hipLaunchKernelGGL(apply_delta_kernel, grid1(P), dim3(256), 0, s, coords1, delta, sd, coords_out, flow_out, B,
+                     HW, W);
   return hipGetLastError();
 }
 

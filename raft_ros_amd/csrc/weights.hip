@@ -1,0 +1,224 @@
+// Weight-side glue of the fused update block, as two HIP kernels instead of
+// ~10 PyTorch ops per conv per step (ops/update_fused.py):
+//
+//   pack_conv_weights: fp32 module parameters -> the bf16 GEMM operands of one
+//     implicit-GEMM conv (reference parameter layout: core/update.py, Conv2d
+//     weight (Cout, Cin, kh, kw) in any memory format):
+//       forward  wf[n][tap*Cin_pad + c]                = s * W[n][c][ky][kx]
+//       dgrad    wd[c][tapflip*Cout_pad + n]           = s * W[n][c][ky][kx]
+//       bias     bf[n]                                 = s * b[n]
+//     Up to two parameters are stacked along N (z||r GRU gates, flow head ||
+//     mask head), input channels can be re-laid into padded segments (corr
+//     features 324 -> 328, flow 2 -> 8), padding is zero.
+//   wgrad_reduce: the per-split fp32 partial slabs of a weight-gradient launch
+//     (csrc/conv_igemm.hip) are summed in a fixed split order (deterministic)
+//     and written -- scaled, un-padded, split back into the stacked
+//     parameters, in the parameters' own strides -- straight into the
+//     parameter gradients, or accumulated into a packed fp32 [N][Kpad] buffer.
+#include "common.h"
+
+namespace raft_amd {
+
+struct ConvParamDesc {
+  float* w[2];     // parameter (pack: read) / gradient (reduce: written) tensors
+  long ws[2][4];   // strides (Cout, Cin, kh, kw) in elements
+  float* b[2];     // biases / bias gradients (may be null)
+  int rows[2];     // Cout of each stacked parameter (rows[1] = 0: single)
+  int nseg;
+  int seg_real[3], seg_pad[3];
+  int Cin, Cin_pad, KH, KW;
+  float scale;
+};
+
+namespace {
+
+// padded input channel -> real channel (-1 for a padding slot)
+__device__ __forceinline__ int real_channel(const ConvParamDesc& d, int cp) {
+  int r0 = 0, p0 = 0;
+  for (int i = 0; i < d.nseg; ++i) {
+    if (cp < p0 + d.seg_pad[i]) {
+      const int o = cp - p0;
+      return o < d.seg_real[i] ? r0 + o : -1;
+    }
+    r0 += d.seg_real[i];
+    p0 += d.seg_pad[i];
+  }
+  return -1;
+}
+
+// real input channel -> padded channel
+__device__ __forceinline__ int padded_channel(const ConvParamDesc& d, int c) {
+  int r0 = 0, p0 = 0;
+  for (int i = 0; i < d.nseg; ++i) {
+    if (c < r0 + d.seg_real[i]) return p0 + (c - r0);
+    r0 += d.seg_real[i];
+    p0 += d.seg_pad[i];
+  }
+  return -1;
+}
+
+__device__ __forceinline__ float param_at(const ConvParamDesc& d, int n, int c, int ky, int kx) {
+  const int which = n < d.rows[0] ? 0 : 1;
+  const int nn = which == 0 ? n : n - d.rows[0];
+  const float* w = d.w[which];
+  return w[nn * d.ws[which][0] + c * d.ws[which][1] + ky * d.ws[which][2] + kx * d.ws[which][3]];
+}
+
+__global__ __launch_bounds__(256) void pack_conv_weights_kernel(ConvParamDesc d, int N, __bf16* __restrict__ wf,
+                                                                int Kf, __bf16* __restrict__ wd, int Kd,
+                                                                int Cout_pad, float* __restrict__ bias) {
+  const int taps = d.KH * d.KW;
+  const long nf = (long)N * Kf;
+  const long nd = wd ? (long)d.Cin_pad * Kd : 0;
+  const long total = nf + nd + N;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    if (i < nf) {
+      const int n = (int)(i / Kf), k = (int)(i - (long)n * Kf);
+      float v = 0.f;
+      const int tap = k / d.Cin_pad;
+      if (tap < taps) {
+        const int c = real_channel(d, k - tap * d.Cin_pad);
+        if (c >= 0) v = d.scale * param_at(d, n, c, tap / d.KW, tap - (tap / d.KW) * d.KW);
+      }
+      wf[i] = static_cast<__bf16>(v);
+    } else if (i < nf + nd) {
+      const long j = i - nf;
+      const int cp = (int)(j / Kd), k = (int)(j - (long)cp * Kd);
+      float v = 0.f;
+      const int tapf = k / Cout_pad, n = k - tapf * Cout_pad;
+      if (tapf < taps && n < N) {
+        const int c = real_channel(d, cp);
+        const int kyf = tapf / d.KW, kxf = tapf - kyf * d.KW;
+        if (c >= 0) v = d.scale * param_at(d, n, c, d.KH - 1 - kyf, d.KW - 1 - kxf);
+      }
+      wd[j] = static_cast<__bf16>(v);
+    } else {
+      const int n = (int)(i - nf - nd);
+      const int which = n < d.rows[0] ? 0 : 1;
+      const float* b = d.b[which];
+      bias[n] = b ? d.scale * b[which == 0 ? n : n - d.rows[0]] : 0.f;
+    }
+  }
+}
+
+// Both reduce kernels: block = 64 consecutive packed columns k of one row n (lane = column),
+// its 4 waves sum interleaved subsets of the splits (so a 128-split reduction keeps 32
+// independent loads per lane in flight instead of 128 dependent ones), LDS combines the 4
+// partial sums in a fixed order.  Blocks past the weight rows reduce the bias partials.
+__device__ __forceinline__ float split_sum(const float* __restrict__ src, long sstride, int nsplit, int wave) {
+  float v = 0.f;
+#pragma unroll 8
+  for (int sp = wave; sp < nsplit; sp += 4) v += src[sp * sstride];
+  return v;
+}
+
+__device__ __forceinline__ float combine4(float v, float* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  red[wave * 64 + lane] = v;
+  __syncthreads();
+  return ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
+}
+
+// Parameter-layout output (scaled, un-padded, split into the stacked parameters).
+__global__ __launch_bounds__(256) void wgrad_reduce_params_kernel(const float* __restrict__ slab, int nsplit,
+                                                                  int Npad, int Kpad,
+                                                                  const float* __restrict__ dbslab, int ndb,
+                                                                  ConvParamDesc d, int N, int accumulate) {
+  __shared__ float red[256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kch = (d.KH * d.KW * d.Cin_pad + 63) / 64;
+  const long blk = blockIdx.x;
+  if (blk < (long)N * kch) {
+    const int n = (int)(blk / kch);
+    const int k = (int)(blk - (long)n * kch) * 64 + lane;
+    const int tap = k / d.Cin_pad;
+    const bool live = tap < d.KH * d.KW;
+    const float v = combine4(live ? split_sum(slab + (long)n * Kpad + k, (long)Npad * Kpad, nsplit, wave) : 0.f,
+                             red);
+    if (wave != 0 || !live) return;
+    const int c = real_channel(d, k - tap * d.Cin_pad);
+    if (c < 0) return;
+    const int which = n < d.rows[0] ? 0 : 1;
+    const int nn = which == 0 ? n : n - d.rows[0];
+    const int ky = tap / d.KW, kx = tap - ky * d.KW;
+    float* o = d.w[which] + nn * d.ws[which][0] + c * d.ws[which][1] + ky * d.ws[which][2] + kx * d.ws[which][3];
+    *o = accumulate ? *o + d.scale * v : d.scale * v;
+  } else {
+    const int n = (int)(blk - (long)N * kch) * 64 + lane;
+    float v = 0.f;
+    if (n < N)
+      for (int j = wave; j < ndb; j += 4) v += dbslab[(long)j * Npad + n];
+    v = combine4(v, red);
+    if (wave != 0 || n >= N) return;
+    const int which = n < d.rows[0] ? 0 : 1;
+    float* b = d.b[which];
+    if (b) {
+      float* o = b + (which == 0 ? n : n - d.rows[0]);
+      *o = accumulate ? *o + d.scale * v : d.scale * v;
+    }
+  }
+}
+
+// Packed output: dw[n][k] (+)= sum_s slab[s][n][k] for n < N, k < Kpad; db[n] (+)= sum of partials.
+__global__ __launch_bounds__(256) void wgrad_reduce_packed_kernel(const float* __restrict__ slab, int nsplit,
+                                                                  int Npad, int Kpad, int K,
+                                                                  const float* __restrict__ dbslab, int ndb,
+                                                                  float* __restrict__ dw, long ldw,
+                                                                  float* __restrict__ db, int N, int accumulate) {
+  __shared__ float red[256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kch = Kpad / 64;
+  const long blk = blockIdx.x;
+  if (blk < (long)N * kch) {
+    const int n = (int)(blk / kch);
+    const int k = (int)(blk - (long)n * kch) * 64 + lane;
+    // slab columns past K may be unwritten
+    const float v = combine4(k < K ? split_sum(slab + (long)n * Kpad + k, (long)Npad * Kpad, nsplit, wave) : 0.f,
+                             red);
+    if (wave != 0) return;
+    float* o = dw + (long)n * ldw + k;
+    *o = accumulate ? *o + v : v;
+  } else {
+    const int n = (int)(blk - (long)N * kch) * 64 + lane;
+    float v = 0.f;
+    if (n < N)
+      for (int j = wave; j < ndb; j += 4) v += dbslab[(long)j * Npad + n];
+    v = combine4(v, red);
+    if (wave != 0 || n >= N || !db) return;
+    db[n] = accumulate ? db[n] + v : v;
+  }
+}
+
+inline dim3 grid_of(long total) {
+  long b = (total + 255) / 256;
+  return dim3((unsigned)(b < 8192 ? (b > 0 ? b : 1) : 8192));
+}
+
+}  // namespace
+
+hipError_t launch_pack_conv_weights(const ConvParamDesc& d, int N, void* wf, int Kf, void* wd, int Kd, int Cout_pad,
+                                    float* bias, hipStream_t s) {
+  const long total = (long)N * Kf + (wd ? (long)d.Cin_pad * Kd : 0) + N;
+  hipLaunchKernelGGL(pack_conv_weights_kernel, grid_of(total), dim3(256), 0, s, d, N, static_cast<__bf16*>(wf), Kf,
+                     static_cast<__bf16*>(wd), Kd, Cout_pad, bias);
+  return hipGetLastError();
+}
+
+hipError_t launch_wgrad_reduce_params(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, int ndb,
+                                      const ConvParamDesc& d, int N, int accumulate, hipStream_t s) {
+  const long kch = (d.KH * d.KW * d.Cin_pad + 63) / 64;
+  const long blocks = (long)N * kch + (dbslab ? (N + 63) / 64 : 0);
+  hipLaunchKernelGGL(wgrad_reduce_params_kernel, dim3((unsigned)blocks), dim3(256), 0, s, slab, nsplit, Npad, Kpad,
+                     dbslab, ndb, d, N, accumulate);
+  return hipGetLastError();
+}
+
+hipError_t launch_wgrad_reduce_packed(const float* slab, int nsplit, int Npad, int Kpad, int K, const float* dbslab,
+                                      int ndb, float* dw, long ldw, float* db, int N, int accumulate, hipStream_t s) {
+  const long blocks = (long)N * (Kpad / 64) + (db ? (N + 63) / 64 : 0);
+  hipLaunchKernelGGL(wgrad_reduce_packed_kernel, dim3((unsigned)blocks), dim3(256), 0, s, slab, nsplit, Npad, Kpad, K,
+                     dbslab, ndb, dw, ldw, db, N, accumulate);
+  return hipGetLastError();
+}
+
+}  // namespace raft_amd

@@ -168,21 +168,22 @@ class RAFT(nn.Module):
                 and update_fused.supported(self.update_block) and use_native(image1))
 
     def _forward_fused(self, corr_fn, net, inp, coords0, coords1, iters: int, test_mode: bool):
-        """Refinement loop with the update block on fused HIP implicit-GEMM kernels
-        (raft_ros_amd/ops/update_fused.py); same math as the loop above."""
-        upd = update_fused.FusedBasicUpdate(self.update_block, inp)
+        """Refinement loop on the fused HIP step (raft_ros_amd/ops/update_fused.py): lookup,
+        update block, coords update and convex upsampling as one autograd node per
+        iteration, weight gradients batched over all iterations; same math as the loop
+        above."""
+        dense = isinstance(corr_fn, CorrPyramid)
+        upd = update_fused.FusedBasicUpdate(self.update_block, inp, iters,
+                                            pyramid=corr_fn.state if dense else None)
         flow_predictions = []
         flow_up = None
-        for _ in range(iters):
-            coords1 = coords1.detach()
-            if isinstance(corr_fn, CorrPyramid):
-                corr = corr_fn.lookup_padded(coords1, update_fused.CORR_PAD)
+        for t in range(iters):
+            if dense:
+                net, flow_up, coords1 = upd.step(t, net, coords1, ptoken=corr_fn.token)
             else:
-                c = corr_fn(coords1, out_dtype=torch.bfloat16).permute(0, 2, 3, 1)
-                corr = torch.nn.functional.pad(c, (0, update_fused.CORR_PAD - c.shape[-1])).contiguous()
-            net, up_mask, delta_flow = upd(net, corr, coords1 - coords0)
-            coords1 = coords1 + delta_flow
-            flow_up = self.upsample_flow(coords1 - coords0, up_mask)
+                c = corr_fn(coords1.detach(), out_dtype=torch.bfloat16).permute(0, 2, 3, 1)
+                corr = torch.nn.functional.pad(c, (0, update_fused.CORR_PAD - c.shape[-1]))
+                net, flow_up, coords1 = upd.step(t, net, coords1, corr=corr)
             flow_predictions.append(flow_up)
         if test_mode:
             return coords1 - coords0, flow_up

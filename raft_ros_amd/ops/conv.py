@@ -96,10 +96,41 @@ EPI_STORE, EPI_GRAD, EPI_GRU_ZR, EPI_GRU_Q = 0, 1, 2, 3
 
 
 def conv_fwd(srcs, wt, g, N, out, bias=None, act=0, alpha=1.0, epi=EPI_STORE, acc_c0=1 << 30, mask=None,
-             h=None, z=None, out2=None):
-    ops().conv_fwd(list(srcs), wt, g, N, bias, epi, act, alpha, out, acc_c0, mask, h, z, out2)
+             h=None, z=None, out2=None, cfg: int = 0):
+    """``cfg`` forces a kernel variant (0 = automatic; tests and microbenchmarks only):
+    1 generic, 8/9 v4 64x128/64x64, 20/21/22/23 v5 halo strip 64x128/128x128/128x256/256x128."""
+    ops().conv_fwd(list(srcs), wt, g, N, bias, epi, act, alpha, out, acc_c0, mask, h, z, out2, cfg)
     return out
 
 
-def conv_wgrad(srcs, dy, g, N, dw, db=None):
-    ops().conv_wgrad(list(srcs), dy, g, N, dw, db)
+def conv_wgrad(srcs, dy, g, N, dw, db=None, accumulate: bool = True):
+    """dw[N][Kpad] (+)= weight gradient in the packed layout (deterministic split reduction)."""
+    ops().conv_wgrad(list(srcs), dy, g, N, dw, db, accumulate)
+
+
+def flat_segments(segments: Sequence[Tuple[int, int]]) -> List[int]:
+    return [v for rp in segments for v in rp]
+
+
+def conv_wgrad_params(srcs, dy, g, wgrads, bgrads, segments, scale: float = 1.0, accumulate: bool = False):
+    """Weight (+bias) gradients of 1..2 stacked conv parameters written straight into
+    ``wgrads`` / ``bgrads`` (parameter layout, any strides).  A source with fewer rows
+    than the pixel count is periodic (row p % rows), e.g. context features shared by
+    every refinement iteration of a batched update-block weight gradient."""
+    ops().conv_wgrad_params(list(srcs), dy, g, list(wgrads), list(bgrads), flat_segments(segments), scale,
+                            accumulate)
+
+
+def pack_weights(weights, biases, segments, scale: float = 1.0, dgrad: bool = True):
+    """One HIP launch: fp32 parameters (1..2 stacked along Cout) -> (wf [N][Kpad] bf16,
+    wd [Cin_pad][Kpad'] bf16 or None, bias fp32 [N]) -- the layouts of ``pack_fwd`` /
+    ``pack_dgrad``."""
+    cout = sum(w.shape[0] for w in weights)
+    _, cin, kh, kw = weights[0].shape
+    cin_p = sum(p for _, p in segments)
+    cout_p = _round(cout, 8)
+    kf = _round(kh * kw * cin_p, KBLK)
+    kd = _round(kh * kw * cout_p, KBLK) if dgrad else 0
+    w = [t.detach() for t in weights]
+    b = [None if t is None else t.detach() for t in biases]
+    return ops().pack_conv_weights(w, b, flat_segments(segments), scale, kf, kd, cout_p)

@@ -1,31 +1,37 @@
-"""Fused RAFT-base update block on hand-written HIP kernels (forward + backward).
+"""Fused RAFT-base refinement step on hand-written HIP kernels (forward + backward).
 
-One refinement iteration of ``BasicUpdateBlock`` (reference core/update.py:79-136:
-BasicMotionEncoder -> SepConvGRU -> FlowHead + mask head) runs as 11
-implicit-GEMM MFMA convolutions with fused epilogues (``csrc/conv_igemm.hip``)
-instead of ~300 PyTorch/MIOpen launches:
+One refinement iteration (reference core/raft.py:122-139 + core/update.py:79-136:
+corr lookup -> BasicMotionEncoder -> SepConvGRU -> FlowHead + mask head ->
+coords update -> convex upsampling) is ONE autograd node, ``_Step``, whose
+forward runs 16 HIP launches:
 
-  corr (P, 328) --convc1 1x1+relu--> c1 --convc2 3x3+relu--> cf[:, :192]
-  flow8 (P, 8)  --convf1 7x7+relu--> f1 --convf2 3x3+relu--> cf[:, 192:]
-  cf --conv 3x3+relu--> motion[:, :126]   (motion[:, 126:] = flow: fused cat)
+  lookup (4 levels x 81 taps)          -> corr (P, 328)             [corr_lookup_into]
+  coords1 - grid                       -> flow8 (P, 8), motion[:, 126:]   [pack_flow]
+  corr --convc1 1x1+relu--> c1 --convc2 3x3+relu--> cf[:, :192]
+  flow8 --convf1 7x7+relu--> f1 --convf2 3x3+relu--> cf[:, 192:]
+  cf --conv 3x3+relu--> motion[:, :126]
   [h | inp | motion] --z||r 1x5 (sigmoid, r*h epilogue)--> zr, rh
   [rh | inp | motion] --q 1x5 (tanh + GRU blend epilogue)--> h1          (x2: 5x1)
   h2 --[flow_head.conv1 || mask.0] 3x3+relu (one 512-wide conv)--> hd
-  hd[:, :256] --flow_head.conv2 3x3--> delta (fp32);  hd[:, 256:] --0.25*mask.2 1x1--> mask
+  hd[:, :256] --flow_head.conv2 3x3--> delta;  hd[:, 256:] --0.25*mask.2 1x1--> mask
+  coords1 + delta, flow = coords1 - grid   [apply_delta];  convex 8x upsample
 
-The backward is hand-scheduled: dgrad convs (same kernel, flipped weights) with
-ReLU' masks and partial accumulation in the epilogue, wgrad kernels that
-accumulate every iteration's weight/bias gradients in place into persistent
-fp32 buffers, and four small elementwise kernels for the GRU gate derivatives.
+Weight gradients are NOT computed per iteration.  The weights are shared by
+every iteration (core/raft.py:122-139), so each step's backward only stores its
+output gradients dY (bf16) in a per-forward arena, next to the activations its
+forward stored there; ``_PackWeights.backward`` -- which autograd runs after
+the last step's backward, since every step consumes its token -- then runs ONE
+weight-gradient GEMM per conv over all ``iters * P`` pixels (the context
+features, shared by all iterations, are a periodic source) and writes the
+parameter gradients directly (csrc/weights.hip: fixed-order split reduction,
+so the result is deterministic).  The dgrad chain stays per iteration.
 
-Weights are packed (bf16, GEMM layout, forward and data-grad variants) ONCE
-per RAFT forward by ``_PackWeights``; its backward -- which autograd runs after
-the last iteration's backward because every step consumes its token -- turns
-the accumulated fp32 buffers into the parameters' gradients.
+Weights are packed (bf16 GEMM operands, forward and data-grad variants) by one
+HIP launch per conv per RAFT forward (``ops.conv.pack_weights``).
 """
 from __future__ import annotations
 
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -34,109 +40,32 @@ from ._ext import ops
 
 HID = 128
 CORR_PAD = 328  # 4 * 81 = 324 lookup channels, padded to a multiple of 8
+_I32 = (1 << 31) - 1
 
-
-def _layers(block) -> List[Tuple[str, torch.nn.Conv2d]]:
-    enc, gru = block.encoder, block.gru
-    return [
-        ("convc1", enc.convc1), ("convc2", enc.convc2), ("convf1", enc.convf1), ("convf2", enc.convf2),
-        ("conv", enc.conv),
-        ("zr1", (gru.convz1, gru.convr1)), ("q1", gru.convq1),
-        ("zr2", (gru.convz2, gru.convr2)), ("q2", gru.convq2),
-        ("heads", (block.flow_head.conv1, block.mask[0])), ("fh2", block.flow_head.conv2), ("mask2", block.mask[2]),
-    ]
-
-
-# input-channel segment layout (real, padded) of every conv
-SEGMENTS: Dict[str, List[Tuple[int, int]]] = {
-    "convc1": [(324, CORR_PAD)],
-    "convc2": [(256, 256)],
-    "convf1": [(2, 8)],
-    "convf2": [(128, 128)],
-    "conv": [(256, 256)],
-    "zr1": [(384, 384)], "q1": [(384, 384)], "zr2": [(384, 384)], "q2": [(384, 384)],
-    "heads": [(128, 128)],
-    "fh2": [(256, 256)],
-    "mask2": [(256, 256)],
-}
-SCALE = {"mask2": 0.25}
+# name -> (modules getter, input segments (real, padded), output scale, needs a dgrad operand)
+_LAYERS = [
+    ("convc1", lambda b: (b.encoder.convc1,), [(324, CORR_PAD)], 1.0, True),
+    ("convc2", lambda b: (b.encoder.convc2,), [(256, 256)], 1.0, True),
+    ("convf1", lambda b: (b.encoder.convf1,), [(2, 8)], 1.0, False),
+    ("convf2", lambda b: (b.encoder.convf2,), [(128, 128)], 1.0, True),
+    ("conv", lambda b: (b.encoder.conv,), [(256, 256)], 1.0, True),
+    ("zr1", lambda b: (b.gru.convz1, b.gru.convr1), [(128, 128)] * 3, 1.0, True),
+    ("q1", lambda b: (b.gru.convq1,), [(128, 128)] * 3, 1.0, True),
+    ("zr2", lambda b: (b.gru.convz2, b.gru.convr2), [(128, 128)] * 3, 1.0, True),
+    ("q2", lambda b: (b.gru.convq2,), [(128, 128)] * 3, 1.0, True),
+    ("heads", lambda b: (b.flow_head.conv1, b.mask[0]), [(128, 128)], 1.0, True),
+    ("fh2", lambda b: (b.flow_head.conv2,), [(256, 256)], 1.0, True),
+    ("mask2", lambda b: (b.mask[2],), [(256, 256)], 0.25, True),  # core/update.py:135
+]
+SEGMENTS = {name: segs for name, _, segs, _, _ in _LAYERS}
 
 
 def _params(block) -> List[torch.Tensor]:
     out = []
-    for _, m in _layers(block):
-        mods = m if isinstance(m, tuple) else (m,)
-        for mod in mods:
-            out += [mod.weight, mod.bias]
+    for _, mods, _, _, _ in _LAYERS:
+        for m in mods(block):
+            out += [m.weight, m.bias]
     return out
-
-
-class _WeightState:
-    """Packed weights of one RAFT forward + fp32 gradient accumulators."""
-
-    def __init__(self, block):
-        self.wf: Dict[str, torch.Tensor] = {}
-        self.wd: Dict[str, torch.Tensor] = {}
-        self.bias: Dict[str, torch.Tensor] = {}
-        self.shape: Dict[str, tuple] = {}
-        self.split: Dict[str, List[int]] = {}
-        self.cout: Dict[str, int] = {}
-        for name, m in _layers(block):
-            mods = m if isinstance(m, tuple) else (m,)
-            w = torch.cat([mm.weight for mm in mods], dim=0) if len(mods) > 1 else mods[0].weight
-            b = torch.cat([mm.bias for mm in mods], dim=0) if len(mods) > 1 else mods[0].bias
-            s = SCALE.get(name, 1.0)
-            segs = SEGMENTS[name]
-            self.shape[name] = tuple(w.shape)
-            self.split[name] = [mm.weight.shape[0] for mm in mods]
-            self.cout[name] = w.shape[0]
-            self.wf[name] = C.pack_fwd(w, segs, scale=s)
-            self.wd[name] = C.pack_dgrad(w, segs, scale=s)
-            self.bias[name] = (b.detach().float() * s).contiguous()
-        self.dw: Dict[str, torch.Tensor] = {}
-        self.db: Dict[str, torch.Tensor] = {}
-
-    def grad_bufs(self, name):
-        if name not in self.dw:
-            wf = self.wf[name]
-            self.dw[name] = torch.zeros(wf.shape, device=wf.device, dtype=torch.float32)
-            self.db[name] = torch.zeros(wf.shape[0], device=wf.device, dtype=torch.float32)
-        return self.dw[name], self.db[name]
-
-
-class _PackWeights(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, state: _WeightState, *params):
-        ctx.state = state
-        return params[0].new_zeros(())
-
-    @staticmethod
-    def backward(ctx, gtoken):
-        st: _WeightState = ctx.state
-        grads = []
-        for name, _ in _layers_from_state(st):
-            s = SCALE.get(name, 1.0)
-            if name in st.dw:
-                gw = C.unpack_grad(st.dw[name], st.shape[name], SEGMENTS[name]) * s
-                gb = st.db[name] * s
-            else:
-                gw = gb = None
-            splits = st.split[name]
-            if len(splits) == 1:
-                grads += [gw, gb]
-            else:
-                o = 0
-                for n in splits:
-                    grads += [None if gw is None else gw[o:o + n].contiguous(),
-                              None if gb is None else gb[o:o + n].contiguous()]
-                    o += n
-        st.dw.clear()
-        st.db.clear()
-        return (None, *grads)
-
-
-def _layers_from_state(st):
-    return [(n, None) for n in st.wf]
 
 
 def _pm(t: torch.Tensor) -> torch.Tensor:
@@ -150,96 +79,236 @@ def _nchw(t: torch.Tensor, B: int, H: int, W: int) -> torch.Tensor:
     return t.reshape(B, H, W, t.shape[1]).permute(0, 3, 1, 2)
 
 
-class _UpdateStep(torch.autograd.Function):
+class _Arena:
+    """Per-forward storage: one (slots * P, C) buffer per name, slot t at rows [t*P, (t+1)*P).
+
+    While training every activation a step's backward or the batched weight gradient
+    reads, and every deferred weight-gradient dY, lives here.  Without autograd
+    (``keep=False``) ``take`` hands out per-call temporaries instead.
+    """
+
+    def __init__(self, iters: int, P: int, device, keep: bool):
+        self.iters, self.P, self.device, self.keep = iters, P, device, keep
+        self.bufs: Dict[str, torch.Tensor] = {}
+
+    def take(self, name: str, t: int, C: int, dtype=torch.bfloat16, slots: Optional[int] = None) -> torch.Tensor:
+        if not self.keep:
+            return torch.empty(self.P, C, device=self.device, dtype=dtype)
+        buf = self.bufs.get(name)
+        if buf is None:
+            buf = torch.empty((slots or self.iters) * self.P, C, device=self.device, dtype=dtype)
+            self.bufs[name] = buf
+        return buf[t * self.P:(t + 1) * self.P]
+
+    def rows(self, name: str, t0: int, t1: int) -> torch.Tensor:
+        return self.bufs[name][t0 * self.P:t1 * self.P]
+
+
+class _Run:
+    """Everything one RAFT forward's fused steps share."""
+
+    def __init__(self, block, inp: torch.Tensor, iters: int, pyramid=None, keep: bool = True):
+        B, _, H, W = inp.shape
+        self.dims = (B, H, W)
+        self.P = P = B * H * W
+        self.iters = iters
+        self.block = block
+        self.pyr = pyramid  # ops.corr._PyramidState or None (local correlation supplies corr)
+        self.arena = _Arena(iters, P, inp.device, keep)
+        self.done = set()  # steps whose backward stored their dY
+        self.coords: Dict[int, torch.Tensor] = {}
+        self.flows: Dict[int, torch.Tensor] = {}
+        self.wf: Dict[str, torch.Tensor] = {}
+        self.wd: Dict[str, Optional[torch.Tensor]] = {}
+        self.bias: Dict[str, torch.Tensor] = {}
+        self.cout: Dict[str, int] = {}
+        for name, mods, segs, scale, dgrad in _LAYERS:
+            ms = mods(block)
+            wf, wd, b = C.pack_weights([m.weight for m in ms], [m.bias for m in ms], segs, scale, dgrad=dgrad)
+            self.wf[name], self.wd[name], self.bias[name] = wf, wd, b
+            self.cout[name] = sum(m.weight.shape[0] for m in ms)
+        # context features: constant over the iterations -> one bf16 pixel-major copy
+        self.inp_bf = _pm(inp.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+
+    def geom(self, kh, kw, T: int = 1):
+        B, H, W = self.dims
+        return C.geom(T * B, H, W, kh, kw, kh // 2, kw // 2)
+
+    def geom_d(self, kh, kw):
+        B, H, W = self.dims
+        return C.geom(B, H, W, kh, kw, kh - 1 - kh // 2, kw - 1 - kw // 2)
+
+    # ------------------------------------------------------------ batched weight gradients
+    def weight_grads(self) -> List[Optional[torch.Tensor]]:
+        T, P, ar = self.iters, self.P, self.arena
+        for t in range(T):  # steps whose outputs fed no loss: zero dY
+            if t not in self.done:
+                for name in ("dmask", "dd8", "dhd", "dq1", "dq2", "dzr1", "dzr2", "dmo", "dcf", "dc1", "df1"):
+                    if name in ar.bufs:
+                        ar.rows(name, t, t + 1).zero_()
+        inp = self.inp_bf
+
+        def srcs_dy(name, t0, t1):
+            r = lambda n: ar.rows(n, t0, t1)  # noqa: E731
+            if name == "convc1":
+                return [r("corr")], r("dc1")
+            if name == "convc2":
+                return [r("c1")], r("dcf")[:, :192]
+            if name == "convf1":
+                return [r("flow8")], r("df1")
+            if name == "convf2":
+                return [r("f1")], r("dcf")[:, 192:]
+            if name == "conv":
+                return [r("cf")], r("dmo")
+            if name == "zr1":
+                return [ar.rows("h", t0, t1), inp, r("motion")], r("dzr1")
+            if name == "q1":
+                return [r("rh1"), inp, r("motion")], r("dq1")
+            if name == "zr2":
+                return [r("h1"), inp, r("motion")], r("dzr2")
+            if name == "q2":
+                return [r("rh2"), inp, r("motion")], r("dq2")
+            if name == "heads":
+                return [ar.rows("h", t0 + 1, t1 + 1)], r("dhd")
+            if name == "fh2":
+                return [r("hd")[:, :256]], r("dd8")
+            return [r("hd")[:, 256:]], r("dmask")  # mask2
+
+        grads: List[Optional[torch.Tensor]] = []
+        for name, mods, segs, scale, _ in _LAYERS:
+            ms = mods(self.block)
+            wg = [torch.empty_like(m.weight) for m in ms]
+            bg = [torch.empty_like(m.bias) for m in ms]
+            kh, kw = ms[0].weight.shape[2:]
+            # one launch over all iterations, unless an operand would exceed the kernels'
+            # 32-bit byte offsets (very large batches / resolutions): then chunks of iterations
+            srcs, dy = srcs_dy(name, 0, T)
+            per_iter = max([s.stride(0) * 2 * P for s in srcs] + [dy.stride(0) * 2 * P])
+            chunk = max(1, min(T, _I32 // max(per_iter, 1)))
+            for t0 in range(0, T, chunk):
+                t1 = min(T, t0 + chunk)
+                srcs, dy = srcs_dy(name, t0, t1)
+                C.conv_wgrad_params(srcs, dy, self.geom(kh, kw, t1 - t0), wg, bg, segs, scale, accumulate=t0 > 0)
+            for w, b in zip(wg, bg):
+                grads += [w, b]
+        return grads
+
+
+class _PackWeights(torch.autograd.Function):
+    """Token node: its backward (after every step's backward) runs the batched weight grads."""
+
     @staticmethod
-    def forward(ctx, token, net, inp32, corr, flow, st: _WeightState, inp_bf):
-        B, _, H, W = net.shape
-        P = B * H * W
+    def forward(ctx, run: _Run, *params):
+        ctx.run = run
+        return params[0].new_zeros(())
+
+    @staticmethod
+    def backward(ctx, gtoken):
+        run: _Run = ctx.run
+        grads = run.weight_grads()
+        run.arena.bufs.clear()
+        return (None, *grads)
+
+
+class _Step(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, wtoken, ptoken, net, inp32, corr_in, coords1, run: _Run, t: int):
+        B, H, W = run.dims
+        P = run.P
         dev = net.device
         bf = torch.bfloat16
         k = ops()
-        g3 = lambda kh, kw: C.geom(B, H, W, kh, kw, kh // 2, kw // 2)  # noqa: E731
+        ar = run.arena
+        g = run.geom
 
-        h0 = _pm(net.to(bf).contiguous(memory_format=torch.channels_last))
-        corr_pm = corr.reshape(P, CORR_PAD)
-        inp = inp_bf
-        flow = flow.float().contiguous()
-        flow8 = torch.empty(P, 8, device=dev, dtype=bf)
-        motion = torch.empty(P, HID, device=dev, dtype=bf)
-        k.pack_flow(flow, flow8, motion[:, 126:])
+        # hidden state: slot t of the "h" arena (slot t+1 = this step's output)
+        h0 = ar.take("h", t, HID, slots=run.iters + 1)
+        net_pm = _pm(net)
+        if net_pm.data_ptr() != h0.data_ptr():
+            h0.copy_(net_pm)
+        # correlation features
+        corr = ar.take("corr", t, CORR_PAD)
+        if run.pyr is not None:
+            k.corr_lookup_into(run.pyr.levels, coords1, run.pyr.radius, corr.view(B, H, W, CORR_PAD))
+        else:
+            corr.copy_(corr_in.reshape(P, CORR_PAD))
+        flow8 = ar.take("flow8", t, 8)
+        motion = ar.take("motion", t, HID)
+        k.pack_flow(coords1, flow8, motion[:, 126:], True)
 
-        c1 = torch.empty(P, 256, device=dev, dtype=bf)
-        C.conv_fwd([corr_pm], st.wf["convc1"], g3(1, 1), 256, c1, bias=st.bias["convc1"], act=1)
-        cf = torch.empty(P, 256, device=dev, dtype=bf)
-        C.conv_fwd([c1], st.wf["convc2"], g3(3, 3), 192, cf[:, :192], bias=st.bias["convc2"], act=1)
-        f1 = torch.empty(P, 128, device=dev, dtype=bf)
-        C.conv_fwd([flow8], st.wf["convf1"], g3(7, 7), 128, f1, bias=st.bias["convf1"], act=1)
-        C.conv_fwd([f1], st.wf["convf2"], g3(3, 3), 64, cf[:, 192:], bias=st.bias["convf2"], act=1)
-        C.conv_fwd([cf], st.wf["conv"], g3(3, 3), 126, motion, bias=st.bias["conv"], act=1)
+        c1 = ar.take("c1", t, 256)
+        C.conv_fwd([corr], run.wf["convc1"], g(1, 1), 256, c1, bias=run.bias["convc1"], act=1)
+        cf = ar.take("cf", t, 256)
+        C.conv_fwd([c1], run.wf["convc2"], g(3, 3), 192, cf[:, :192], bias=run.bias["convc2"], act=1)
+        f1 = ar.take("f1", t, 128)
+        C.conv_fwd([flow8], run.wf["convf1"], g(7, 7), 128, f1, bias=run.bias["convf1"], act=1)
+        C.conv_fwd([f1], run.wf["convf2"], g(3, 3), 64, cf[:, 192:], bias=run.bias["convf2"], act=1)
+        C.conv_fwd([cf], run.wf["conv"], g(3, 3), 126, motion, bias=run.bias["conv"], act=1)
 
-        saved_gru = []
+        inp = run.inp_bf
         h = h0
         for stage, (kh, kw) in ((1, (1, 5)), (2, (5, 1))):
-            zr = torch.empty(P, 2 * HID, device=dev, dtype=bf)
-            rh = torch.empty(P, HID, device=dev, dtype=bf)
-            C.conv_fwd([h, inp, motion], st.wf[f"zr{stage}"], g3(kh, kw), 2 * HID, zr,
-                       bias=st.bias[f"zr{stage}"], epi=C.EPI_GRU_ZR, h=h, out2=rh)
-            hn = torch.empty(P, HID, device=dev, dtype=bf)
-            q = torch.empty(P, HID, device=dev, dtype=bf)
-            C.conv_fwd([rh, inp, motion], st.wf[f"q{stage}"], g3(kh, kw), HID, hn,
-                       bias=st.bias[f"q{stage}"], epi=C.EPI_GRU_Q, h=h, z=zr[:, :HID], out2=q)
-            saved_gru += [h, zr, rh, q]
+            zr = ar.take(f"zr{stage}", t, 2 * HID)
+            rh = ar.take(f"rh{stage}", t, HID)
+            C.conv_fwd([h, inp, motion], run.wf[f"zr{stage}"], g(kh, kw), 2 * HID, zr,
+                       bias=run.bias[f"zr{stage}"], epi=C.EPI_GRU_ZR, h=h, out2=rh)
+            hn = ar.take("h1", t, HID) if stage == 1 else ar.take("h", t + 1, HID, slots=run.iters + 1)
+            q = ar.take(f"q{stage}", t, HID)
+            C.conv_fwd([rh, inp, motion], run.wf[f"q{stage}"], g(kh, kw), HID, hn,
+                       bias=run.bias[f"q{stage}"], epi=C.EPI_GRU_Q, h=h, z=zr[:, :HID], out2=q)
             h = hn
 
-        hd = torch.empty(P, 512, device=dev, dtype=bf)
-        C.conv_fwd([h], st.wf["heads"], g3(3, 3), 512, hd, bias=st.bias["heads"], act=1)
+        hd = ar.take("hd", t, 512)
+        C.conv_fwd([h], run.wf["heads"], g(3, 3), 512, hd, bias=run.bias["heads"], act=1)
         delta = torch.empty(P, 8, device=dev, dtype=torch.float32)
-        C.conv_fwd([hd[:, :256]], st.wf["fh2"], g3(3, 3), 2, delta, bias=st.bias["fh2"])
-        mask = torch.empty(P, 576, device=dev, dtype=bf)
-        C.conv_fwd([hd[:, 256:]], st.wf["mask2"], g3(1, 1), 576, mask, bias=st.bias["mask2"])
+        C.conv_fwd([hd[:, :256]], run.wf["fh2"], g(3, 3), 2, delta, bias=run.bias["fh2"])
+        mask = ar.take("mask", t, 576)
+        C.conv_fwd([hd[:, 256:]], run.wf["mask2"], g(1, 1), 576, mask, bias=run.bias["mask2"])
 
-        ctx.st = st
-        ctx.dims = (B, H, W)
+        coords_out = torch.empty_like(coords1)
+        flow = torch.empty_like(coords1)
+        k.apply_delta(coords1, delta, coords_out, flow)
+        flow_up = k.convex_upsample(flow, _nchw(mask, B, H, W))
+
+        ctx.run, ctx.t = run, t
         ctx.net_dtype = net.dtype
-        ctx.save_for_backward(corr, flow8, c1, cf, f1, motion, inp, h, hd, *saved_gru)
-        net_out = _nchw(h, B, H, W)
-        mask_out = _nchw(mask, B, H, W)
-        delta_out = _nchw(delta[:, :2], B, H, W)
-        return net_out, mask_out, delta_out
+        ctx.has_corr_in = corr_in is not None
+        run.coords[t] = coords1
+        run.flows[t] = flow
+        ctx.mark_non_differentiable(coords_out)
+        return _nchw(h, B, H, W), flow_up, coords_out
 
     @staticmethod
-    def backward(ctx, g_net, g_mask, g_delta):
-        st: _WeightState = ctx.st
-        B, H, W = ctx.dims
-        P = B * H * W
-        (corr, flow8, c1, cf, f1, motion, inp, h2, hd, *sg) = ctx.saved_tensors
-        dev = corr.device
+    def backward(ctx, g_net, g_flow_up, _g_coords):
+        run: _Run = ctx.run
+        t = ctx.t
+        B, H, W = run.dims
+        P = run.P
+        dev = g_flow_up.device if g_flow_up is not None else run.inp_bf.device
         bf = torch.bfloat16
         k = ops()
-        g3 = lambda kh, kw: C.geom(B, H, W, kh, kw, kh // 2, kw // 2)  # noqa: E731
-        gd = lambda kh, kw: C.geom(B, H, W, kh, kw, kh - 1 - kh // 2, kw - 1 - kw // 2)  # noqa: E731
+        ar = run.arena
+        gd = run.geom_d
 
-        def wgrad(name, srcs, dy, kh, kw):
-            dw, db = st.grad_bufs(name)
-            C.conv_wgrad(srcs, dy, g3(kh, kw), st.cout[name], dw, db)
+        def R(name):  # this step's slot of a forward arena
+            return ar.rows(name, t, t + 1)
 
         def dgrad(name, dy, kh, kw, out, n, mask=None, acc_c0=1 << 30):
-            C.conv_fwd([dy], st.wd[name], gd(kh, kw), n, out, epi=C.EPI_GRAD, mask=mask, acc_c0=acc_c0)
+            C.conv_fwd([dy], run.wd[name], gd(kh, kw), n, out, epi=C.EPI_GRAD, mask=mask, acc_c0=acc_c0)
 
-        # ---- heads
-        dhd = torch.empty(P, 512, device=dev, dtype=bf)
-        if g_mask is not None:
-            dmask = _pm(g_mask.to(bf).contiguous(memory_format=torch.channels_last))
-            wgrad("mask2", [hd[:, 256:]], dmask, 1, 1)
-            dgrad("mask2", dmask, 1, 1, dhd[:, 256:], 256, mask=hd[:, 256:])
+        hd, mask = R("hd"), R("mask")
+        # ---- upsampler + heads
+        dmask = ar.take("dmask", t, 576)
+        dd8 = ar.take("dd8", t, 8)
+        if g_flow_up is not None:
+            k.convex_upsample_backward_into(run.flows[t], _nchw(mask, B, H, W), g_flow_up,
+                                            _nchw(dmask, B, H, W), dd8)
         else:
-            dhd[:, 256:].zero_()
-        ddelta = torch.zeros(P, 8, device=dev, dtype=bf)
-        if g_delta is not None:
-            ddelta[:, :2] = g_delta.permute(0, 2, 3, 1).reshape(P, 2)
-        wgrad("fh2", [hd[:, :256]], ddelta, 3, 3)
-        dgrad("fh2", ddelta, 3, 3, dhd[:, :256], 256, mask=hd[:, :256])
-        wgrad("heads", [h2], dhd, 3, 3)
+            dmask.zero_()
+            dd8.zero_()
+        dhd = ar.take("dhd", t, 512)
+        dgrad("mask2", dmask, 1, 1, dhd[:, 256:], 256, mask=hd[:, 256:])
+        dgrad("fh2", dd8, 3, 3, dhd[:, :256], 256, mask=hd[:, :256])
         dh = torch.empty(P, HID, device=dev, dtype=torch.float32)
         if g_net is not None:
             dh.copy_(_pm(g_net))
@@ -251,57 +320,65 @@ class _UpdateStep(torch.autograd.Function):
         # ---- GRU stages (reverse order); G = [dh | d inp | d motion] accumulates over stages
         G = torch.empty(P, 3 * HID, device=dev, dtype=torch.float32)
         carry = torch.empty(P, HID, device=dev, dtype=torch.float32)
-        dq = torch.empty(P, HID, device=dev, dtype=bf)
-        dzr = torch.empty(P, 2 * HID, device=dev, dtype=bf)
+        inp = run.inp_bf
         first = True
         for stage, (kh, kw) in ((2, (5, 1)), (1, (1, 5))):
-            h, zr, rh, q = sg[(stage - 1) * 4:(stage - 1) * 4 + 4]
+            h = ar.rows("h", t, t + 1) if stage == 1 else R("h1")
+            zr, rh, q = R(f"zr{stage}"), R(f"rh{stage}"), R(f"q{stage}")
+            dq = ar.take(f"dq{stage}", t, HID)
+            dzr = ar.take(f"dzr{stage}", t, 2 * HID)
             dH = dh if stage == 2 else G[:, :HID]
             k.gru_bwd_a(dH, zr[:, :HID], q, h, dq, dzr[:, :HID], carry)
-            wgrad(f"q{stage}", [rh, inp, motion], dq, kh, kw)
             # fresh write of d(rh); x part fresh on the first stage, accumulated afterwards
             dgrad(f"q{stage}", dq, kh, kw, G, 3 * HID, acc_c0=(3 * HID if first else HID))
             k.gru_bwd_b(G[:, :HID], zr[:, HID:], h, carry, dzr[:, HID:])
-            wgrad(f"zr{stage}", [h, inp, motion], dzr, kh, kw)
             dgrad(f"zr{stage}", dzr, kh, kw, G, 3 * HID, acc_c0=0)
             first = False
 
         # ---- motion encoder
-        dmo = torch.empty(P, HID, device=dev, dtype=bf)
+        motion, cf, c1, f1 = R("motion"), R("cf"), R("c1"), R("f1")
+        dmo = ar.take("dmo", t, HID)
         k.masked_cast(G[:, 2 * HID:2 * HID + 126], motion, dmo)  # relu' ; flow channels -> 0
-        wgrad("conv", [cf], dmo, 3, 3)
-        dcf = torch.empty(P, 256, device=dev, dtype=bf)
+        dcf = ar.take("dcf", t, 256)
         dgrad("conv", dmo, 3, 3, dcf, 256, mask=cf)
-        wgrad("convc2", [c1], dcf[:, :192], 3, 3)
-        dc1 = torch.empty(P, 256, device=dev, dtype=bf)
+        dc1 = ar.take("dc1", t, 256)
         dgrad("convc2", dcf[:, :192], 3, 3, dc1, 256, mask=c1)
-        wgrad("convc1", [corr.reshape(P, CORR_PAD)], dc1, 1, 1)
         dcorr = torch.empty(P, CORR_PAD, device=dev, dtype=bf)
         dgrad("convc1", dc1, 1, 1, dcorr, CORR_PAD)
-        wgrad("convf2", [f1], dcf[:, 192:], 3, 3)
-        df1 = torch.empty(P, 128, device=dev, dtype=bf)
+        df1 = ar.take("df1", t, 128)
         dgrad("convf2", dcf[:, 192:], 3, 3, df1, 128, mask=f1)
-        wgrad("convf1", [flow8], df1, 7, 7)
+        run.done.add(t)
 
+        d_corr_in = None
+        if ctx.has_corr_in:
+            d_corr_in = dcorr.reshape(B, H, W, CORR_PAD)
+        elif run.pyr is not None and run.pyr.levels:
+            k.corr_lookup_backward_(run.pyr.grad_buffers(), run.coords[t], dcorr.reshape(B, H, W, CORR_PAD),
+                                    run.pyr.radius)
         d_net = _nchw(G[:, :HID].to(ctx.net_dtype), B, H, W)
-        d_inp = _nchw(G[:, HID:2 * HID].contiguous(), B, H, W)
-        d_corr = dcorr.reshape(B, H, W, CORR_PAD)
-        return torch.zeros((), device=dev), d_net, d_inp, d_corr, None, None, None
+        d_inp = _nchw(G[:, HID:2 * HID], B, H, W)
+        zero = torch.zeros((), device=dev)
+        return zero, zero, d_net, d_inp, d_corr_in, None, None, None
 
 
 class FusedBasicUpdate:
-    """Per-forward driver: packs weights once, then runs fused iterations."""
+    """Per-forward driver: packs the weights once, then runs fused refinement steps."""
 
-    def __init__(self, block, inp: torch.Tensor):
-        self.state = _WeightState(block)
-        self.token = _PackWeights.apply(self.state, *_params(block))
-        # the context features are constant over iterations: one bf16 pixel-major copy,
-        # while the fp32 ``inp`` keeps autograd's cross-iteration gradient sum in fp32
+    def __init__(self, block, inp: torch.Tensor, iters: int, pyramid=None):
+        keep = torch.is_grad_enabled()
+        self.run = _Run(block, inp, iters, pyramid=pyramid, keep=keep)
+        self.token = _PackWeights.apply(self.run, *_params(block))
+        # the fp32 ``inp`` keeps autograd's cross-iteration gradient sum in fp32
         self.inp32 = inp.float().contiguous(memory_format=torch.channels_last)
-        self.inp_bf = _pm(inp.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
 
-    def __call__(self, net, corr_padded, flow):
-        return _UpdateStep.apply(self.token, net, self.inp32, corr_padded, flow, self.state, self.inp_bf)
+    def step(self, t: int, net, coords1, ptoken=None, corr=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """One refinement iteration -> (net, flow_up (B, 2, 8H, 8W) fp32, coords1 after the
+        update (no grad)).  ``ptoken``: the correlation pyramid's autograd token (dense path);
+        ``corr``: (B, H, W, 328) bf16 features (local-correlation path)."""
+        if ptoken is None:
+            ptoken = self.token.new_zeros(())
+        return _Step.apply(self.token, ptoken, net, self.inp32, corr, coords1.detach().float().contiguous(),
+                           self.run, t)
 
 
 def supported(block) -> bool:

@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--hw", type=int, nargs=2, default=[46, 62])
     ap.add_argument("--cfg", default="")
+    ap.add_argument("--iters", type=int, default=12,
+                    help="wgrad is timed batched over this many refinement iterations (as in training)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     torch.backends.cudnn.benchmark = True
@@ -73,20 +75,22 @@ def main():
         dx = torch.empty(P, cin_p, device=dev, dtype=torch.bfloat16)
         dw = torch.zeros(wt.shape, device=dev)
         db = torch.zeros(cout, device=dev)
+        T = args.iters
+        xT = torch.randn(T * P, cin_p, device=dev).bfloat16()
+        dyT = torch.randn(T * P, cout_p, device=dev).bfloat16()
+        gT = C.geom(T * B, H, W, kh, kw, ph, pw)
         g = C.geom(B, H, W, kh, kw, ph, pw)
         gd = C.geom(B, H, W, kh, kw, kh - 1 - ph, kw - 1 - pw)
         line = [f"{name:7s} M={P} N={cout:4d} K={cin * kh * kw:5d}"]
         for cfg in cfgs:
-            if cfg is not None:
-                os.environ["RAFT_CONV_FWD_CFG"] = str(cfg)
-            tf = timeit(lambda: C.conv_fwd([x], wt, g, cout, out[:, :cout], bias=b, act=1))
-            td = timeit(lambda: C.conv_fwd([dy], wd, gd, cin_p, dx, epi=C.EPI_GRAD))
+            c = cfg or 0
+            tf = timeit(lambda: C.conv_fwd([x], wt, g, cout, out[:, :cout], bias=b, act=1, cfg=c))
+            td = timeit(lambda: C.conv_fwd([dy], wd, gd, cin_p, dx, epi=C.EPI_GRAD, cfg=c))
             line.append(f"cfg{cfg}: fwd {tf:7.1f}us ({2 * macs / tf / 1e6:5.0f}TF) dgrad {td:7.1f}us "
                         f"({2 * macs / td / 1e6:5.0f}TF)")
-        os.environ.pop("RAFT_CONV_FWD_CFG", None)
-        tw = timeit(lambda: C.conv_wgrad([x], dy, g, cout, dw, db))
-        tw0 = timeit(lambda: C.conv_wgrad([x], dy, g, cout, dw, None))
-        line.append(f"wgrad {tw:7.1f}us (no db {tw0:6.1f}us {2 * macs / tw0 / 1e6:5.0f}TF)")
+        tw = timeit(lambda: C.conv_wgrad([xT], dyT, gT, cout, dw, db, False), reps=5) / T
+        tw0 = timeit(lambda: C.conv_wgrad([xT], dyT, gT, cout, dw, None, False), reps=5) / T
+        line.append(f"wgrad/iter (x{T} batched) {tw:7.1f}us (no db {tw0:6.1f}us {2 * macs / tw0 / 1e6:5.0f}TF)")
         # MIOpen reference
         xt = x[:, :cin].float().reshape(B, H, W, cin).permute(0, 3, 1, 2).bfloat16().contiguous(
             memory_format=torch.channels_last).requires_grad_(True)

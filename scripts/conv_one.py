@@ -15,8 +15,7 @@ from scripts.bench_convs import SHAPES  # noqa: E402
 
 def main():
     name, kind = sys.argv[1], sys.argv[2]
-    if len(sys.argv) > 3:
-        os.environ["RAFT_CONV_FWD_CFG"] = sys.argv[3]
+    cfg = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     segs, cout, kh, kw = SHAPES[name]
     B, H, W = 8, 46, 62
     P = B * H * W
@@ -32,12 +31,12 @@ def main():
     g = C.geom(B, H, W, kh, kw, kh // 2, kw // 2)
     if kind == "fwd":
         wt = C.pack_fwd(w, segs)
-        fn = lambda: C.conv_fwd([x], wt, g, cout, out[:, :cout], bias=b, act=1)  # noqa: E731
+        fn = lambda: C.conv_fwd([x], wt, g, cout, out[:, :cout], bias=b, act=1, cfg=cfg)  # noqa: E731
     elif kind == "dgrad":
         wd = C.pack_dgrad(w, segs)
         dx = torch.empty(P, cin_p, device=dev, dtype=torch.bfloat16)
         gd = C.geom(B, H, W, kh, kw, kh - 1 - kh // 2, kw - 1 - kw // 2)
-        fn = lambda: C.conv_fwd([dy], wd, gd, cin_p, dx, epi=C.EPI_GRAD)  # noqa: E731
+        fn = lambda: C.conv_fwd([dy], wd, gd, cin_p, dx, epi=C.EPI_GRAD, cfg=cfg)  # noqa: E731
     else:
         wt = C.pack_fwd(w, segs)
         dw = torch.zeros(wt.shape, device=dev)

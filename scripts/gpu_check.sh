@@ -20,13 +20,13 @@ run() {  # run <name> <timeout-seconds> <cmd...>
 
 STEPS=${STEPS:-10}
 if [ "${TESTS:-1}" = "1" ]; then
-  run pytest_gpu 900 python -m pytest tests -m gpu -q -rf --tb=short
+  run pytest_gpu 900 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -q -rf --tb=short --timeout 200 --timeout-method thread ${PYTEST_ARGS:-}
   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "${BENCH:-1}" = "1" ]; then
-  run bench_native 600 python bench.py --steps "$STEPS" --warmup 3
+  run bench_native 600 python bench.py --steps "$STEPS" --warmup 3 ${BENCH_ARGS:-}
 fi
-if [ "${SKIP_REF:-0}" != "1" ]; then
+if [ "${SKIP_REF:-1}" != "1" ]; then
   run bench_reference 900 python bench.py --steps "$STEPS" --warmup 3 --impl reference
 fi
 if [ "${PROFILE:-1}" = "1" ]; then

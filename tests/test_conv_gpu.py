@@ -168,7 +168,7 @@ def test_gru_epilogues(cuda):
     assert _rel(_from_pm(hn, B, H, W), hn_ref) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", ["20", "21", "22"])
+@pytest.mark.parametrize("cfg", [20, 21, 22, 23, 1, 8, 9])
 @pytest.mark.parametrize("segs,cout,kh,kw,hw", [
     ([(256, 256)], 192, 3, 3, (46, 62)),
     ([(128, 128), (128, 128), (128, 128)], 256, 1, 5, (46, 62)),
@@ -176,9 +176,9 @@ def test_gru_epilogues(cuda):
     ([(128, 128)], 512, 3, 3, (23, 31)),
     ([(64, 64)], 128, 3, 3, (17, 21)),
 ])
-def test_fwd_halo_strip_full_size(cuda, monkeypatch, cfg, segs, cout, kh, kw, hw):
-    """v5 (halo-strip) forward at RAFT sizes vs an fp32 conv2d, every tile config."""
-    monkeypatch.setenv("RAFT_CONV_FWD_CFG", cfg)
+def test_fwd_every_variant_full_size(cuda, cfg, segs, cout, kh, kw, hw):
+    """Every forward kernel variant (v5 halo-strip tiles, v4 tiles, generic) at RAFT sizes
+    vs an fp32 conv2d."""
     torch.manual_seed(4)
     B, (H, W) = 8, hw
     P = B * H * W
@@ -187,7 +187,54 @@ def test_fwd_halo_strip_full_size(cuda, monkeypatch, cfg, segs, cout, kh, kw, hw
     w = torch.randn(cout, cin, kh, kw, device=cuda) / (cin * kh * kw) ** 0.5
     bias = torch.randn(cout, device=cuda)
     out = torch.full((P, cout), float("nan"), device=cuda, dtype=torch.bfloat16)
-    C.conv_fwd(srcs, C.pack_fwd(w, segs), C.geom(B, H, W, kh, kw, kh // 2, kw // 2), cout, out, bias=bias, act=1)
+    C.conv_fwd(srcs, C.pack_fwd(w, segs), C.geom(B, H, W, kh, kw, kh // 2, kw // 2), cout, out, bias=bias, act=1,
+               cfg=cfg)
     x = torch.cat([_from_pm(s, B, H, W) for s in srcs], dim=1)
     ref = F.relu(F.conv2d(x, w.bfloat16().float(), bias, padding=(kh // 2, kw // 2)))
     assert _rel(_from_pm(out, B, H, W), ref) < 1e-2
+
+
+@pytest.mark.parametrize("segs,couts,kh,kw", [([(128, 128), (128, 128), (128, 128)], (128, 128), 1, 5),
+                                               ([(324, 328)], (256,), 1, 1), ([(2, 8)], (128,), 7, 7),
+                                               ([(128, 128)], (256, 256), 3, 3), ([(256, 256)], (2,), 3, 3)])
+def test_pack_weights_matches_python_packing(cuda, segs, couts, kh, kw):
+    torch.manual_seed(5)
+    cin = sum(r for r, _ in segs)
+    ws = [torch.randn(c, cin, kh, kw, device=cuda).to(memory_format=torch.channels_last) for c in couts]
+    bs = [torch.randn(c, device=cuda) for c in couts]
+    wf, wd, b = C.pack_weights(ws, bs, segs, scale=0.25)
+    wcat = torch.cat(ws, 0)
+    assert torch.equal(wf, C.pack_fwd(wcat, segs, scale=0.25))
+    assert torch.equal(wd, C.pack_dgrad(wcat, segs, scale=0.25))
+    torch.testing.assert_close(b, torch.cat(bs) * 0.25)
+
+
+def test_wgrad_params_periodic_source_and_param_layout(cuda):
+    """Batched weight gradient over T iterations: a periodic (shared) source equals the
+    per-iteration sum; stacked parameters get their own (channels-last) gradients."""
+    torch.manual_seed(6)
+    T, B, H, W = 3, 2, 11, 13
+    P = B * H * W
+    segs = [(128, 128), (128, 128), (128, 128)]
+    hs = torch.randn(T * P, 128, device=cuda).bfloat16()
+    inp = torch.randn(P, 128, device=cuda).bfloat16()  # shared by every iteration
+    mo = torch.randn(T * P, 128, device=cuda).bfloat16()
+    dy = torch.randn(T * P, 256, device=cuda).bfloat16()
+    gz = torch.empty(128, 384, 1, 5, device=cuda).to(memory_format=torch.channels_last)
+    gr = torch.empty_like(gz)
+    bz = torch.empty(128, device=cuda)
+    br = torch.empty(128, device=cuda)
+    C.conv_wgrad_params([hs, inp, mo], dy, C.geom(T * B, H, W, 1, 5, 0, 2), [gz, gr], [bz, br], segs, scale=0.5)
+    ref_w = torch.zeros(256, 384, 1, 5, device=cuda)
+    for t in range(T):
+        sl = slice(t * P, (t + 1) * P)
+        x = torch.cat([_from_pm(hs[sl], B, H, W), _from_pm(inp, B, H, W), _from_pm(mo[sl], B, H, W)], 1)
+        wr = torch.zeros(256, 384, 1, 5, device=cuda, requires_grad=True)
+        F.conv2d(x, wr, padding=(0, 2)).backward(_from_pm(dy[sl], B, H, W))
+        ref_w += wr.grad
+    assert _rel(torch.cat([gz, gr]), 0.5 * ref_w) < 1e-3
+    assert _rel(torch.cat([bz, br]), 0.5 * dy.float().sum(0)) < 1e-4
+    # deterministic: a second run is bitwise identical
+    gz2 = torch.empty_like(gz)
+    C.conv_wgrad_params([hs, inp, mo], dy, C.geom(T * B, H, W, 1, 5, 0, 2), [gz2, gr], [bz, br], segs, scale=0.5)
+    assert torch.equal(gz, gz2)
