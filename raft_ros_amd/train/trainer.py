@@ -70,6 +70,7 @@ def train(args: Namespace) -> str:
         model.freeze_bn()
     net = ddp.wrap_model(model, info, bucket_cap_mb=getattr(args, "bucket_mb", 32.0))
 
+    args.device = str(dev)  # batched augmentation runs on the rank's device
     train_loader = fetch_dataloader(args)
     optimizer, scheduler = fetch_optimizer(args, model)
     use_scaler = bool(args.mixed_precision) and getattr(args, "amp_dtype", "bf16") == "fp16" and dev.type == "cuda"

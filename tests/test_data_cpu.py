@@ -1,4 +1,4 @@
-"""Augmentation, datasets (fake on-disk layouts) and the data loader."""
+"""Augmentation (batched, device-side), datasets (fake on-disk layouts) and the data loader."""
 import os
 from argparse import Namespace
 
@@ -7,70 +7,115 @@ import pytest
 import torch
 from PIL import Image
 
-from raft_ros_amd.data import frame_utils as fu
-from raft_ros_amd.data.augmentor import ColorJitter, FlowAugmentor, SparseFlowAugmentor, resize_linear
+from raft_ros_amd.data import augment as A
 from raft_ros_amd.data import datasets as D
+from raft_ros_amd.data import frame_utils as fu
 from raft_ros_amd.data.synthetic import synthetic_batch, warp_backward
 
 
-def test_resize_linear_matches_half_pixel_bilinear():
-    img = np.arange(4 * 6, dtype=np.float32).reshape(4, 6)
-    out = resize_linear(img, 2.0, 2.0)
-    assert out.shape == (8, 12)
-    # half-pixel centres: dst x=1 samples src x=0.25 -> 0.25 (first row)
-    assert abs(out[0, 1] - 0.25) < 1e-5 and out[0, 0] == 0.0
-    assert resize_linear(np.zeros((10, 10, 3), np.uint8), 0.55, 1.26).shape == (13, 6, 3)
+def _sample(h, w, seed=0, sparse=False):
+    g = torch.Generator().manual_seed(seed)
+    s = {"img1": (torch.rand(h, w, 3, generator=g) * 255).to(torch.uint8),
+         "img2": (torch.rand(h, w, 3, generator=g) * 255).to(torch.uint8),
+         "flow": torch.randn(h, w, 2, generator=g) * 3,
+         "valid": (torch.rand(h, w, generator=g) > 0.5).float() if sparse else torch.ones(h, w)}
+    return s
 
 
-def test_color_jitter_statistics():
+def test_reference_constants_are_pinned():
+    """Probabilities / ranges of core/utils/augmentor.py:16-34,122-140."""
+    assert A.DENSE["jitter"] == (0.4, 0.4, 0.4, 0.5 / 3.14) and A.SPARSE["jitter"] == (0.3, 0.3, 0.3, 0.3 / 3.14)
+    assert A.DENSE["asym_prob"] == 0.2 and A.SPARSE["asym_prob"] == 0.0
+    assert A.DENSE["eraser_prob"] == A.SPARSE["eraser_prob"] == 0.5
+    assert A.DENSE["eraser_box"] == (50, 100)
+    assert A.DENSE["spatial_prob"] == A.SPARSE["spatial_prob"] == 0.8
+    assert A.DENSE["stretch_prob"] == 0.8 and A.DENSE["max_stretch"] == 0.2 and A.SPARSE["stretch_prob"] == 0.0
+    assert (A.DENSE["hflip_prob"], A.DENSE["vflip_prob"]) == (0.5, 0.1) and A.SPARSE["vflip_prob"] == 0.0
+    assert A.DENSE["crop_pad"] == 8 and A.SPARSE["crop_pad"] == 1 and A.SPARSE["margin"] == (20, 50)
+
+
+def test_batched_augmentation_shapes_and_mixed_specs():
+    specs = [A.AugSpec((64, 96), -0.1, 1.0, True, False), A.AugSpec((64, 96), -0.2, 0.4, True, True)]
+    aug = A.BatchAugmentor(specs, seed=0)
+    samples = [_sample(100, 150, 0), _sample(80, 120, 1, sparse=True), _sample(120, 110, 2)]
+    for s, sid in zip(samples, (0, 1, 0)):
+        s["spec"] = sid
+    i1, i2, f, v = aug(A.collate_padded(samples))
+    assert i1.shape == i2.shape == (3, 3, 64, 96) and f.shape == (3, 2, 64, 96) and v.shape == (3, 64, 96)
+    assert i1.min() >= 0 and i1.max() <= 255 and torch.equal(i1, i1.round())  # uint8-valued
+    assert set(v[1].unique().tolist()) <= {0.0, 1.0}
+
+
+def test_statistics_of_random_choices():
+    """Over many draws: resize ~80 %, h-flip ~50 %, v-flip ~10 %, eraser ~50 % (dense)."""
     torch.manual_seed(0)
-    img = Image.fromarray((np.random.rand(32, 32, 3) * 255).astype(np.uint8))
-    cj = ColorJitter(0.4, 0.4, 0.4, 0.5 / 3.14)
-    outs = [np.array(cj(img)) for _ in range(8)]
-    assert all(o.shape == (32, 32, 3) and o.dtype == np.uint8 for o in outs)
-    assert len({o.tobytes() for o in outs}) > 1
-    assert np.array_equal(np.array(ColorJitter()(img)), np.array(img))  # all-zero jitter = identity
+    n = 400
+    spec = A.AugSpec((32, 32), 0.0, 0.0, True, False)  # scale 2**0 = 1: resize is identity-sized
+    aug = A.BatchAugmentor([spec], seed=3)
+    s = _sample(48, 48)
+    # a flow field whose sign reveals the flips: u = +1, v = +1 everywhere
+    s["flow"] = torch.ones(48, 48, 2)
+    s["spec"] = 0
+    i1, i2, f, _ = aug(A.collate_padded([s] * n))
+    hflip = (f[:, 0, 0, 0] < 0).float().mean().item()
+    vflip = (f[:, 1, 0, 0] < 0).float().mean().item()
+    assert abs(hflip - 0.5) < 0.08 and abs(vflip - 0.1) < 0.05
 
 
-def test_dense_augmentor_shapes():
-    np.random.seed(0)
-    aug = FlowAugmentor(crop_size=[96, 128], min_scale=-0.1, max_scale=1.0, do_flip=True)
+def test_hflip_and_crop_are_exact_without_resize():
+    spec = A.AugSpec((10, 10), 0.0, 0.0, True, False)
+    aug = A.BatchAugmentor([spec], seed=1)
+    h = w = 20
+    s = _sample(h, w)
+    s["flow"] = torch.stack(torch.meshgrid(torch.arange(h).float(), torch.arange(w).float(), indexing="ij")[::-1], -1)
+    s["spec"] = 0
+    _, _, f, _ = aug(A.collate_padded([s] * 64))
+    # u(x) = x resized by sx and multiplied by sx stays a unit-slope field (bilinear is exact
+    # on linear data; only crops touching the clamped image border deviate), flipped or not
+    du = (f[:, 0, :, 1:] - f[:, 0, :, :-1]).abs()
+    assert ((du - 1).abs() < 1e-3).float().mean() > 0.9
+
+
+def test_sparse_scatter_keeps_samples_on_rounded_positions():
+    spec = A.AugSpec((30, 40), 1.0, 1.0, False, True)  # scale 2: every resized sample lands on even coords
+    aug = A.BatchAugmentor([spec], seed=2)
+    s = _sample(40, 60, sparse=True)
+    s["valid"] = torch.zeros(40, 60)
+    s["valid"][10:20, 10:30] = 1
+    s["flow"][...] = torch.tensor([1.0, -2.0])
+    s["spec"] = 0
+    _, _, f, v = aug(A.collate_padded([s] * 32))
+    on = v > 0
+    assert on.any()
+    vals = f.permute(0, 2, 3, 1)[on]
+    # resized samples carry 2x flow; unresized (20 %) the original
+    ok = torch.isclose(vals, torch.tensor([2.0, -4.0])).all(1) | torch.isclose(vals, torch.tensor([1.0, -2.0])).all(1)
+    assert ok.all()
+    assert (f.permute(0, 2, 3, 1)[~on] == 0).all()
+
+
+def test_color_jitter_identity_and_ranges():
+    img = torch.rand(2, 3, 16, 16) * 255
+    img = img.round()
+    mask = torch.ones(2, 1, 16, 16)
+    ident = torch.tensor([[1.0, 1.0, 1.0, 0.0]] * 2)
+    order = torch.tensor([[0, 1, 2, 3], [3, 2, 1, 0]])
+    out = A.color_jitter(img, mask, ident, order)
+    assert (out - img).abs().max() <= 1.0  # hue round trip through HSV: rounding only
+    dark = A.color_jitter(img, mask, torch.tensor([[0.0, 1.0, 1.0, 0.0]] * 2), order)
+    assert dark.max() == 0  # brightness 0 -> black regardless of order
+
+
+def test_per_item_augmentors_numpy_api():
+    a = A.FlowAugmentor(crop_size=[96, 128], min_scale=-0.1, max_scale=1.0, do_flip=True, seed=0)
     img = (np.random.rand(150, 200, 3) * 255).astype(np.uint8)
     flow = np.random.randn(150, 200, 2).astype(np.float32)
-    for _ in range(5):
-        a, b, f = aug(img, img.copy(), flow)
-        assert a.shape == b.shape == (96, 128, 3) and f.shape == (96, 128, 2) and f.dtype == np.float32
-
-
-def test_hflip_negates_u():
-    aug = FlowAugmentor(crop_size=[10, 10], do_flip=True)
-    aug.spatial_aug_prob = 0.0
-    aug.h_flip_prob, aug.v_flip_prob = 1.0, 0.0
-    img = np.zeros((12, 12, 3), np.uint8)
-    flow = np.zeros((12, 12, 2), np.float32)
-    flow[..., 0], flow[..., 1] = 3.0, -2.0
-    _, _, f = aug.spatial_transform(img, img, flow)
-    assert np.all(f[..., 0] == -3.0) and np.all(f[..., 1] == -2.0)
-
-
-def test_sparse_flow_resize_scatters_valid_points():
-    flow = np.zeros((10, 10, 2), np.float32)
-    valid = np.zeros((10, 10), np.float32)
-    flow[4, 6] = [1.0, -2.0]
-    valid[4, 6] = 1
-    f2, v2 = SparseFlowAugmentor.resize_sparse_flow_map(flow, valid, fx=2.0, fy=2.0)
-    assert f2.shape == (20, 20, 2) and v2.sum() == 1
-    assert np.allclose(f2[8, 12], [2.0, -4.0]) and v2[8, 12] == 1
-
-
-def test_sparse_augmentor_shapes():
-    np.random.seed(1)
-    aug = SparseFlowAugmentor(crop_size=[64, 96], min_scale=-0.2, max_scale=0.4, do_flip=True)
-    img = (np.random.rand(100, 150, 3) * 255).astype(np.uint8)
-    flow = np.random.randn(100, 150, 2).astype(np.float32)
+    i1, i2, f = a(img, img.copy(), flow)
+    assert i1.shape == (96, 128, 3) and i1.dtype == np.uint8 and f.shape == (96, 128, 2) and f.dtype == np.float32
+    sp = A.SparseFlowAugmentor(crop_size=[64, 96], seed=0)
     valid = (np.random.rand(100, 150) > 0.5).astype(np.float32)
-    a, b, f, v = aug(img, img, flow, valid)
-    assert a.shape == (64, 96, 3) and f.shape == (64, 96, 2) and v.shape == (64, 96)
+    out = sp((np.random.rand(100, 150, 3) * 255).astype(np.uint8), img[:100, :150], flow[:100, :150], valid)
+    assert out[0].shape == (64, 96, 3) and out[3].shape == (64, 96)
 
 
 def test_synthetic_ground_truth_is_exact():
@@ -106,7 +151,7 @@ def test_sintel_and_kitti_datasets(tmp_path, monkeypatch):
     _fake_sintel(str(tmp_path))
     _fake_kitti(str(tmp_path))
     s = D.MpiSintel(split="training", dstype="clean")
-    assert len(s) == 2 and len(s.flow_list) == 2
+    assert len(s) == 2 and len(s.flow_list) == 2 and s.extra_info[1] == ("alley_1", 1)
     i1, i2, flow, valid = s[1]
     assert i1.shape == (3, 48, 64) and flow.shape == (2, 48, 64) and valid.shape == (48, 64)
     k = D.KITTI(split="training")
@@ -117,6 +162,29 @@ def test_sintel_and_kitti_datasets(tmp_path, monkeypatch):
     assert len(mix) == 6
     x = mix[4]
     assert x[0].shape == (3, 32, 48)
+
+
+def test_stage_mixture_proportions(tmp_path, monkeypatch):
+    monkeypatch.setenv("RAFT_DATASET_ROOT", str(tmp_path))
+    _fake_sintel(str(tmp_path))
+    _fake_kitti(str(tmp_path))
+    ds, specs = D.build_train_dataset("sintel", [32, 48])
+    # 100 * clean(2) + 100 * final(2) + 200 * kitti(2) + 5 * hd1k(0) + things(0)
+    assert len(ds) == 200 + 200 + 400
+    sparse = [sp.sparse for sp in specs]
+    assert sorted(sparse) == [False, True, True]  # dense sintel/things spec, KITTI, HD1K specs
+    n_sparse = sum(specs[sid].sparse for _, sid in ds.entries)
+    assert n_sparse == 400
+
+
+def test_fetch_dataloader_on_disk_mixture(tmp_path, monkeypatch):
+    monkeypatch.setenv("RAFT_DATASET_ROOT", str(tmp_path))
+    _fake_sintel(str(tmp_path), h=96, w=128)
+    _fake_kitti(str(tmp_path), h=96, w=140)
+    args = Namespace(stage="sintel", image_size=[64, 96], batch_size=4, num_workers=0, device="cpu")
+    loader = D.fetch_dataloader(args)
+    i1, i2, flow, valid = next(iter(loader))
+    assert i1.shape == (4, 3, 64, 96) and flow.shape == (4, 2, 64, 96) and valid.shape == (4, 64, 96)
 
 
 def test_fetch_dataloader_synthetic():
