@@ -10,6 +10,7 @@
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
 
+#include <algorithm>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -20,15 +21,34 @@ struct PyrDesc {
   float* ptr[4];
   int H[4];
   int W[4];
+  long ld[4];
   int levels;
+};
+struct CorrGemmArgs {
+  const void* A;
+  long lda, sA;
+  const void* B;
+  long ldb, sB;
+  void* C;
+  long ldc, sC;
+  int M, N, K, batch;
+  float alpha;
+  int a_f32, b_f32, a_trans, split, c_bf16;
+  int epi;  // layouts must match corr_volume.hip
+};
+struct UnpoolArgs {
+  const float* G;
+  long sG;
+  float* out;
+  int B, H, W, C, nseg;
+  int off[4], h[4], w[4];
 };
 
 enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 
 // launchers (defined in the .hip translation units)
-hipError_t launch_gemm_nt_bf16(const void* A, long lda, long strideA, const void* B, long ldb,
-                               long strideB, void* C, int out_dtype, long ldc, long strideC, int M,
-                               int N, int K, float alpha, int batch, hipStream_t stream);
+hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s);
+hipError_t launch_pyramid_unpool(const UnpoolArgs& u, hipStream_t s);
 hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int W, hipStream_t s);
 hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void* out, int out_dtype,
                                   int B, int H, int W, int r, int out_ch, hipStream_t s);
@@ -46,8 +66,6 @@ hipError_t launch_pack_flow(const float* flow, void* flow8, void* motion, long s
                             int from_coords, hipStream_t s);
 hipError_t launch_apply_delta(const float* coords1, const float* delta, long sd, float* coords_out,
                               float* flow_out, int B, int HW, int W, hipStream_t s);
-hipError_t launch_pyramid_grad_combine(const PyrDesc& dpyr, void* dC, void* dCt, int B, int H,
-                                       int W, int ldp, float alpha, hipStream_t s);
 hipError_t launch_convex_up_fwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
                                 long msH, long msW, float* out, int B, int H, int W, hipStream_t s);
 hipError_t launch_convex_up_bwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
@@ -186,6 +204,8 @@ void check_gpu(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), "raft_amd: ", name, " must be a GPU tensor");
 }
 
+// Pyramid levels: (rows, Hl, Wl) fp32 views with unit x stride and y stride Wl; the row
+// stride may exceed Hl*Wl (padded rows, as the GEMM operands need 8-element-aligned pitches).
 PyrDesc make_desc(const std::vector<at::Tensor>& levels, long rows) {
   TORCH_CHECK(levels.size() >= 1 && levels.size() <= 4, "raft_amd: 1..4 pyramid levels supported");
   PyrDesc d{};
@@ -193,42 +213,107 @@ PyrDesc make_desc(const std::vector<at::Tensor>& levels, long rows) {
   for (size_t l = 0; l < levels.size(); ++l) {
     const auto& t = levels[l];
     check_gpu(t, "pyramid level");
-    TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous() && t.dim() == 3,
-                "raft_amd: pyramid levels must be contiguous fp32 (B*H*W, Hl, Wl)");
+    TORCH_CHECK(t.scalar_type() == at::kFloat && t.dim() == 3 && t.stride(2) == 1 && t.stride(1) == t.size(2) &&
+                    t.stride(0) >= t.size(1) * t.size(2),
+                "raft_amd: pyramid levels must be fp32 (B*H*W, Hl, Wl) row views");
     TORCH_CHECK(t.size(0) == rows, "raft_amd: pyramid level rows mismatch");
+    TORCH_CHECK(t.storage_offset() + (rows - 1) * t.stride(0) + t.size(1) * t.size(2) <=
+                    (long)(t.storage().nbytes() / sizeof(float)),
+                "raft_amd: pyramid level view exceeds its storage");
     d.ptr[l] = t.data_ptr<float>();
     d.H[l] = static_cast<int>(t.size(1));
     d.W[l] = static_cast<int>(t.size(2));
+    d.ld[l] = t.stride(0);
   }
   return d;
 }
 
 // ---------------------------------------------------------------- GEMM
+long elem_span(const at::Tensor& t) {  // elements addressable from data_ptr()
+  return (long)(t.storage().nbytes() / t.element_size()) - t.storage_offset();
+}
+
+// C (op)= alpha * A . B^T on the correlation-path MFMA kernel (csrc/corr_volume.hip): flat
+// operands with explicit pitches, fp32/bf16 inputs (split = 3-pass bf16 for fp32 accuracy),
+// transposed A, epilogues store (epi 0) / accumulate (epi 1, fp32).
+void corr_gemm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t M, int64_t N, int64_t K,
+               int64_t batch, int64_t lda, int64_t sA, int64_t ldb, int64_t sB, int64_t ldc, int64_t sC, double alpha,
+               bool a_trans, bool split, int64_t epi) {
+  check_gpu(A, "A");
+  check_gpu(B, "B");
+  check_gpu(C, "C");
+  auto ok_t = [](const at::Tensor& t) { return t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16; };
+  TORCH_CHECK(ok_t(A) && ok_t(B) && ok_t(C), "raft_amd::corr_gemm: operands must be fp32 or bf16");
+  TORCH_CHECK(epi == 0 || C.scalar_type() == at::kFloat, "raft_amd::corr_gemm: accumulating epilogues write fp32");
+  TORCH_CHECK(M >= 0 && N >= 0 && K > 0 && batch >= 1 && (epi == 0 || epi == 1), "raft_amd::corr_gemm: bad sizes");
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && sA % 8 == 0 && sB % 8 == 0,
+              "raft_amd::corr_gemm: operand pitches must be multiples of 8 elements");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
+              "raft_amd::corr_gemm: operands must be 16-byte aligned");
+  auto r8 = [](long v) { return (v + 7) / 8 * 8; };
+  // every 8-element chunk the kernel may touch lies inside the storage
+  const long a_need = a_trans ? (batch - 1) * sA + (K - 1) * lda + r8(M) : (batch - 1) * sA + (M - 1) * lda + r8(K);
+  const long b_need = (batch - 1) * sB + (N - 1) * ldb + r8(K);
+  TORCH_CHECK(a_need <= elem_span(A), "raft_amd::corr_gemm: A too small");
+  TORCH_CHECK(b_need <= elem_span(B), "raft_amd::corr_gemm: B too small");
+  const long c_need = (batch - 1) * sC + (M - 1) * ldc + N;
+  CorrGemmArgs g{};
+  TORCH_CHECK(c_need <= elem_span(C), "raft_amd::corr_gemm: C too small");
+  if (M == 0 || N == 0) return;
+  g.A = A.data_ptr(); g.lda = lda; g.sA = sA;
+  g.B = B.data_ptr(); g.ldb = ldb; g.sB = sB;
+  g.C = C.data_ptr(); g.ldc = ldc; g.sC = sC;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K; g.batch = (int)batch;
+  g.alpha = (float)alpha;
+  g.a_f32 = A.scalar_type() == at::kFloat;
+  g.b_f32 = B.scalar_type() == at::kFloat;
+  g.a_trans = a_trans;
+  g.split = split;
+  g.c_bf16 = C.scalar_type() == at::kBFloat16;
+  g.epi = (int)epi;
+  const c10::DeviceGuard guard(A.device());
+  HIP_OK(launch_corr_gemm(g, cur_stream()));
+}
+
 at::Tensor gemm_nt(const at::Tensor& A, const at::Tensor& B, double alpha, at::ScalarType out_dtype) {
   check_gpu(A, "A");
   check_gpu(B, "B");
-  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16,
-              "raft_amd::gemm_nt expects bf16 operands");
   TORCH_CHECK(A.dim() == 3 && B.dim() == 3, "raft_amd::gemm_nt expects (batch, rows, K)");
   TORCH_CHECK(A.stride(2) == 1 && B.stride(2) == 1, "raft_amd::gemm_nt: K must be contiguous");
   const long batch = A.size(0), M = A.size(1), K = A.size(2), N = B.size(1);
   TORCH_CHECK(B.size(0) == batch && B.size(2) == K, "raft_amd::gemm_nt: shape mismatch");
-  TORCH_CHECK(K % 64 == 0, "raft_amd::gemm_nt: K must be a multiple of 64 (got ", K, ")");
-  TORCH_CHECK(A.stride(1) % 8 == 0 && B.stride(1) % 8 == 0 && A.stride(0) % 8 == 0 &&
-                  B.stride(0) % 8 == 0,
-              "raft_amd::gemm_nt: row strides must be multiples of 8 elements");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 &&
-                  reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
-              "raft_amd::gemm_nt: operands must be 16-byte aligned");
-  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16,
-              "raft_amd::gemm_nt: out dtype must be fp32 or bf16");
-  const c10::DeviceGuard guard(A.device());
+  TORCH_CHECK(K % 8 == 0, "raft_amd::gemm_nt: K must be a multiple of 8 (got ", K, ")");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "raft_amd::gemm_nt: out dtype must be fp32 or bf16");
   auto C = at::empty({batch, M, N}, A.options().dtype(out_dtype));
   if (batch == 0 || M == 0 || N == 0) return C;
-  HIP_OK(launch_gemm_nt_bf16(A.data_ptr(), A.stride(1), A.stride(0), B.data_ptr(), B.stride(1),
-                             B.stride(0), C.data_ptr(), dtype_code(out_dtype), N, M * N, M, N, K,
-                             static_cast<float>(alpha), batch, cur_stream()));
+  corr_gemm(A, B, C, M, N, K, batch, A.stride(1), A.stride(0), B.stride(1), B.stride(0), N, M * N, alpha, false,
+            false, 0);
   return C;
+}
+
+// out (B, H*W, C) = adjoint of the pyramid pools applied to the concatenated level rows of G
+// (B, ld, C); segs = [off, Hl, Wl] per level (level l pools 2^l x 2^l blocks).
+at::Tensor pyramid_unpool(const at::Tensor& G, int64_t H, int64_t W, at::IntArrayRef segs) {
+  check_gpu(G, "G");
+  TORCH_CHECK(G.scalar_type() == at::kFloat && G.dim() == 3 && G.is_contiguous(),
+              "raft_amd::pyramid_unpool: G must be contiguous fp32 (B, rows, C)");
+  TORCH_CHECK(segs.size() % 3 == 0 && segs.size() >= 3 && segs.size() <= 12, "raft_amd::pyramid_unpool: 1..4 levels");
+  UnpoolArgs u{};
+  u.B = (int)G.size(0); u.C = (int)G.size(2); u.H = (int)H; u.W = (int)W;
+  u.nseg = (int)(segs.size() / 3);
+  for (int l = 0; l < u.nseg; ++l) {
+    u.off[l] = (int)segs[3 * l]; u.h[l] = (int)segs[3 * l + 1]; u.w[l] = (int)segs[3 * l + 2];
+    TORCH_CHECK(u.off[l] >= 0 && u.h[l] <= (H >> l) && u.w[l] <= (W >> l) &&
+                    (long)u.off[l] + (long)u.h[l] * u.w[l] <= G.size(1),
+                "raft_amd::pyramid_unpool: level ", l, " does not fit");
+  }
+  u.G = G.data_ptr<float>();
+  u.sG = G.stride(0);
+  const c10::DeviceGuard guard(G.device());
+  auto out = at::empty({G.size(0), H * W, G.size(2)}, G.options());
+  u.out = out.data_ptr<float>();
+  HIP_OK(launch_pyramid_unpool(u, cur_stream()));
+  return out;
 }
 
 // ---------------------------------------------------------------- pyramid
@@ -282,21 +367,6 @@ void corr_lookup_backward_(at::TensorList dpyr, const at::Tensor& coords, const 
   HIP_OK(launch_corr_lookup_bwd(d, coords.data_ptr<float>(), g.data_ptr(),
                                 dtype_code(g.scalar_type()), B, H, W, static_cast<int>(radius),
                                 static_cast<int>(g.size(3)), cur_stream()));
-}
-
-std::tuple<at::Tensor, at::Tensor> pyramid_grad_combine(at::TensorList dpyr, int64_t B, int64_t H,
-                                                        int64_t W, int64_t ldp, double alpha) {
-  std::vector<at::Tensor> lv(dpyr.begin(), dpyr.end());
-  PyrDesc d = make_desc(lv, B * H * W);
-  TORCH_CHECK(lv[0].size(1) == H && lv[0].size(2) == W, "raft_amd: level 0 must be (B*H*W, H, W)");
-  TORCH_CHECK(ldp >= H * W && ldp % 64 == 0, "raft_amd: ldp must be >= H*W and a multiple of 64");
-  const c10::DeviceGuard guard(lv[0].device());
-  auto opts = lv[0].options().dtype(at::kBFloat16);
-  auto dC = at::empty({B, H * W, ldp}, opts);
-  auto dCt = at::empty({B, H * W, ldp}, opts);
-  HIP_OK(launch_pyramid_grad_combine(d, dC.data_ptr(), dCt.data_ptr(), B, H, W, ldp,
-                                     static_cast<float>(alpha), cur_stream()));
-  return {dC, dCt};
 }
 
 // ---------------------------------------------------------------- convex upsampling
@@ -954,8 +1024,9 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("convex_upsample_backward_into(Tensor flow, Tensor mask, Tensor grad, Tensor(a!) dmask, Tensor(b!) rows) -> ()");
   m.def("corr_lookup_backward_(Tensor(a!)[] dpyramid, Tensor coords, Tensor grad, int radius) -> ()");
   m.def(
-      "pyramid_grad_combine(Tensor[] dpyramid, int B, int H, int W, int ldp, float alpha) -> (Tensor, "
-      "Tensor)");
+      "corr_gemm(Tensor A, Tensor B, Tensor(a!) C, int M, int N, int K, int batch, int lda, int sA, int ldb, int sB, "
+      "int ldc, int sC, float alpha, bool a_trans, bool split, int epi) -> ()");
+  m.def("pyramid_unpool(Tensor G, int H, int W, int[] segs) -> Tensor");
   m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");
   m.def("convex_upsample_backward(Tensor flow, Tensor mask, Tensor grad) -> (Tensor, Tensor)");
   m.def("seq_loss(Tensor[] preds, Tensor gt, Tensor valid, float gamma, float max_flow) -> Tensor");
@@ -973,7 +1044,8 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("avgpool2x2", &raft_amd::avgpool2x2);
   m.impl("corr_lookup", &raft_amd::corr_lookup);
   m.impl("corr_lookup_backward_", &raft_amd::corr_lookup_backward_);
-  m.impl("pyramid_grad_combine", &raft_amd::pyramid_grad_combine);
+  m.impl("corr_gemm", &raft_amd::corr_gemm);
+  m.impl("pyramid_unpool", &raft_amd::pyramid_unpool);
   m.impl("convex_upsample", &raft_amd::convex_upsample);
   m.impl("convex_upsample_backward", &raft_amd::convex_upsample_backward);
   m.impl("seq_loss", &raft_amd::seq_loss);

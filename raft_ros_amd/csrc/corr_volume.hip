@@ -1,0 +1,451 @@
+// All-pairs correlation on gfx950: pyramid build, radius-r lookup (fwd/bwd) and the
+// pyramid backward, for the reference CorrBlock (core/corr.py:12-60).
+//
+// Semantics kept from the reference:
+//   * level l = 2x2 / stride-2 average pool (floor) of level l-1 over the image-2 dims;
+//   * lookup at coords / 2^l, window [-r, r]^2, bilinear, align_corners=True, zero padding
+//     (grid_sample, core/utils/utils.py:57-71); channel order level-major, then x-offset
+//     major (ch = l*(2r+1)^2 + ix*(2r+1) + iy, core/corr.py:37-43).
+//
+// MI355X design:
+//   * the volume is linear in fmap2, so level l = alpha * f1 . pool_l(f2)^T: every level is
+//     its own MFMA GEMM against the avg-pooled fmap2 (K = C), written once -- no pooling
+//     pass over the O(HW^2) volume;
+//   * the backward needs no dense dC / dC^T either: with dL_l the accumulated fp32 gradient
+//     of level l (the lookup backward adds each iteration's window gradients into it),
+//         dF1 = alpha * sum_l dL_l . pool_l(f2)             (GEMM, K = HW_l, accumulated)
+//         dF2 = alpha * sum_l unpool_l(dL_l^T . f1)         (GEMM with a transposed A
+//                                                           operand read straight from dL_l,
+//                                                           the adjoint pool fused in the
+//                                                           epilogue)
+//   * every GEMM reads fp32 or bf16 operands and converts while staging to LDS; in split
+//     mode an fp32 operand is x = hi + lo (two bf16) and the product takes three bf16 MFMAs
+//     (hi.hi + hi.lo + lo.hi): fp32-faithful correlation for non-AMP runs (the reference
+//     keeps the volume in fp32, core/raft.py:102-103) at 3x bf16 cost instead of the 16x of
+//     the fp32 MFMA;
+//   * lookup: one wave per query pixel and level loads the (2r+2)^2 integer neighbourhood
+//     of its volume row once (one float per lane, rows of 2r+2 contiguous floats), stages it
+//     in LDS and blends the (2r+1)^2 taps from there; the backward is the transpose (taps ->
+//     neighbourhood gradients in LDS, one read-modify-write per neighbour, no atomics: a
+//     query owns its volume row).
+#include "common.h"
+
+namespace raft_amd {
+
+struct PyrDesc {
+  float* ptr[4];
+  int H[4];
+  int W[4];
+  long ld[4];  // row pitch (floats) of level l: row `pix` starts at ptr[l] + pix * ld[l]
+  int levels;
+};
+
+// One GEMM of the correlation path: C[b][m][n] (op)= alpha * sum_k A[b][m][k] * B[b][n][k]
+struct CorrGemmArgs {
+  const void* A;  // fp32 or bf16; a_trans: element (m, k) at A[k * lda + m]
+  long lda, sA;
+  const void* B;  // fp32 or bf16, element (n, k) at B[n * ldb + k]
+  long ldb, sB;
+  void* C;  // fp32 (or bf16 for epi 0)
+  long ldc, sC;
+  int M, N, K, batch;
+  float alpha;
+  int a_f32, b_f32, a_trans, split, c_bf16;
+  int epi;  // 0 store, 1 accumulate
+};
+
+// Adjoint of the pyramid pools: out[b][y][x][c] = sum_l G[b][off_l + (y>>l)*w_l + (x>>l)][c] / 4^l
+// over the levels whose (floor-sized) plane covers (y, x).  G holds the per-level gradients
+// of all levels (rows = concatenated levels), so each output element is one thread's sum:
+// deterministic, no read-modify-write races between levels.
+struct UnpoolArgs {
+  const float* G;
+  long sG;  // batch stride of G (elements); row pitch = C
+  float* out;
+  int B, H, W, C, nseg;
+  int off[4], h[4], w[4];
+};
+
+namespace {
+
+constexpr int GBM = 128, GBN = 128, GBK = 32;
+constexpr int KP = GBK + 8;     // [m][k] LDS pitch (bf16): 80-byte rows
+constexpr int TP = GBM + 32;    // [k][m] LDS pitch for a transposed A operand
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ s16x4 tr_read(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(reinterpret_cast<uintptr_t>(p) & 0xffffffffu));
+}
+
+__device__ __forceinline__ __bf16 bf_hi(float x) { return static_cast<__bf16>(x); }
+__device__ __forceinline__ __bf16 bf_lo(float x) { return static_cast<__bf16>(x - static_cast<float>(static_cast<__bf16>(x))); }
+
+// 8 consecutive elements (k or m) of an operand row -> hi / lo bf16 (lo = 0 unless split)
+__device__ __forceinline__ void load8(const void* base, long off, bool f32, bool ok, bf16x8& hi, bf16x8& lo) {
+  if (!ok) {
+    hi = bf16x8{};
+    lo = bf16x8{};
+    return;
+  }
+  if (f32) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(static_cast<const float*>(base) + off);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(static_cast<const float*>(base) + off + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      hi[i] = bf_hi(a[i]);
+      lo[i] = bf_lo(a[i]);
+      hi[4 + i] = bf_hi(b[i]);
+      lo[4 + i] = bf_lo(b[i]);
+    }
+  } else {
+    hi = *reinterpret_cast<const bf16x8*>(static_cast<const __bf16*>(base) + off);
+    lo = bf16x8{};
+  }
+}
+
+template <bool SPLIT, bool ATRANS>
+__global__ __launch_bounds__(256) void corr_gemm_kernel(const CorrGemmArgs g) {
+  // LDS: A (hi[, lo]) then B (hi[, lo])
+  constexpr int ASZ = ATRANS ? GBK * TP : GBM * KP;
+  constexpr int BSZ = GBN * KP;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[(SPLIT ? 2 : 1) * (ASZ + BSZ)];
+  __bf16* sAh = smem;
+  __bf16* sAl = smem + ASZ;                              // used when SPLIT
+  __bf16* sBh = smem + (SPLIT ? 2 : 1) * ASZ;
+  __bf16* sBl = sBh + BSZ;
+
+  const int tilesM = (g.M + GBM - 1) / GBM, tilesN = (g.N + GBN - 1) / GBN;
+  const int per_b = tilesM * tilesN;
+  const int wg = xcd_remap(blockIdx.x, per_b * g.batch);
+  const int b = wg / per_b, t = wg - b * per_b;
+  const int m0 = (t / tilesN) * GBM, n0 = (t - (t / tilesN) * tilesN) * GBN;
+  const void* A = static_cast<const char*>(g.A) + b * g.sA * (g.a_f32 ? 4 : 2);
+  const void* B = static_cast<const char*>(g.B) + b * g.sB * (g.b_f32 ? 4 : 2);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // staging: 512 chunks of 8 elements per operand per K step -> 2 per thread
+  bf16x8 rah[2], ral[2], rbh[2], rbl[2];
+  auto load = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      if (ATRANS) {  // k row (32) x 16 chunks of 8 m
+        const int kr = c >> 4, mc = (c & 15) * 8;
+        const bool ok = k0 + kr < g.K && m0 + mc < g.M;
+        load8(A, (long)(k0 + kr) * g.lda + m0 + mc, g.a_f32, ok, rah[i], ral[i]);
+      } else {  // m row (128) x 4 chunks of 8 k
+        const int mr = c >> 2, kc = (c & 3) * 8;
+        const bool ok = m0 + mr < g.M && k0 + kc < g.K;
+        load8(A, (long)(m0 + mr) * g.lda + k0 + kc, g.a_f32, ok, rah[i], ral[i]);
+      }
+      const int nr = c >> 2, kc = (c & 3) * 8;
+      const bool okb = n0 + nr < g.N && k0 + kc < g.K;
+      load8(B, (long)(n0 + nr) * g.ldb + k0 + kc, g.b_f32, okb, rbh[i], rbl[i]);
+    }
+  };
+  auto store = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int ao = ATRANS ? (c >> 4) * TP + (c & 15) * 8 : (c >> 2) * KP + (c & 3) * 8;
+      *reinterpret_cast<bf16x8*>(sAh + ao) = rah[i];
+      if (SPLIT) *reinterpret_cast<bf16x8*>(sAl + ao) = ral[i];
+      const int bo = (c >> 2) * KP + (c & 3) * 8;
+      *reinterpret_cast<bf16x8*>(sBh + bo) = rbh[i];
+      if (SPLIT) *reinterpret_cast<bf16x8*>(sBl + bo) = rbl[i];
+    }
+  };
+
+  const int fr = lane & 31, fk = (lane >> 5) * 8;
+  const int hh = lane >> 5, gi = (lane >> 4) & 1, q = (lane & 15) >> 2, pq = lane & 3;
+  auto afrag = [&](const __bf16* s, int i, int ks) __attribute__((always_inline)) {
+    if (ATRANS) {
+      const int col = wm * 64 + i * 32 + gi * 16 + 4 * pq;
+      const int r0 = ks * 16 + hh * 8 + q;
+      const s16x4 lo = tr_read(s + r0 * TP + col);
+      const s16x4 hi = tr_read(s + (r0 + 4) * TP + col);
+      return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+    return *reinterpret_cast<const bf16x8*>(s + (wm * 64 + i * 32 + fr) * KP + ks * 16 + fk);
+  };
+
+  load(0);
+  for (int k0 = 0; k0 < g.K; k0 += GBK) {
+    store();
+    __syncthreads();
+    if (k0 + GBK < g.K) load(k0 + GBK);
+#pragma unroll
+    for (int ks = 0; ks < GBK / 16; ++ks) {
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        ah[i] = afrag(sAh, i, ks);
+        if (SPLIT) al[i] = afrag(sAl, i, ks);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int o = (wn * 64 + j * 32 + fr) * KP + ks * 16 + fk;
+        bh[j] = *reinterpret_cast<const bf16x8*>(sBh + o);
+        if (SPLIT) bl[j] = *reinterpret_cast<const bf16x8*>(sBl + o);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if (SPLIT) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+  }
+
+  // epilogue: C/D map of the 32x32 MFMA: col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + j * 32 + (lane & 31);
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m >= g.M) continue;
+        const float v = g.alpha * acc[i][j][r];
+        if (g.epi == 0) {
+          if (g.c_bf16)
+            static_cast<__bf16*>(g.C)[b * g.sC + (long)m * g.ldc + n] = static_cast<__bf16>(v);
+          else
+            static_cast<float*>(g.C)[b * g.sC + (long)m * g.ldc + n] = v;
+        } else {
+          static_cast<float*>(g.C)[b * g.sC + (long)m * g.ldc + n] += v;
+        }
+      }
+    }
+}
+
+__global__ __launch_bounds__(256) void pyramid_unpool_kernel(const UnpoolArgs u) {
+  const long total = (long)u.B * u.H * u.W * u.C;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % u.C);
+    const long pix = i / u.C;
+    const int x = (int)(pix % u.W);
+    const long t = pix / u.W;
+    const int y = (int)(t % u.H);
+    const int b = (int)(t / u.H);
+    const float* G = u.G + b * u.sG;
+    float v = 0.f, s = 1.f;
+    for (int l = 0; l < u.nseg; ++l, s *= 0.25f) {
+      const int yl = y >> l, xl = x >> l;
+      if (yl < u.h[l] && xl < u.w[l]) v += s * G[(long)(u.off[l] + yl * u.w[l] + xl) * u.C + c];
+    }
+    u.out[i] = v;
+  }
+}
+
+__device__ __forceinline__ float safe_floor(float v) {
+  // keep far-out-of-range / non-finite coordinates from overflowing int math
+  v = fminf(fmaxf(v, -1.0e6f), 1.0e6f);
+  return floorf(v);
+}
+
+// ---------------------------------------------------------------------------- lookup
+// One wave per query pixel, looping over the levels; 4 waves per block.  LDS per wave:
+// the (2r+2)^2 neighbourhood (<= 14 x 14 for r <= 6) as fp32.
+constexpr int NBMAX = 14 * 14;
+
+template <typename OutT>
+__global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const float* __restrict__ coords,
+                                                         OutT* __restrict__ out, int B, int H, int W, int r,
+                                                         int out_ch) {
+  __shared__ float nb[4][NBMAX];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int HW = H * W;
+  const long pix0 = (long)blockIdx.x * 4 + wave;
+  const bool live = pix0 < (long)B * HW;  // no early exit: the block synchronises per level
+  const long pix = live ? pix0 : 0;
+  const int b = pix / HW, p = pix - (long)b * HW;
+  const int rd = 2 * r + 1, nd = rd + 1, win = rd * rd;
+  const float cx0 = coords[(long)b * 2 * HW + p], cy0 = coords[(long)b * 2 * HW + HW + p];
+  const bool finite = isfinite(cx0) && isfinite(cy0);
+  OutT* o = out + pix * out_ch;
+  for (int l = 0; l < pyr.levels; ++l) {
+    const float s = 1.0f / float(1 << l);
+    const float cx = finite ? cx0 * s : 0.f, cy = finite ? cy0 * s : 0.f;
+    const float fx0 = safe_floor(cx), fy0 = safe_floor(cy);
+    const float fx = cx - fx0, fy = cy - fy0;
+    const int xb = (int)fx0 - r, yb = (int)fy0 - r;
+    const int Hl = pyr.H[l], Wl = pyr.W[l];
+    const float* row = pyr.ptr[l] + pix * pyr.ld[l];
+    for (int e = lane; e < nd * nd; e += 64) {
+      const int a = e / nd, c = e - a * nd;  // neighbour (y = yb + a, x = xb + c)
+      const int y = yb + a, x = xb + c;
+      nb[wave][e] = (live && finite && (unsigned)y < (unsigned)Hl && (unsigned)x < (unsigned)Wl) ? row[y * Wl + x]
+                                                                                                 : 0.f;
+    }
+    __syncthreads();
+    if (live)
+      for (int ch = lane; ch < win; ch += 64) {
+        const int ix = ch / rd, iy = ch - ix * rd;  // x-offset-major window order
+        const float* n0 = nb[wave] + iy * nd + ix;
+        const float v =
+            (1.f - fy) * ((1.f - fx) * n0[0] + fx * n0[1]) + fy * ((1.f - fx) * n0[nd] + fx * n0[nd + 1]);
+        o[l * win + ch] = from_f32<OutT>(v);
+      }
+    __syncthreads();
+  }
+  if (live)
+    for (int ch = pyr.levels * win + lane; ch < out_ch; ch += 64) o[ch] = from_f32<OutT>(0.f);
+}
+
+// dpyr[l][pix][y][x] += window gradient, transposed bilinear blend; one wave per query.
+template <typename GT>
+__global__ __launch_bounds__(256) void lookup_bwd_kernel(PyrDesc dpyr, const float* __restrict__ coords,
+                                                         const GT* __restrict__ gout, int B, int H, int W, int r,
+                                                         int gstride) {
+  __shared__ float gs[4][NBMAX];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int HW = H * W;
+  const long pix0 = (long)blockIdx.x * 4 + wave;
+  const long pix = pix0 < (long)B * HW ? pix0 : 0;
+  const int b = pix / HW, p = pix - (long)b * HW;
+  const int rd = 2 * r + 1, nd = rd + 1, win = rd * rd;
+  const float cx0 = coords[(long)b * 2 * HW + p], cy0 = coords[(long)b * 2 * HW + HW + p];
+  // no early exit: the block synchronises per level
+  const bool live = pix0 < (long)B * HW && isfinite(cx0) && isfinite(cy0);
+  const GT* g = gout + pix * gstride;
+  for (int l = 0; l < dpyr.levels; ++l) {
+    const float s = 1.0f / float(1 << l);
+    const float cx = live ? cx0 * s : 0.f, cy = live ? cy0 * s : 0.f;
+    const float fx0 = safe_floor(cx), fy0 = safe_floor(cy);
+    const float fx = cx - fx0, fy = cy - fy0;
+    const int xb = (int)fx0 - r, yb = (int)fy0 - r;
+    const int Hl = dpyr.H[l], Wl = dpyr.W[l];
+    // window gradient in LDS as [iy][ix] (transposed from the x-major channel order)
+    for (int ch = lane; ch < win; ch += 64) {
+      const int ix = ch / rd, iy = ch - ix * rd;
+      gs[wave][iy * rd + ix] = live ? to_f32(g[l * win + ch]) : 0.f;
+    }
+    __syncthreads();
+    float* row = dpyr.ptr[l] + pix * dpyr.ld[l];
+    for (int e = lane; live && e < nd * nd; e += 64) {
+      const int a = e / nd, c = e - a * nd;
+      const int y = yb + a, x = xb + c;
+      if ((unsigned)y >= (unsigned)Hl || (unsigned)x >= (unsigned)Wl) continue;
+      // neighbour (a, c) is corner (0,0) of tap (c, a), (0,1) of (c-1, a), (1,0) of (c, a-1),
+      // (1,1) of (c-1, a-1)
+      const float* gw = gs[wave];
+      float v = 0.f;
+      if (a < rd) {
+        if (c < rd) v += (1.f - fx) * (1.f - fy) * gw[a * rd + c];
+        if (c > 0) v += fx * (1.f - fy) * gw[a * rd + c - 1];
+      }
+      if (a > 0) {
+        if (c < rd) v += (1.f - fx) * fy * gw[(a - 1) * rd + c];
+        if (c > 0) v += fx * fy * gw[(a - 1) * rd + c - 1];
+      }
+      row[y * Wl + x] += v;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void avgpool2x2_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                         long rows, int H, int W, int Ho, int Wo) {
+  const long total = rows * Ho * Wo;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int x = i % Wo;
+    const long t = i / Wo;
+    const int y = t % Ho;
+    const long rr = t / Ho;
+    const float* src = in + rr * H * W + (2 * y) * W + 2 * x;
+    out[i] = 0.25f * (src[0] + src[1] + src[W] + src[W + 1]);
+  }
+}
+
+inline int grid_for(long total) {
+  long blocks = (total + 255) / 256;
+  return (int)(blocks < (1L << 20) ? blocks : (1L << 20));
+}
+
+}  // namespace
+
+hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s) {
+  if (g.M == 0 || g.N == 0 || g.batch == 0) return hipSuccess;
+  const dim3 grid((unsigned)(((g.M + GBM - 1) / GBM) * ((g.N + GBN - 1) / GBN) * g.batch)), blk(256);
+  if (g.split) {
+    if (g.a_trans) hipLaunchKernelGGL((corr_gemm_kernel<true, true>), grid, blk, 0, s, g);
+    else hipLaunchKernelGGL((corr_gemm_kernel<true, false>), grid, blk, 0, s, g);
+  } else {
+    if (g.a_trans) hipLaunchKernelGGL((corr_gemm_kernel<false, true>), grid, blk, 0, s, g);
+    else hipLaunchKernelGGL((corr_gemm_kernel<false, false>), grid, blk, 0, s, g);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_pyramid_unpool(const UnpoolArgs& u, hipStream_t s) {
+  const long total = (long)u.B * u.H * u.W * u.C;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(pyramid_unpool_kernel, dim3(grid_for(total)), dim3(256), 0, s, u);
+  return hipGetLastError();
+}
+
+hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int W, hipStream_t s) {
+  const int Ho = H / 2, Wo = W / 2;
+  const long total = rows * Ho * Wo;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(avgpool2x2_kernel, dim3(grid_for(total)), dim3(256), 0, s, in, out, rows, H, W, Ho, Wo);
+  return hipGetLastError();
+}
+
+hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void* out, int out_dtype, int B, int H,
+                                  int W, int r, int out_ch, hipStream_t s) {
+  const long npix = (long)B * H * W;
+  if (npix == 0) return hipSuccess;
+  if (r > 6) return hipErrorInvalidValue;
+  const dim3 g((unsigned)((npix + 3) / 4)), blk(256);
+  if (out_dtype == kBF16)
+    hipLaunchKernelGGL(lookup_fwd_kernel<__bf16>, g, blk, 0, s, pyr, coords, static_cast<__bf16*>(out), B, H, W, r,
+                       out_ch);
+  else if (out_dtype == kF16)
+    hipLaunchKernelGGL(lookup_fwd_kernel<_Float16>, g, blk, 0, s, pyr, coords, static_cast<_Float16*>(out), B, H, W,
+                       r, out_ch);
+  else
+    hipLaunchKernelGGL(lookup_fwd_kernel<float>, g, blk, 0, s, pyr, coords, static_cast<float*>(out), B, H, W, r,
+                       out_ch);
+  return hipGetLastError();
+}
+
+hipError_t launch_corr_lookup_bwd(const PyrDesc& dpyr, const float* coords, const void* gout, int g_dtype, int B,
+                                  int H, int W, int r, int gstride, hipStream_t s) {
+  const long npix = (long)B * H * W;
+  if (npix == 0) return hipSuccess;
+  if (r > 6) return hipErrorInvalidValue;
+  const dim3 g((unsigned)((npix + 3) / 4)), blk(256);
+  if (g_dtype == kBF16)
+    hipLaunchKernelGGL(lookup_bwd_kernel<__bf16>, g, blk, 0, s, dpyr, coords, static_cast<const __bf16*>(gout), B, H,
+                       W, r, gstride);
+  else if (g_dtype == kF16)
+    hipLaunchKernelGGL(lookup_bwd_kernel<_Float16>, g, blk, 0, s, dpyr, coords, static_cast<const _Float16*>(gout), B,
+                       H, W, r, gstride);
+  else
+    hipLaunchKernelGGL(lookup_bwd_kernel<float>, g, blk, 0, s, dpyr, coords, static_cast<const float*>(gout), B, H,
+                       W, r, gstride);
+  return hipGetLastError();
+}
+
+}  // namespace raft_amd

@@ -126,7 +126,9 @@ class RAFT(nn.Module):
         if self.args.alternate_corr:
             corr_fn = LocalCorrPyramid(fmap1, fmap2, radius=self.args.corr_radius)
         else:
-            corr_fn = CorrPyramid(fmap1, fmap2, radius=self.args.corr_radius)
+            # without AMP the volume stays fp32-faithful (split bf16 MFMA), as the reference
+            # computes it in fp32 in every mode (core/raft.py:102-103)
+            corr_fn = CorrPyramid(fmap1, fmap2, radius=self.args.corr_radius, split=not bool(self.args.mixed_precision))
 
         with self._autocast(dev):
             cnet = self.cnet(image1)

@@ -4,21 +4,25 @@
 (core/corr.py:12-50) and ``LocalCorrPyramid`` for ``AlternateCorrBlock``
 (core/corr.py:63-91).  Both expose ``__call__(coords) -> (B, L*(2r+1)^2, H, W)``.
 
-Autograd design of the dense path (GPU):
+Dense path on the GPU (kernels: csrc/corr_volume.hip):
 
-* ``_BuildPyramid`` runs the bf16 MFMA GEMM (``raft_amd::gemm_nt``, fp32
-  accumulate, 1/sqrt(C) in the epilogue) and the pyramid pools once per
-  forward.  Its only differentiable output is a scalar *token*.
-* every refinement iteration calls ``_Lookup(token, coords)``.  Its backward
-  does not return a dense pyramid gradient: it accumulates, in place and
-  without atomics, into one shared fp32 pyramid-gradient buffer owned by the
-  pyramid state, and returns a zero token gradient.
+* ``_BuildPyramid`` computes every level as its own MFMA GEMM,
+  ``level_l = f1 . pool_l(f2)^T / sqrt(C)`` (the volume is linear in fmap2, so
+  pooling fmap2 equals pooling the volume; no pass over the O(HW^2) volume).
+  Without AMP the GEMMs run in split mode (fp32 operands as hi+lo bf16, three
+  MFMAs per product), which keeps the volume fp32-faithful like the reference
+  (core/raft.py:102-103); under AMP the operands are rounded to bf16.
+  Its only differentiable output is a scalar *token*.
+* every refinement iteration calls ``_Lookup(token, coords)`` (or the fused
+  update step does the same lookup); the backward adds the window gradients, in
+  place and without atomics, into one fp32 gradient buffer per level.
 * autograd runs ``_BuildPyramid.backward`` only after every lookup's backward
-  has run (they all feed the token), so it folds the accumulated 4-level
-  gradient to level 0 once, and runs two MFMA GEMMs for dfmap1/dfmap2.
+  (they all feed the token): ``dF1 = sum_l dL_l . pool_l(f2)`` and
+  ``dF2 = sum_l unpool_l(dL_l^T . f1)`` as GEMMs straight from the level
+  gradients -- no dense HW x HW ``dC`` / ``dC^T`` is ever formed.
 
-The reference instead materialises a full-pyramid ``grid_sample`` gradient
-per iteration and sums them (12 dense buffers per training step).
+Level rows are padded to a multiple of 8 floats (16-byte aligned GEMM rows);
+the lookup kernels take the row pitch from the view's stride.
 """
 from __future__ import annotations
 
@@ -37,46 +41,91 @@ def _pad_to(n: int, m: int) -> int:
 
 
 class _PyramidState:
-    """Forward/backward state shared by a pyramid build and its lookups."""
+    """Forward/backward state shared by a pyramid build and its lookups.
+
+    All levels live in ONE fp32 buffer of B*HW rows: level l occupies columns
+    [off_l, off_l + Hl*Wl) (each level's width padded to a multiple of 8), so the
+    pyramid build, dF1 and dF2 are one GEMM each over the concatenated levels."""
 
     def __init__(self, num_levels: int, radius: int):
         self.num_levels = num_levels
         self.radius = radius
-        self.levels: List[torch.Tensor] = []
+        self.buf: Optional[torch.Tensor] = None
+        self.levels: List[torch.Tensor] = []   # (B*HW, Hl, Wl) views into buf
+        self.dbuf: Optional[torch.Tensor] = None
         self.dlevels: Optional[List[torch.Tensor]] = None
+        self.sizes = []                        # (Hl, Wl, off) per level
+        self.ld = 0
         self.shape = None
+
+    def views(self, buf: torch.Tensor) -> List[torch.Tensor]:
+        return [buf.as_strided((buf.shape[0], Hl, Wl), (self.ld, Wl, 1), buf.storage_offset() + off)
+                for Hl, Wl, off in self.sizes]
 
     def grad_buffers(self) -> List[torch.Tensor]:
         if self.dlevels is None:
-            self.dlevels = [torch.zeros_like(l) for l in self.levels]
+            self.dbuf = torch.zeros_like(self.buf)
+            self.dlevels = self.views(self.dbuf)
         return self.dlevels
 
+    def segments(self) -> List[int]:
+        out = []
+        for Hl, Wl, off in self.sizes:
+            out += [off, Hl, Wl]
+        return out
+
     def release(self):
+        self.buf = None
         self.levels = []
+        self.dbuf = None
         self.dlevels = None
+
+
+def _pooled(f: torch.Tensor, levels: int) -> List[torch.Tensor]:
+    """fmap (B, C, H, W) fp32 and its 2x2 average pools (floor), levels in total."""
+    out = [f]
+    for _ in range(levels - 1):
+        out.append(F.avg_pool2d(out[-1], 2, stride=2))
+    return out
+
+
+def _concat_levels(fs: List[torch.Tensor], ld: int, offs: List[int], nchw: bool) -> torch.Tensor:
+    """Pooled fmaps -> one zero-padded operand: (B, ld, C) (NHWC rows q) or (B, C, ld)."""
+    B, C = fs[0].shape[:2]
+    out = fs[0].new_zeros((B, C, ld) if nchw else (B, ld, C))
+    for f, off in zip(fs, offs):
+        n = f.shape[2] * f.shape[3]
+        if nchw:
+            out[:, :, off:off + n] = f.reshape(B, C, n)
+        else:
+            out[:, off:off + n] = f.permute(0, 2, 3, 1).reshape(B, n, C)
+    return out
 
 
 class _BuildPyramid(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, fmap1, fmap2, state: _PyramidState):
+    def forward(ctx, fmap1, fmap2, state: _PyramidState, split: bool):
         B, C, H, W = fmap1.shape
         HW = H * W
         k = ops()
-        f1 = fmap1.detach().permute(0, 2, 3, 1).to(torch.bfloat16).reshape(B, HW, C).contiguous()
-        f2 = fmap2.detach().permute(0, 2, 3, 1).to(torch.bfloat16).reshape(B, HW, C).contiguous()
-        if C % 64 != 0:
-            pad = _pad_to(C, 64) - C
-            f1 = F.pad(f1, (0, pad))
-            f2 = F.pad(f2, (0, pad))
-        corr = k.gemm_nt(f1, f2, 1.0 / math.sqrt(C), torch.float32)
-        lvl = corr.view(B * HW, H, W)
-        levels = [lvl]
-        for _ in range(state.num_levels - 1):
-            lvl = k.avgpool2x2(lvl)
-            levels.append(lvl)
-        state.levels = levels
+        alpha = 1.0 / math.sqrt(C)
+        f1 = fmap1.detach().float().permute(0, 2, 3, 1).reshape(B, HW, C).contiguous()
+        f2s = _pooled(fmap2.detach().float(), state.num_levels)
+        sizes, off = [], 0
+        for f in f2s:
+            Hl, Wl = f.shape[-2:]
+            sizes.append((Hl, Wl, off))
+            off += _pad_to(Hl * Wl, 8)
+        ld = off
+        state.sizes, state.ld = sizes, ld
+        f2cat = _concat_levels(f2s, ld, [o for _, _, o in sizes], nchw=False)  # (B, ld, C), pad rows 0
+        buf = torch.empty(B * HW, ld, device=f1.device)
+        # every level at once: buf[p][q] = alpha * f1[p] . f2cat[q]  (pad columns get 0)
+        k.corr_gemm(f1, f2cat, buf, HW, ld, C, B, C, HW * C, C, ld * C, ld, HW * ld, alpha, False, split, 0)
+        state.buf = buf
+        state.levels = state.views(buf)
         state.shape = (B, C, H, W)
-        ctx.state = state
+        ctx.state, ctx.split = state, split
         ctx.save_for_backward(fmap1, fmap2)
         return fmap1.new_zeros((), dtype=torch.float32)
 
@@ -84,25 +133,32 @@ class _BuildPyramid(torch.autograd.Function):
     def backward(ctx, gtoken):
         state: _PyramidState = ctx.state
         fmap1, fmap2 = ctx.saved_tensors
-        if state.dlevels is None:
+        if state.dbuf is None:
             state.release()
-            return None, None, None
+            return None, None, None, None
         B, C, H, W = state.shape
-        HW = H * W
-        ldp = _pad_to(HW, 64)
+        HW, ld = H * W, state.ld
         k = ops()
-        dC, dCt = k.pyramid_grad_combine(state.dlevels, B, H, W, ldp, 1.0 / math.sqrt(C))
+        alpha = 1.0 / math.sqrt(C)
+        split = ctx.split
+        f2s = _pooled(fmap2.detach().float(), state.num_levels)
+        f2t = _concat_levels(f2s, ld, [o for _, _, o in state.sizes], nchw=True)  # (B, C, ld)
+        f1t = fmap1.detach().float().new_zeros(B, C, _pad_to(HW, 8))
+        f1t[:, :, :HW] = fmap1.detach().float().reshape(B, C, HW)
+        d1 = torch.empty(B, HW, C, device=fmap1.device)
+        G = torch.empty(B, ld, C, device=fmap1.device)
+        dbuf = state.dbuf
+        # dF1 = alpha * dL . f2cat            (M = HW, N = C, K = all levels)
+        k.corr_gemm(dbuf, f2t, d1, HW, C, ld, B, ld, HW * ld, ld, C * ld, C, HW * C, alpha, False, split, 0)
+        # G = alpha * dL^T . f1  per level row (M = all levels, N = C, K = HW; A read transposed),
+        # dF2 = sum_l unpool_l(G_l)
+        k.corr_gemm(dbuf, f1t, G, ld, C, HW, B, ld, HW * ld, f1t.shape[2], C * f1t.shape[2], C, ld * C, alpha,
+                    True, split, 0)
+        d2 = k.pyramid_unpool(G, H, W, state.segments())
         state.release()
-
-        def nchw_pad(f):
-            f = f.detach().reshape(B, C, HW).to(torch.bfloat16)
-            return F.pad(f, (0, ldp - HW)).contiguous()
-
-        g1 = k.gemm_nt(dC, nchw_pad(fmap2), 1.0, torch.float32)  # (B, HW, C)
-        g2 = k.gemm_nt(dCt, nchw_pad(fmap1), 1.0, torch.float32)
-        g1 = g1.view(B, H, W, C).permute(0, 3, 1, 2)
-        g2 = g2.view(B, H, W, C).permute(0, 3, 1, 2)
-        return g1.to(fmap1.dtype), g2.to(fmap2.dtype), None
+        g1 = d1.view(B, H, W, C).permute(0, 3, 1, 2)
+        g2 = d2.view(B, H, W, C).permute(0, 3, 1, 2)
+        return g1.to(fmap1.dtype), g2.to(fmap2.dtype), None, None
 
 
 class _Lookup(torch.autograd.Function):
@@ -126,18 +182,20 @@ class _Lookup(torch.autograd.Function):
 class CorrPyramid:
     """All-pairs correlation pyramid with radius-``radius`` lookup.
 
-    GPU: native HIP/MFMA path (see module docstring).  CPU: reference ops.
-    ``out_dtype`` selects the dtype of the looked-up features (bf16 under
-    autocast feeds the motion encoder without an extra cast).
+    GPU: native HIP/MFMA path (see module docstring); ``split=True`` keeps the volume
+    fp32-faithful (use it without AMP).  CPU: reference ops.  ``out_dtype`` selects the
+    dtype of the looked-up features (bf16 under autocast feeds the motion encoder
+    without an extra cast).
     """
 
-    def __init__(self, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4):
+    def __init__(self, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4,
+                 split: bool = False):
         self.num_levels = num_levels
         self.radius = radius
         self.native = use_native(fmap1)
         if self.native:
             self.state = _PyramidState(num_levels, radius)
-            self.token = _BuildPyramid.apply(fmap1, fmap2, self.state)
+            self.token = _BuildPyramid.apply(fmap1, fmap2, self.state, bool(split))
         else:
             corr = ref.corr_volume(fmap1.float(), fmap2.float())
             self.pyramid = ref.build_pyramid(corr, num_levels)

@@ -8,7 +8,7 @@ boundary kernel (one launch per step), drops the first ``--skip`` steps and
 prints / writes a per-step breakdown grouped by kernel name.
 
     python scripts/kernel_summary.py gpurun_out/prof/run_kernel_trace.csv \
-        --boundary pyramid_grad_combine --skip 2 --out profiles/x.csv
+        --boundary seq_loss_fwd --skip 2 --out profiles/x.csv
 """
 from __future__ import annotations
 
@@ -26,7 +26,7 @@ def short(name: str) -> str:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--boundary", default="pyramid_grad_combine")
+    ap.add_argument("--boundary", default="seq_loss_fwd")
     ap.add_argument("--skip", type=int, default=2)
     ap.add_argument("--every", type=int, default=1, help="boundary launches per step")
     ap.add_argument("--out", default=None)

@@ -37,6 +37,65 @@ def test_gemm_nt_identity_asymmetric(cuda):
     torch.testing.assert_close(C[0], B[0].float().t())
 
 
+@pytest.mark.parametrize("split", [False, True])
+def test_corr_gemm_modes(cuda, split):
+    """Transposed A operand, fp32 inputs (split: 3-pass bf16), accumulate and unpool epilogues."""
+    torch.manual_seed(5)
+    ops = _ops()
+    B, M, N, K = 2, 90, 40, 200  # odd sizes: partial tiles, K % 8 == 0
+    A = torch.randn(B, K, M + 6, device=cuda)  # stored transposed, padded pitch
+    Bm = torch.randn(B, N, K, device=cuda)
+    C = torch.randn(B, M, N, device=cuda)
+    C0 = C.clone()
+    ops.corr_gemm(A, Bm, C, M, N, K, B, M + 6, K * (M + 6), K, N * K, N, M * N, 0.5, True, split, 1)
+    want = C0 + 0.5 * torch.matmul(A[:, :, :M].transpose(1, 2), Bm.transpose(1, 2))
+    tol = 1e-4 if split else 2e-2
+    assert ((C - want).norm() / want.norm()).item() < tol
+
+
+def test_pyramid_unpool_is_the_pool_adjoint(cuda):
+    torch.manual_seed(7)
+    B, C, H, W = 2, 16, 13, 22
+    sizes, off = [], 0
+    for l in range(4):
+        Hl, Wl = H >> l, W >> l
+        sizes.append((off, Hl, Wl))
+        off += (Hl * Wl + 7) // 8 * 8
+    G = torch.randn(B, off, C, device=cuda)
+    out = _ops().pyramid_unpool(G, H, W, [v for s_ in sizes for v in s_])
+    # adjoint check: <unpool(G), x> == sum_l <G_l, pool_l(x)>
+    x = torch.randn(B, C, H, W, device=cuda, dtype=torch.float64)
+    lhs = (out.double() * x.permute(0, 2, 3, 1).reshape(B, H * W, C)).sum()
+    rhs, p = 0.0, x
+    for l, (o, Hl, Wl) in enumerate(sizes):
+        if l:
+            p = F.avg_pool2d(p, 2, 2)
+        rhs = rhs + (G[:, o:o + Hl * Wl].double() * p.permute(0, 2, 3, 1).reshape(B, Hl * Wl, C)).sum()
+    assert abs((lhs - rhs) / rhs).item() < 1e-6
+
+
+def test_corr_pyramid_split_is_fp32_faithful(cuda):
+    """Without AMP the native pyramid (split bf16 MFMA) matches the fp32 reference volume and
+    its gradients closely (reference core/raft.py:102-103 keeps the volume fp32)."""
+    torch.manual_seed(6)
+    from raft_ros_amd.ops.corr import CorrPyramid
+
+    B, C, H, W, r = 2, 256, 46, 62, 4
+    f1 = torch.randn(B, C, H, W, device=cuda, requires_grad=True)
+    f2 = torch.randn(B, C, H, W, device=cuda, requires_grad=True)
+    coords = ref.coords_grid(B, H, W, cuda) + 4 * torch.randn(B, 2, H, W, device=cuda)
+    g = torch.randn(B, 4 * (2 * r + 1) ** 2, H, W, device=cuda)
+    out = CorrPyramid(f1, f2, 4, r, split=True)(coords)
+    f1r = f1.detach().clone().requires_grad_(True)
+    f2r = f2.detach().clone().requires_grad_(True)
+    want = ref.pyramid_lookup(ref.build_pyramid(ref.corr_volume(f1r, f2r), 4), coords, r)
+    assert ((out - want).norm() / want.norm()).item() < 3e-5
+    (out * g).sum().backward()
+    (want * g).sum().backward()
+    for got, exp in ((f1.grad, f1r.grad), (f2.grad, f2r.grad)):
+        assert ((got - exp).norm() / exp.norm()).item() < 3e-5
+
+
 def test_avgpool(cuda):
     x = torch.randn(37, 23, 31, device=cuda)
     torch.testing.assert_close(_ops().avgpool2x2(x), F.avg_pool2d(x[:, None], 2, 2)[:, 0])
