@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU-box session of measurements (each step has its own time limit; any abnormal exit
+# -- crash, abort, timeout -- ends the script).  Outputs land in gpurun_out/measure/.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/measure
+mkdir -p $OUT
+export TMPDIR=/tmp
+
+run() {  # run <name> <timeout-seconds> <cmd...>
+  local name=$1 lim=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "    rc=$rc"; tail -n 2 "$OUT/$name.log" | cut -c1-600
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+
+for step in ${STEPS_LIST:-infer1080 infer_sintel alt_kitti dense_kitti conv_native conv_reference}; do
+  case $step in
+    infer1080) run infer1080 300 python bench.py --mode infer --image_size 1080 1920 --iters 32 --batch 1 --steps 10 --warmup 3 ;;
+    infer_sintel) run infer_sintel 300 python bench.py --mode infer --image_size 440 1024 --iters 32 --batch 1 --steps 20 --warmup 3 ;;
+    alt_kitti) run alt_kitti 300 python bench.py --alternate_corr --image_size 376 1248 --batch 3 --steps 10 --warmup 3 ;;
+    dense_kitti) run dense_kitti 300 python bench.py --image_size 376 1248 --batch 3 --steps 10 --warmup 3 ;;
+    conv_native) run conv_native 600 python scripts/convergence.py --impl native --steps ${CONV_STEPS:-2000} ;;
+    conv_reference) run conv_reference 900 python scripts/convergence.py --impl reference --steps ${CONV_STEPS:-2000} ;;
+    ref_bench) run ref_bench 600 python bench.py --impl reference --steps 10 --warmup 3 ;;
+  esac
+done
+echo done
