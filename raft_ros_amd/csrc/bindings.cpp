@@ -48,6 +48,25 @@ enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 
 // launchers (defined in the .hip translation units)
 hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s);
+struct LocalCorrArgs {
+  const void* f1;
+  const void* f2;
+  long f2_bstride;
+  const float* coords;
+  int B, H, W, C, r, levels;
+  int off[4], h[4], w[4];
+  float scale;
+  void* out;
+  long ostride;
+  int out_f32;
+  int out_ch;
+  const void* gout;
+  long gstride;
+  int gout_bf16;
+  float* g1;
+  float* g2;  // layout must match local_corr_mfma.hip
+};
+hipError_t launch_local_corr_mfma(const LocalCorrArgs& a, bool backward, hipStream_t s);
 hipError_t launch_pyramid_unpool(const UnpoolArgs& u, hipStream_t s);
 hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int W, hipStream_t s);
 hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void* out, int out_dtype,
@@ -543,6 +562,69 @@ std::tuple<at::Tensor, at::Tensor> local_corr_backward(const at::Tensor& f1, con
   return {g1, g2};
 }
 
+// ---------------------------------------------------------------- local correlation on MFMA
+// f1 (P, C) bf16 query rows; f2 (B, R, C) bf16 concatenated pooled fmap2 levels with
+// segs = [off, h, w] per level; coords (B, 2, H, W).
+LocalCorrArgs local_mfma_args(const at::Tensor& f1, const at::Tensor& f2, const at::Tensor& coords,
+                              at::IntArrayRef segs, int64_t radius, double scale) {
+  check_gpu(f1, "fmap1");
+  check_gpu(f2, "fmap2");
+  check_coords(coords);
+  TORCH_CHECK(f1.scalar_type() == at::kBFloat16 && f2.scalar_type() == at::kBFloat16 && f1.dim() == 2 &&
+                  f2.dim() == 3 && f1.is_contiguous() && f2.is_contiguous(),
+              "raft_amd::local_corr_mfma: fmap1 (P, C) and fmap2 (B, R, C) must be contiguous bf16");
+  const long B = coords.size(0), H = coords.size(2), W = coords.size(3), C = f1.size(1);
+  TORCH_CHECK(f1.size(0) == B * H * W && f2.size(0) == B && f2.size(2) == C && C % 64 == 0 && C <= 256,
+              "raft_amd::local_corr_mfma: shape mismatch (C must be a multiple of 64, <= 256)");
+  TORCH_CHECK(radius >= 1 && radius <= 4, "raft_amd::local_corr_mfma: radius 1..4");
+  TORCH_CHECK(segs.size() % 3 == 0 && segs.size() >= 3 && segs.size() <= 12, "raft_amd::local_corr_mfma: 1..4 levels");
+  LocalCorrArgs a{};
+  a.levels = (int)(segs.size() / 3);
+  for (int l = 0; l < a.levels; ++l) {
+    a.off[l] = (int)segs[3 * l]; a.h[l] = (int)segs[3 * l + 1]; a.w[l] = (int)segs[3 * l + 2];
+    TORCH_CHECK(a.off[l] >= 0 && a.h[l] > 0 && a.w[l] > 0 && (long)a.off[l] + (long)a.h[l] * a.w[l] <= f2.size(1),
+                "raft_amd::local_corr_mfma: level ", l, " exceeds fmap2");
+  }
+  a.f1 = f1.data_ptr(); a.f2 = f2.data_ptr(); a.f2_bstride = f2.stride(0);
+  a.coords = coords.data_ptr<float>();
+  a.B = (int)B; a.H = (int)H; a.W = (int)W; a.C = (int)C; a.r = (int)radius;
+  a.scale = (float)scale;
+  return a;
+}
+
+void local_corr_mfma(const at::Tensor& f1, const at::Tensor& f2, const at::Tensor& coords, at::IntArrayRef segs,
+                     int64_t radius, double scale, const at::Tensor& out) {
+  LocalCorrArgs a = local_mfma_args(f1, f2, coords, segs, radius, scale);
+  const long win = (2 * radius + 1) * (2 * radius + 1);
+  check_gpu(out, "out");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(0) == f1.size(0) && out.size(1) >= a.levels * win &&
+                  (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat),
+              "raft_amd::local_corr_mfma: out must be a (P, >= L*(2r+1)^2) bf16/fp32 row view");
+  a.out = out.data_ptr(); a.ostride = out.stride(0); a.out_f32 = out.scalar_type() == at::kFloat;
+  a.out_ch = (int)out.size(1);
+  const c10::DeviceGuard guard(f1.device());
+  HIP_OK(launch_local_corr_mfma(a, false, cur_stream()));
+}
+
+void local_corr_mfma_backward(const at::Tensor& f1, const at::Tensor& f2, const at::Tensor& coords,
+                              at::IntArrayRef segs, int64_t radius, double scale, const at::Tensor& gout,
+                              const at::Tensor& g1, const at::Tensor& g2) {
+  LocalCorrArgs a = local_mfma_args(f1, f2, coords, segs, radius, scale);
+  const long win = (2 * radius + 1) * (2 * radius + 1);
+  check_gpu(gout, "gout");
+  TORCH_CHECK(gout.dim() == 2 && gout.stride(1) == 1 && gout.size(0) == f1.size(0) && gout.size(1) >= a.levels * win &&
+                  (gout.scalar_type() == at::kBFloat16 || gout.scalar_type() == at::kFloat),
+              "raft_amd::local_corr_mfma_backward: gout must be a (P, >= L*(2r+1)^2) row view");
+  TORCH_CHECK(g1.scalar_type() == at::kFloat && g1.sizes() == f1.sizes() && g1.is_contiguous(),
+              "raft_amd::local_corr_mfma_backward: g1 must be contiguous fp32 like fmap1");
+  TORCH_CHECK(g2.scalar_type() == at::kFloat && g2.sizes() == f2.sizes() && g2.is_contiguous(),
+              "raft_amd::local_corr_mfma_backward: g2 must be contiguous fp32 like fmap2 (accumulated)");
+  a.gout = gout.data_ptr(); a.gstride = gout.stride(0); a.gout_bf16 = gout.scalar_type() == at::kBFloat16;
+  a.g1 = g1.data_ptr<float>(); a.g2 = g2.data_ptr<float>();
+  const c10::DeviceGuard guard(f1.device());
+  HIP_OK(launch_local_corr_mfma(a, true, cur_stream()));
+}
+
 // ---------------------------------------------------------------- fused GRU gates
 void check_cl(const at::Tensor& t, const char* name) {
   check_gpu(t, name);
@@ -1034,6 +1116,10 @@ TORCH_LIBRARY(raft_amd, m) {
       "seq_loss_backward(Tensor[] preds, Tensor gt, Tensor valid, Tensor dloss, float gamma, float "
       "max_flow) -> Tensor[]");
   m.def("local_corr(Tensor fmap1, Tensor fmap2, Tensor coords, int radius, float scale) -> Tensor");
+  m.def("local_corr_mfma(Tensor f1, Tensor f2, Tensor coords, int[] segs, int radius, float scale, Tensor(a!) out) -> ()");
+  m.def(
+      "local_corr_mfma_backward(Tensor f1, Tensor f2, Tensor coords, int[] segs, int radius, float scale, Tensor gout, "
+      "Tensor(a!) g1, Tensor(b!) g2) -> ()");
   m.def(
       "local_corr_backward(Tensor fmap1, Tensor fmap2, Tensor coords, Tensor grad, int radius, float "
       "scale) -> (Tensor, Tensor)");
@@ -1051,6 +1137,8 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("seq_loss", &raft_amd::seq_loss);
   m.impl("seq_loss_backward", &raft_amd::seq_loss_backward);
   m.impl("local_corr", &raft_amd::local_corr);
+  m.impl("local_corr_mfma", &raft_amd::local_corr_mfma);
+  m.impl("local_corr_mfma_backward", &raft_amd::local_corr_mfma_backward);
   m.impl("local_corr_backward", &raft_amd::local_corr_backward);
   m.impl("conv_fwd", &raft_amd::conv_fwd);
   m.impl("instance_norm_fwd", &raft_amd::instance_norm_fwd);

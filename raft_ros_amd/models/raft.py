@@ -124,7 +124,8 @@ class RAFT(nn.Module):
             fmap1, fmap2 = self.fnet([image1, image2])
         fmap1, fmap2 = fmap1.float(), fmap2.float()
         if self.args.alternate_corr:
-            corr_fn = LocalCorrPyramid(fmap1, fmap2, radius=self.args.corr_radius)
+            corr_fn = LocalCorrPyramid(fmap1, fmap2, radius=self.args.corr_radius,
+                                       split=not (amp and dev == "cuda" and self.amp_dtype == torch.bfloat16))
         else:
             # without AMP the volume stays fp32-faithful (split bf16 MFMA), as the reference
             # computes it in fp32 in every mode (core/raft.py:102-103)
@@ -182,6 +183,9 @@ class RAFT(nn.Module):
         for t in range(iters):
             if dense:
                 net, flow_up, coords1 = upd.step(t, net, coords1, ptoken=corr_fn.token)
+            elif getattr(corr_fn, "mfma", False):  # features already in the fused layout
+                corr = corr_fn.lookup_padded(coords1.detach(), update_fused.CORR_PAD)
+                net, flow_up, coords1 = upd.step(t, net, coords1, corr=corr)
             else:
                 c = corr_fn(coords1.detach(), out_dtype=torch.bfloat16).permute(0, 2, 3, 1)
                 corr = torch.nn.functional.pad(c, (0, update_fused.CORR_PAD - c.shape[-1]))

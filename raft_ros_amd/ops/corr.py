@@ -216,6 +216,8 @@ class CorrPyramid:
 
 # --------------------------------------------------------------------- local path
 class _LocalCorr(torch.autograd.Function):
+    """fp32 scalar kernel (csrc/local_corr.hip): the exact path used without AMP."""
+
     @staticmethod
     def forward(ctx, f1, f2, coords, radius: int, scale: float):
         coords = coords.detach().float().contiguous()
@@ -231,22 +233,68 @@ class _LocalCorr(torch.autograd.Function):
         return g1.to(f1.dtype), g2.to(f2.dtype), None, None, None
 
 
+class _LocalCorrMFMA(torch.autograd.Function):
+    """All levels in one MFMA launch (csrc/local_corr_mfma.hip); output (P, out_channels)
+    rows, level l taps at channel l*(2r+1)^2 (the fused update block's layout)."""
+
+    @staticmethod
+    def forward(ctx, fmap1, fmap2, coords, st: "LocalCorrPyramid", out_channels: int, out_dtype):
+        coords = coords.detach().float().contiguous()
+        P = st.f1.shape[0]
+        out = torch.empty(P, out_channels, device=coords.device, dtype=out_dtype)
+        ops().local_corr_mfma(st.f1, st.f2cat, coords, st.segs, st.radius, st.scale, out)
+        ctx.st = st
+        ctx.save_for_backward(coords)
+        ctx.dtypes = (fmap1.dtype, fmap2.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        (coords,) = ctx.saved_tensors
+        st: LocalCorrPyramid = ctx.st
+        g1 = torch.empty(st.f1.shape, device=gout.device)
+        g2 = torch.zeros(st.f2cat.shape, device=gout.device)
+        gout = gout.reshape(st.f1.shape[0], -1).contiguous()
+        ops().local_corr_mfma_backward(st.f1, st.f2cat, coords, st.segs, st.radius, st.scale, gout, g1, g2)
+        B, C, H, W = st.shape
+        d2 = ops().pyramid_unpool(g2, H, W, st.segs)  # level gradients -> level 0 (adjoint pools)
+        d1 = g1.view(B, H, W, C).permute(0, 3, 1, 2)
+        d2 = d2.view(B, H, W, C).permute(0, 3, 1, 2)
+        return d1.to(ctx.dtypes[0]), d2.to(ctx.dtypes[1]), None, None, None, None
+
+
 class LocalCorrPyramid:
     """Memory-efficient correlation: no HW x HW volume is ever stored.
 
-    Pools fmap2 (not the volume; equivalent by linearity) into ``num_levels``
-    levels once, and per lookup computes the (2r+1)^2 window correlations on
-    the fly with the HIP ``local_corr`` kernel (fwd + bwd, so unlike the
-    reference's alt_cuda_corr path this one can train).
+    Pools fmap2 (not the volume; equivalent by linearity) into ``num_levels`` levels once,
+    and per lookup computes the (2r+1)^2 window correlations on the fly.  Under AMP (bf16)
+    every level is done by one MFMA kernel over 8x4 query tiles (``local_corr_mfma``);
+    without AMP (``split=True``) the exact fp32 kernel runs.  Both train (the reference's
+    alt_cuda_corr path is forward-only, core/corr.py:86).
     """
 
     def __init__(self, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4,
-                 feature_dtype: Optional[torch.dtype] = None):
+                 feature_dtype: Optional[torch.dtype] = None, split: bool = True):
         self.num_levels = num_levels
         self.radius = radius
         self.native = use_native(fmap1)
-        self.C = fmap1.shape[1]
-        if self.native:
+        B, C, H, W = fmap1.shape
+        self.C = C
+        self.shape = (B, C, H, W)
+        self.scale = 1.0 / math.sqrt(C)
+        self.mfma = self.native and not split and C % 64 == 0 and C <= 256 and radius <= 4
+        self.fmap1, self.fmap2 = fmap1, fmap2
+        if self.mfma:
+            self.f1 = fmap1.detach().permute(0, 2, 3, 1).reshape(B * H * W, C).to(torch.bfloat16).contiguous()
+            f2s = _pooled(fmap2.detach().float(), num_levels)
+            segs, off = [], 0
+            for f in f2s:
+                Hl, Wl = f.shape[-2:]
+                segs += [off, Hl, Wl]
+                off += _pad_to(Hl * Wl, 8)
+            self.segs = segs
+            self.f2cat = _concat_levels(f2s, off, segs[0::3], nchw=False).to(torch.bfloat16)
+        elif self.native:
             dt = feature_dtype or torch.float32
             self.f1 = fmap1.permute(0, 2, 3, 1).to(dt).contiguous()
             f2 = fmap2
@@ -261,15 +309,24 @@ class LocalCorrPyramid:
             for i in range(1, num_levels):
                 self.fmap2.append(F.avg_pool2d(self.fmap2[-1], 2, stride=2))
 
+    def lookup_padded(self, coords: torch.Tensor, out_channels: int, out_dtype=torch.bfloat16) -> torch.Tensor:
+        """MFMA path only: (B, H, W, out_channels) features, zero beyond L*(2r+1)^2."""
+        B, _, H, W = self.shape
+        out = _LocalCorrMFMA.apply(self.fmap1, self.fmap2, coords, self, out_channels, out_dtype)
+        return out.view(B, H, W, out_channels)
+
     def __call__(self, coords: torch.Tensor, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
-        scale = 1.0 / math.sqrt(self.C)
+        if self.mfma:
+            win = (2 * self.radius + 1) ** 2
+            out = self.lookup_padded(coords, self.num_levels * win, out_dtype or torch.float32)
+            return out.permute(0, 3, 1, 2)
         outs = []
         for i in range(self.num_levels):
             ci = coords / (2 ** i)
             if self.native:
-                o = _LocalCorr.apply(self.f1, self.f2[i], ci.detach().contiguous(), self.radius, scale)
+                o = _LocalCorr.apply(self.f1, self.f2[i], ci.detach().contiguous(), self.radius, self.scale)
                 outs.append(o)  # (B, H, W, win)
             else:
-                outs.append(ref.local_corr(self.fmap1, self.fmap2[i], ci, self.radius).permute(0, 2, 3, 1) * scale)
+                outs.append(ref.local_corr(self.fmap1, self.fmap2[i], ci, self.radius).permute(0, 2, 3, 1) * self.scale)
         out = torch.cat(outs, dim=-1).permute(0, 3, 1, 2)
         return out if out_dtype is None else out.to(out_dtype)

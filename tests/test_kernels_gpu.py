@@ -251,3 +251,31 @@ def test_instance_norm_nhwc(cuda, C, relu, dtype):
     (dx,) = torch.autograd.grad(y, x, g.to(dtype))
     (dxr,) = torch.autograd.grad(yr, xr, g)
     torch.testing.assert_close(dx.float(), dxr, **tol)
+
+
+@pytest.mark.parametrize("jitter", [3.0, 40.0])  # smooth flow (one window chunk) / wild flow (many chunks)
+def test_local_corr_mfma_matches_dense_reference(cuda, jitter):
+    """MFMA local correlation (all levels, one launch) vs the dense reference pyramid lookup,
+    forward and both feature gradients (bf16 operands -> bf16-level tolerance)."""
+    torch.manual_seed(8)
+    from raft_ros_amd.ops.corr import LocalCorrPyramid
+
+    B, C, H, W, r = 2, 256, 23, 37, 4
+    f1 = torch.randn(B, C, H, W, device=cuda).bfloat16().float().requires_grad_(True)
+    f2 = torch.randn(B, C, H, W, device=cuda).bfloat16().float().requires_grad_(True)
+    coords = ref.coords_grid(B, H, W, cuda) + jitter * torch.randn(B, 2, H, W, device=cuda)
+    lc = LocalCorrPyramid(f1, f2, 4, r, split=False)
+    assert lc.mfma
+    out = lc(coords)
+    f1r = f1.detach().clone().requires_grad_(True)
+    f2r = f2.detach().clone().requires_grad_(True)
+    want = ref.pyramid_lookup(ref.build_pyramid(ref.corr_volume(f1r, f2r), 4), coords, r)
+    assert ((out - want).norm() / want.norm()).item() < 1e-2
+    g = torch.randn_like(want)
+    (out * g).sum().backward()
+    (want * g).sum().backward()
+    for got, exp in ((f1.grad, f1r.grad), (f2.grad, f2r.grad)):
+        assert ((got - exp).norm() / exp.norm()).item() < 2e-2
+    # padded fused layout: zeros beyond the 324 taps
+    padded = lc.lookup_padded(coords, 328)
+    assert padded.shape == (B, H, W, 328) and (padded[..., 324:] == 0).all()
