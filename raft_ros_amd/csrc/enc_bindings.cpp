@@ -1,0 +1,521 @@
+// Torch dispatcher ops for the native encoders (csrc/encoder.hip): host-side planning
+// of the strided implicit-GEMM convolutions (K-chunk decode tables, stride-parity
+// classes of the data gradient, pixel splits of the weight gradient) and the norm ops.
+// Autograd wiring: raft_ros_amd/ops/encoder.py.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+namespace raft_amd {
+
+constexpr int kEncTab = 256;
+struct EncSrc {
+  const void* ptr;
+  int stride, C, H, W, is;
+};
+struct EncClass {
+  int t0, Gh, Gw, oy0, ox0, K, Kpad, tiles_img, blk0;
+  long wofs;
+};
+struct EncConvArgs {
+  EncSrc src[2];
+  int B;
+  int tab[kEncTab];
+  int ptab[kEncTab];
+  EncClass cls[4];
+  int ncls, N, tilesN;
+  const void* wt;
+  int Ho, Wo, os;
+  void* out;
+  int out_stride;
+  const float* bias;
+  const void* res;
+  int res_stride;
+  const void* mask;
+  int mask_stride;
+  float* stats;
+  const float* w[2];
+  long ws[2][4];
+  int wcin[2];
+  int pack_dgrad;
+};
+struct EncWgradArgs {
+  const void* x;
+  int xstride, Cx;
+  int B, Hx, Wx, Ho, Wo, KH, KW, stride, pad;
+  const void* dy;
+  int dy_stride, N;
+  int K, Kpad, Npad, tilesM, tilesN;
+  long P;
+  int pix_per_split, nsplit;
+  float* slab;
+  float* dbslab;
+};
+struct NormFinArgs {
+  const float* stats;
+  int B, T, BM, HW, N, kind;
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  long long* nbt;
+  float momentum, eps;
+  float* coef;
+};
+struct NormBwdArgs {
+  const void* g;
+  const void* a0;
+  const float* c0;
+  int relu0;
+  const void* a1;
+  const float* c1;
+  float* part;
+  int B, HW, N, R, kind;
+  float* bcoef;
+  float* dgamma[2];
+  float* dbeta[2];
+  void* out0;
+  void* out1;
+};
+
+// launchers (encoder.hip); the device-side structs hold __bf16 pointers with the same layout
+int enc_tile_bn(int N);
+hipError_t launch_enc_pack(const EncConvArgs& a, int rows, void* out, hipStream_t s);
+hipError_t launch_enc_conv(const EncConvArgs& a, int nblocks, hipStream_t s);
+hipError_t launch_enc_wgrad(const EncWgradArgs& a, int BM, hipStream_t s);
+hipError_t launch_enc_wgrad_reduce(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, float* dw,
+                                   const long* ws, int Cout, int Cin, int Cx, int KH, int KW, float* db,
+                                   bool accumulate, hipStream_t s);
+hipError_t launch_enc_prep(const float* i0, const float* i1, const long* st, int B, int H, int W, int nimg,
+                           void* out, hipStream_t s);
+hipError_t launch_enc_norm_finalize(const NormFinArgs& a, hipStream_t s);
+hipError_t launch_enc_apply(const void* a, const float* ca, bool relu_a, const void* r, const float* cr,
+                            bool relu_out, void* out, int B, int HW, int N, hipStream_t s);
+hipError_t launch_enc_norm_bwd(const NormBwdArgs& a, hipStream_t s);
+
+namespace {
+
+constexpr int kBM = 128;  // conv M tile (pixels), fixed for every encoder conv
+constexpr int kNormChunks = 32;
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e));
+}
+
+void check_nhwc(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4 && t.is_contiguous(), name,
+              ": expected a contiguous [B, H, W, C] bf16 CUDA tensor");
+  TORCH_CHECK(t.size(3) % 8 == 0, name, ": channels must be a multiple of 8");
+  TORCH_CHECK(t.numel() < (1L << 31), name, ": too large");
+}
+
+void check_w(const at::Tensor& w, const char* name) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4, name, ": expected a fp32 4-D CUDA weight");
+}
+
+int round_up(long v, int m) { return (int)((v + m - 1) / m * m); }
+
+int enc_tab_entry(int dy, int dx, int src, int c) {
+  TORCH_CHECK(dy > -128 && dy < 128 && dx > -128 && dx < 128 && c < (1 << 14), "decode table range");
+  return (dy + 128) | ((dx + 128) << 8) | (src << 16) | (c << 17);
+}
+int enc_ptab_entry(int w, int ky, int kx, int local) {
+  TORCH_CHECK(ky < 16 && kx < 16, "kernel size");
+  return w | (ky << 4) | (kx << 8) | (local << 12);
+}
+
+void set_weight(EncConvArgs& a, int j, const at::Tensor& w) {
+  a.w[j] = w.data_ptr<float>();
+  for (int d = 0; d < 4; ++d) a.ws[j][d] = w.stride(d);
+  a.wcin[j] = (int)w.size(1);
+}
+
+// Pack + run one planned conv launch (fwd or dgrad); classes and tables already filled.
+void run_conv(EncConvArgs& a, int rows, const at::TensorOptions& o) {
+  long wtotal = 0;
+  int blocks = 0;
+  a.tilesN = (a.N + enc_tile_bn(a.N) - 1) / enc_tile_bn(a.N);
+  for (int c = 0; c < a.ncls; ++c) {
+    EncClass& cl = a.cls[c];
+    cl.wofs = wtotal;
+    wtotal += (long)rows * cl.Kpad;
+    cl.tiles_img = (cl.Gh * cl.Gw + kBM - 1) / kBM;
+    cl.blk0 = blocks;
+    blocks += a.B * cl.tiles_img * a.tilesN;
+  }
+  at::Tensor wt = at::empty({wtotal}, o.dtype(at::kBFloat16));
+  a.wt = wt.data_ptr();
+  check(launch_enc_pack(a, rows, wt.data_ptr(), stream()), "enc_pack");
+  if (blocks > 0) check(launch_enc_conv(a, blocks, stream()), "enc_conv");
+}
+
+void init_args(EncConvArgs& a) {
+  std::memset(&a, 0, sizeof(a));
+  for (int i = 0; i < kEncTab; ++i) a.tab[i] = a.ptab[i] = -1;
+}
+
+}  // namespace
+
+// y[B,Ho,Wo,N] = conv(x[B,H,W,Cx], w[N,Cin,KH,KW]) + bias; stats [B, T, 2, N] (column sum, M2 per 128-pixel tile)
+std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::Tensor& w,
+                                                const c10::optional<at::Tensor>& bias, int64_t stride, int64_t pad,
+                                                bool want_stats) {
+  check_nhwc(x, "x");
+  check_w(w, "w");
+  const int B = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), Cx = (int)x.size(3);
+  const int N = (int)w.size(0), Cin = (int)w.size(1), KH = (int)w.size(2), KW = (int)w.size(3);
+  TORCH_CHECK(Cin <= Cx, "weight has more input channels than x");
+  TORCH_CHECK(N % 8 == 0 && N <= 1024, "out channels");
+  const int Ho = (H + 2 * (int)pad - KH) / (int)stride + 1, Wo = (W + 2 * (int)pad - KW) / (int)stride + 1;
+  EncConvArgs a;
+  init_args(a);
+  a.src[0] = {x.data_ptr(), Cx, Cx, H, W, (int)stride};
+  a.B = B;
+  a.N = N;
+  int e = 0;
+  for (int ky = 0; ky < KH; ++ky)
+    for (int kx = 0; kx < KW; ++kx)
+      for (int c = 0; c < Cx; c += 8) {
+        TORCH_CHECK(e < kEncTab, "conv too deep for the decode table");
+        a.tab[e] = enc_tab_entry(ky - (int)pad, kx - (int)pad, 0, c);
+        a.ptab[e] = enc_ptab_entry(0, ky, kx, c);
+        ++e;
+      }
+  const int K = e * 8, Kpad = round_up(K, 64);
+  TORCH_CHECK(Kpad / 8 <= kEncTab, "conv too deep for the decode table");
+  a.cls[0] = EncClass{0, Ho, Wo, 0, 0, K, Kpad, 0, 0, 0};
+  a.ncls = 1;
+  at::Tensor y = at::empty({B, Ho, Wo, N}, x.options());
+  a.Ho = Ho;
+  a.Wo = Wo;
+  a.os = 1;
+  a.out = y.data_ptr();
+  a.out_stride = N;
+  at::Tensor b;
+  if (bias.has_value() && bias->defined()) {
+    b = bias->to(at::kFloat).contiguous();
+    a.bias = b.data_ptr<float>();
+  }
+  const int T = (Ho * Wo + kBM - 1) / kBM;
+  at::Tensor st = want_stats ? at::empty({B, T, 2, N}, x.options().dtype(at::kFloat)) : at::Tensor();
+  if (want_stats) a.stats = st.data_ptr<float>();
+  set_weight(a, 0, w);
+  a.pack_dgrad = 0;
+  run_conv(a, N, x.options());
+  return {y, st};
+}
+
+// dx[B,H,W,Cin] = sum_j conv_transpose(dys[j], ws[j]) (+ res) (* [mask > 0]);
+// stride[j] / pad[j] per conv, every conv maps x[B,H,W,Cin] -> dys[j].
+at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef strides, at::IntArrayRef pads,
+                          int64_t H, int64_t W, const c10::optional<at::Tensor>& res,
+                          const c10::optional<at::Tensor>& mask) {
+  const int nconv = (int)dys.size();
+  TORCH_CHECK(nconv >= 1 && nconv <= 2 && (int)ws.size() == nconv && (int)strides.size() == nconv &&
+                  (int)pads.size() == nconv,
+              "enc_conv_dgrad: 1 or 2 convs");
+  const int B = (int)dys[0].size(0);
+  const int Cin = (int)ws[0].size(1);
+  TORCH_CHECK(Cin % 8 == 0 && Cin <= 1024, "in channels");
+  int S = 1;
+  for (int j = 0; j < nconv; ++j) S = std::max<int>(S, (int)strides[j]);
+  EncConvArgs a;
+  init_args(a);
+  a.B = B;
+  a.N = Cin;
+  for (int j = 0; j < nconv; ++j) {
+    check_nhwc(dys[j], "dy");
+    check_w(ws[j], "w");
+    TORCH_CHECK(dys[j].size(0) == B && ws[j].size(1) == Cin && dys[j].size(3) == ws[j].size(0), "dgrad shapes");
+    TORCH_CHECK(S % strides[j] == 0, "strides must divide the largest stride");
+    const int KH = (int)ws[j].size(2), KW = (int)ws[j].size(3);
+    const int Ho = ((int)H + 2 * (int)pads[j] - KH) / (int)strides[j] + 1;
+    const int Wo = ((int)W + 2 * (int)pads[j] - KW) / (int)strides[j] + 1;
+    TORCH_CHECK(dys[j].size(1) == Ho && dys[j].size(2) == Wo, "dy spatial shape does not match the conv");
+    const int C = (int)dys[j].size(3);
+    a.src[j] = {dys[j].data_ptr(), C, C, Ho, Wo, S / (int)strides[j]};
+    set_weight(a, j, ws[j]);
+  }
+  int e = 0, ncls = 0;
+  for (int py = 0; py < S; ++py)
+    for (int px = 0; px < S; ++px) {
+      const int Gh = ((int)H - py + S - 1) / S, Gw = ((int)W - px + S - 1) / S;
+      if (Gh <= 0 || Gw <= 0) continue;
+      const int t0 = e;
+      for (int j = 0; j < nconv; ++j) {
+        const int s = (int)strides[j], p = (int)pads[j];
+        const int KH = (int)ws[j].size(2), KW = (int)ws[j].size(3), C = (int)dys[j].size(3);
+        for (int ky = 0; ky < KH; ++ky) {
+          const int vy = py + p - ky;
+          if (((vy % s) + s) % s) continue;
+          for (int kx = 0; kx < KW; ++kx) {
+            const int vx = px + p - kx;
+            if (((vx % s) + s) % s) continue;
+            for (int c = 0; c < C; c += 8) {
+              TORCH_CHECK(e < kEncTab, "dgrad too deep for the decode table");
+              a.tab[e] = enc_tab_entry(vy / s, vx / s, j, c);
+              a.ptab[e] = enc_ptab_entry(j, ky, kx, c);
+              ++e;
+            }
+          }
+        }
+      }
+      const int K = (e - t0) * 8, Kpad = std::max(64, round_up(K, 64));
+      TORCH_CHECK(t0 + Kpad / 8 <= kEncTab, "dgrad too deep for the decode table");
+      e = t0 + Kpad / 8;  // padded entries stay -1
+      a.cls[ncls++] = EncClass{t0, Gh, Gw, py, px, K, Kpad, 0, 0, 0};
+    }
+  a.ncls = ncls;
+  at::Tensor dx = at::empty({B, H, W, Cin}, dys[0].options());
+  a.Ho = (int)H;
+  a.Wo = (int)W;
+  a.os = S;
+  a.out = dx.data_ptr();
+  a.out_stride = Cin;
+  if (res.has_value() && res->defined()) {
+    check_nhwc(*res, "res");
+    TORCH_CHECK(res->sizes() == dx.sizes(), "res shape");
+    a.res = res->data_ptr();
+    a.res_stride = Cin;
+  }
+  if (mask.has_value() && mask->defined()) {
+    check_nhwc(*mask, "mask");
+    TORCH_CHECK(mask->sizes() == dx.sizes(), "mask shape");
+    a.mask = mask->data_ptr();
+    a.mask_stride = Cin;
+  }
+  a.pack_dgrad = 1;
+  run_conv(a, Cin, dys[0].options());
+  return dx;
+}
+
+// dw (fp32, any strides, [Cout, Cin, KH, KW]) (+)= wgrad; db (+)= sum_p dy
+void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, const c10::optional<at::Tensor>& db,
+                    int64_t stride, int64_t pad, bool accumulate, bool db_zero) {
+  check_nhwc(x, "x");
+  check_nhwc(dy, "dy");
+  TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == at::kFloat && dw.dim() == 4, "dw: fp32 4-D");
+  const int B = (int)x.size(0), Hx = (int)x.size(1), Wx = (int)x.size(2), Cx = (int)x.size(3);
+  const int N = (int)dw.size(0), Cin = (int)dw.size(1), KH = (int)dw.size(2), KW = (int)dw.size(3);
+  const int Ho = (int)dy.size(1), Wo = (int)dy.size(2);
+  TORCH_CHECK(dy.size(0) == B && dy.size(3) == N && Cin <= Cx, "wgrad shapes");
+  TORCH_CHECK(Ho == (Hx + 2 * (int)pad - KH) / (int)stride + 1 && Wo == (Wx + 2 * (int)pad - KW) / (int)stride + 1,
+              "wgrad spatial shapes");
+  EncWgradArgs a{};
+  a.x = x.data_ptr();
+  a.xstride = Cx;
+  a.Cx = Cx;
+  a.B = B;
+  a.Hx = Hx;
+  a.Wx = Wx;
+  a.Ho = Ho;
+  a.Wo = Wo;
+  a.KH = KH;
+  a.KW = KW;
+  a.stride = (int)stride;
+  a.pad = (int)pad;
+  a.dy = dy.data_ptr();
+  a.dy_stride = N;
+  a.N = N;
+  const int BM = (N % 128 == 0) ? 128 : 64;
+  a.tilesM = (N + BM - 1) / BM;
+  a.Npad = a.tilesM * BM;
+  a.K = KH * KW * Cx;
+  a.tilesN = (a.K + 63) / 64;
+  a.Kpad = a.tilesN * 64;
+  a.P = (long)B * Ho * Wo;
+  const long tiles = (long)a.tilesM * a.tilesN;
+  // ~640 workgroups (2.5 per CU): long pixel loops per workgroup, few slabs to reduce
+  long pps = (a.P * tiles + 639) / 640;
+  pps = std::max<long>(256, (pps + 63) / 64 * 64);
+  a.pix_per_split = (int)pps;
+  a.nsplit = (int)((a.P + pps - 1) / pps);
+  at::Tensor slab = at::empty({(long)a.nsplit * a.Npad * a.Kpad}, x.options().dtype(at::kFloat));
+  a.slab = slab.data_ptr<float>();
+  const bool want_db = db.has_value() && db->defined();
+  at::Tensor dbslab;
+  if (want_db) {
+    TORCH_CHECK(db->scalar_type() == at::kFloat && db->numel() == N && db->is_contiguous(), "db: fp32 [N]");
+  }
+  if (want_db && !db_zero) {
+    dbslab = at::empty({(long)a.nsplit * a.Npad}, x.options().dtype(at::kFloat));
+    a.dbslab = dbslab.data_ptr<float>();
+  }
+  check(launch_enc_wgrad(a, BM, stream()), "enc_wgrad");
+  long wsd[4];
+  for (int d = 0; d < 4; ++d) wsd[d] = dw.stride(d);
+  check(launch_enc_wgrad_reduce(a.slab, a.nsplit, a.Npad, a.Kpad, a.dbslab, dw.data_ptr<float>(), wsd, N, Cin, Cx, KH,
+                                KW, want_db ? db->data_ptr<float>() : nullptr, accumulate, stream()),
+        "enc_wgrad_reduce");
+}
+
+// [img0; img1] (fp32 0..255, [B,3,H,W] any strides) -> [nimg, H, W, 8] bf16 in [-1, 1]
+at::Tensor enc_prep(const at::Tensor& img0, const c10::optional<at::Tensor>& img1) {
+  TORCH_CHECK(img0.is_cuda() && img0.scalar_type() == at::kFloat && img0.dim() == 4 && img0.size(1) == 3,
+              "images: fp32 [B, 3, H, W]");
+  const int B = (int)img0.size(0), H = (int)img0.size(2), W = (int)img0.size(3);
+  int nimg = B;
+  if (img1.has_value() && img1->defined()) {
+    TORCH_CHECK(img1->sizes() == img0.sizes() && img1->strides() == img0.strides() &&
+                    img1->scalar_type() == at::kFloat,
+                "paired images must match");
+    nimg = 2 * B;
+  }
+  at::Tensor out = at::empty({nimg, H, W, 8}, img0.options().dtype(at::kBFloat16));
+  long st[4] = {img0.stride(0), img0.stride(1), img0.stride(2), img0.stride(3)};
+  check(launch_enc_prep(img0.data_ptr<float>(), nimg > B ? img1->data_ptr<float>() : nullptr, st, B, H, W, nimg,
+                        out.data_ptr(), stream()),
+        "enc_prep");
+  return out;
+}
+
+// coef [B, 4, N] = (scale, shift, rstd, mean) from conv tile statistics (kind 1 / 2) or running statistics (3)
+at::Tensor enc_norm_stats(const c10::optional<at::Tensor>& stats, int64_t B, int64_t HW, int64_t N, int64_t kind,
+                          const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
+                          const c10::optional<at::Tensor>& rmean, const c10::optional<at::Tensor>& rvar,
+                          const c10::optional<at::Tensor>& nbt, double momentum, double eps) {
+  NormFinArgs a{};
+  a.B = (int)B;
+  a.HW = (int)HW;
+  a.N = (int)N;
+  a.kind = (int)kind;
+  a.BM = kBM;
+  const bool has_stats = stats.has_value() && stats->defined();
+  TORCH_CHECK(!(kind == 1 || kind == 2) || has_stats, "training statistics need the conv tile statistics");
+  at::TensorOptions o;
+  if (has_stats) {
+    TORCH_CHECK(stats->dim() == 4 && stats->size(0) == B && stats->size(2) == 2 && stats->size(3) == N, "stats shape");
+    a.stats = stats->data_ptr<float>();
+    a.T = (int)stats->size(1);
+    o = stats->options();
+  }
+  auto fp = [](const c10::optional<at::Tensor>& t) -> float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "norm parameters: contiguous fp32");
+    return t->data_ptr<float>();
+  };
+  a.gamma = fp(gamma);
+  a.beta = fp(beta);
+  a.rmean = fp(rmean);
+  a.rvar = fp(rvar);
+  if (!has_stats) {
+    TORCH_CHECK(rmean.has_value() && rmean->defined(), "enc_norm_stats: pass the conv statistics or running stats");
+    o = rmean->options();
+  }
+  if (kind == 3) TORCH_CHECK(a.rmean && a.rvar, "running statistics");
+  if (nbt.has_value() && nbt->defined()) {
+    TORCH_CHECK(nbt->scalar_type() == at::kLong, "num_batches_tracked");
+    a.nbt = reinterpret_cast<long long*>(nbt->data_ptr<int64_t>());
+  }
+  a.momentum = (float)momentum;
+  a.eps = (float)eps;
+  at::Tensor coef = at::empty({B, 4, N}, o.dtype(at::kFloat));
+  a.coef = coef.data_ptr<float>();
+  check(launch_enc_norm_finalize(a, stream()), "enc_norm_finalize");
+  return coef;
+}
+
+at::Tensor enc_apply(const at::Tensor& x, const at::Tensor& coef, bool relu_a, const c10::optional<at::Tensor>& r,
+                     const c10::optional<at::Tensor>& coef_r, bool relu_out) {
+  check_nhwc(x, "a");
+  const int B = (int)x.size(0), HW = (int)(x.size(1) * x.size(2)), N = (int)x.size(3);
+  TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() == (long)B * 4 * N, "coef");
+  const void* rp = nullptr;
+  const float* crp = nullptr;
+  if (r.has_value() && r->defined()) {
+    check_nhwc(*r, "r");
+    TORCH_CHECK(r->sizes() == x.sizes(), "residual shape");
+    rp = r->data_ptr();
+    if (coef_r.has_value() && coef_r->defined()) {
+      TORCH_CHECK(coef_r->numel() == (long)B * 4 * N && coef_r->is_contiguous(), "coef_r");
+      crp = coef_r->data_ptr<float>();
+    }
+  }
+  at::Tensor out = at::empty_like(x);
+  check(launch_enc_apply(x.data_ptr(), coef.data_ptr<float>(), relu_a, rp, crp, relu_out, out.data_ptr(), B, HW, N,
+                         stream()),
+        "enc_apply");
+  return out;
+}
+
+// returns [da0, da1 | empty, dgamma0, dbeta0, dgamma1, dbeta1] (BatchNorm kinds; empty otherwise)
+std::vector<at::Tensor> enc_norm_bwd(const at::Tensor& g, const at::Tensor& a0, const at::Tensor& c0, bool relu0,
+                                     const c10::optional<at::Tensor>& a1, const c10::optional<at::Tensor>& c1,
+                                     int64_t kind) {
+  check_nhwc(g, "g");
+  check_nhwc(a0, "a0");
+  TORCH_CHECK(a0.sizes() == g.sizes(), "a0 shape");
+  const int B = (int)g.size(0), HW = (int)(g.size(1) * g.size(2)), N = (int)g.size(3);
+  TORCH_CHECK(N <= 256, "norm backward: at most 256 channels");
+  NormBwdArgs a{};
+  a.g = g.data_ptr();
+  a.a0 = a0.data_ptr();
+  a.c0 = c0.data_ptr<float>();
+  a.relu0 = relu0 ? 1 : 0;
+  const bool two = a1.has_value() && a1->defined();
+  if (two) {
+    check_nhwc(*a1, "a1");
+    TORCH_CHECK(a1->sizes() == g.sizes(), "a1 shape");
+    a.a1 = a1->data_ptr();
+    a.c1 = c1->data_ptr<float>();
+  }
+  a.B = B;
+  a.HW = HW;
+  a.N = N;
+  a.R = std::min(kNormChunks, std::max(1, HW / 256));
+  a.kind = (int)kind;
+  auto fo = g.options().dtype(at::kFloat);
+  at::Tensor part = at::empty({(long)B * a.R * 4 * N}, fo);
+  at::Tensor bcoef = at::empty({(long)B * 2 * 3 * N}, fo);
+  a.part = part.data_ptr<float>();
+  a.bcoef = bcoef.data_ptr<float>();
+  at::Tensor da0 = at::empty_like(g), da1 = two ? at::empty_like(g) : at::Tensor();
+  a.out0 = da0.data_ptr();
+  a.out1 = two ? da1.data_ptr() : nullptr;
+  std::vector<at::Tensor> out{da0, da1, at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor()};
+  if (kind == 2 || kind == 3) {
+    for (int j = 0; j < (two ? 2 : 1); ++j) {
+      out[2 + 2 * j] = at::empty({N}, fo);
+      out[3 + 2 * j] = at::empty({N}, fo);
+      a.dgamma[j] = out[2 + 2 * j].data_ptr<float>();
+      a.dbeta[j] = out[3 + 2 * j].data_ptr<float>();
+    }
+  }
+  check(launch_enc_norm_bwd(a, stream()), "enc_norm_bwd");
+  return out;
+}
+
+}  // namespace raft_amd
+
+TORCH_LIBRARY_FRAGMENT(raft_amd, m) {
+  m.def("enc_conv_fwd(Tensor x, Tensor w, Tensor? bias, int stride, int pad, bool stats) -> (Tensor, Tensor)");
+  m.def(
+      "enc_conv_dgrad(Tensor[] dys, Tensor[] ws, int[] strides, int[] pads, int H, int W, Tensor? res, Tensor? mask) "
+      "-> Tensor");
+  m.def("enc_conv_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, Tensor(b!)? db, int stride, int pad, bool accumulate, "
+        "bool db_zero=False) -> ()");
+  m.def("enc_prep(Tensor img0, Tensor? img1) -> Tensor");
+  m.def(
+      "enc_norm_stats(Tensor? stats, int B, int HW, int N, int kind, Tensor? gamma, Tensor? beta, Tensor(a!)? rmean, "
+      "Tensor(b!)? rvar, Tensor(c!)? nbt, float momentum, float eps) -> Tensor");
+  m.def("enc_apply(Tensor a, Tensor coef, bool relu_a, Tensor? r, Tensor? coef_r, bool relu_out) -> Tensor");
+  m.def("enc_norm_bwd(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind) -> Tensor[]");
+}
+
+TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
+  m.impl("enc_conv_fwd", &raft_amd::enc_conv_fwd);
+  m.impl("enc_conv_dgrad", &raft_amd::enc_conv_dgrad);
+  m.impl("enc_conv_wgrad", &raft_amd::enc_conv_wgrad);
+  m.impl("enc_prep", &raft_amd::enc_prep);
+  m.impl("enc_norm_stats", &raft_amd::enc_norm_stats);
+  m.impl("enc_apply", &raft_amd::enc_apply);
+  m.impl("enc_norm_bwd", &raft_amd::enc_norm_bwd);
+}

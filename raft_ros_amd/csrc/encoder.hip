@@ -1,0 +1,1022 @@
+// Residual CNN encoders on gfx950 MFMA: strided NHWC convolutions (forward, data and
+// weight gradients) and the normalisation / residual glue around them.
+//
+// Reference: core/extractor.py:6-267 (BasicEncoder / SmallEncoder: 7x7/s2 stem,
+// ResidualBlock / BottleneckBlock stages at strides 1, 2, 2, 1x1 output conv; norms
+// batch / instance / none).  The reference runs these on cuDNN with separate norm,
+// ReLU and add kernels; here an encoder is one native op sequence:
+//
+//   conv (implicit GEMM, M = output pixels, N = out channels, K = taps x in channels)
+//     epilogue: + bias, per-tile (sum, M2) statistics of the output -> no separate
+//     statistics pass for the following InstanceNorm / BatchNorm;
+//   stats finalize: Chan-combined per-(image, channel) [instance] or per-channel [batch]
+//     mean / variance in a fixed order (deterministic), BatchNorm running statistics;
+//   apply: relu(norm(a)) or the residual tail relu(relu(norm(a2)) + norm3(ad) | x);
+//   backward: data gradients as the same conv kernel over dY with flipped / transposed
+//     packed weights; a stride-2 conv's data gradient is split into its 4 output parity
+//     classes (each a dense conv over the taps that hit it) so no zero-stuffed dY or
+//     wasted MFMA; the 3x3/s2 conv and the 1x1/s2 downsample of a block share one launch
+//     (their K ranges are concatenated); the epilogue adds the identity-residual gradient
+//     and applies the ReLU' mask of the block input;
+//   norm backward: partial sums of dy' and dy'*xhat -> coefficients -> one apply pass
+//     (both tail branches at once);
+//   weight gradient: dW[co][k] = sum_p dY[p][co] im2col(X)[p][k] over a pixel split
+//     (fp32 slab per split, fixed-order reduce into the fp32 parameter layout).
+//
+// All gathers use a per-launch K-chunk decode table (8 consecutive K columns = 8
+// channels of one tap of one source): every conv shape of both encoders, including the
+// 3-channel stem (padded to 8) and the small encoder's 8/16/24-channel bottlenecks, runs
+// through one kernel family.
+#include "common.h"
+
+#include <algorithm>
+
+namespace raft_amd {
+
+constexpr int kEncTab = 256;  // K/8 decode-table entries per launch (all classes)
+
+struct EncSrc {
+  const __bf16* ptr;
+  int stride;  // elements between consecutive pixels
+  int C;       // channels (multiple of 8)
+  int H, W;    // spatial dims
+  int is;      // source step per grid step
+};
+
+struct EncClass {
+  int t0;            // first decode-table entry
+  int Gh, Gw;        // pixel grid per image
+  int oy0, ox0;      // output coordinate = grid * os + o0
+  int K, Kpad;       // GEMM depth (Kpad: multiple of 64)
+  int tiles_img;     // BM-row tiles per image
+  int blk0;          // first workgroup of this class
+  long wofs;         // element offset of the class's packed weights [N][Kpad]
+};
+
+struct EncConvArgs {
+  EncSrc src[2];
+  int B;
+  // decode table: (dy+128) | (dx+128) << 8 | src << 16 | c << 17, -1 = zero columns
+  int tab[kEncTab];
+  // packing table: w | ky << 4 | kx << 8 | local << 12, -1 = zero columns
+  int ptab[kEncTab];
+  EncClass cls[4];
+  int ncls, N, tilesN;
+  const __bf16* wt;
+  int Ho, Wo, os;
+  __bf16* out;
+  int out_stride;
+  const float* bias;
+  const __bf16* res;
+  int res_stride;
+  const __bf16* mask;
+  int mask_stride;
+  float* stats;  // [B * tiles_img][2][N]: per tile column sum and M2
+  // weight packing
+  const float* w[2];
+  long ws[2][4];
+  int wcin[2];
+  int pack_dgrad;
+};
+
+struct EncWgradArgs {
+  const __bf16* x;
+  int xstride, Cx;
+  int B, Hx, Wx, Ho, Wo, KH, KW, stride, pad;
+  const __bf16* dy;
+  int dy_stride, N;
+  int K, Kpad, Npad, tilesM, tilesN;
+  long P;
+  int pix_per_split, nsplit;
+  float* slab;    // [nsplit][Npad][Kpad]
+  float* dbslab;  // [nsplit][Npad] or null
+};
+
+struct NormFinArgs {
+  const float* stats;  // conv epilogue tiles [B][T][2][N]
+  int B, T, BM, HW, N, kind;
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  long long* nbt;
+  float momentum, eps;
+  float* coef;
+};
+
+struct NormBwdArgs {
+  const __bf16* g;
+  const __bf16* a0;
+  const float* c0;
+  int relu0;
+  const __bf16* a1;  // null: one branch
+  const float* c1;
+  float* part;
+  int B, HW, N, R, kind;
+  float* bcoef;  // [B][2][3][N]: da = k1 * dy + k2 * xhat + k3
+  float* dgamma[2];
+  float* dbeta[2];
+  __bf16* out0;
+  __bf16* out1;
+};
+
+namespace {
+
+constexpr int EBK = 64, ELDK = EBK + 8;
+
+__device__ __forceinline__ void load8(const __bf16* p, float* v) {
+  const bf16x8 x = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = static_cast<float>(x[i]);
+}
+__device__ __forceinline__ void store8(__bf16* p, const float* v) {
+  bf16x8 x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x[i] = static_cast<__bf16>(v[i]);
+  *reinterpret_cast<bf16x8*>(p) = x;
+}
+__device__ __forceinline__ void loadf8(const float* p, float* v) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = a[i];
+    v[i + 4] = b[i];
+  }
+}
+
+__device__ __forceinline__ EncClass pick_class(const EncConvArgs& a, int wg, int& ci) {
+  ci = 0;
+#pragma unroll
+  for (int c = 1; c < 4; ++c)
+    if (c < a.ncls && wg >= a.cls[c].blk0) ci = c;
+  EncClass cl = a.cls[0];
+  if (ci == 1) cl = a.cls[1];
+  if (ci == 2) cl = a.cls[2];
+  if (ci == 3) cl = a.cls[3];
+  return cl;
+}
+
+// ============================================================================ conv fwd / dgrad
+// BM x BN output tile, BK = 64, 256 threads as WM x WN waves, each wave TM x TN MFMA
+// 32x32x16 tiles; register-staged double-buffered LDS, one barrier per K step.
+template <int BM, int BN, int WM, int WN>
+struct EncCfg {
+  static constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  static constexpr int ACH = BM * EBK / 8 / 256, BCH = BN * EBK / 8 / 256;
+  static constexpr int STAGE = (BM + BN) * ELDK;
+  static constexpr int RING_BYTES = 2 * STAGE * 2;
+  static constexpr int EPI_BYTES = (BM * (BN + 4) + 2 * WM * BN) * 4;
+  static constexpr int SMEM = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
+  static_assert(TM * 32 * WM == BM && TN * 32 * WN == BN && WM * WN == 4, "tile shape");
+  static_assert(ACH * 256 * 8 == BM * EBK && BCH * 256 * 8 == BN * EBK, "staging shape");
+};
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
+  using C = EncCfg<BM, BN, WM, WN>;
+  constexpr int TM = C::TM, TN = C::TN, ACH = C::ACH, BCH = C::BCH, STAGE = C::STAGE;
+  __shared__ __attribute__((aligned(16))) char smem_raw[C::SMEM];
+  __shared__ int s_tab[kEncTab];
+  __bf16* smem = reinterpret_cast<__bf16*>(smem_raw);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int e = tid; e < kEncTab; e += 256) s_tab[e] = a.tab[e];
+
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  int ci;
+  const EncClass cl = pick_class(a, wg, ci);
+  const int local = wg - cl.blk0;
+  const int tm = local / a.tilesN, tn = local - (local / a.tilesN) * a.tilesN;
+  const int b = tm / cl.tiles_img, tile = tm - (tm / cl.tiles_img) * cl.tiles_img;
+  const int GHW = cl.Gh * cl.Gw;
+  const int q0 = tile * BM;
+  const int n0 = tn * BN;
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  const int kc = tid & 7;
+
+  // rows this thread stages: grid coordinates of pixel q (far outside when q is past the grid)
+  int ry[ACH], rx[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) {
+    const int q = q0 + (tid >> 3) + 32 * i;
+    if (q < GHW) {
+      const int gy = q / cl.Gw;
+      ry[i] = gy;
+      rx[i] = q - gy * cl.Gw;
+    } else {
+      ry[i] = -(1 << 20);
+      rx[i] = 0;
+    }
+  }
+  const __bf16* wt = a.wt + cl.wofs;
+  const int nk = cl.Kpad / EBK;
+
+  __syncthreads();  // s_tab
+
+  u32x4 ra[ACH], rb[BCH];
+  auto load = [&](int k0) __attribute__((always_inline)) {
+    const int ent = s_tab[cl.t0 + (k0 >> 3) + kc];
+    if (ent < 0) {
+#pragma unroll
+      for (int i = 0; i < ACH; ++i) ra[i] = u32x4{0, 0, 0, 0};
+    } else {
+      const int dy = (ent & 0xff) - 128, dx = ((ent >> 8) & 0xff) - 128;
+      const int sidx = (ent >> 16) & 1, c = ent >> 17;
+      const EncSrc& S0 = a.src[0];
+      const EncSrc& S1 = a.src[1];
+      const __bf16* sp = sidx ? S1.ptr : S0.ptr;
+      const int sst = sidx ? S1.stride : S0.stride;
+      const int sH = sidx ? S1.H : S0.H, sW = sidx ? S1.W : S0.W, sis = sidx ? S1.is : S0.is;
+      const long img0 = (long)b * sH * sW;
+#pragma unroll
+      for (int i = 0; i < ACH; ++i) {
+        const int y = ry[i] * sis + dy, x = rx[i] * sis + dx;
+        const bool ok = (unsigned)y < (unsigned)sH && (unsigned)x < (unsigned)sW;
+        ra[i] = ok ? *reinterpret_cast<const u32x4*>(sp + (img0 + (long)y * sW + x) * sst + c) : u32x4{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int n = n0 + (tid >> 3) + 32 * i;
+      rb[i] = n < a.N ? *reinterpret_cast<const u32x4*>(wt + (long)n * cl.Kpad + k0 + kc * 8) : u32x4{0, 0, 0, 0};
+    }
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+    __bf16* sA = smem + buf * STAGE;
+    __bf16* sB = sA + BM * ELDK;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) *reinterpret_cast<u32x4*>(sA + ((tid >> 3) + 32 * i) * ELDK + kc * 8) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) *reinterpret_cast<u32x4*>(sB + ((tid >> 3) + 32 * i) * ELDK + kc * 8) = rb[i];
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int fr = lane & 31, fk = (lane >> 5) * 8;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) load((t + 1) * EBK);
+    const __bf16* sA = smem + (t & 1) * STAGE;
+    const __bf16* sB = sA + BM * ELDK;
+#pragma unroll
+    for (int s = 0; s < EBK / 16; ++s) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(sA + (wm * (BM / WM) + i * 32 + fr) * ELDK + s * 16 + fk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(sB + (wn * (BN / WN) + j * 32 + fr) * ELDK + s * 16 + fk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nk) store((t + 1) & 1);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------------ epilogue
+  const int rows = min(BM, GHW - q0);  // valid rows of this tile
+  float* stile = reinterpret_cast<float*>(smem_raw);
+  float* sst1 = stile + BM * (BN + 4);
+  float* sst2 = sst1 + WM * BN;
+  float biasv[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * (BN / WN) + j * 32 + (lane & 31);
+    biasv[j] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
+  }
+  if (a.stats) {
+    // per-column (sum, M2) of this tile's valid rows: two passes over the registers
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (rl < rows) s += acc[i][j][r] + biasv[j];
+        }
+      s += __shfl_xor(s, 32, 64);
+      if (lane < 32) sst1[wm * BN + wn * (BN / WN) + j * 32 + lane] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cl_ = wn * (BN / WN) + j * 32 + (lane & 31);
+      float tot = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) tot += sst1[w * BN + cl_];
+      const float mean = tot / (float)rows;
+      float m2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int rl = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const float d = acc[i][j][r] + biasv[j] - mean;
+          if (rl < rows) m2 += d * d;
+        }
+      m2 += __shfl_xor(m2, 32, 64);
+      if (lane < 32) sst2[wm * BN + cl_] = m2;
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.N) {
+      float s = 0.f, m2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s += sst1[w * BN + tid];
+        m2 += sst2[w * BN + tid];
+      }
+      float* st = a.stats + ((long)(b * cl.tiles_img + tile) * 2) * a.N;
+      st[n0 + tid] = s;
+      st[a.N + n0 + tid] = m2;
+    }
+  }
+  // stage the tile (+ bias) in LDS, then 16-byte stores of 8 channels per thread
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int cl_ = wn * (BN / WN) + j * 32 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rl = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        stile[rl * (BN + 4) + cl_] = acc[i][j][r] + biasv[j];
+      }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int ch = tid; ch < BM * CPR; ch += 256) {
+    const int rl = ch / CPR, cc = ch - (ch / CPR) * CPR;
+    const int n = n0 + cc * 8;
+    if (rl >= rows || n >= a.N) continue;
+    const int q = q0 + rl;
+    const int gy = q / cl.Gw, gx = q - (q / cl.Gw) * cl.Gw;
+    const long pix = ((long)b * a.Ho + gy * a.os + cl.oy0) * a.Wo + gx * a.os + cl.ox0;
+    float v[8];
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(stile + rl * (BN + 4) + cc * 8);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(stile + rl * (BN + 4) + cc * 8 + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = lo[e];
+      v[e + 4] = hi[e];
+    }
+    if (a.res) {
+      float r[8];
+      load8(a.res + pix * a.res_stride + n, r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += r[e];
+    }
+    if (a.mask) {
+      float m[8];
+      load8(a.mask + pix * a.mask_stride + n, m);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = m[e] > 0.f ? v[e] : 0.f;
+    }
+    store8(a.out + pix * a.out_stride + n, v);
+  }
+}
+
+// ============================================================================ weight packing
+// out[wofs + row * Kpad + k] (bf16) from fp32 parameters (any strides):
+//   forward: row = out channel, column (tap, in channel)   -> W[row][local][ky][kx]
+//   dgrad:   row = in channel,  column (conv, tap, out ch) -> W_w[local][row][ky][kx]
+__global__ __launch_bounds__(256) void enc_pack_kernel(const EncConvArgs a, __bf16* out) {
+  const int ci = blockIdx.y;
+  EncClass cl = a.cls[0];
+  if (ci == 1) cl = a.cls[1];
+  if (ci == 2) cl = a.cls[2];
+  if (ci == 3) cl = a.cls[3];
+  const int row = blockIdx.x;
+  for (int k = threadIdx.x; k < cl.Kpad; k += 256) {
+    const int ent = (k < cl.K) ? a.ptab[cl.t0 + (k >> 3)] : -1;
+    float v = 0.f;
+    if (ent >= 0) {
+      const int w = ent & 15, ky = (ent >> 4) & 15, kx = (ent >> 8) & 15, loc = (ent >> 12) + (k & 7);
+      const float* wp = w ? a.w[1] : a.w[0];
+      const long s0 = w ? a.ws[1][0] : a.ws[0][0], s1 = w ? a.ws[1][1] : a.ws[0][1];
+      const long s2 = w ? a.ws[1][2] : a.ws[0][2], s3 = w ? a.ws[1][3] : a.ws[0][3];
+      const int cin = w ? a.wcin[1] : a.wcin[0];
+      if (a.pack_dgrad)
+        v = wp[loc * s0 + row * s1 + ky * s2 + kx * s3];
+      else if (loc < cin)
+        v = wp[row * s0 + loc * s1 + ky * s2 + kx * s3];
+    }
+    out[cl.wofs + (long)row * cl.Kpad + k] = static_cast<__bf16>(v);
+  }
+}
+
+// ============================================================================ wgrad
+// dW[co][k] = sum_p dY[p][co] * im2col(X)[p][k] over one pixel split.  Both operands are
+// staged [pixel][column] (register staged, XOR-swizzled 16-byte chunks) and consumed
+// with ds_read_b64_tr_b16 transposed reads (pixels = the MFMA K dimension).
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ s16x4 tr_read(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(reinterpret_cast<uintptr_t>(p) & 0xffffffffu));
+}
+template <int COLS>
+__device__ __forceinline__ int wswz(int row, int chunk) {
+  return COLS == 128 ? (chunk ^ ((row & 3) << 2)) : (chunk ^ (((row >> 1) & 1) << 2));
+}
+
+template <int BM>
+__global__ __launch_bounds__(256) void enc_wgrad_kernel(const EncWgradArgs a) {
+  constexpr int BN = 64;
+  constexpr int TM = BM / 64;
+  constexpr int ACPR = BM / 8, ARP = 256 / ACPR, AI = 64 / ARP;
+  constexpr int BI = 2;
+  constexpr int STAGE = 64 * (BM + BN);
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+
+  const int tiles = a.tilesM * a.tilesN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wg / tiles, t0 = wg - (wg / tiles) * tiles;
+  const int tm = t0 / a.tilesN, tn = t0 - (t0 / a.tilesN) * a.tilesN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const long pbeg = (long)split * a.pix_per_split;
+  const long pend = min(pbeg + (long)a.pix_per_split, a.P);
+  const int nsteps = pend > pbeg ? (int)((pend - pbeg + 63) / 64) : 0;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int ca = tid % ACPR;
+  const bool a_ok = m0 + ca * 8 < a.N;
+  const int cb = tid & 7;
+  const int kb = n0 + cb * 8;
+  const bool b_ok = kb < a.K;
+  int ky = 0, kx = 0, c = 0;
+  if (b_ok) {
+    const int tap = kb / a.Cx;
+    c = kb - tap * a.Cx;
+    ky = tap / a.KW;
+    kx = tap - ky * a.KW;
+  }
+  const int HoWo = a.Ho * a.Wo;
+  const bool do_db = a.dbslab != nullptr && tn == 0;
+  float dbacc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) dbacc[e] = 0.f;
+
+  u32x4 ra[AI], rb[BI];
+  auto load = [&](int step) __attribute__((always_inline)) {
+    const long p0 = pbeg + (long)step * 64;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const long p = p0 + tid / ACPR + ARP * i;
+      ra[i] = (a_ok && p < pend) ? *reinterpret_cast<const u32x4*>(a.dy + p * a.dy_stride + m0 + ca * 8)
+                                 : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const long p = p0 + (tid >> 3) + 32 * i;
+      rb[i] = u32x4{0, 0, 0, 0};
+      if (b_ok && p < pend) {
+        const int bb = (int)(p / HoWo);
+        const int rem = (int)(p - (long)bb * HoWo);
+        const int oy = rem / a.Wo, ox = rem - (rem / a.Wo) * a.Wo;
+        const int y = oy * a.stride + ky - a.pad, x = ox * a.stride + kx - a.pad;
+        if ((unsigned)y < (unsigned)a.Hx && (unsigned)x < (unsigned)a.Wx)
+          rb[i] = *reinterpret_cast<const u32x4*>(a.x + (((long)bb * a.Hx + y) * a.Wx + x) * a.xstride + c);
+      }
+    }
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+    __bf16* sA = smem + buf * STAGE;
+    __bf16* sB = sA + 64 * BM;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int row = tid / ACPR + ARP * i;
+      *reinterpret_cast<u32x4*>(sA + row * BM + wswz<BM>(row, ca) * 8) = ra[i];
+      if (do_db) {
+        const bf16x8 v = __builtin_bit_cast(bf16x8, ra[i]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dbacc[e] += static_cast<float>(v[e]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      *reinterpret_cast<u32x4*>(sB + row * BN + wswz<BN>(row, cb) * 8) = rb[i];
+    }
+  };
+
+  f32x16 acc[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+
+  const int hh = lane >> 5, gi = (lane >> 4) & 1, q = (lane & 15) >> 2, pq = lane & 3;
+  if (nsteps > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int t = 0; t < nsteps; ++t) {
+    if (t + 1 < nsteps) load(t + 1);
+    const __bf16* sA = smem + (t & 1) * STAGE;
+    const __bf16* sB = sA + 64 * BM;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int r0 = s * 16 + hh * 8 + q, r1 = r0 + 4;
+      bf16x8 af[TM], bfr;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int col = wm * (BM / 2) + i * 32 + gi * 16 + 4 * pq;
+        const s16x4 lo = tr_read(sA + r0 * BM + wswz<BM>(r0, col >> 3) * 8 + (col & 7));
+        const s16x4 hi = tr_read(sA + r1 * BM + wswz<BM>(r1, col >> 3) * 8 + (col & 7));
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+      {
+        const int col = wn * (BN / 2) + gi * 16 + 4 * pq;
+        const s16x4 lo = tr_read(sB + r0 * BN + wswz<BN>(r0, col >> 3) * 8 + (col & 7));
+        const s16x4 hi = tr_read(sB + r1 * BN + wswz<BN>(r1, col >> 3) * 8 + (col & 7));
+        bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr, acc[i], 0, 0, 0);
+    }
+    if (t + 1 < nsteps) store((t + 1) & 1);
+    __syncthreads();
+  }
+
+  float* slab = a.slab + (long)split * a.Npad * a.Kpad;
+  {
+    const int col = n0 + wn * (BN / 2) + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        slab[(long)row * a.Kpad + col] = acc[i][r];
+      }
+  }
+  if (a.dbslab != nullptr && tn == 0) {
+    // fixed-order reduction of the per-thread column sums (threads sharing a chunk column)
+    float* sdb = reinterpret_cast<float*>(smem);  // [ARP][BM]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sdb[(tid / ACPR) * BM + ca * 8 + e] = dbacc[e];
+    __syncthreads();
+    if (tid < BM) {
+      float s = 0.f;
+      for (int r = 0; r < ARP; ++r) s += sdb[r * BM + tid];
+      a.dbslab[(long)split * a.Npad + m0 + tid] = s;
+    }
+  }
+}
+
+// Sum the split slabs in a fixed order into the fp32 parameter gradient (any strides).
+// Threads walk (co, tap, ci) so slab reads are coalesced.
+__global__ __launch_bounds__(256) void enc_wgrad_reduce_kernel(const float* __restrict__ slab, int nsplit, int Npad,
+                                                               int Kpad, const float* __restrict__ dbslab,
+                                                               float* __restrict__ dw, long s0, long s1, long s2,
+                                                               long s3, int Cout, int Cin, int Cx, int KW, int taps,
+                                                               float* __restrict__ db, int accumulate) {
+  const long total = (long)Cout * taps * Cin;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e < total) {
+    const int ci = (int)(e % Cin);
+    const long r = e / Cin;
+    const int tap = (int)(r % taps), co = (int)(r / taps);
+    const long k = (long)tap * Cx + ci;
+    // independent loads, 8 in flight per thread (the split sum is latency-, not bandwidth-bound)
+    const float* src = slab + (long)co * Kpad + k;
+    const long sstride = (long)Npad * Kpad;
+    float s = 0.f;
+    int sp = 0;
+    for (; sp + 8 <= nsplit; sp += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(sp + u) * sstride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; sp < nsplit; ++sp) s += src[sp * sstride];
+    const int ky = tap / KW, kx = tap - (tap / KW) * KW;
+    float* d = dw + co * s0 + ci * s1 + ky * s2 + kx * s3;
+    *d = accumulate ? *d + s : s;
+  }
+  if (db != nullptr && blockIdx.x == 0) {
+    for (int co = threadIdx.x; co < Cout; co += 256) {
+      float s = 0.f;  // no slab: the bias feeds a re-centring norm, its gradient is exactly 0
+      if (dbslab != nullptr)
+        for (int sp = 0; sp < nsplit; ++sp) s += dbslab[(long)sp * Npad + co];
+      db[co] = accumulate ? db[co] + s : s;
+    }
+  }
+}
+
+// ============================================================================ input prep
+// out[b][y][x][0..7] = (2 * img / 255 - 1, channels 3..7 zero), bf16; images NCHW-any-strides
+// fp32, b < B from img0, b >= B from img1 (the feature encoder's paired batch).
+__global__ __launch_bounds__(256) void enc_prep_kernel(const float* __restrict__ i0, const float* __restrict__ i1,
+                                                       long sb, long sc, long sh, long sw, int B, int H, int W,
+                                                       int nimg, __bf16* __restrict__ out) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = (long)nimg * H * W;
+  if (p >= total) return;
+  const int b = (int)(p / ((long)H * W));
+  const int rem = (int)(p - (long)b * H * W);
+  const int y = rem / W, x = rem - (rem / W) * W;
+  const float* src = b < B ? i0 + (long)b * sb : i1 + (long)(b - B) * sb;
+  const long o = (long)y * sh + (long)x * sw;
+  float v[8];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) v[c] = 2.f * (src[o + c * sc] / 255.f) - 1.f;
+#pragma unroll
+  for (int c = 3; c < 8; ++c) v[c] = 0.f;
+  store8(out + p * 8, v);
+}
+
+// ============================================================================ norms
+// coef layout [B][4][N]: scale, shift (y = a * scale + shift), rstd, mean (xhat = (a - mean) * rstd)
+// kinds: 0 none, 1 instance, 2 batch (training statistics), 3 batch (running statistics)
+
+
+__global__ __launch_bounds__(256) void enc_norm_finalize_kernel(const NormFinArgs a) {
+  const int n = blockIdx.x, g = blockIdx.y;  // channel, group (image for instance norm)
+  const int tid = threadIdx.x;
+  __shared__ float sn[256], sm[256], s2[256];
+  float mean = 0.f, var = 1.f;
+  if (a.kind == 1 || a.kind == 2) {
+    const int b0 = a.kind == 1 ? g : 0, b1 = a.kind == 1 ? g + 1 : a.B;
+    const int E = (b1 - b0) * a.T;
+    float cn = 0.f, cm = 0.f, cM2 = 0.f;
+    for (int e = tid; e < E; e += 256) {
+      const int b = b0 + e / a.T, t = e - (e / a.T) * a.T;
+      const float nb = (float)min(a.BM, a.HW - t * a.BM);
+      const float* st = a.stats + ((long)(b * a.T + t) * 2) * a.N;
+      const float mb = st[n] / nb, M2b = st[a.N + n];
+      const float nn = cn + nb, d = mb - cm;
+      cm += d * nb / nn;
+      cM2 += M2b + d * d * cn * nb / nn;
+      cn = nn;
+    }
+    sn[tid] = cn;
+    sm[tid] = cm;
+    s2[tid] = cM2;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+      if (tid < off) {
+        const float na = sn[tid], nb = sn[tid + off];
+        const float nn = na + nb;
+        if (nb > 0.f) {
+          const float d = sm[tid + off] - sm[tid];
+          sm[tid] += d * nb / nn;
+          s2[tid] += s2[tid + off] + d * d * na * nb / nn;
+          sn[tid] = nn;
+        }
+      }
+      __syncthreads();
+    }
+    mean = sm[0];
+    var = s2[0] / sn[0];
+    if (tid == 0 && a.kind == 2 && a.rmean) {
+      const float cnt = sn[0];
+      a.rmean[n] = (1.f - a.momentum) * a.rmean[n] + a.momentum * mean;
+      a.rvar[n] = (1.f - a.momentum) * a.rvar[n] + a.momentum * var * cnt / fmaxf(cnt - 1.f, 1.f);
+      if (n == 0 && a.nbt) *a.nbt += 1;
+    }
+  } else if (a.kind == 3) {
+    mean = a.rmean[n];
+    var = a.rvar[n];
+  }
+  if (tid != 0) return;
+  float scale = 1.f, shift = 0.f, rstd = 1.f;
+  if (a.kind != 0) {
+    rstd = rsqrtf(var + a.eps);
+    const float gm = a.gamma ? a.gamma[n] : 1.f, bt = a.beta ? a.beta[n] : 0.f;
+    scale = gm * rstd;
+    shift = bt - mean * scale;
+  } else {
+    mean = 0.f;
+  }
+  const int b0 = a.kind == 1 ? g : 0, b1 = a.kind == 1 ? g + 1 : a.B;
+  for (int b = b0; b < b1; ++b) {
+    float* c = a.coef + (long)b * 4 * a.N;
+    c[n] = scale;
+    c[a.N + n] = shift;
+    c[2 * a.N + n] = rstd;
+    c[3 * a.N + n] = mean;
+  }
+}
+
+// y = relu_out( f(a) + g(r) ),  f(a) = [relu](a * scale + shift),  g(r) = r * scale_r + shift_r | r | 0
+__global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict__ a, const float* __restrict__ ca,
+                                                        int relu_a, const __bf16* __restrict__ r,
+                                                        const float* __restrict__ cr, int relu_out,
+                                                        __bf16* __restrict__ out, int B, int HW, int N) {
+  const int G = N / 8;
+  const long total = (long)B * HW * G;
+  for (long ch = (long)blockIdx.x * 256 + threadIdx.x; ch < total; ch += (long)gridDim.x * 256) {
+    const long p = ch / G;
+    const int n = (int)(ch - p * G) * 8;
+    const int b = (int)(p / HW);
+    float v[8], s[8], t[8];
+    load8(a + p * N + n, v);
+    loadf8(ca + (long)b * 4 * N + n, s);
+    loadf8(ca + (long)b * 4 * N + N + n, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] = v[e] * s[e] + t[e];
+      if (relu_a) v[e] = fmaxf(v[e], 0.f);
+    }
+    if (r) {
+      float rv[8];
+      load8(r + p * N + n, rv);
+      if (cr) {
+        loadf8(cr + (long)b * 4 * N + n, s);
+        loadf8(cr + (long)b * 4 * N + N + n, t);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rv[e] = rv[e] * s[e] + t[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += rv[e];
+    }
+    if (relu_out)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    store8(out + p * N + n, v);
+  }
+}
+
+// Norm backward, pass 1: per (image, chunk) partial sums over pixels of
+//   branch 0: dy0 = g * [a0 * scale0 + shift0 > 0 if relu0],  S1 = sum dy0, S2 = sum dy0 * xhat0
+//   branch 1: dy1 = g,                                           S1, S2 with xhat1
+// part [B][R][4][N] (no atomics; fixed reduction order).
+
+
+__global__ __launch_bounds__(256) void enc_norm_bwd_reduce_kernel(const NormBwdArgs a) {
+  __shared__ float red[2048];
+  const int r = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int N = a.N, G = N / 8, PPB = 256 / G;
+  const int cg = tid % G, pr = tid / G;
+  const bool active = pr < PPB;
+  const int n = cg * 8;
+  const int chunk = (a.HW + a.R - 1) / a.R;
+  const int pb = r * chunk, pe = min(a.HW, pb + chunk);
+  float S[4][8];
+#pragma unroll
+  for (int qd = 0; qd < 4; ++qd)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) S[qd][e] = 0.f;
+  if (active) {
+    float sc0[8], sh0[8], rs0[8], mu0[8], rs1[8], mu1[8];
+    const float* c0 = a.c0 + (long)b * 4 * N;
+    loadf8(c0 + n, sc0);
+    loadf8(c0 + N + n, sh0);
+    loadf8(c0 + 2 * N + n, rs0);
+    loadf8(c0 + 3 * N + n, mu0);
+    if (a.a1) {
+      const float* c1 = a.c1 + (long)b * 4 * N;
+      loadf8(c1 + 2 * N + n, rs1);
+      loadf8(c1 + 3 * N + n, mu1);
+    }
+    const long base = (long)b * a.HW;
+    for (int p = pb + pr; p < pe; p += PPB) {
+      float gv[8], av[8];
+      load8(a.g + (base + p) * N + n, gv);
+      load8(a.a0 + (base + p) * N + n, av);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dy = (a.relu0 && !(av[e] * sc0[e] + sh0[e] > 0.f)) ? 0.f : gv[e];
+        S[0][e] += dy;
+        S[1][e] += dy * (av[e] - mu0[e]) * rs0[e];
+      }
+      if (a.a1) {
+        load8(a.a1 + (base + p) * N + n, av);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          S[2][e] += gv[e];
+          S[3][e] += gv[e] * (av[e] - mu1[e]) * rs1[e];
+        }
+      }
+    }
+  }
+  const int nq = a.a1 ? 4 : 2;
+  for (int qd = 0; qd < nq; ++qd) {
+    if (active)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[pr * N + n + e] = S[qd][e];
+    __syncthreads();
+    if (tid < N) {
+      float s = 0.f;
+      for (int k = 0; k < PPB; ++k) s += red[k * N + tid];
+      a.part[(((long)b * a.R + r) * 4 + qd) * N + tid] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// pass 2: coefficients per (group, channel) and the BatchNorm parameter gradients.
+// Block = (group, 64-channel chunk); 4 threads per channel split the (image, chunk)
+// partials, combined in LDS in a fixed order.
+__global__ __launch_bounds__(256) void enc_norm_bwd_finalize_kernel(const NormBwdArgs a) {
+  __shared__ float red[4][4][64];
+  const int N = a.N;
+  const int nb = a.a1 ? 2 : 1;
+  const int g = blockIdx.x, n = blockIdx.y * 64 + (threadIdx.x & 63), sub = threadIdx.x >> 6;
+  const int b0 = a.kind == 1 ? g : 0, b1 = a.kind == 1 ? g + 1 : a.B;
+  const int E = (b1 - b0) * a.R;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (n < N) {
+    for (int e = sub; e < E; e += 4) {
+      const float* pp = a.part + ((long)(b0 * a.R + e) * 4) * N + n;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q < 2 * nb) acc[q] += pp[q * N];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[q][sub][threadIdx.x & 63] = acc[q];
+  __syncthreads();
+  if (sub != 0 || n >= N) return;
+  const float M = (float)(b1 - b0) * a.HW;
+  for (int j = 0; j < nb; ++j) {
+    float S1 = 0.f, S2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      S1 += red[2 * j][k][threadIdx.x];
+      S2 += red[2 * j + 1][k][threadIdx.x];
+    }
+    const float* c = (j ? a.c1 : a.c0) + (long)b0 * 4 * N;
+    const float scale = c[n];
+    float k1 = scale, k2 = 0.f, k3 = 0.f;
+    if (a.kind == 1 || a.kind == 2) {
+      k2 = -scale * S2 / M;
+      k3 = -scale * S1 / M;
+    }
+    if (a.kind == 0) k1 = 1.f;
+    for (int b = b0; b < b1; ++b) {
+      float* bc = a.bcoef + ((long)b * 2 + j) * 3 * N;
+      bc[n] = k1;
+      bc[N + n] = k2;
+      bc[2 * N + n] = k3;
+    }
+    if ((a.kind == 2 || a.kind == 3) && a.dgamma[j]) {
+      a.dgamma[j][n] = S2;
+      a.dbeta[j][n] = S1;
+    }
+  }
+}
+
+// pass 3: da_j = k1 * dy_j + k2 * xhat_j + k3
+__global__ __launch_bounds__(256) void enc_norm_bwd_apply_kernel(const NormBwdArgs a) {
+  const int N = a.N, G = N / 8;
+  const long total = (long)a.B * a.HW * G;
+  for (long ch = (long)blockIdx.x * 256 + threadIdx.x; ch < total; ch += (long)gridDim.x * 256) {
+    const long p = ch / G;
+    const int n = (int)(ch - p * G) * 8;
+    const int b = (int)(p / a.HW);
+    float gv[8], av[8], k1[8], k2[8], k3[8], rs[8], mu[8], o[8];
+    load8(a.g + p * N + n, gv);
+    load8(a.a0 + p * N + n, av);
+    const float* c0 = a.c0 + (long)b * 4 * N;
+    const float* bc = a.bcoef + (long)b * 2 * 3 * N;
+    loadf8(bc + n, k1);
+    loadf8(bc + N + n, k2);
+    loadf8(bc + 2 * N + n, k3);
+    loadf8(c0 + 2 * N + n, rs);
+    loadf8(c0 + 3 * N + n, mu);
+    if (a.relu0) {
+      float sc[8], sh[8];
+      loadf8(c0 + n, sc);
+      loadf8(c0 + N + n, sh);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dy = (av[e] * sc[e] + sh[e] > 0.f) ? gv[e] : 0.f;
+        o[e] = k1[e] * dy + k2[e] * (av[e] - mu[e]) * rs[e] + k3[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = k1[e] * gv[e] + k2[e] * (av[e] - mu[e]) * rs[e] + k3[e];
+    }
+    store8(a.out0 + p * N + n, o);
+    if (a.a1) {
+      load8(a.a1 + p * N + n, av);
+      const float* c1 = a.c1 + (long)b * 4 * N;
+      loadf8(bc + 3 * N + n, k1);
+      loadf8(bc + 4 * N + n, k2);
+      loadf8(bc + 5 * N + n, k3);
+      loadf8(c1 + 2 * N + n, rs);
+      loadf8(c1 + 3 * N + n, mu);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = k1[e] * gv[e] + k2[e] * (av[e] - mu[e]) * rs[e] + k3[e];
+      store8(a.out1 + p * N + n, o);
+    }
+  }
+}
+
+int grid_for(long chunks) {
+  const long g = (chunks + 255) / 256;
+  return (int)std::min<long>(std::max<long>(g, 1), 4096);
+}
+
+}  // namespace
+
+// ============================================================================ launchers
+// Tile configurations by output-channel count.
+enum EncTile : int { kT128x128 = 0, kT128x96 = 1, kT128x64 = 2, kT128x32 = 3 };
+
+int enc_tile_bn(int N) {
+  if (N % 128 == 0) return 128;
+  if (N == 96) return 96;
+  if (N % 64 == 0) return 64;
+  if (N <= 32) return 32;
+  return 64;
+}
+constexpr int kEncBM = 128;
+
+hipError_t launch_enc_pack(const EncConvArgs& a, int rows, void* out, hipStream_t s) {
+  hipLaunchKernelGGL(enc_pack_kernel, dim3(rows, a.ncls), dim3(256), 0, s, a, static_cast<__bf16*>(out));
+  return hipGetLastError();
+}
+
+hipError_t launch_enc_conv(const EncConvArgs& a, int nblocks, hipStream_t s) {
+  const int BN = enc_tile_bn(a.N);
+  switch (BN) {
+    case 128:
+      hipLaunchKernelGGL((enc_conv_kernel<128, 128, 2, 2>), dim3(nblocks), dim3(256), 0, s, a);
+      break;
+    case 96:
+      hipLaunchKernelGGL((enc_conv_kernel<128, 96, 4, 1>), dim3(nblocks), dim3(256), 0, s, a);
+      break;
+    case 64:
+      hipLaunchKernelGGL((enc_conv_kernel<128, 64, 2, 2>), dim3(nblocks), dim3(256), 0, s, a);
+      break;
+    default:
+      hipLaunchKernelGGL((enc_conv_kernel<128, 32, 4, 1>), dim3(nblocks), dim3(256), 0, s, a);
+      break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_enc_wgrad(const EncWgradArgs& a, int BM, hipStream_t s) {
+  const int nwg = a.nsplit * a.tilesM * a.tilesN;
+  if (BM == 128)
+    hipLaunchKernelGGL((enc_wgrad_kernel<128>), dim3(nwg), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((enc_wgrad_kernel<64>), dim3(nwg), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_enc_wgrad_reduce(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, float* dw,
+                                   const long* ws, int Cout, int Cin, int Cx, int KH, int KW, float* db,
+                                   bool accumulate, hipStream_t s) {
+  const long total = (long)Cout * KH * KW * Cin;
+  const int blocks = (int)std::max<long>((total + 255) / 256, 1);
+  hipLaunchKernelGGL(enc_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, slab, nsplit, Npad, Kpad, dbslab, dw,
+                     ws[0], ws[1], ws[2], ws[3], Cout, Cin, Cx, KW, KH * KW, db, accumulate ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_enc_prep(const float* i0, const float* i1, const long* st, int B, int H, int W, int nimg,
+                           void* out, hipStream_t s) {
+  const long total = (long)nimg * H * W;
+  hipLaunchKernelGGL(enc_prep_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, i0, i1, st[0], st[1],
+                     st[2], st[3], B, H, W, nimg, static_cast<__bf16*>(out));
+  return hipGetLastError();
+}
+
+hipError_t launch_enc_norm_finalize(const NormFinArgs& a, hipStream_t s) {
+  const int groups = a.kind == 1 ? a.B : 1;
+  hipLaunchKernelGGL(enc_norm_finalize_kernel, dim3(a.N, groups), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_enc_apply(const void* a, const float* ca, bool relu_a, const void* r, const float* cr,
+                            bool relu_out, void* out, int B, int HW, int N, hipStream_t s) {
+  const long chunks = (long)B * HW * (N / 8);
+  hipLaunchKernelGGL(enc_apply_kernel, dim3(grid_for(chunks)), dim3(256), 0, s, static_cast<const __bf16*>(a), ca,
+                     relu_a ? 1 : 0, static_cast<const __bf16*>(r), cr, relu_out ? 1 : 0, static_cast<__bf16*>(out), B,
+                     HW, N);
+  return hipGetLastError();
+}
+
+hipError_t launch_enc_norm_bwd(const NormBwdArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(enc_norm_bwd_reduce_kernel, dim3(a.R, a.B), dim3(256), 0, s, a);
+  RAFT_HIP_CHECK(hipGetLastError());
+  const int groups = a.kind == 1 ? a.B : 1;
+  hipLaunchKernelGGL(enc_norm_bwd_finalize_kernel, dim3(groups, (a.N + 63) / 64), dim3(256), 0, s, a);
+  RAFT_HIP_CHECK(hipGetLastError());
+  const long chunks = (long)a.B * a.HW * (a.N / 8);
+  hipLaunchKernelGGL(enc_norm_bwd_apply_kernel, dim3(grid_for(chunks)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace raft_amd

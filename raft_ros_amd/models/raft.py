@@ -14,6 +14,8 @@ Execution differences (GPU):
 
 * the correlation pyramid build / lookup / backward, the convex upsampler and
   the GRU gate math are native HIP kernels (``raft_ros_amd.ops``);
+* under bf16 AMP both encoders run on native HIP kernels as one autograd node
+  each (``ops/encoder.py``; ``args.native_encoder=False`` selects the module path);
 * the lookup emits channels-last features already in the autocast dtype;
 * mixed precision uses ``args.amp_dtype`` (default bf16 on MI355X; 'fp16'
   reproduces the reference's fp16 autocast);
@@ -27,6 +29,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import CorrPyramid, LocalCorrPyramid, convex_upsample, upflow8
+from ..ops import encoder as encoder_native
 from ..ops import update_fused
 from ..ops._ext import use_native
 from ..ops.reference import coords_grid
@@ -115,13 +118,20 @@ class RAFT(nn.Module):
         cl = dev == "cuda" and _arg(self.args, "channels_last", True)
         fmt = torch.channels_last if cl else torch.contiguous_format
 
-        image1 = (2 * (image1 / 255.0) - 1.0).contiguous(memory_format=fmt)
-        image2 = (2 * (image2 / 255.0) - 1.0).contiguous(memory_format=fmt)
         hdim, cdim = self.hidden_dim, self.context_dim
         amp = bool(self.args.mixed_precision)
+        native = self._use_native_encoders(image1, amp)
+        raw1, raw2 = image1, image2
+        if not native:
+            image1 = (2 * (image1 / 255.0) - 1.0).contiguous(memory_format=fmt)
+            image2 = (2 * (image2 / 255.0) - 1.0).contiguous(memory_format=fmt)
 
-        with self._autocast(dev):
-            fmap1, fmap2 = self.fnet([image1, image2])
+        if native:
+            # both encoders on the native HIP kernels (ops/encoder.py), input normalisation fused
+            fmap1, fmap2 = encoder_native.encode(self.fnet, raw1, raw2).split(raw1.shape[0], dim=0)
+        else:
+            with self._autocast(dev):
+                fmap1, fmap2 = self.fnet([image1, image2])
         fmap1, fmap2 = fmap1.float(), fmap2.float()
         if self.args.alternate_corr:
             corr_fn = LocalCorrPyramid(fmap1, fmap2, radius=self.args.corr_radius,
@@ -132,12 +142,12 @@ class RAFT(nn.Module):
             corr_fn = CorrPyramid(fmap1, fmap2, radius=self.args.corr_radius, split=not bool(self.args.mixed_precision))
 
         with self._autocast(dev):
-            cnet = self.cnet(image1)
+            cnet = encoder_native.encode(self.cnet, raw1) if native else self.cnet(image1)
             net, inp = torch.split(cnet, [hdim, cdim], dim=1)
             net = torch.tanh(net)
             inp = torch.relu(inp)
 
-        coords0, coords1 = self.initialize_flow(image1)
+        coords0, coords1 = self.initialize_flow(raw1)
         if flow_init is not None:
             coords1 = coords1 + flow_init
 
@@ -164,6 +174,11 @@ class RAFT(nn.Module):
         if test_mode:
             return coords1 - coords0, flow_up
         return flow_predictions
+
+    # ------------------------------------------------------------------ native encoders
+    def _use_native_encoders(self, image1, amp: bool) -> bool:
+        return (amp and self.amp_dtype == torch.bfloat16 and _arg(self.args, "native_encoder", True)
+                and encoder_native.supported(self.fnet, image1) and encoder_native.supported(self.cnet, image1))
 
     # ------------------------------------------------------------------ fused (HIP) update path
     def _use_fused(self, image1, amp: bool) -> bool:

@@ -1,0 +1,262 @@
+"""Native (HIP) execution of the residual CNN encoders, one autograd node per encoder.
+
+The encoder modules (``models/extractor.py``, reference core/extractor.py:6-267) keep
+their parameters and names; on the GPU bf16 path ``encode(module, img1, img2)`` runs
+the whole network on the kernels of ``csrc/encoder.hip``:
+
+* activations are NHWC bf16 ``[B, H, W, C]`` end to end; the stem reads the raw 0..255
+  fp32 images and normalises them on the fly (``2 * img / 255 - 1``, channels padded
+  3 -> 8), both frames of the feature encoder as one batch;
+* every conv epilogue emits per-tile (sum, M2) statistics, so InstanceNorm / BatchNorm
+  need no statistics pass: a tiny finalize (Chan combine, fixed order; BatchNorm running
+  statistics updated in place) and one apply pass that also fuses the ReLU and, at the
+  end of a residual block, the downsample norm, the residual add and the final ReLU;
+* backward: stride-parity-split data gradients (the first conv of a block and its
+  downsample share one launch; the epilogue adds the identity-residual gradient and
+  applies the ReLU' of the block input), three-pass norm backward (both tail branches
+  at once), split-pixel weight gradients reduced into the fp32 parameter layout.
+
+Nothing here goes through MIOpen, so the encoder is also safe inside a captured HIP
+graph (``runtime/train_graph.py``): MIOpen convolutions produced non-finite gradients
+from the second replay of a captured training step.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ._ext import ops, use_native
+from .norm import InstanceNorm2dNHWC
+
+# norm kinds shared with csrc/encoder.hip
+_NONE, _INSTANCE, _BATCH_TRAIN, _BATCH_EVAL = 0, 1, 2, 3
+
+
+def _norm_kind(m: nn.Module):
+    if isinstance(m, InstanceNorm2dNHWC):
+        return _INSTANCE
+    if isinstance(m, nn.BatchNorm2d):
+        return _BATCH_TRAIN if m.training else _BATCH_EVAL
+    if isinstance(m, nn.Sequential) and len(m) == 0:
+        return _NONE
+    return None
+
+
+def _unit_convs(block):
+    """(conv, norm) chain of a residual / bottleneck block, plus its downsample pair."""
+    if hasattr(block, "conv3"):  # BottleneckBlock
+        units = [(block.conv1, block.norm1), (block.conv2, block.norm2), (block.conv3, block.norm3)]
+        down = (block.downsample[0], block.norm4) if block.downsample is not None else None
+    else:  # ResidualBlock
+        units = [(block.conv1, block.norm1), (block.conv2, block.norm2)]
+        down = (block.downsample[0], block.norm3) if block.downsample is not None else None
+    return units, down
+
+
+def supported(enc: nn.Module, image: torch.Tensor) -> bool:
+    """True when ``enc`` can run on the native encoder kernels for this input."""
+    if not image.is_cuda or not use_native(image):
+        return False
+    if enc.training and enc.dropout is not None:
+        return False
+    norms = [enc.norm1]
+    for layer in (enc.layer1, enc.layer2, enc.layer3):
+        for blk in layer:
+            units, down = _unit_convs(blk)
+            norms += [n for _, n in units] + ([down[1]] if down else [])
+    return all(_norm_kind(n) is not None for n in norms)
+
+
+class _Layout:
+    """Flat parameter order of one encoder (the autograd inputs) and its norm kinds."""
+
+    def __init__(self, enc):
+        self.params = []
+        self.index = {}
+
+        def add(t):
+            if t is None:
+                return -1
+            self.index[id(t)] = len(self.params)
+            self.params.append(t)
+            return self.index[id(t)]
+
+        def conv(c):
+            return {"w": add(c.weight), "b": add(c.bias), "stride": c.stride[0], "pad": c.padding[0],
+                    "module": c}
+
+        def norm(n):
+            k = _norm_kind(n)
+            d = {"kind": k, "module": n}
+            if k in (_BATCH_TRAIN, _BATCH_EVAL):
+                d["g"], d["bt"] = add(n.weight), add(n.bias)
+            return d
+
+        self.stem = (conv(enc.conv1), norm(enc.norm1))
+        self.blocks = []
+        for layer in (enc.layer1, enc.layer2, enc.layer3):
+            for blk in layer:
+                units, down = _unit_convs(blk)
+                self.blocks.append(([(conv(c), norm(n)) for c, n in units],
+                                    (conv(down[0]), norm(down[1])) if down else None))
+        self.out = conv(enc.conv2)
+
+
+def _stats(a, st, nd, P):
+    """coef [B, 4, N] of the norm ``nd`` for the conv output ``a``."""
+    m = nd["module"]
+    B, H, W, N = a.shape
+    k = nd["kind"]
+    if k in (_BATCH_TRAIN, _BATCH_EVAL):
+        return ops().enc_norm_stats(st if k == _BATCH_TRAIN else None, B, H * W, N, k, P[nd["g"]], P[nd["bt"]],
+                                    m.running_mean, m.running_var,
+                                    m.num_batches_tracked if k == _BATCH_TRAIN else None,
+                                    m.momentum if m.momentum is not None else 0.1, m.eps)
+    eps = getattr(m, "eps", 1e-5)
+    return ops().enc_norm_stats(st, B, H * W, N, k, None, None, None, None, None, 0.0, eps)
+
+
+def _conv(x, cd, P, stats):
+    b = P[cd["b"]] if cd["b"] >= 0 else None
+    return ops().enc_conv_fwd(x, P[cd["w"]], b, cd["stride"], cd["pad"], stats)
+
+
+def _forward(L, x0, P):
+    """Run the encoder; returns (output NHWC, saved records)."""
+    o = ops()
+    sc, sn = L.stem
+    a0, st = _conv(x0, sc, P, True)
+    c0 = _stats(a0, st, sn, P)
+    h = o.enc_apply(a0, c0, True, None, None, False)
+    stem_rec = (x0, a0, c0, h)
+    recs = []
+    for units, down in L.blocks:
+        hin = h
+        ins, acts, coefs, outs = [], [], [], []
+        cur = hin
+        for ui, (cd, nd) in enumerate(units):
+            a, st = _conv(cur, cd, P, nd["kind"] != _BATCH_EVAL)
+            c = _stats(a, st, nd, P)
+            ins.append(cur)
+            acts.append(a)
+            coefs.append(c)
+            if ui + 1 < len(units):
+                cur = o.enc_apply(a, c, True, None, None, False)
+        drec = None
+        if down is not None:
+            dcd, dnd = down
+            ad, st = _conv(hin, dcd, P, dnd["kind"] != _BATCH_EVAL)
+            cdn = _stats(ad, st, dnd, P)
+            h = o.enc_apply(acts[-1], coefs[-1], True, ad, cdn, True)
+            drec = (ad, cdn)
+        else:
+            h = o.enc_apply(acts[-1], coefs[-1], True, hin, None, True)
+        recs.append((ins, acts, coefs, drec, h))
+    y, _ = _conv(h, L.out, P, False)
+    return y, stem_rec, recs
+
+
+def _wgrad(x, dy, cd, P, grads, nd=None):
+    """Weight / bias gradient of conv ``cd``; ``nd``: the norm it feeds.  InstanceNorm and
+    training-mode BatchNorm subtract the per-channel mean, so a conv bias in front of them
+    has an exactly zero gradient (written as 0, not as bf16 rounding noise)."""
+    w = P[cd["w"]]
+    dw = torch.empty_like(w, dtype=torch.float32)
+    db = torch.empty(w.shape[0], device=w.device, dtype=torch.float32) if cd["b"] >= 0 else None
+    zero = nd is not None and nd["kind"] in (_INSTANCE, _BATCH_TRAIN)
+    ops().enc_conv_wgrad(x, dy, dw, db, cd["stride"], cd["pad"], False, zero)
+    grads[cd["w"]] = dw.to(w.dtype) if w.dtype != torch.float32 else dw
+    if db is not None:
+        b = P[cd["b"]]
+        grads[cd["b"]] = db.to(b.dtype) if b.dtype != torch.float32 else db
+
+
+def _norm_grads(nd, dg, dbt, grads):
+    if nd["kind"] in (_BATCH_TRAIN, _BATCH_EVAL) and dg is not None:
+        grads[nd["g"]] = dg
+        grads[nd["bt"]] = dbt
+
+
+def _backward(L, P, gy, stem_rec, recs):
+    o = ops()
+    grads = [None] * len(P)
+    last_h = recs[-1][4] if recs else stem_rec[3]
+    _wgrad(last_h, gy, L.out, P, grads)
+    oc = L.out
+    g = o.enc_conv_dgrad([gy], [P[oc["w"]]], [oc["stride"]], [oc["pad"]], last_h.shape[1], last_h.shape[2],
+                         None, last_h)
+    for (units, down), (ins, acts, coefs, drec, _h) in zip(reversed(L.blocks), reversed(recs)):
+        dnd = down[1] if down is not None else None
+        kind = units[-1][1]["kind"]
+        r = o.enc_norm_bwd(g, acts[-1], coefs[-1], True, drec[0] if drec else None, drec[1] if drec else None, kind)
+        # both tail norms of a block share a kind (one norm_fn per encoder)
+        da, dad = r[0], r[1] if drec else None
+        _norm_grads(units[-1][1], r[2], r[3], grads)
+        if down is not None:
+            _norm_grads(dnd, r[4], r[5], grads)
+        for u in range(len(units) - 1, -1, -1):
+            cd, nd = units[u]
+            x = ins[u]
+            _wgrad(x, da, cd, P, grads, nd)
+            if u > 0:
+                dh = o.enc_conv_dgrad([da], [P[cd["w"]]], [cd["stride"]], [cd["pad"]], x.shape[1], x.shape[2],
+                                      None, x)
+                pnd = units[u - 1][1]
+                r = o.enc_norm_bwd(dh, acts[u - 1], coefs[u - 1], False, None, None, pnd["kind"])
+                da = r[0]
+                _norm_grads(pnd, r[2], r[3], grads)
+            else:
+                dys, ws, ss, ps = [da], [P[cd["w"]]], [cd["stride"]], [cd["pad"]]
+                if down is not None:
+                    dcd = down[0]
+                    dys.append(dad)
+                    ws.append(P[dcd["w"]])
+                    ss.append(dcd["stride"])
+                    ps.append(dcd["pad"])
+                    _wgrad(x, dad, dcd, P, grads, dnd)
+                g = o.enc_conv_dgrad(dys, ws, ss, ps, x.shape[1], x.shape[2], None if down is not None else g, x)
+    x0, a0, c0, _h0 = stem_rec
+    sc, sn = L.stem
+    r = o.enc_norm_bwd(g, a0, c0, False, None, None, sn["kind"])
+    _norm_grads(sn, r[2], r[3], grads)
+    _wgrad(x0, r[0], sc, P, grads, sn)
+    return grads
+
+
+class _EncoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, layout, x0, *params):
+        y, stem_rec, recs = _forward(layout, x0, params)
+        ctx.layout = layout
+        ctx.params = params
+        # records hold only tensors created here (activations, statistics coefficients)
+        ctx.stem_rec, ctx.recs = stem_rec, recs
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        gy = gy.contiguous().to(torch.bfloat16)
+        grads = _backward(ctx.layout, ctx.params, gy, ctx.stem_rec, ctx.recs)
+        ctx.stem_rec = ctx.recs = None
+        return (None, None, *grads)
+
+
+def _layout(enc):
+    # the parameter objects and the BatchNorm train/eval state define the layout
+    key = tuple(id(p) for p in enc.parameters()) + tuple(
+        m.training for m in enc.modules() if isinstance(m, nn.BatchNorm2d))
+    cached = getattr(enc, "_native_layout", None)
+    if cached is None or cached[0] != key:
+        cached = (key, _Layout(enc))
+        object.__setattr__(enc, "_native_layout", cached)
+    return cached[1]
+
+
+def encode(enc, image1: torch.Tensor, image2: torch.Tensor | None = None) -> torch.Tensor:
+    """Run ``enc`` natively on raw 0..255 fp32 images (``image2``: second frame of a
+    paired batch).  Returns the (n, C, H/8, W/8) bf16 feature map in channels-last
+    layout (``n`` = 2B when paired)."""
+    L = _layout(enc)
+    x0 = ops().enc_prep(image1.float(), image2.float() if image2 is not None else None)
+    y = _EncoderFn.apply(L, x0, *L.params)
+    return y.permute(0, 3, 1, 2)

@@ -46,8 +46,6 @@ def test_graphed_step_eager_matches_plain_step_cpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.xfail(strict=False, reason="open issue: from the 2nd replay the fnet (instance-norm encoder) "
-                   "weight grads come out non-finite; bench keeps the train graph off by default")
 def test_graphed_step_replay_matches_eager_gpu(cuda):
     torch.manual_seed(0)
     mk = lambda: RAFT(Namespace(small=False, mixed_precision=True, amp_dtype="bf16")).to(cuda).to(  # noqa: E731
