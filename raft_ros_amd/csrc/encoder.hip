@@ -171,12 +171,13 @@ struct EncCfg {
   static_assert(ACH * 256 * 8 == BM * EBK && BCH * 256 * 8 == BN * EBK, "staging shape");
 };
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NSRC>
 __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
   using C = EncCfg<BM, BN, WM, WN>;
   constexpr int TM = C::TM, TN = C::TN, ACH = C::ACH, BCH = C::BCH, STAGE = C::STAGE;
   __shared__ __attribute__((aligned(16))) char smem_raw[C::SMEM];
   __shared__ int s_tab[kEncTab];
+  __shared__ int s_out[BM];  // output pixel offset of each tile row (-1: past the grid)
   __bf16* smem = reinterpret_cast<__bf16*>(smem_raw);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -193,25 +194,44 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
   const int n0 = tn * BN;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int kc = tid & 7;
+  for (int r = tid; r < BM; r += 256) {
+    const int q = q0 + r;
+    int off = -1;
+    if (q < GHW) {
+      const int gy = q / cl.Gw, gx = q - (q / cl.Gw) * cl.Gw;
+      off = ((b * a.Ho + gy * a.os + cl.oy0) * a.Wo + gx * a.os + cl.ox0);
+    }
+    s_out[r] = off;
+  }
 
-  // rows this thread stages: grid coordinates of pixel q (far outside when q is past the grid)
-  int ry[ACH], rx[ACH];
+  // rows this thread stages, per source: top-left source coordinate of the grid pixel and
+  // its 32-bit element offset (rows past the grid get a coordinate that fails every bounds test)
+  int sy[NSRC][ACH], sx[NSRC][ACH], sbase[NSRC][ACH];
 #pragma unroll
   for (int i = 0; i < ACH; ++i) {
     const int q = q0 + (tid >> 3) + 32 * i;
-    if (q < GHW) {
-      const int gy = q / cl.Gw;
-      ry[i] = gy;
-      rx[i] = q - gy * cl.Gw;
-    } else {
-      ry[i] = -(1 << 20);
-      rx[i] = 0;
+    const bool valid = q < GHW;
+    const int gy = valid ? q / cl.Gw : 0;
+    const int gx = valid ? q - gy * cl.Gw : 0;
+#pragma unroll
+    for (int s2 = 0; s2 < NSRC; ++s2) {
+      const EncSrc& S = a.src[s2];
+      sy[s2][i] = valid ? gy * S.is : -(1 << 20);
+      sx[s2][i] = gx * S.is;
+      sbase[s2][i] = ((b * S.H + gy * S.is) * S.W + gx * S.is) * S.stride;
     }
+  }
+  // weight rows: 32-bit offsets of this thread's chunk column (K offset added per step)
+  int wrow[BCH];
+#pragma unroll
+  for (int i = 0; i < BCH; ++i) {
+    const int n = n0 + (tid >> 3) + 32 * i;
+    wrow[i] = n < a.N ? n * cl.Kpad + kc * 8 : -1;
   }
   const __bf16* wt = a.wt + cl.wofs;
   const int nk = cl.Kpad / EBK;
 
-  __syncthreads();  // s_tab
+  __syncthreads();  // s_tab, s_out
 
   u32x4 ra[ACH], rb[BCH];
   auto load = [&](int k0) __attribute__((always_inline)) {
@@ -220,26 +240,34 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
 #pragma unroll
       for (int i = 0; i < ACH; ++i) ra[i] = u32x4{0, 0, 0, 0};
     } else {
-      const int dy = (ent & 0xff) - 128, dx = ((ent >> 8) & 0xff) - 128;
-      const int sidx = (ent >> 16) & 1, c = ent >> 17;
-      const EncSrc& S0 = a.src[0];
-      const EncSrc& S1 = a.src[1];
-      const __bf16* sp = sidx ? S1.ptr : S0.ptr;
-      const int sst = sidx ? S1.stride : S0.stride;
-      const int sH = sidx ? S1.H : S0.H, sW = sidx ? S1.W : S0.W, sis = sidx ? S1.is : S0.is;
-      const long img0 = (long)b * sH * sW;
+      const int dy = (ent & 0xff) - 128, dx = ((ent >> 8) & 0xff) - 128, c = ent >> 17;
+      if constexpr (NSRC == 1) {
+        const EncSrc& S = a.src[0];
+        const int tapoff = (dy * S.W + dx) * S.stride + c;
 #pragma unroll
-      for (int i = 0; i < ACH; ++i) {
-        const int y = ry[i] * sis + dy, x = rx[i] * sis + dx;
-        const bool ok = (unsigned)y < (unsigned)sH && (unsigned)x < (unsigned)sW;
-        ra[i] = ok ? *reinterpret_cast<const u32x4*>(sp + (img0 + (long)y * sW + x) * sst + c) : u32x4{0, 0, 0, 0};
+        for (int i = 0; i < ACH; ++i) {
+          const bool ok = (unsigned)(sy[0][i] + dy) < (unsigned)S.H && (unsigned)(sx[0][i] + dx) < (unsigned)S.W;
+          ra[i] = ok ? *reinterpret_cast<const u32x4*>(S.ptr + (sbase[0][i] + tapoff)) : u32x4{0, 0, 0, 0};
+        }
+      } else {
+        const int sidx = (ent >> 16) & 1;
+        const EncSrc& S0 = a.src[0];
+        const EncSrc& S1 = a.src[1];
+        const __bf16* sp = sidx ? S1.ptr : S0.ptr;
+        const int sH = sidx ? S1.H : S0.H, sW = sidx ? S1.W : S0.W;
+        const int tapoff = (dy * sW + dx) * (sidx ? S1.stride : S0.stride) + c;
+#pragma unroll
+        for (int i = 0; i < ACH; ++i) {
+          const int y = (sidx ? sy[1][i] : sy[0][i]) + dy, x = (sidx ? sx[1][i] : sx[0][i]) + dx;
+          const bool ok = (unsigned)y < (unsigned)sH && (unsigned)x < (unsigned)sW;
+          ra[i] = ok ? *reinterpret_cast<const u32x4*>(sp + ((sidx ? sbase[1][i] : sbase[0][i]) + tapoff))
+                     : u32x4{0, 0, 0, 0};
+        }
       }
     }
 #pragma unroll
-    for (int i = 0; i < BCH; ++i) {
-      const int n = n0 + (tid >> 3) + 32 * i;
-      rb[i] = n < a.N ? *reinterpret_cast<const u32x4*>(wt + (long)n * cl.Kpad + k0 + kc * 8) : u32x4{0, 0, 0, 0};
-    }
+    for (int i = 0; i < BCH; ++i)
+      rb[i] = wrow[i] >= 0 ? *reinterpret_cast<const u32x4*>(wt + (wrow[i] + k0)) : u32x4{0, 0, 0, 0};
   };
   auto store = [&](int buf) __attribute__((always_inline)) {
     __bf16* sA = smem + buf * STAGE;
@@ -362,9 +390,7 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
     const int rl = ch / CPR, cc = ch - (ch / CPR) * CPR;
     const int n = n0 + cc * 8;
     if (rl >= rows || n >= a.N) continue;
-    const int q = q0 + rl;
-    const int gy = q / cl.Gw, gx = q - (q / cl.Gw) * cl.Gw;
-    const long pix = ((long)b * a.Ho + gy * a.os + cl.oy0) * a.Wo + gx * a.os + cl.ox0;
+    const long pix = s_out[rl];
     float v[8];
     const f32x4 lo = *reinterpret_cast<const f32x4*>(stile + rl * (BN + 4) + cc * 8);
     const f32x4 hi = *reinterpret_cast<const f32x4*>(stile + rl * (BN + 4) + cc * 8 + 4);
@@ -467,31 +493,49 @@ __global__ __launch_bounds__(256) void enc_wgrad_kernel(const EncWgradArgs a) {
     kx = tap - ky * a.KW;
   }
   const int HoWo = a.Ho * a.Wo;
-  const bool do_db = a.dbslab != nullptr && tn == 0;
+  const bool do_db = a.dbslab != nullptr && tn == 0;  // (HoWo: walker initialisation)
   float dbacc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) dbacc[e] = 0.f;
 
+  // pixel walkers of this thread's im2col rows (advanced by 64 pixels per step, no divisions
+  // in the loop); 32-bit element offsets (host checks every tensor is < 2^31 elements)
+  int wp[BI], wb[BI], wy[BI], wx[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int p = (int)pbeg + (tid >> 3) + 32 * i;
+    wp[i] = p;
+    wb[i] = p / HoWo;
+    const int rem = p - wb[i] * HoWo;
+    wy[i] = rem / a.Wo;
+    wx[i] = rem - wy[i] * a.Wo;
+  }
+  const int kyp = ky - a.pad, kxp = kx - a.pad;
+  const int pe = (int)pend;
+  const int aoff = m0 + ca * 8;
+
   u32x4 ra[AI], rb[BI];
   auto load = [&](int step) __attribute__((always_inline)) {
-    const long p0 = pbeg + (long)step * 64;
+    const int p0 = (int)pbeg + step * 64;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
-      const long p = p0 + tid / ACPR + ARP * i;
-      ra[i] = (a_ok && p < pend) ? *reinterpret_cast<const u32x4*>(a.dy + p * a.dy_stride + m0 + ca * 8)
-                                 : u32x4{0, 0, 0, 0};
+      const int p = p0 + tid / ACPR + ARP * i;
+      ra[i] = (a_ok && p < pe) ? *reinterpret_cast<const u32x4*>(a.dy + (p * a.dy_stride + aoff)) : u32x4{0, 0, 0, 0};
     }
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
-      const long p = p0 + (tid >> 3) + 32 * i;
-      rb[i] = u32x4{0, 0, 0, 0};
-      if (b_ok && p < pend) {
-        const int bb = (int)(p / HoWo);
-        const int rem = (int)(p - (long)bb * HoWo);
-        const int oy = rem / a.Wo, ox = rem - (rem / a.Wo) * a.Wo;
-        const int y = oy * a.stride + ky - a.pad, x = ox * a.stride + kx - a.pad;
-        if ((unsigned)y < (unsigned)a.Hx && (unsigned)x < (unsigned)a.Wx)
-          rb[i] = *reinterpret_cast<const u32x4*>(a.x + (((long)bb * a.Hx + y) * a.Wx + x) * a.xstride + c);
+      const int y = wy[i] * a.stride + kyp, x = wx[i] * a.stride + kxp;
+      const bool ok = b_ok && wp[i] < pe && (unsigned)y < (unsigned)a.Hx && (unsigned)x < (unsigned)a.Wx;
+      rb[i] = ok ? *reinterpret_cast<const u32x4*>(a.x + (((wb[i] * a.Hx + y) * a.Wx + x) * a.xstride + c))
+                 : u32x4{0, 0, 0, 0};
+      wp[i] += 64;
+      wx[i] += 64;
+      while (wx[i] >= a.Wo) {
+        wx[i] -= a.Wo;
+        if (++wy[i] >= a.Ho) {
+          wy[i] = 0;
+          ++wb[i];
+        }
       }
     }
   };
@@ -947,22 +991,29 @@ hipError_t launch_enc_pack(const EncConvArgs& a, int rows, void* out, hipStream_
   return hipGetLastError();
 }
 
-hipError_t launch_enc_conv(const EncConvArgs& a, int nblocks, hipStream_t s) {
-  const int BN = enc_tile_bn(a.N);
-  switch (BN) {
+template <int NSRC>
+void launch_enc_conv_n(const EncConvArgs& a, int nblocks, hipStream_t s) {
+  switch (enc_tile_bn(a.N)) {
     case 128:
-      hipLaunchKernelGGL((enc_conv_kernel<128, 128, 2, 2>), dim3(nblocks), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((enc_conv_kernel<128, 128, 2, 2, NSRC>), dim3(nblocks), dim3(256), 0, s, a);
       break;
     case 96:
-      hipLaunchKernelGGL((enc_conv_kernel<128, 96, 4, 1>), dim3(nblocks), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((enc_conv_kernel<128, 96, 4, 1, NSRC>), dim3(nblocks), dim3(256), 0, s, a);
       break;
     case 64:
-      hipLaunchKernelGGL((enc_conv_kernel<128, 64, 2, 2>), dim3(nblocks), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((enc_conv_kernel<128, 64, 2, 2, NSRC>), dim3(nblocks), dim3(256), 0, s, a);
       break;
     default:
-      hipLaunchKernelGGL((enc_conv_kernel<128, 32, 4, 1>), dim3(nblocks), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((enc_conv_kernel<128, 32, 4, 1, NSRC>), dim3(nblocks), dim3(256), 0, s, a);
       break;
   }
+}
+
+hipError_t launch_enc_conv(const EncConvArgs& a, int nblocks, hipStream_t s) {
+  if (a.src[1].ptr != nullptr)
+    launch_enc_conv_n<2>(a, nblocks, s);
+  else
+    launch_enc_conv_n<1>(a, nblocks, s);
   return hipGetLastError();
 }
 
