@@ -102,7 +102,7 @@ hipError_t launch_enc_norm_bwd(const NormBwdArgs& a, hipStream_t s);
 namespace {
 
 constexpr int kBM = 128;  // conv M tile (pixels), fixed for every encoder conv
-constexpr int kNormChunks = 32;
+constexpr int kNormChunks = 64;
 
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 

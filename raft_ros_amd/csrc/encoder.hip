@@ -625,43 +625,58 @@ __global__ __launch_bounds__(256) void enc_wgrad_kernel(const EncWgradArgs a) {
 }
 
 // Sum the split slabs in a fixed order into the fp32 parameter gradient (any strides).
-// Threads walk (co, tap, ci) so slab reads are coalesced.
+// Block = 16 outputs x 16 split lanes (outputs fastest: 64-byte coalesced slab rows); each
+// lane sums every 16th split with 4 independent loads in flight, the 16 lane sums are
+// combined in a fixed order -- the sum is latency-bound for small weights, so the split
+// dimension is spread over threads.  Outputs walk (co, tap, ci).
 __global__ __launch_bounds__(256) void enc_wgrad_reduce_kernel(const float* __restrict__ slab, int nsplit, int Npad,
                                                                int Kpad, const float* __restrict__ dbslab,
                                                                float* __restrict__ dw, long s0, long s1, long s2,
                                                                long s3, int Cout, int Cin, int Cx, int KW, int taps,
                                                                float* __restrict__ db, int accumulate) {
+  __shared__ float red[16][17];
+  const int o = threadIdx.x & 15, sub = threadIdx.x >> 4;
   const long total = (long)Cout * taps * Cin;
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  const long nout = total + (db != nullptr ? Cout : 0);  // bias gradients ride as extra outputs
+  const long e = (long)blockIdx.x * 16 + o;
+  float s = 0.f;
+  const float* src = nullptr;
+  long sstride = 0;
+  int co = 0, ci = 0, tap = 0;
   if (e < total) {
-    const int ci = (int)(e % Cin);
+    ci = (int)(e % Cin);
     const long r = e / Cin;
-    const int tap = (int)(r % taps), co = (int)(r / taps);
-    const long k = (long)tap * Cx + ci;
-    // independent loads, 8 in flight per thread (the split sum is latency-, not bandwidth-bound)
-    const float* src = slab + (long)co * Kpad + k;
-    const long sstride = (long)Npad * Kpad;
-    float s = 0.f;
-    int sp = 0;
-    for (; sp + 8 <= nsplit; sp += 8) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = src[(sp + u) * sstride];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
+    tap = (int)(r % taps);
+    co = (int)(r / taps);
+    src = slab + (long)co * Kpad + (long)tap * Cx + ci;
+    sstride = (long)Npad * Kpad;
+  } else if (e < nout && dbslab != nullptr) {
+    src = dbslab + (e - total);
+    sstride = Npad;
+  }
+  if (src != nullptr) {
+    int sp = sub;
+    for (; sp + 48 < nsplit; sp += 64) {
+      const float v0 = src[sp * sstride], v1 = src[(sp + 16) * sstride];
+      const float v2 = src[(sp + 32) * sstride], v3 = src[(sp + 48) * sstride];
+      s += (v0 + v1) + (v2 + v3);
     }
-    for (; sp < nsplit; ++sp) s += src[sp * sstride];
+    for (; sp < nsplit; sp += 16) s += src[sp * sstride];
+  }
+  red[sub][o] = s;
+  __syncthreads();
+  if (sub != 0 || e >= nout) return;
+  float t = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) t += red[k][o];
+  if (e < total) {
     const int ky = tap / KW, kx = tap - (tap / KW) * KW;
     float* d = dw + co * s0 + ci * s1 + ky * s2 + kx * s3;
-    *d = accumulate ? *d + s : s;
-  }
-  if (db != nullptr && blockIdx.x == 0) {
-    for (int co = threadIdx.x; co < Cout; co += 256) {
-      float s = 0.f;  // no slab: the bias feeds a re-centring norm, its gradient is exactly 0
-      if (dbslab != nullptr)
-        for (int sp = 0; sp < nsplit; ++sp) s += dbslab[(long)sp * Npad + co];
-      db[co] = accumulate ? db[co] + s : s;
-    }
+    *d = accumulate ? *d + t : t;
+  } else {
+    // no slab: the bias feeds a re-centring norm, its gradient is exactly 0
+    float* d = db + (e - total);
+    *d = accumulate ? *d + t : t;
   }
 }
 
@@ -832,35 +847,48 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_reduce_kernel(const NormBwdA
       loadf8(c1 + 3 * N + n, mu1);
     }
     const long base = (long)b * a.HW;
-    for (int p = pb + pr; p < pe; p += PPB) {
-      float gv[8], av[8];
-      load8(a.g + (base + p) * N + n, gv);
-      load8(a.a0 + (base + p) * N + n, av);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float dy = (a.relu0 && !(av[e] * sc0[e] + sh0[e] > 0.f)) ? 0.f : gv[e];
-        S[0][e] += dy;
-        S[1][e] += dy * (av[e] - mu0[e]) * rs0[e];
+    // two pixels per iteration: all of their loads are issued before the math
+    for (int p = pb + pr; p < pe; p += 2 * PPB) {
+      const bool two = p + PPB < pe;
+      float gv[2][8], av[2][8], dv[2][8];
+      load8(a.g + (base + p) * N + n, gv[0]);
+      load8(a.a0 + (base + p) * N + n, av[0]);
+      if (a.a1) load8(a.a1 + (base + p) * N + n, dv[0]);
+      if (two) {
+        load8(a.g + (base + p + PPB) * N + n, gv[1]);
+        load8(a.a0 + (base + p + PPB) * N + n, av[1]);
+        if (a.a1) load8(a.a1 + (base + p + PPB) * N + n, dv[1]);
       }
-      if (a.a1) {
-        load8(a.a1 + (base + p) * N + n, av);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          S[2][e] += gv[e];
-          S[3][e] += gv[e] * (av[e] - mu1[e]) * rs1[e];
+          const float dy = (a.relu0 && !(av[u][e] * sc0[e] + sh0[e] > 0.f)) ? 0.f : gv[u][e];
+          S[0][e] += dy;
+          S[1][e] += dy * (av[u][e] - mu0[e]) * rs0[e];
+        }
+        if (a.a1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            S[2][e] += gv[u][e];
+            S[3][e] += gv[u][e] * (dv[u][e] - mu1[e]) * rs1[e];
+          }
         }
       }
     }
   }
   const int nq = a.a1 ? 4 : 2;
   for (int qd = 0; qd < nq; ++qd) {
+    // layout [e][pr][cg]: consecutive lanes (consecutive cg) hit consecutive banks
     if (active)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) red[pr * N + n + e] = S[qd][e];
+      for (int e = 0; e < 8; ++e) red[(e * PPB + pr) * G + cg] = S[qd][e];
     __syncthreads();
     if (tid < N) {
+      const int tc = tid >> 3, te = tid & 7;
       float s = 0.f;
-      for (int k = 0; k < PPB; ++k) s += red[k * N + tid];
+      for (int k = 0; k < PPB; ++k) s += red[(te * PPB + k) * G + tc];
       a.part[(((long)b * a.R + r) * 4 + qd) * N + tid] = s;
     }
     __syncthreads();
@@ -1029,8 +1057,8 @@ hipError_t launch_enc_wgrad(const EncWgradArgs& a, int BM, hipStream_t s) {
 hipError_t launch_enc_wgrad_reduce(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, float* dw,
                                    const long* ws, int Cout, int Cin, int Cx, int KH, int KW, float* db,
                                    bool accumulate, hipStream_t s) {
-  const long total = (long)Cout * KH * KW * Cin;
-  const int blocks = (int)std::max<long>((total + 255) / 256, 1);
+  const long total = (long)Cout * KH * KW * Cin + (db != nullptr ? Cout : 0);
+  const int blocks = (int)std::max<long>((total + 15) / 16, 1);
   hipLaunchKernelGGL(enc_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, slab, nsplit, Npad, Kpad, dbslab, dw,
                      ws[0], ws[1], ws[2], ws[3], Cout, Cin, Cx, KW, KH * KW, db, accumulate ? 1 : 0);
   return hipGetLastError();
