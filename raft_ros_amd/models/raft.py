@@ -30,7 +30,7 @@ import torch.nn as nn
 
 from ..ops import CorrPyramid, LocalCorrPyramid, convex_upsample, upflow8
 from ..ops import encoder as encoder_native
-from ..ops import update_fused
+from ..ops import update_fused, update_fused_small
 from ..ops._ext import use_native
 from ..ops.reference import coords_grid
 from .extractor import BasicEncoder, SmallEncoder
@@ -183,7 +183,8 @@ class RAFT(nn.Module):
     # ------------------------------------------------------------------ fused (HIP) update path
     def _use_fused(self, image1, amp: bool) -> bool:
         return (amp and self.amp_dtype == torch.bfloat16 and _arg(self.args, "fused_update", True)
-                and update_fused.supported(self.update_block) and use_native(image1))
+                and (update_fused.supported(self.update_block) or update_fused_small.supported(self.update_block))
+                and use_native(image1))
 
     def _forward_fused(self, corr_fn, net, inp, coords0, coords1, iters: int, test_mode: bool):
         """Refinement loop on the fused HIP step (raft_ros_amd/ops/update_fused.py): lookup,
@@ -191,19 +192,21 @@ class RAFT(nn.Module):
         iteration, weight gradients batched over all iterations; same math as the loop
         above."""
         dense = isinstance(corr_fn, CorrPyramid)
-        upd = update_fused.FusedBasicUpdate(self.update_block, inp, iters,
-                                            pyramid=corr_fn.state if dense else None)
+        small = update_fused_small.supported(self.update_block)
+        fused = update_fused_small.FusedSmallUpdate if small else update_fused.FusedBasicUpdate
+        pad = update_fused_small.CORR_PAD if small else update_fused.CORR_PAD
+        upd = fused(self.update_block, inp, iters, pyramid=corr_fn.state if dense else None)
         flow_predictions = []
         flow_up = None
         for t in range(iters):
             if dense:
                 net, flow_up, coords1 = upd.step(t, net, coords1, ptoken=corr_fn.token)
             elif getattr(corr_fn, "mfma", False):  # features already in the fused layout
-                corr = corr_fn.lookup_padded(coords1.detach(), update_fused.CORR_PAD)
+                corr = corr_fn.lookup_padded(coords1.detach(), pad)
                 net, flow_up, coords1 = upd.step(t, net, coords1, corr=corr)
             else:
                 c = corr_fn(coords1.detach(), out_dtype=torch.bfloat16).permute(0, 2, 3, 1)
-                corr = torch.nn.functional.pad(c, (0, update_fused.CORR_PAD - c.shape[-1]))
+                corr = torch.nn.functional.pad(c, (0, pad - c.shape[-1]))
                 net, flow_up, coords1 = upd.step(t, net, coords1, corr=corr)
             flow_predictions.append(flow_up)
         if test_mode:

@@ -33,5 +33,20 @@ def convex_upsample(flow: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
     return ref.convex_upsample(flow.float(), mask.float())
 
 
+class _Upflow8(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, flow):
+        ctx.hw = flow.shape[-2:]
+        return ops().upflow8(flow.float().contiguous())
+
+    @staticmethod
+    def backward(ctx, gout):
+        H, W = ctx.hw
+        return ops().upflow8_backward(gout.float().contiguous(), H, W, None)
+
+
 def upflow8(flow: torch.Tensor, mode: str = "bilinear") -> torch.Tensor:
+    """8x bilinear (align_corners) upsampling of a (B, 2, H, W) flow, times 8 (HIP on GPU)."""
+    if mode == "bilinear" and use_native(flow):
+        return _Upflow8.apply(flow)
     return ref.upflow8(flow, mode)

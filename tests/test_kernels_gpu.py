@@ -279,3 +279,26 @@ def test_local_corr_mfma_matches_dense_reference(cuda, jitter):
     # padded fused layout: zeros beyond the 324 taps
     padded = lc.lookup_padded(coords, 328)
     assert padded.shape == (B, H, W, 328) and (padded[..., 324:] == 0).all()
+
+
+@pytest.mark.parametrize("hw", [(1, 1), (5, 7), (46, 62)])
+def test_upflow8_matches_reference_fwd_bwd(hw):
+    from raft_ros_amd.ops import reference as ref
+    from raft_ros_amd.ops._ext import ops
+
+    cuda = torch.device("cuda", 0)
+    H, W = hw
+    g = torch.Generator(device=cuda).manual_seed(3)
+    flow = torch.randn(2, 2, H, W, device=cuda, generator=g)
+    out = ops().upflow8(flow)
+    fr = flow.clone().requires_grad_(True)
+    r = ref.upflow8(fr)
+    torch.testing.assert_close(out, r, rtol=1e-5, atol=2e-4)  # fma contraction vs ATen's order
+    go = torch.randn(r.shape, device=cuda, generator=g)
+    r.backward(go)
+    rows = torch.empty(2 * H * W, 8, device=cuda, dtype=torch.bfloat16)
+    d = ops().upflow8_backward(go, H, W, rows)
+    torch.testing.assert_close(d, fr.grad, rtol=1e-4, atol=1e-3)
+    got = rows.float().reshape(2, H, W, 8)
+    torch.testing.assert_close(got[..., :2], fr.grad.permute(0, 2, 3, 1), rtol=1e-2, atol=1e-2)
+    assert (got[..., 2:] == 0).all()

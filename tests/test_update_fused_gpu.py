@@ -1,4 +1,10 @@
-"""Fused HIP update block vs the PyTorch (MIOpen) update block: forward flows and all gradients."""
+"""Fused HIP path (native encoders + fused update steps) vs the fp32 module path.
+
+Oracle: the same RAFT in fp32 (``mixed_precision=False``: PyTorch/MIOpen convs, fp32-
+faithful correlation).  Tolerance: the error of the module path's own bf16 autocast
+(MIOpen, ``fused_update=False, native_encoder=False``) against that oracle -- the fused
+bf16 kernels must be at least about as close to fp32 as PyTorch's bf16 AMP is.
+"""
 from argparse import Namespace
 
 import pytest
@@ -13,48 +19,49 @@ def _rel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
 
 
-@pytest.mark.parametrize("shape", [(2, 128, 192), (1, 136, 200)])
-def test_fused_update_matches_torch_path(cuda, shape):
-    from raft_ros_amd.data.synthetic import synthetic_batch
+def _run(m, batch, iters):
     from raft_ros_amd.train.loss import sequence_loss
+
+    i1, i2, flow, valid = batch
+    m.zero_grad()
+    preds = m(i1, i2, iters=iters)
+    loss, _ = sequence_loss(preds, flow, valid)
+    loss.backward()
+    return preds, {n: p.grad.float().clone() for n, p in m.named_parameters() if p.grad is not None}
+
+
+@pytest.mark.parametrize("small,shape", [(False, (2, 128, 192)), (False, (1, 136, 200)), (True, (2, 128, 192))])
+def test_fused_path_matches_fp32_module(cuda, small, shape):
+    from raft_ros_amd.data.synthetic import synthetic_batch
 
     B, H, W = shape
     torch.manual_seed(0)
-    ref = RAFT(Namespace(small=False, mixed_precision=True, amp_dtype="bf16", fused_update=False)).to(cuda)
-    fused = RAFT(Namespace(small=False, mixed_precision=True, amp_dtype="bf16", fused_update=True)).to(cuda)
-    fused.load_state_dict(ref.state_dict())
-    ref.train(); fused.train()
-    ref.freeze_bn(); fused.freeze_bn()  # identical BN statistics in both runs
-    i1, i2, flow, valid = synthetic_batch(B, H, W, max_disp=6, seed=1, device=cuda)
-    outs = {}
-    for name, m in (("ref", ref), ("fused", fused)):
-        m.zero_grad()
-        preds = m(i1, i2, iters=3)
-        loss, _ = sequence_loss(preds, flow, valid)
-        loss.backward()
-        outs[name] = (preds, {n: p.grad for n, p in m.named_parameters() if p.grad is not None})
-    (pr, gr), (pf, gf) = outs["ref"], outs["fused"]
-    for a, b in zip(pf, pr):
-        assert _rel(a, b) < 3e-2, _rel(a, b)
+    mk = lambda **kw: RAFT(Namespace(small=small, **kw)).to(cuda)  # noqa: E731
+    f32 = mk(mixed_precision=False)
+    amp = mk(mixed_precision=True, amp_dtype="bf16", fused_update=False, native_encoder=False)
+    fused = mk(mixed_precision=True, amp_dtype="bf16")
+    for m in (amp, fused):
+        m.load_state_dict(f32.state_dict())
+    for m in (f32, amp, fused):
+        m.train()
+        m.freeze_bn()  # identical BN statistics in every run
+    batch = synthetic_batch(B, H, W, max_disp=6, seed=1, device=cuda)
+    pr, gr = _run(f32, batch, 3)
+    pa, ga = _run(amp, batch, 3)
+    pf, gf = _run(fused, batch, 3)
+    for a, m, r in zip(pf, pa, pr):
+        assert _rel(a, r) <= 1.5 * _rel(m, r) + 1e-2, (_rel(a, r), _rel(m, r))
     assert set(gf) == set(gr), set(gr) ^ set(gf)
-    # parameters whose true gradient vanishes (biases feeding InstanceNorm) are pure noise:
-    # compare every tensor against the norm of its module group's gradient instead
-    groups = {}
-    for n in gr:
-        groups.setdefault(n.split(".")[0], []).append(n)
     bad = {}
-    # conv biases directly followed by InstanceNorm have an identically-zero true gradient
-    noise = {n for n in gr if n.startswith("fnet.") and n.endswith(".bias") and not n.startswith("fnet.conv2")}
-    for grp, names in groups.items():
-        names = [n for n in names if n not in noise]
-        if not names:
+    for n in gr:
+        ref_norm = gr[n].norm().item()
+        floor = (ga[n] - gr[n]).norm().item()
+        err = (gf[n] - gr[n]).norm().item()
+        # conv biases in front of InstanceNorm: the true gradient is 0 (fused writes exactly 0)
+        if ref_norm < 1e-6:
+            if gf[n].abs().max().item() > 1e-3:
+                bad[n] = ("nonzero", gf[n].abs().max().item())
             continue
-        scale = max(torch.stack([gr[n].float().norm() for n in names]).max().item(), 1e-12)
-        for n in names:
-            err = (gf[n].float() - gr[n].float()).norm().item()
-            # encoder grads pass through the bf16 corr GEMM backward and 10+ bf16 layers in both
-            # paths; the update block itself is held to 10 %
-            tol = 0.1 if grp == "update_block" else 0.25
-            if err > tol * max(gr[n].float().norm().item(), 1e-2 * scale):
-                bad[n] = (err, gr[n].float().norm().item())
+        if err > 1.5 * floor + 0.02 * ref_norm:
+            bad[n] = (err / ref_norm, floor / ref_norm)
     assert not bad, bad
