@@ -87,3 +87,42 @@ def test_graphed_inference_matches_eager(cuda, small, amp):
             torch.testing.assert_close(up, ref_up, rtol=1e-3, atol=1e-3)
             torch.testing.assert_close(low, ref_low, rtol=1e-3, atol=1e-3)
     assert runner.num_graphs == 1
+
+
+def _epe(a, b):
+    return (a.float() - b.float()).norm(dim=1).mean().item()
+
+
+@pytest.mark.parametrize("iters", [12, 32])
+def test_bench_resolution_epe_vs_fp32_reference(cuda, iters):
+    """368x496 (BASELINE config #2 resolution), test_mode flows after 12 / 32 iterations.
+
+    * native fp32 path (mixed_precision=False: fp32-faithful split-bf16 correlation, native
+      lookup / upsampling) vs the reference op sequence in fp32: EPE delta <= 0.01 px;
+    * native bf16 path (native encoders + fused update kernels) vs the same fp32 oracle:
+      bounded by 3x the delta of PyTorch's own bf16 autocast (module path, MIOpen) and by
+      5 % of the mean flow magnitude.  The measured deltas are printed (pytest -s).
+    """
+    torch.manual_seed(0)
+    f32 = RAFT(Namespace(small=False, mixed_precision=False)).to(cuda).eval()
+    bf = RAFT(Namespace(small=False, mixed_precision=True, amp_dtype="bf16")).to(cuda).eval()
+    amp = RAFT(Namespace(small=False, mixed_precision=True, amp_dtype="bf16", fused_update=False,
+                         native_encoder=False)).to(cuda).eval()
+    for m in (bf, amp):
+        m.load_state_dict(f32.state_dict())
+    i1, i2, _, _ = _pair(cuda, B=1, H=368, W=496, seed=5)
+    with torch.no_grad():
+        _ext.set_backend("reference")
+        try:
+            _, up_ref = f32(i1, i2, iters=iters, test_mode=True)
+        finally:
+            _ext.set_backend("native")
+        _, up_f32 = f32(i1, i2, iters=iters, test_mode=True)
+        _, up_bf = bf(i1, i2, iters=iters, test_mode=True)
+        _, up_amp = amp(i1, i2, iters=iters, test_mode=True)
+    mag = up_ref.norm(dim=1).mean().item()
+    d32, dbf, damp = _epe(up_f32, up_ref), _epe(up_bf, up_ref), _epe(up_amp, up_ref)
+    print(f"\niters={iters} mean|flow|={mag:.3f}  EPE delta: native fp32 {d32:.5f}  native bf16 {dbf:.4f}  "
+          f"torch bf16 autocast {damp:.4f}")
+    assert d32 <= 0.01, d32
+    assert dbf <= max(3 * damp, 1e-3) and dbf <= 0.05 * max(mag, 1.0), (dbf, damp, mag)
