@@ -65,7 +65,9 @@ struct LocalCorrArgs {
   int gout_bf16;
   float* g1;
   float* g2;  // layout must match local_corr_mfma.hip
+  long long* g2fix;
 };
+hipError_t launch_fixed_to_float(const long long* in, float* out, long n, hipStream_t s);
 hipError_t launch_local_corr_mfma(const LocalCorrArgs& a, bool backward, hipStream_t s);
 hipError_t launch_pyramid_unpool(const UnpoolArgs& u, hipStream_t s);
 hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int W, hipStream_t s);
@@ -109,7 +111,7 @@ hipError_t launch_local_corr_fwd(const void* f1, const void* f2, int dtype, cons
                                  float* out, int B, int H1, int W1, int H2, int W2, int C, int r,
                                  float scale, hipStream_t s);
 hipError_t launch_local_corr_bwd(const void* f1, const void* f2, int dtype, const float* coords,
-                                 const float* gout, float* g1, float* g2, int B, int H1, int W1,
+                                 const float* gout, float* g1, float* g2, long long* g2fix, int B, int H1, int W1,
                                  int H2, int W2, int C, int r, float scale, hipStream_t s);
 
 hipError_t launch_gru_gates_fwd(int dtype, const void* zr, const void* h, void* z, void* rh, long npix,
@@ -544,7 +546,7 @@ at::Tensor local_corr(const at::Tensor& f1, const at::Tensor& f2, const at::Tens
 std::tuple<at::Tensor, at::Tensor> local_corr_backward(const at::Tensor& f1, const at::Tensor& f2,
                                                        const at::Tensor& coords,
                                                        const at::Tensor& grad, int64_t radius,
-                                                       double scale) {
+                                                       double scale, bool deterministic) {
   check_local(f1, f2, coords);
   const long B = f1.size(0), H1 = f1.size(1), W1 = f1.size(2), C = f1.size(3);
   const long H2 = f2.size(1), W2 = f2.size(2);
@@ -555,10 +557,13 @@ std::tuple<at::Tensor, at::Tensor> local_corr_backward(const at::Tensor& f1, con
   const c10::DeviceGuard guard(f1.device());
   auto g1 = at::empty({B, H1, W1, C}, f1.options().dtype(at::kFloat));
   auto g2 = at::zeros({B, H2, W2, C}, f1.options().dtype(at::kFloat));
+  at::Tensor fix = deterministic ? at::zeros({B, H2, W2, C}, f1.options().dtype(at::kLong)) : at::Tensor();
+  long long* fp = deterministic ? reinterpret_cast<long long*>(fix.data_ptr<int64_t>()) : nullptr;
   HIP_OK(launch_local_corr_bwd(f1.data_ptr(), f2.data_ptr(), dtype_code(f1.scalar_type()),
                                coords.data_ptr<float>(), g.data_ptr<float>(), g1.data_ptr<float>(),
-                               g2.data_ptr<float>(), B, H1, W1, H2, W2, C, static_cast<int>(radius),
+                               g2.data_ptr<float>(), fp, B, H1, W1, H2, W2, C, static_cast<int>(radius),
                                static_cast<float>(scale), cur_stream()));
+  if (deterministic) HIP_OK(launch_fixed_to_float(fp, g2.data_ptr<float>(), g2.numel(), cur_stream()));
   return {g1, g2};
 }
 
@@ -608,7 +613,7 @@ void local_corr_mfma(const at::Tensor& f1, const at::Tensor& f2, const at::Tenso
 
 void local_corr_mfma_backward(const at::Tensor& f1, const at::Tensor& f2, const at::Tensor& coords,
                               at::IntArrayRef segs, int64_t radius, double scale, const at::Tensor& gout,
-                              const at::Tensor& g1, const at::Tensor& g2) {
+                              const at::Tensor& g1, const at::Tensor& g2, bool deterministic) {
   LocalCorrArgs a = local_mfma_args(f1, f2, coords, segs, radius, scale);
   const long win = (2 * radius + 1) * (2 * radius + 1);
   check_gpu(gout, "gout");
@@ -622,7 +627,11 @@ void local_corr_mfma_backward(const at::Tensor& f1, const at::Tensor& f2, const 
   a.gout = gout.data_ptr(); a.gstride = gout.stride(0); a.gout_bf16 = gout.scalar_type() == at::kBFloat16;
   a.g1 = g1.data_ptr<float>(); a.g2 = g2.data_ptr<float>();
   const c10::DeviceGuard guard(f1.device());
+  // deterministic: 32.32 fixed-point integer atomics (order-independent), then added into g2
+  at::Tensor fix = deterministic ? at::zeros(g2.sizes(), g2.options().dtype(at::kLong)) : at::Tensor();
+  a.g2fix = deterministic ? reinterpret_cast<long long*>(fix.data_ptr<int64_t>()) : nullptr;
   HIP_OK(launch_local_corr_mfma(a, true, cur_stream()));
+  if (deterministic) HIP_OK(launch_fixed_to_float(a.g2fix, a.g2, g2.numel(), cur_stream()));
 }
 
 // ---------------------------------------------------------------- fused GRU gates
@@ -1119,10 +1128,10 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("local_corr_mfma(Tensor f1, Tensor f2, Tensor coords, int[] segs, int radius, float scale, Tensor(a!) out) -> ()");
   m.def(
       "local_corr_mfma_backward(Tensor f1, Tensor f2, Tensor coords, int[] segs, int radius, float scale, Tensor gout, "
-      "Tensor(a!) g1, Tensor(b!) g2) -> ()");
+      "Tensor(a!) g1, Tensor(b!) g2, bool deterministic=False) -> ()");
   m.def(
       "local_corr_backward(Tensor fmap1, Tensor fmap2, Tensor coords, Tensor grad, int radius, float "
-      "scale) -> (Tensor, Tensor)");
+      "scale, bool deterministic=False) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {

@@ -51,6 +51,15 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 
 inline int cdiv(long a, long b) { return static_cast<int>((a + b - 1) / b); }
 
+// Deterministic scatter-add: contributions are rounded to 32.32 fixed point and added with
+// 64-bit integer atomics, which are associative -- the sum no longer depends on the order the
+// waves arrive in (torch.use_deterministic_algorithms).  Resolution 2^-32, range +-2^31.
+constexpr double kFixScale = 4294967296.0;
+__device__ __forceinline__ void fixed_atomic_add(long long* p, float v) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(p),
+            static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v) * kFixScale)));
+}
+
 }  // namespace raft_amd
 
 #define RAFT_HIP_CHECK(expr)                                                   \

@@ -26,6 +26,8 @@
 // level gradients are folded to level 0 afterwards (pyramid_unpool).
 #include "common.h"
 
+#include <algorithm>
+
 namespace raft_amd {
 
 struct LocalCorrArgs {
@@ -47,6 +49,7 @@ struct LocalCorrArgs {
   int gout_bf16;
   float* g1;  // (B*H*W, C) fp32
   float* g2;  // (B, R, C) fp32, accumulated (atomics)
+  long long* g2fix;  // non-null: deterministic mode, 32.32 fixed-point accumulator like g2
 };
 
 namespace {
@@ -371,9 +374,16 @@ __global__ __launch_bounds__(256) void local_corr_mfma_bwd_kernel(const LocalCor
             const int n = chunk * WCAP + wave * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
             if (n >= area) continue;
             const int wy = n / g.bw, wx = n - (n / g.bw) * g.bw;
-            float* dst = g2l + ((long)(g.by0 + wy) * a.w[l] + g.bx0 + wx) * a.C + s * KC + (lane & 31);
+            const long di = ((long)(g.by0 + wy) * a.w[l] + g.bx0 + wx) * a.C + s * KC + (lane & 31);
+            if (a.g2fix != nullptr) {
+              long long* dst = a.g2fix + (g2l - a.g2) + di;
 #pragma unroll
-            for (int j = 0; j < 2; ++j) atomicAdd(dst + j * 32, acc2[i][j][e]);
+              for (int j = 0; j < 2; ++j) fixed_atomic_add(dst + j * 32, acc2[i][j][e]);
+            } else {
+              float* dst = g2l + di;
+#pragma unroll
+              for (int j = 0; j < 2; ++j) atomicAdd(dst + j * 32, acc2[i][j][e]);
+            }
           }
         __syncthreads();
       }
@@ -394,7 +404,20 @@ __global__ __launch_bounds__(256) void local_corr_mfma_bwd_kernel(const LocalCor
   }
 }
 
+__global__ __launch_bounds__(256) void fixed_to_float_kernel(const long long* __restrict__ in, float* __restrict__ out,
+                                                             long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    out[i] += static_cast<float>(static_cast<double>(in[i]) / kFixScale);
+}
+
 }  // namespace
+
+hipError_t launch_fixed_to_float(const long long* in, float* out, long n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const long blocks = std::min<long>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(fixed_to_float_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, out, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_local_corr_mfma(const LocalCorrArgs& a, bool backward, hipStream_t s) {
   if (a.r > 4 || a.C % KC != 0 || a.C > 256 || a.levels < 1 || a.levels > 4) return hipErrorInvalidValue;

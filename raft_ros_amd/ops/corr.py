@@ -229,7 +229,8 @@ class _LocalCorr(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         f1, f2, coords = ctx.saved_tensors
-        g1, g2 = ops().local_corr_backward(f1, f2, coords, gout, ctx.radius, ctx.scale)
+        g1, g2 = ops().local_corr_backward(f1, f2, coords, gout, ctx.radius, ctx.scale,
+                                           torch.are_deterministic_algorithms_enabled())
         return g1.to(f1.dtype), g2.to(f2.dtype), None, None, None
 
 
@@ -255,7 +256,8 @@ class _LocalCorrMFMA(torch.autograd.Function):
         g1 = torch.empty(st.f1.shape, device=gout.device)
         g2 = torch.zeros(st.f2cat.shape, device=gout.device)
         gout = gout.reshape(st.f1.shape[0], -1).contiguous()
-        ops().local_corr_mfma_backward(st.f1, st.f2cat, coords, st.segs, st.radius, st.scale, gout, g1, g2)
+        ops().local_corr_mfma_backward(st.f1, st.f2cat, coords, st.segs, st.radius, st.scale, gout, g1, g2,
+                                       torch.are_deterministic_algorithms_enabled())
         B, C, H, W = st.shape
         d2 = ops().pyramid_unpool(g2, H, W, st.segs)  # level gradients -> level 0 (adjoint pools)
         d1 = g1.view(B, H, W, C).permute(0, 3, 1, 2)

@@ -60,16 +60,26 @@ def init_distributed(backend: str | None = None, device_type: str | None = None)
     return DistInfo(rank, world, local, device)
 
 
-def wrap_model(model: torch.nn.Module, info: DistInfo, bucket_cap_mb: float = 32.0, static_graph: bool = True):
+def wrap_model(model: torch.nn.Module, info: DistInfo, bucket_cap_mb: float = 32.0, static_graph: bool = True,
+               bf16_grads: bool = False):
     """DDP wrapper sized for xGMI: the whole RAFT-base gradient (21 MB fp32) fits in one
     32 MB bucket, i.e. one ring all-reduce per step, launched as soon as backward has
-    produced it (earlier buckets overlap with the rest of backward)."""
+    produced it (earlier buckets overlap with the rest of backward).
+
+    ``bf16_grads``: register the bf16 compression hook -- buckets are cast to bf16 for the
+    ring all-reduce and back to fp32 (halves the bytes over the per-link-bound xGMI ring;
+    the mean is exact up to bf16 rounding of each rank's contribution)."""
     if not info.distributed:
         return model
     kw = dict(bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True, static_graph=static_graph)
     if info.device.type == "cuda":
         kw["device_ids"] = [info.device.index]
-    return torch.nn.parallel.DistributedDataParallel(model, **kw)
+    net = torch.nn.parallel.DistributedDataParallel(model, **kw)
+    if bf16_grads:
+        from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
+
+        net.register_comm_hook(None, default_hooks.bf16_compress_hook)
+    return net
 
 
 def all_reduce_mean(values: Dict[str, float], info: DistInfo) -> Dict[str, float]:

@@ -11,7 +11,7 @@ import torch.multiprocessing as mp
 from raft_ros_amd.parallel import ddp
 
 
-def _worker(rank, world, port, tmpdir):
+def _worker(rank, world, port, tmpdir, bf16=False):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     torch.set_num_threads(2)
@@ -22,7 +22,7 @@ def _worker(rank, world, port, tmpdir):
     info = ddp.init_distributed(device_type="cpu")
     torch.manual_seed(0)
     model = RAFT(Namespace(small=True, mixed_precision=False))
-    net = ddp.wrap_model(model, info)
+    net = ddp.wrap_model(model, info, bf16_grads=bf16)
     i1, i2, flow, valid = synthetic_batch(4, 128, 128, max_disp=4, seed=7)
     sl = slice(2 * rank, 2 * rank + 2)
     loss, metrics = sequence_loss(net(i1[sl], i2[sl], iters=2), flow[sl], valid[sl])
@@ -37,13 +37,14 @@ def _worker(rank, world, port, tmpdir):
 
 
 @pytest.mark.timeout(600)
-def test_ddp_gradients_match_full_batch():
+@pytest.mark.parametrize("bf16", [False, True], ids=["fp32", "bf16_hook"])
+def test_ddp_gradients_match_full_batch(bf16):
     from raft_ros_amd.data.synthetic import synthetic_batch
     from raft_ros_amd.models import RAFT
     from raft_ros_amd.train.loss import sequence_loss
 
     with tempfile.TemporaryDirectory() as tmp:
-        mp.start_processes(_worker, args=(2, ddp.free_port(), tmp), nprocs=2, start_method="spawn")
+        mp.start_processes(_worker, args=(2, ddp.free_port(), tmp, bf16), nprocs=2, start_method="spawn")
         grads = torch.load(os.path.join(tmp, "ddp.pt"), weights_only=True)
         red = torch.load(os.path.join(tmp, "red.pt"), weights_only=True)
     assert red["rank"] == 0.5
@@ -59,4 +60,10 @@ def test_ddp_gradients_match_full_batch():
     for n, p in model.named_parameters():
         if p.grad is None:
             continue
-        torch.testing.assert_close(grads[n], p.grad, rtol=1e-4, atol=1e-6)
+        if bf16:  # each rank's contribution is rounded to bf16 before the sum
+            # (biases in front of InstanceNorm have a ~0 true gradient: bound those absolutely)
+            scale = max(float(q.grad.norm()) for q in model.parameters() if q.grad is not None)
+            err = float((grads[n] - p.grad).norm())
+            assert err < 1e-2 * max(float(p.grad.norm()), 1e-3 * scale), (n, err, float(p.grad.norm()))
+        else:
+            torch.testing.assert_close(grads[n], p.grad, rtol=1e-4, atol=1e-6)

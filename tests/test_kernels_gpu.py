@@ -302,3 +302,34 @@ def test_upflow8_matches_reference_fwd_bwd(hw):
     got = rows.float().reshape(2, H, W, 8)
     torch.testing.assert_close(got[..., :2], fr.grad.permute(0, 2, 3, 1), rtol=1e-2, atol=1e-2)
     assert (got[..., 2:] == 0).all()
+
+
+@pytest.mark.parametrize("alt", [False, True])
+def test_training_step_bitwise_deterministic(alt):
+    """torch.use_deterministic_algorithms(True): two identical training steps give bitwise
+    identical gradients (every native backward is atomic-free or uses order-independent
+    fixed-point integer atomics)."""
+    from argparse import Namespace
+    from raft_ros_amd.data.synthetic import synthetic_batch
+    from raft_ros_amd.models import RAFT
+    from raft_ros_amd.train.loss import sequence_loss
+
+    cuda = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = RAFT(Namespace(small=False, mixed_precision=True, amp_dtype="bf16", alternate_corr=alt)).to(cuda)
+    model = model.to(memory_format=torch.channels_last).train()
+    model.freeze_bn()
+    batch = synthetic_batch(2, 128, 192, seed=4, device=cuda)
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        grads = []
+        for _ in range(2):
+            model.zero_grad(set_to_none=True)
+            loss, _ = sequence_loss(model(batch[0], batch[1], iters=3), batch[2], batch[3])
+            loss.backward()
+            grads.append([p.grad.clone() for p in model.parameters()])
+    finally:
+        torch.use_deterministic_algorithms(prev)
+    for (n, _), a, b in zip(model.named_parameters(), grads[0], grads[1]):
+        assert torch.equal(a, b), n

@@ -53,6 +53,11 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--dataset_root", default=None, help="directory holding Sintel/, KITTI/, ... (default ./datasets)")
     g.add_argument("--bucket_mb", type=float, default=32.0, help="DDP gradient bucket size")
     g.add_argument("--seed", type=int, default=1234)
+    g.add_argument("--deterministic", action="store_true",
+                   help="bitwise-reproducible steps: torch.use_deterministic_algorithms + the native kernels' "
+                        "atomic-free / fixed-point-atomic backward paths")
+    g.add_argument("--ddp_bf16_grads", action="store_true",
+                   help="all-reduce gradients in bf16 (DDP compression hook; halves xGMI traffic)")
     g.add_argument("--profile_dir", default=None, help="capture a torch.profiler trace of steps 5-7 here")
     return p
 
@@ -63,6 +68,9 @@ def _main(args) -> str:
     rank = int(os.environ.get("RANK", "0"))
     torch.manual_seed(args.seed + rank)
     np.random.seed(args.seed + rank)
+    if getattr(args, "deterministic", False):
+        torch.use_deterministic_algorithms(True, warn_only=True)
+        torch.backends.cudnn.benchmark = False
     os.makedirs(args.ckpt_dir, exist_ok=True)
     return train(args)
 
