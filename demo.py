@@ -3,6 +3,10 @@
 
     python demo.py --model=models/raft-things.pth --path=demo-frames
 
+Without ``--path`` the frames are read from ``demo-frames/``; when that directory holds no
+frames a synthetic sequence (textured background drift + a moving disc,
+``data/synthetic.demo_sequence``) is written there first.
+
 Runs every consecutive pair of *.png / *.jpg frames in ``--path`` (sorted) with
 20 refinement iterations.  The reference shows [image; flow] in a cv2 window;
 here the visualisation is shown with cv2 when it is importable and a display is
@@ -54,6 +58,21 @@ def viz(img, flo, out_path=None, show=False):
     return img_flo
 
 
+def write_demo_frames(path, n_frames: int = 6):
+    """No frames at ``path``: write a synthetic sequence there (the reference's Sintel demo
+    frames are not redistributed with this repository)."""
+    from raft_ros_amd.data.synthetic import demo_sequence
+
+    os.makedirs(path, exist_ok=True)
+    out = []
+    for k, fr in enumerate(demo_sequence(n_frames)):
+        f = os.path.join(path, "frame_%04d.png" % (16 + k))
+        Image.fromarray(fr.permute(1, 2, 0).numpy()).save(f)
+        out.append(f)
+    print(f"demo: no frames in {path}; wrote {len(out)} synthetic frames there")
+    return out
+
+
 def demo(args):
     model = RAFT(args)
     if args.model:
@@ -61,6 +80,8 @@ def demo(args):
     model.to(args.device).eval()
     os.makedirs(args.output, exist_ok=True)
     images = sorted(glob.glob(os.path.join(args.path, "*.png")) + glob.glob(os.path.join(args.path, "*.jpg")))
+    if not images:
+        images = write_demo_frames(args.path)
     outs = []
     with torch.inference_mode():
         for k, (imfile1, imfile2) in enumerate(zip(images[:-1], images[1:])):
@@ -78,7 +99,8 @@ def demo(args):
 def main(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--model", help="restore checkpoint")
-    p.add_argument("--path", help="dataset for evaluation")
+    p.add_argument("--path", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "demo-frames"),
+                   help="directory of frames (default: demo-frames/, synthesised on first use)")
     p.add_argument("--small", action="store_true", help="use small model")
     p.add_argument("--mixed_precision", action="store_true", help="use mixed precision")
     p.add_argument("--alternate_corr", action="store_true", help="use efficent correlation implementation")

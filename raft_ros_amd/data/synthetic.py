@@ -83,3 +83,32 @@ class SyntheticFlowDataset(torch.utils.data.Dataset):
     def __getitem__(self, index):
         i1, i2, f, v = synthetic_batch(1, self.h, self.w, self.max_disp, seed=self.seed * 1000003 + index)
         return i1[0], i2[0], f[0], v[0]
+
+
+def demo_sequence(n_frames: int = 6, h: int = 436, w: int = 1024, seed: int = 16, device="cpu"):
+    """A short synthetic video (list of (3, h, w) uint8 frames) for ``demo.py``: a textured
+    background under a slow global drift plus a textured disc moving on its own path, so
+    consecutive frames have a piecewise-smooth flow with a motion boundary.  Default size is
+    the Sintel frame size used by the reference demo."""
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    bg = random_texture(1, h + 64, w + 64, gen, device)
+    fg = random_texture(1, h, w, gen, device) * 0.6 + 60.0
+    ys = torch.arange(h, device=device, dtype=torch.float32).view(h, 1)
+    xs = torch.arange(w, device=device, dtype=torch.float32).view(1, w)
+    frames = []
+    for t in range(n_frames):
+        ox, oy = 32 + 3.0 * t, 32 + 1.5 * t  # background drift (crop window moves)
+        flow_bg = torch.zeros(1, 2, h, w, device=device)
+        flow_bg[:, 0], flow_bg[:, 1] = ox - 32, oy - 32
+        frame = warp_backward(bg[:, :, 32:32 + h, 32:32 + w], flow_bg)
+        cx, cy, r = 0.3 * w + 14.0 * t, 0.55 * h - 6.0 * t, 0.18 * h
+        mask = (((xs - cx) ** 2 + (ys - cy) ** 2) <= r * r).float()[None, None]
+        flow_fg = torch.zeros(1, 2, h, w, device=device)
+        flow_fg[:, 0], flow_fg[:, 1] = -14.0 * t, 6.0 * t
+        frame = mask * warp_backward(fg, flow_fg) + (1 - mask) * frame
+        frames.append(frame[0].clamp(0, 255).round().to(torch.uint8))
+    return frames
+
+
+_demo_full = demo_sequence  # (tests substitute smaller frames through demo_sequence)

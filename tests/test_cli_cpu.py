@@ -49,3 +49,24 @@ def test_evaluate_cli_synthetic(tmp_path):
     assert set(res) == {"synthetic-epe", "synthetic-1px", "synthetic-3px", "synthetic-5px"}
     out = evaluate.main(["--model", ck, "--small", "--dataset", "synthetic", "--device", "cpu", "--iters", "1"])
     assert out["synthetic-epe"] >= 0
+
+
+def test_demo_synthesises_frames_when_path_is_empty(tmp_path, monkeypatch):
+    import demo
+    from raft_ros_amd.data import synthetic
+
+    # small frames keep the CPU run short; the default sequence is Sintel-sized (436x1024)
+    monkeypatch.setattr(synthetic, "demo_sequence",
+                        lambda n=6: [f[:, :128, :160] for f in synthetic.__dict__["_demo_full"](3)])
+    outs = demo.main(["--small", "--path", str(tmp_path / "frames"), "--device", "cpu", "--iters", "1",
+                      "--output", str(tmp_path / "out")])
+    assert len(outs) == 2 and len(os.listdir(tmp_path / "frames")) == 3
+
+
+def test_demo_sequence_shape_and_motion():
+    import torch
+    from raft_ros_amd.data.synthetic import demo_sequence
+
+    fr = demo_sequence(3, 96, 128)
+    assert len(fr) == 3 and fr[0].shape == (3, 96, 128) and fr[0].dtype == torch.uint8
+    assert (fr[0].float() - fr[1].float()).abs().mean() > 1.0  # frames actually move
