@@ -38,7 +38,7 @@ import torch.distributed as dist
 
 METRIC = "image-pairs/sec training + Sintel-clean EPE, RAFT base at 1/2/4/8 MI355X"
 # Eager PyTorch baseline of the reference algorithm on 1x MI355X (pairs/s), see BASELINE.md
-BASELINE_PAIRS_PER_SEC = 94.932  # measured r1: bench.py --impl reference, bf16, batch 8
+BASELINE_PAIRS_PER_SEC = 96.593  # measured r2 (profiles/r2_bench_ref_bench_v3.json): bench.py --impl reference, bf16, batch 8
 
 
 def parse():
