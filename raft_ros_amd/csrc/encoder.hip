@@ -144,6 +144,16 @@ __device__ __forceinline__ void loadf8(const float* p, float* v) {
   }
 }
 
+// Raw buffer loads: out-of-range offsets return zeros, so padding / masked lanes need no
+// branch (an exec-masked branch per row costs more VALU/SALU than the load itself).
+constexpr unsigned kEncOOB = 0xFFFFFFF0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t enc_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ u32x4 bload(__amdgpu_buffer_rsrc_t r, unsigned voff) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+}
+
 __device__ __forceinline__ EncClass pick_class(const EncConvArgs& a, int wg, int& ci) {
   ci = 0;
 #pragma unroll
@@ -194,11 +204,23 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
   const int n0 = tn * BN;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int kc = tid & 7;
+  // grid coordinates of tile row r = (gy0, gx0) + r: one uniform division, then small
+  // float-reciprocal divisions (exact after the +-1 fix-up) instead of an integer division per row
+  const int gy0 = q0 / cl.Gw, gx0 = q0 - (q0 / cl.Gw) * cl.Gw;
+  const float inv_gw = 1.f / (float)cl.Gw;
+  auto row_coord = [&](int r, int& gy, int& gx) __attribute__((always_inline)) {
+    const int v = gx0 + r;
+    int d = (int)((float)v * inv_gw);
+    d -= (d * cl.Gw > v) ? 1 : 0;
+    d += ((d + 1) * cl.Gw <= v) ? 1 : 0;
+    gy = gy0 + d;
+    gx = v - d * cl.Gw;
+  };
   for (int r = tid; r < BM; r += 256) {
-    const int q = q0 + r;
     int off = -1;
-    if (q < GHW) {
-      const int gy = q / cl.Gw, gx = q - (q / cl.Gw) * cl.Gw;
+    if (q0 + r < GHW) {
+      int gy, gx;
+      row_coord(r, gy, gx);
       off = ((b * a.Ho + gy * a.os + cl.oy0) * a.Wo + gx * a.os + cl.ox0);
     }
     s_out[r] = off;
@@ -211,8 +233,8 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
   for (int i = 0; i < ACH; ++i) {
     const int q = q0 + (tid >> 3) + 32 * i;
     const bool valid = q < GHW;
-    const int gy = valid ? q / cl.Gw : 0;
-    const int gx = valid ? q - gy * cl.Gw : 0;
+    int gy = 0, gx = 0;
+    if (valid) row_coord((tid >> 3) + 32 * i, gy, gx);
 #pragma unroll
     for (int s2 = 0; s2 < NSRC; ++s2) {
       const EncSrc& S = a.src[s2];
@@ -233,49 +255,52 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
 
   __syncthreads();  // s_tab, s_out
 
-  u32x4 ra[ACH], rb[BCH];
-  auto load = [&](int k0) __attribute__((always_inline)) {
+  // two register sets: the global loads of step t+2 are in flight while step t computes
+  u32x4 ra[2][ACH], rb[2][BCH];
+  __amdgpu_buffer_rsrc_t rs[NSRC];
+#pragma unroll
+  for (int s2 = 0; s2 < NSRC; ++s2)
+    rs[s2] = enc_rsrc(a.src[s2].ptr, (unsigned)((long)a.B * a.src[s2].H * a.src[s2].W * a.src[s2].stride * 2));
+  const __amdgpu_buffer_rsrc_t rw = enc_rsrc(wt, (unsigned)((long)a.N * cl.Kpad * 2));
+  auto load = [&](int k0, u32x4 (&ra_)[ACH], u32x4 (&rb_)[BCH]) __attribute__((always_inline)) {
     const int ent = s_tab[cl.t0 + (k0 >> 3) + kc];
-    if (ent < 0) {
+    const bool ev = ent >= 0;  // -1: zero columns (K padding)
+    const int dy = (ent & 0xff) - 128, dx = ((ent >> 8) & 0xff) - 128, c = ent >> 17;
+    if constexpr (NSRC == 1) {
+      const EncSrc& S = a.src[0];
+      const int tapoff = (dy * S.W + dx) * S.stride + c;
 #pragma unroll
-      for (int i = 0; i < ACH; ++i) ra[i] = u32x4{0, 0, 0, 0};
+      for (int i = 0; i < ACH; ++i) {
+        const bool ok = ev && (unsigned)(sy[0][i] + dy) < (unsigned)S.H && (unsigned)(sx[0][i] + dx) < (unsigned)S.W;
+        ra_[i] = bload(rs[0], ok ? (unsigned)(sbase[0][i] + tapoff) * 2u : kEncOOB);
+      }
     } else {
-      const int dy = (ent & 0xff) - 128, dx = ((ent >> 8) & 0xff) - 128, c = ent >> 17;
-      if constexpr (NSRC == 1) {
-        const EncSrc& S = a.src[0];
-        const int tapoff = (dy * S.W + dx) * S.stride + c;
+      // per-lane source: one load per source, the other one masked out-of-range (zeros)
+      const int sidx = (ent >> 16) & 1;
 #pragma unroll
-        for (int i = 0; i < ACH; ++i) {
-          const bool ok = (unsigned)(sy[0][i] + dy) < (unsigned)S.H && (unsigned)(sx[0][i] + dx) < (unsigned)S.W;
-          ra[i] = ok ? *reinterpret_cast<const u32x4*>(S.ptr + (sbase[0][i] + tapoff)) : u32x4{0, 0, 0, 0};
-        }
-      } else {
-        const int sidx = (ent >> 16) & 1;
-        const EncSrc& S0 = a.src[0];
-        const EncSrc& S1 = a.src[1];
-        const __bf16* sp = sidx ? S1.ptr : S0.ptr;
-        const int sH = sidx ? S1.H : S0.H, sW = sidx ? S1.W : S0.W;
-        const int tapoff = (dy * sW + dx) * (sidx ? S1.stride : S0.stride) + c;
+      for (int i = 0; i < ACH; ++i) {
+        u32x4 v = {0, 0, 0, 0};
 #pragma unroll
-        for (int i = 0; i < ACH; ++i) {
-          const int y = (sidx ? sy[1][i] : sy[0][i]) + dy, x = (sidx ? sx[1][i] : sx[0][i]) + dx;
-          const bool ok = (unsigned)y < (unsigned)sH && (unsigned)x < (unsigned)sW;
-          ra[i] = ok ? *reinterpret_cast<const u32x4*>(sp + ((sidx ? sbase[1][i] : sbase[0][i]) + tapoff))
-                     : u32x4{0, 0, 0, 0};
+        for (int s2 = 0; s2 < NSRC; ++s2) {
+          const EncSrc& S = a.src[s2];
+          const int tapoff = (dy * S.W + dx) * S.stride + c;
+          const bool ok = ev && sidx == s2 && (unsigned)(sy[s2][i] + dy) < (unsigned)S.H &&
+                          (unsigned)(sx[s2][i] + dx) < (unsigned)S.W;
+          v |= bload(rs[s2], ok ? (unsigned)(sbase[s2][i] + tapoff) * 2u : kEncOOB);
         }
+        ra_[i] = v;
       }
     }
 #pragma unroll
-    for (int i = 0; i < BCH; ++i)
-      rb[i] = wrow[i] >= 0 ? *reinterpret_cast<const u32x4*>(wt + (wrow[i] + k0)) : u32x4{0, 0, 0, 0};
+    for (int i = 0; i < BCH; ++i) rb_[i] = bload(rw, wrow[i] >= 0 ? (unsigned)(wrow[i] + k0) * 2u : kEncOOB);
   };
-  auto store = [&](int buf) __attribute__((always_inline)) {
+  auto store = [&](int buf, const u32x4 (&ra_)[ACH], const u32x4 (&rb_)[BCH]) __attribute__((always_inline)) {
     __bf16* sA = smem + buf * STAGE;
     __bf16* sB = sA + BM * ELDK;
 #pragma unroll
-    for (int i = 0; i < ACH; ++i) *reinterpret_cast<u32x4*>(sA + ((tid >> 3) + 32 * i) * ELDK + kc * 8) = ra[i];
+    for (int i = 0; i < ACH; ++i) *reinterpret_cast<u32x4*>(sA + ((tid >> 3) + 32 * i) * ELDK + kc * 8) = ra_[i];
 #pragma unroll
-    for (int i = 0; i < BCH; ++i) *reinterpret_cast<u32x4*>(sB + ((tid >> 3) + 32 * i) * ELDK + kc * 8) = rb[i];
+    for (int i = 0; i < BCH; ++i) *reinterpret_cast<u32x4*>(sB + ((tid >> 3) + 32 * i) * ELDK + kc * 8) = rb_[i];
   };
 
   f32x16 acc[TM][TN];
@@ -287,12 +312,8 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int fr = lane & 31, fk = (lane >> 5) * 8;
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int t = 0; t < nk; ++t) {
-    if (t + 1 < nk) load((t + 1) * EBK);
-    const __bf16* sA = smem + (t & 1) * STAGE;
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const __bf16* sA = smem + buf * STAGE;
     const __bf16* sB = sA + BM * ELDK;
 #pragma unroll
     for (int s = 0; s < EBK / 16; ++s) {
@@ -309,7 +330,22 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < nk) store((t + 1) & 1);
+  };
+  // step t computes LDS buffer t&1; registers: set t&1 receives step t+2, set (t+1)&1 holds
+  // step t+1 (stored after the compute); the loop is unrolled by 2 so the sets are static
+  load(0, ra[0], rb[0]);
+  if (nk > 1) load(EBK, ra[1], rb[1]);
+  store(0, ra[0], rb[0]);
+  __syncthreads();
+  for (int t = 0; t < nk; t += 2) {
+    if (t + 2 < nk) load((t + 2) * EBK, ra[0], rb[0]);
+    compute(0);
+    if (t + 1 < nk) store(1, ra[1], rb[1]);
+    __syncthreads();
+    if (t + 1 >= nk) break;
+    if (t + 3 < nk) load((t + 3) * EBK, ra[1], rb[1]);
+    compute(1);
+    if (t + 2 < nk) store(0, ra[0], rb[0]);
     __syncthreads();
   }
 
@@ -325,51 +361,40 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
     biasv[j] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
   }
   if (a.stats) {
-    // per-column (sum, M2) of this tile's valid rows: two passes over the registers
+    // per-column (sum, M2) of this tile's valid rows in one pass: sum and sum of squares,
+    // M2 = sq - s^2 / n (n <= BM values per tile: fp32 cancellation is negligible; the
+    // tiles are Chan-combined by the finalize kernel)
+    const bool full = rows == BM;  // uniform: every tile but the last of an image
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      float s = 0.f;
+      float sm = 0.f, sq = 0.f;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int rl = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          if (rl < rows) s += acc[i][j][r] + biasv[j];
+          const float v = (full || rl < rows) ? acc[i][j][r] + biasv[j] : 0.f;
+          sm += v;
+          sq += v * v;
         }
-      s += __shfl_xor(s, 32, 64);
-      if (lane < 32) sst1[wm * BN + wn * (BN / WN) + j * 32 + lane] = s;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int cl_ = wn * (BN / WN) + j * 32 + (lane & 31);
-      float tot = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) tot += sst1[w * BN + cl_];
-      const float mean = tot / (float)rows;
-      float m2 = 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rl = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          const float d = acc[i][j][r] + biasv[j] - mean;
-          if (rl < rows) m2 += d * d;
-        }
-      m2 += __shfl_xor(m2, 32, 64);
-      if (lane < 32) sst2[wm * BN + cl_] = m2;
+      sm += __shfl_xor(sm, 32, 64);
+      sq += __shfl_xor(sq, 32, 64);
+      if (lane < 32) {
+        sst1[wm * BN + wn * (BN / WN) + j * 32 + lane] = sm;
+        sst2[wm * BN + wn * (BN / WN) + j * 32 + lane] = sq;
+      }
     }
     __syncthreads();
     if (tid < BN && n0 + tid < a.N) {
-      float s = 0.f, m2 = 0.f;
+      float sm = 0.f, sq = 0.f;
 #pragma unroll
       for (int w = 0; w < WM; ++w) {
-        s += sst1[w * BN + tid];
-        m2 += sst2[w * BN + tid];
+        sm += sst1[w * BN + tid];
+        sq += sst2[w * BN + tid];
       }
       float* st = a.stats + ((long)(b * cl.tiles_img + tile) * 2) * a.N;
-      st[n0 + tid] = s;
-      st[a.N + n0 + tid] = m2;
+      st[n0 + tid] = sm;
+      st[a.N + n0 + tid] = fmaxf(sq - sm * sm / (float)rows, 0.f);
     }
   }
   // stage the tile (+ bias) in LDS, then 16-byte stores of 8 channels per thread
@@ -896,18 +921,19 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_reduce_kernel(const NormBwdA
 }
 
 // pass 2: coefficients per (group, channel) and the BatchNorm parameter gradients.
-// Block = (group, 64-channel chunk); 4 threads per channel split the (image, chunk)
-// partials, combined in LDS in a fixed order.
+// Block = (group, 16-channel chunk); 16 threads per channel split the (image, chunk)
+// partials (independent loads in flight), combined in LDS in a fixed order.
 __global__ __launch_bounds__(256) void enc_norm_bwd_finalize_kernel(const NormBwdArgs a) {
-  __shared__ float red[4][4][64];
+  __shared__ float red[4][16][17];
   const int N = a.N;
   const int nb = a.a1 ? 2 : 1;
-  const int g = blockIdx.x, n = blockIdx.y * 64 + (threadIdx.x & 63), sub = threadIdx.x >> 6;
+  const int c16 = threadIdx.x & 15, sub = threadIdx.x >> 4;
+  const int g = blockIdx.x, n = blockIdx.y * 16 + c16;
   const int b0 = a.kind == 1 ? g : 0, b1 = a.kind == 1 ? g + 1 : a.B;
   const int E = (b1 - b0) * a.R;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   if (n < N) {
-    for (int e = sub; e < E; e += 4) {
+    for (int e = sub; e < E; e += 16) {
       const float* pp = a.part + ((long)(b0 * a.R + e) * 4) * N + n;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -915,16 +941,16 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_finalize_kernel(const NormBw
     }
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) red[q][sub][threadIdx.x & 63] = acc[q];
+  for (int q = 0; q < 4; ++q) red[q][sub][c16] = acc[q];
   __syncthreads();
   if (sub != 0 || n >= N) return;
   const float M = (float)(b1 - b0) * a.HW;
   for (int j = 0; j < nb; ++j) {
     float S1 = 0.f, S2 = 0.f;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      S1 += red[2 * j][k][threadIdx.x];
-      S2 += red[2 * j + 1][k][threadIdx.x];
+    for (int k = 0; k < 16; ++k) {
+      S1 += red[2 * j][k][c16];
+      S2 += red[2 * j + 1][k][c16];
     }
     const float* c = (j ? a.c1 : a.c0) + (long)b0 * 4 * N;
     const float scale = c[n];
@@ -1091,7 +1117,7 @@ hipError_t launch_enc_norm_bwd(const NormBwdArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(enc_norm_bwd_reduce_kernel, dim3(a.R, a.B), dim3(256), 0, s, a);
   RAFT_HIP_CHECK(hipGetLastError());
   const int groups = a.kind == 1 ? a.B : 1;
-  hipLaunchKernelGGL(enc_norm_bwd_finalize_kernel, dim3(groups, (a.N + 63) / 64), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(enc_norm_bwd_finalize_kernel, dim3(groups, (a.N + 15) / 16), dim3(256), 0, s, a);
   RAFT_HIP_CHECK(hipGetLastError());
   const long chunks = (long)a.B * a.HW * (a.N / 8);
   hipLaunchKernelGGL(enc_norm_bwd_apply_kernel, dim3(grid_for(chunks)), dim3(256), 0, s, a);

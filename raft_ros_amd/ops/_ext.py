@@ -33,6 +33,10 @@ def _try_load() -> bool:
         _loaded = True
     except Exception as exc:  # pragma: no cover - depends on the host
         _load_error = f"failed to load {_LIB_PATH}: {exc}"
+    if _loaded:
+        from . import _meta
+
+        _meta.register()  # FakeTensor / meta-device shape functions of every op
     return _loaded
 
 
