@@ -18,11 +18,12 @@
 namespace raft_amd {
 
 struct PyrDesc {
-  float* ptr[4];
+  float* ptr[4];  // bf16 data when vbf16 (forward lookups of an AMP volume)
   int H[4];
   int W[4];
   long ld[4];
   int levels;
+  int vbf16;
 };
 struct CorrGemmArgs {
   const void* A;
@@ -227,21 +228,24 @@ void check_gpu(const at::Tensor& t, const char* name) {
 
 // Pyramid levels: (rows, Hl, Wl) fp32 views with unit x stride and y stride Wl; the row
 // stride may exceed Hl*Wl (padded rows, as the GEMM operands need 8-element-aligned pitches).
-PyrDesc make_desc(const std::vector<at::Tensor>& levels, long rows) {
+PyrDesc make_desc(const std::vector<at::Tensor>& levels, long rows, bool allow_bf16 = false) {
   TORCH_CHECK(levels.size() >= 1 && levels.size() <= 4, "raft_amd: 1..4 pyramid levels supported");
   PyrDesc d{};
   d.levels = static_cast<int>(levels.size());
   for (size_t l = 0; l < levels.size(); ++l) {
     const auto& t = levels[l];
     check_gpu(t, "pyramid level");
-    TORCH_CHECK(t.scalar_type() == at::kFloat && t.dim() == 3 && t.stride(2) == 1 && t.stride(1) == t.size(2) &&
-                    t.stride(0) >= t.size(1) * t.size(2),
-                "raft_amd: pyramid levels must be fp32 (B*H*W, Hl, Wl) row views");
+    const bool bf = t.scalar_type() == at::kBFloat16;
+    TORCH_CHECK((t.scalar_type() == at::kFloat || (allow_bf16 && bf)) && t.dim() == 3 && t.stride(2) == 1 &&
+                    t.stride(1) == t.size(2) && t.stride(0) >= t.size(1) * t.size(2),
+                "raft_amd: pyramid levels must be fp32 (bf16: forward lookups only) (B*H*W, Hl, Wl) row views");
+    TORCH_CHECK(l == 0 || (bf ? 1 : 0) == d.vbf16, "raft_amd: pyramid levels must share one dtype");
+    d.vbf16 = bf ? 1 : 0;
     TORCH_CHECK(t.size(0) == rows, "raft_amd: pyramid level rows mismatch");
     TORCH_CHECK(t.storage_offset() + (rows - 1) * t.stride(0) + t.size(1) * t.size(2) <=
-                    (long)(t.storage().nbytes() / sizeof(float)),
+                    (long)(t.storage().nbytes() / t.element_size()),
                 "raft_amd: pyramid level view exceeds its storage");
-    d.ptr[l] = t.data_ptr<float>();
+    d.ptr[l] = static_cast<float*>(t.data_ptr());
     d.H[l] = static_cast<int>(t.size(1));
     d.W[l] = static_cast<int>(t.size(2));
     d.ld[l] = t.stride(0);
@@ -361,7 +365,7 @@ at::Tensor corr_lookup(at::TensorList pyramid, const at::Tensor& coords, int64_t
   check_coords(coords);
   const long B = coords.size(0), H = coords.size(2), W = coords.size(3);
   std::vector<at::Tensor> lv(pyramid.begin(), pyramid.end());
-  PyrDesc d = make_desc(lv, B * H * W);
+  PyrDesc d = make_desc(lv, B * H * W, true);
   const long win = (2 * radius + 1) * (2 * radius + 1);
   const c10::DeviceGuard guard(coords.device());
   const long och = out_channels > 0 ? out_channels : d.levels * win;
@@ -1036,7 +1040,7 @@ void corr_lookup_into(at::TensorList pyramid, const at::Tensor& coords, int64_t 
   check_coords(coords);
   const long B = coords.size(0), H = coords.size(2), W = coords.size(3);
   std::vector<at::Tensor> lv(pyramid.begin(), pyramid.end());
-  PyrDesc d = make_desc(lv, B * H * W);
+  PyrDesc d = make_desc(lv, B * H * W, true);
   const long win = (2 * radius + 1) * (2 * radius + 1);
   check_gpu(out, "out");
   TORCH_CHECK(out.dim() == 4 && out.is_contiguous() && out.size(0) == B && out.size(1) == H && out.size(2) == W &&

@@ -36,8 +36,9 @@ struct PyrDesc {
   float* ptr[4];
   int H[4];
   int W[4];
-  long ld[4];  // row pitch (floats) of level l: row `pix` starts at ptr[l] + pix * ld[l]
+  long ld[4];  // row pitch (elements) of level l: row `pix` starts at ptr[l] + pix * ld[l]
   int levels;
+  int vbf16;   // levels hold bf16 (the AMP volume; forward lookups only -- gradients stay fp32)
 };
 
 // One GEMM of the correlation path: C[b][m][n] (op)= alpha * sum_k A[b][m][k] * B[b][n][k]
@@ -264,134 +265,93 @@ __device__ __forceinline__ float safe_floor(float v) {
 }
 
 // ---------------------------------------------------------------------------- lookup
-// One wave per query pixel; 4 waves per block, each with its own LDS slice, so the waves
-// never wait for each other (wave-level ordering only).  All levels' neighbourhood loads are
-// issued before any is consumed (4 levels x <= 4 per lane in flight), then the bilinear
-// blends read the (2r+2)^2 neighbourhoods (<= 14 x 14 for r <= 6) from LDS.
+// One wave per query pixel, looping over the levels; 4 waves per block.  LDS per wave:
+// the (2r+2)^2 neighbourhood (<= 14 x 14 for r <= 6) as fp32.
 constexpr int NBMAX = 14 * 14;
-constexpr int NBL = (NBMAX + 63) / 64;  // neighbourhood elements per lane and level
-
-__device__ __forceinline__ void wave_sync_lds() {
-  // the slice is private to the wave: LDS ops of one wave complete in order; keep the
-  // compiler from moving accesses across this point
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
 
 template <typename OutT>
 __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const float* __restrict__ coords,
                                                          OutT* __restrict__ out, int B, int H, int W, int r,
                                                          int out_ch) {
-  __shared__ float nb[4][4][NBMAX];
+  __shared__ float nb[4][NBMAX];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
-  const long pix = (long)blockIdx.x * 4 + wave;
-  if (pix >= (long)B * HW) return;  // waves are independent: early exit is safe
+  const long pix0 = (long)blockIdx.x * 4 + wave;
+  const bool live = pix0 < (long)B * HW;  // no early exit: the block synchronises per level
+  const long pix = live ? pix0 : 0;
   const int b = pix / HW, p = pix - (long)b * HW;
-  const int rd = 2 * r + 1, nd = rd + 1, win = rd * rd, nn = nd * nd;
+  const int rd = 2 * r + 1, nd = rd + 1, win = rd * rd;
   const float cx0 = coords[(long)b * 2 * HW + p], cy0 = coords[(long)b * 2 * HW + HW + p];
   const bool finite = isfinite(cx0) && isfinite(cy0);
-  float fxs[4], fys[4], v[4][NBL];
-#pragma unroll
-  for (int l = 0; l < 4; ++l) {
-    fxs[l] = fys[l] = 0.f;
-    if (l >= pyr.levels) continue;
+  OutT* o = out + pix * out_ch;
+  for (int l = 0; l < pyr.levels; ++l) {
     const float s = 1.0f / float(1 << l);
     const float cx = finite ? cx0 * s : 0.f, cy = finite ? cy0 * s : 0.f;
     const float fx0 = safe_floor(cx), fy0 = safe_floor(cy);
-    fxs[l] = cx - fx0;
-    fys[l] = cy - fy0;
+    const float fx = cx - fx0, fy = cy - fy0;
     const int xb = (int)fx0 - r, yb = (int)fy0 - r;
     const int Hl = pyr.H[l], Wl = pyr.W[l];
-    const float* row = pyr.ptr[l] + pix * pyr.ld[l];
-#pragma unroll
-    for (int k = 0; k < NBL; ++k) {
-      const int e = lane + 64 * k;
+    const long rbase = pix * pyr.ld[l];
+    const float* row = pyr.ptr[l] + rbase;
+    const __bf16* rowb = reinterpret_cast<const __bf16*>(pyr.ptr[l]) + rbase;
+    for (int e = lane; e < nd * nd; e += 64) {
       const int a = e / nd, c = e - a * nd;  // neighbour (y = yb + a, x = xb + c)
       const int y = yb + a, x = xb + c;
-      v[l][k] = (e < nn && finite && (unsigned)y < (unsigned)Hl && (unsigned)x < (unsigned)Wl) ? row[y * Wl + x] : 0.f;
+      const bool in = live && finite && (unsigned)y < (unsigned)Hl && (unsigned)x < (unsigned)Wl;
+      nb[wave][e] = in ? (pyr.vbf16 ? static_cast<float>(rowb[y * Wl + x]) : row[y * Wl + x]) : 0.f;
     }
+    __syncthreads();
+    if (live)
+      for (int ch = lane; ch < win; ch += 64) {
+        const int ix = ch / rd, iy = ch - ix * rd;  // x-offset-major window order
+        const float* n0 = nb[wave] + iy * nd + ix;
+        const float v =
+            (1.f - fy) * ((1.f - fx) * n0[0] + fx * n0[1]) + fy * ((1.f - fx) * n0[nd] + fx * n0[nd + 1]);
+        o[l * win + ch] = from_f32<OutT>(v);
+      }
+    __syncthreads();
   }
-#pragma unroll
-  for (int l = 0; l < 4; ++l)
-#pragma unroll
-    for (int k = 0; k < NBL; ++k)
-      if (l < pyr.levels && lane + 64 * k < nn) nb[wave][l][lane + 64 * k] = v[l][k];
-  wave_sync_lds();
-  OutT* o = out + pix * out_ch;
-  for (int l = 0; l < pyr.levels; ++l) {
-    const float fx = fxs[l], fy = fys[l];
-    for (int ch = lane; ch < win; ch += 64) {
-      const int ix = ch / rd, iy = ch - ix * rd;  // x-offset-major window order
-      const float* n0 = nb[wave][l] + iy * nd + ix;
-      const float val =
-          (1.f - fy) * ((1.f - fx) * n0[0] + fx * n0[1]) + fy * ((1.f - fx) * n0[nd] + fx * n0[nd + 1]);
-      o[l * win + ch] = from_f32<OutT>(val);
-    }
-  }
-  for (int ch = pyr.levels * win + lane; ch < out_ch; ch += 64) o[ch] = from_f32<OutT>(0.f);
+  if (live)
+    for (int ch = pyr.levels * win + lane; ch < out_ch; ch += 64) o[ch] = from_f32<OutT>(0.f);
 }
 
 // dpyr[l][pix][y][x] += window gradient, transposed bilinear blend; one wave per query.
-// The read-modify-write loads of every level's neighbourhood are issued together with the
-// gradient loads, before any blend.
 template <typename GT>
 __global__ __launch_bounds__(256) void lookup_bwd_kernel(PyrDesc dpyr, const float* __restrict__ coords,
                                                          const GT* __restrict__ gout, int B, int H, int W, int r,
                                                          int gstride) {
-  __shared__ float gs[4][4][NBMAX];
+  __shared__ float gs[4][NBMAX];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
-  const long pix = (long)blockIdx.x * 4 + wave;
-  if (pix >= (long)B * HW) return;
+  const long pix0 = (long)blockIdx.x * 4 + wave;
+  const long pix = pix0 < (long)B * HW ? pix0 : 0;
   const int b = pix / HW, p = pix - (long)b * HW;
-  const int rd = 2 * r + 1, nd = rd + 1, win = rd * rd, nn = nd * nd;
+  const int rd = 2 * r + 1, nd = rd + 1, win = rd * rd;
   const float cx0 = coords[(long)b * 2 * HW + p], cy0 = coords[(long)b * 2 * HW + HW + p];
-  if (!(isfinite(cx0) && isfinite(cy0))) return;
+  // no early exit: the block synchronises per level
+  const bool live = pix0 < (long)B * HW && isfinite(cx0) && isfinite(cy0);
   const GT* g = gout + pix * gstride;
-  float fxs[4], fys[4], old[4][NBL];
-  int idx[4][NBL];
-#pragma unroll
-  for (int l = 0; l < 4; ++l) {
-    fxs[l] = fys[l] = 0.f;
-    if (l >= dpyr.levels) continue;
+  for (int l = 0; l < dpyr.levels; ++l) {
     const float s = 1.0f / float(1 << l);
-    const float cx = cx0 * s, cy = cy0 * s;
+    const float cx = live ? cx0 * s : 0.f, cy = live ? cy0 * s : 0.f;
     const float fx0 = safe_floor(cx), fy0 = safe_floor(cy);
-    fxs[l] = cx - fx0;
-    fys[l] = cy - fy0;
+    const float fx = cx - fx0, fy = cy - fy0;
     const int xb = (int)fx0 - r, yb = (int)fy0 - r;
     const int Hl = dpyr.H[l], Wl = dpyr.W[l];
-    const float* row = dpyr.ptr[l] + pix * dpyr.ld[l];
-#pragma unroll
-    for (int k = 0; k < NBL; ++k) {
-      const int e = lane + 64 * k;
-      const int a = e / nd, c = e - a * nd;
-      const int y = yb + a, x = xb + c;
-      const bool in = e < nn && (unsigned)y < (unsigned)Hl && (unsigned)x < (unsigned)Wl;
-      idx[l][k] = in ? y * Wl + x : -1;
-      old[l][k] = in ? row[y * Wl + x] : 0.f;
-    }
     // window gradient in LDS as [iy][ix] (transposed from the x-major channel order)
     for (int ch = lane; ch < win; ch += 64) {
       const int ix = ch / rd, iy = ch - ix * rd;
-      gs[wave][l][iy * rd + ix] = to_f32(g[l * win + ch]);
+      gs[wave][iy * rd + ix] = live ? to_f32(g[l * win + ch]) : 0.f;
     }
-  }
-  wave_sync_lds();
-#pragma unroll
-  for (int l = 0; l < 4; ++l) {
-    if (l >= dpyr.levels) continue;
-    const float fx = fxs[l], fy = fys[l];
-    const float* gw = gs[wave][l];
+    __syncthreads();
     float* row = dpyr.ptr[l] + pix * dpyr.ld[l];
-#pragma unroll
-    for (int k = 0; k < NBL; ++k) {
-      if (idx[l][k] < 0) continue;
-      const int e = lane + 64 * k;
+    for (int e = lane; live && e < nd * nd; e += 64) {
       const int a = e / nd, c = e - a * nd;
+      const int y = yb + a, x = xb + c;
+      if ((unsigned)y >= (unsigned)Hl || (unsigned)x >= (unsigned)Wl) continue;
       // neighbour (a, c) is corner (0,0) of tap (c, a), (0,1) of (c-1, a), (1,0) of (c, a-1),
       // (1,1) of (c-1, a-1)
+      const float* gw = gs[wave];
       float v = 0.f;
       if (a < rd) {
         if (c < rd) v += (1.f - fx) * (1.f - fy) * gw[a * rd + c];
@@ -401,8 +361,9 @@ __global__ __launch_bounds__(256) void lookup_bwd_kernel(PyrDesc dpyr, const flo
         if (c < rd) v += (1.f - fx) * fy * gw[(a - 1) * rd + c];
         if (c > 0) v += fx * fy * gw[(a - 1) * rd + c - 1];
       }
-      row[idx[l][k]] = old[l][k] + v;
+      row[y * Wl + x] += v;
     }
+    __syncthreads();
   }
 }
 

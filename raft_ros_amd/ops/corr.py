@@ -43,7 +43,7 @@ def _pad_to(n: int, m: int) -> int:
 class _PyramidState:
     """Forward/backward state shared by a pyramid build and its lookups.
 
-    All levels live in ONE fp32 buffer of B*HW rows: level l occupies columns
+    All levels live in ONE buffer of B*HW rows (fp32; bf16 under AMP): level l occupies columns
     [off_l, off_l + Hl*Wl) (each level's width padded to a multiple of 8), so the
     pyramid build, dF1 and dF2 are one GEMM each over the concatenated levels."""
 
@@ -63,8 +63,8 @@ class _PyramidState:
                 for Hl, Wl, off in self.sizes]
 
     def grad_buffers(self) -> List[torch.Tensor]:
-        if self.dlevels is None:
-            self.dbuf = torch.zeros_like(self.buf)
+        if self.dlevels is None:  # fp32 even for a bf16 volume: 12 iterations accumulate here
+            self.dbuf = torch.zeros(self.buf.shape, device=self.buf.device, dtype=torch.float32)
             self.dlevels = self.views(self.dbuf)
         return self.dlevels
 
@@ -119,7 +119,9 @@ class _BuildPyramid(torch.autograd.Function):
         ld = off
         state.sizes, state.ld = sizes, ld
         f2cat = _concat_levels(f2s, ld, [o for _, _, o in sizes], nchw=False)  # (B, ld, C), pad rows 0
-        buf = torch.empty(B * HW, ld, device=f1.device)
+        # AMP (not split): the volume is stored in bf16 -- its lookups feed bf16 convs, and the
+        # lookup kernels are bound by the bytes they gather; split mode keeps it fp32-faithful
+        buf = torch.empty(B * HW, ld, device=f1.device, dtype=torch.float32 if split else torch.bfloat16)
         # every level at once: buf[p][q] = alpha * f1[p] . f2cat[q]  (pad columns get 0)
         k.corr_gemm(f1, f2cat, buf, HW, ld, C, B, C, HW * C, C, ld * C, ld, HW * ld, alpha, False, split, 0)
         state.buf = buf
