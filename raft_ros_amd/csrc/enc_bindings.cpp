@@ -88,7 +88,7 @@ struct NormBwdArgs {
 int enc_tile_bn(int N);
 hipError_t launch_enc_pack(const EncConvArgs& a, int rows, void* out, hipStream_t s);
 hipError_t launch_enc_conv(const EncConvArgs& a, int nblocks, hipStream_t s);
-hipError_t launch_enc_wgrad(const EncWgradArgs& a, int BM, hipStream_t s);
+hipError_t launch_enc_wgrad(const EncWgradArgs& a, int BM, int BN, hipStream_t s);
 hipError_t launch_enc_wgrad_reduce(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, float* dw,
                                    const long* ws, int Cout, int Cin, int Cx, int KH, int KW, float* db,
                                    bool accumulate, hipStream_t s);
@@ -329,8 +329,12 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
   a.tilesM = (N + BM - 1) / BM;
   a.Npad = a.tilesM * BM;
   a.K = KH * KW * Cx;
-  a.tilesN = (a.K + 63) / 64;
-  a.Kpad = a.tilesN * 64;
+  // 128 K-columns per workgroup when there are enough (twice the MFMAs per staged dY tile)
+  // (small pixel counts keep 64 columns: more workgroups -- scripts/bench_enc.py on MI355X)
+  const long Pn = (long)B * Ho * Wo;
+  const int BN = (a.K >= 256 && Pn >= 100000) ? 128 : 64;
+  a.tilesN = (a.K + BN - 1) / BN;
+  a.Kpad = a.tilesN * BN;
   a.P = (long)B * Ho * Wo;
   const long tiles = (long)a.tilesM * a.tilesN;
   // ~640 workgroups (2.5 per CU): long pixel loops per workgroup, few slabs to reduce
@@ -349,7 +353,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
     dbslab = at::empty({(long)a.nsplit * a.Npad}, x.options().dtype(at::kFloat));
     a.dbslab = dbslab.data_ptr<float>();
   }
-  check(launch_enc_wgrad(a, BM, stream()), "enc_wgrad");
+  check(launch_enc_wgrad(a, BM, BN, stream()), "enc_wgrad");
   long wsd[4];
   for (int d = 0; d < 4; ++d) wsd[d] = dw.stride(d);
   check(launch_enc_wgrad_reduce(a.slab, a.nsplit, a.Npad, a.Kpad, a.dbslab, dw.data_ptr<float>(), wsd, N, Cin, Cx, KH,

@@ -484,12 +484,12 @@ __device__ __forceinline__ int wswz(int row, int chunk) {
   return COLS == 128 ? (chunk ^ ((row & 3) << 2)) : (chunk ^ (((row >> 1) & 1) << 2));
 }
 
-template <int BM>
+template <int BM, int BN>
 __global__ __launch_bounds__(256) void enc_wgrad_kernel(const EncWgradArgs a) {
-  constexpr int BN = 64;
-  constexpr int TM = BM / 64;
+  // 2x2 waves of (BM/2) x (BN/2): TM x TN MFMA 32x32x16 tiles per wave
+  constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int ACPR = BM / 8, ARP = 256 / ACPR, AI = 64 / ARP;
-  constexpr int BI = 2;
+  constexpr int BCPR = BN / 8, BRP = 256 / BCPR, BI = 64 / BRP;
   constexpr int STAGE = 64 * (BM + BN);
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
 
@@ -507,7 +507,7 @@ __global__ __launch_bounds__(256) void enc_wgrad_kernel(const EncWgradArgs a) {
 
   const int ca = tid % ACPR;
   const bool a_ok = m0 + ca * 8 < a.N;
-  const int cb = tid & 7;
+  const int cb = tid % BCPR;
   const int kb = n0 + cb * 8;
   const bool b_ok = kb < a.K;
   int ky = 0, kx = 0, c = 0;
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(256) void enc_wgrad_kernel(const EncWgradArgs a) {
   int wp[BI], wb[BI], wy[BI], wx[BI];
 #pragma unroll
   for (int i = 0; i < BI; ++i) {
-    const int p = (int)pbeg + (tid >> 3) + 32 * i;
+    const int p = (int)pbeg + tid / BCPR + BRP * i;
     wp[i] = p;
     wb[i] = p / HoWo;
     const int rem = p - wb[i] * HoWo;
@@ -579,16 +579,18 @@ __global__ __launch_bounds__(256) void enc_wgrad_kernel(const EncWgradArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
-      const int row = (tid >> 3) + 32 * i;
+      const int row = tid / BCPR + BRP * i;
       *reinterpret_cast<u32x4*>(sB + row * BN + wswz<BN>(row, cb) * 8) = rb[i];
     }
   };
 
-  f32x16 acc[TM];
+  f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int hh = lane >> 5, gi = (lane >> 4) & 1, q = (lane & 15) >> 2, pq = lane & 3;
   if (nsteps > 0) {
@@ -603,7 +605,7 @@ __global__ __launch_bounds__(256) void enc_wgrad_kernel(const EncWgradArgs a) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int r0 = s * 16 + hh * 8 + q, r1 = r0 + 4;
-      bf16x8 af[TM], bfr;
+      bf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int col = wm * (BM / 2) + i * 32 + gi * 16 + 4 * pq;
@@ -611,28 +613,33 @@ __global__ __launch_bounds__(256) void enc_wgrad_kernel(const EncWgradArgs a) {
         const s16x4 hi = tr_read(sA + r1 * BM + wswz<BM>(r1, col >> 3) * 8 + (col & 7));
         af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
-      {
-        const int col = wn * (BN / 2) + gi * 16 + 4 * pq;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * (BN / 2) + j * 32 + gi * 16 + 4 * pq;
         const s16x4 lo = tr_read(sB + r0 * BN + wswz<BN>(r0, col >> 3) * 8 + (col & 7));
         const s16x4 hi = tr_read(sB + r1 * BN + wswz<BN>(r1, col >> 3) * 8 + (col & 7));
-        bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
-      for (int i = 0; i < TM; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr, acc[i], 0, 0, 0);
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (t + 1 < nsteps) store((t + 1) & 1);
     __syncthreads();
   }
 
   float* slab = a.slab + (long)split * a.Npad * a.Kpad;
-  {
-    const int col = n0 + wn * (BN / 2) + (lane & 31);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        slab[(long)row * a.Kpad + col] = acc[i][r];
+        slab[(long)row * a.Kpad + col] = acc[i][j][r];
       }
   }
   if (a.dbslab != nullptr && tn == 0) {
@@ -1071,12 +1078,16 @@ hipError_t launch_enc_conv(const EncConvArgs& a, int nblocks, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_enc_wgrad(const EncWgradArgs& a, int BM, hipStream_t s) {
+hipError_t launch_enc_wgrad(const EncWgradArgs& a, int BM, int BN, hipStream_t s) {
   const int nwg = a.nsplit * a.tilesM * a.tilesN;
-  if (BM == 128)
-    hipLaunchKernelGGL((enc_wgrad_kernel<128>), dim3(nwg), dim3(256), 0, s, a);
+  if (BM == 128 && BN == 128)
+    hipLaunchKernelGGL((enc_wgrad_kernel<128, 128>), dim3(nwg), dim3(256), 0, s, a);
+  else if (BM == 128)
+    hipLaunchKernelGGL((enc_wgrad_kernel<128, 64>), dim3(nwg), dim3(256), 0, s, a);
+  else if (BN == 128)
+    hipLaunchKernelGGL((enc_wgrad_kernel<64, 128>), dim3(nwg), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((enc_wgrad_kernel<64>), dim3(nwg), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((enc_wgrad_kernel<64, 64>), dim3(nwg), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
