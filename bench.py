@@ -53,7 +53,9 @@ def parse():
     ap.add_argument("--small", action="store_true")
     ap.add_argument("--amp_dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--lr", type=float, default=4e-4)
-    ap.add_argument("--bucket_mb", type=float, default=32.0)
+    # ~10 MB buckets: the update-block gradients (12.5 MB, ready first -- batched wgrads run
+    # before the encoders' backward) all-reduce over xGMI while the encoders backpropagate
+    ap.add_argument("--bucket_mb", type=float, default=10.0)
     ap.add_argument("--no_fused", action="store_true", help="update block on PyTorch/MIOpen convs")
     ap.add_argument("--mode", choices=["train", "infer"], default="train",
                     help="infer: forward-only test_mode passes (BASELINE config #5: --image_size 1080 1920 --iters 32)")

@@ -24,6 +24,7 @@ struct PyrDesc {
   long ld[4];
   int levels;
   int vbf16;
+  int blk;
 };
 struct CorrGemmArgs {
   const void* A;
@@ -43,6 +44,7 @@ struct UnpoolArgs {
   float* out;
   int B, H, W, C, nseg;
   int off[4], h[4], w[4];
+  int blk;
 };
 
 enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
@@ -229,6 +231,7 @@ void check_gpu(const at::Tensor& t, const char* name) {
 // Pyramid levels: (rows, Hl, Wl) fp32 views with unit x stride and y stride Wl; the row
 // stride may exceed Hl*Wl (padded rows, as the GEMM operands need 8-element-aligned pitches).
 PyrDesc make_desc(const std::vector<at::Tensor>& levels, long rows, bool allow_bf16 = false) {
+  // level views: (rows, Hl, Wl) row-major images, or (rows, Wl/16, Hl, 16) 16-column blocks
   TORCH_CHECK(levels.size() >= 1 && levels.size() <= 4, "raft_amd: 1..4 pyramid levels supported");
   PyrDesc d{};
   d.levels = static_cast<int>(levels.size());
@@ -236,18 +239,28 @@ PyrDesc make_desc(const std::vector<at::Tensor>& levels, long rows, bool allow_b
     const auto& t = levels[l];
     check_gpu(t, "pyramid level");
     const bool bf = t.scalar_type() == at::kBFloat16;
-    TORCH_CHECK((t.scalar_type() == at::kFloat || (allow_bf16 && bf)) && t.dim() == 3 && t.stride(2) == 1 &&
-                    t.stride(1) == t.size(2) && t.stride(0) >= t.size(1) * t.size(2),
-                "raft_amd: pyramid levels must be fp32 (bf16: forward lookups only) (B*H*W, Hl, Wl) row views");
-    TORCH_CHECK(l == 0 || (bf ? 1 : 0) == d.vbf16, "raft_amd: pyramid levels must share one dtype");
+    const bool blk = t.dim() == 4;
+    TORCH_CHECK(t.scalar_type() == at::kFloat || (allow_bf16 && bf),
+                "raft_amd: pyramid levels must be fp32 (bf16: forward lookups only)");
+    if (blk) {
+      TORCH_CHECK(t.size(3) == 16 && t.stride(3) == 1 && t.stride(2) == 16 && t.stride(1) == t.size(2) * 16 &&
+                      t.stride(0) >= t.size(1) * t.size(2) * 16,
+                  "raft_amd: blocked pyramid levels must be (rows, W/16, H, 16) views");
+    } else {
+      TORCH_CHECK(t.dim() == 3 && t.stride(2) == 1 && t.stride(1) == t.size(2) && t.stride(0) >= t.size(1) * t.size(2),
+                  "raft_amd: pyramid levels must be (B*H*W, Hl, Wl) row views");
+    }
+    TORCH_CHECK(l == 0 || ((bf ? 1 : 0) == d.vbf16 && (blk ? 1 : 0) == d.blk),
+                "raft_amd: pyramid levels must share one dtype and layout");
     d.vbf16 = bf ? 1 : 0;
+    d.blk = blk ? 1 : 0;
     TORCH_CHECK(t.size(0) == rows, "raft_amd: pyramid level rows mismatch");
-    TORCH_CHECK(t.storage_offset() + (rows - 1) * t.stride(0) + t.size(1) * t.size(2) <=
-                    (long)(t.storage().nbytes() / t.element_size()),
+    const long span = blk ? t.size(1) * t.size(2) * 16 : t.size(1) * t.size(2);
+    TORCH_CHECK(t.storage_offset() + (rows - 1) * t.stride(0) + span <= (long)(t.storage().nbytes() / t.element_size()),
                 "raft_amd: pyramid level view exceeds its storage");
     d.ptr[l] = static_cast<float*>(t.data_ptr());
-    d.H[l] = static_cast<int>(t.size(1));
-    d.W[l] = static_cast<int>(t.size(2));
+    d.H[l] = static_cast<int>(blk ? t.size(2) : t.size(1));
+    d.W[l] = static_cast<int>(blk ? t.size(1) * 16 : t.size(2));
     d.ld[l] = t.stride(0);
   }
   return d;
@@ -318,7 +331,7 @@ at::Tensor gemm_nt(const at::Tensor& A, const at::Tensor& B, double alpha, at::S
 
 // out (B, H*W, C) = adjoint of the pyramid pools applied to the concatenated level rows of G
 // (B, ld, C); segs = [off, Hl, Wl] per level (level l pools 2^l x 2^l blocks).
-at::Tensor pyramid_unpool(const at::Tensor& G, int64_t H, int64_t W, at::IntArrayRef segs) {
+at::Tensor pyramid_unpool(const at::Tensor& G, int64_t H, int64_t W, at::IntArrayRef segs, bool blocked) {
   check_gpu(G, "G");
   TORCH_CHECK(G.scalar_type() == at::kFloat && G.dim() == 3 && G.is_contiguous(),
               "raft_amd::pyramid_unpool: G must be contiguous fp32 (B, rows, C)");
@@ -326,10 +339,11 @@ at::Tensor pyramid_unpool(const at::Tensor& G, int64_t H, int64_t W, at::IntArra
   UnpoolArgs u{};
   u.B = (int)G.size(0); u.C = (int)G.size(2); u.H = (int)H; u.W = (int)W;
   u.nseg = (int)(segs.size() / 3);
+  u.blk = blocked ? 1 : 0;
   for (int l = 0; l < u.nseg; ++l) {
     u.off[l] = (int)segs[3 * l]; u.h[l] = (int)segs[3 * l + 1]; u.w[l] = (int)segs[3 * l + 2];
-    TORCH_CHECK(u.off[l] >= 0 && u.h[l] <= (H >> l) && u.w[l] <= (W >> l) &&
-                    (long)u.off[l] + (long)u.h[l] * u.w[l] <= G.size(1),
+    const long span = blocked ? (long)((u.w[l] + 15) / 16) * u.h[l] * 16 : (long)u.h[l] * u.w[l];
+    TORCH_CHECK(u.off[l] >= 0 && u.h[l] <= (H >> l) && u.w[l] <= (W >> l) && (long)u.off[l] + span <= G.size(1),
                 "raft_amd::pyramid_unpool: level ", l, " does not fit");
   }
   u.G = G.data_ptr<float>();
@@ -1121,7 +1135,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def(
       "corr_gemm(Tensor A, Tensor B, Tensor(a!) C, int M, int N, int K, int batch, int lda, int sA, int ldb, int sB, "
       "int ldc, int sC, float alpha, bool a_trans, bool split, int epi) -> ()");
-  m.def("pyramid_unpool(Tensor G, int H, int W, int[] segs) -> Tensor");
+  m.def("pyramid_unpool(Tensor G, int H, int W, int[] segs, bool blocked=False) -> Tensor");
   m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");
   m.def("convex_upsample_backward(Tensor flow, Tensor mask, Tensor grad) -> (Tensor, Tensor)");
   m.def("seq_loss(Tensor[] preds, Tensor gt, Tensor valid, float gamma, float max_flow) -> Tensor");

@@ -39,7 +39,13 @@ struct PyrDesc {
   long ld[4];  // row pitch (elements) of level l: row `pix` starts at ptr[l] + pix * ld[l]
   int levels;
   int vbf16;   // levels hold bf16 (the AMP volume; forward lookups only -- gradients stay fp32)
+  int blk;     // levels stored in 16-column blocks [W/16][H][16] (W = blocks * 16)
 };
+
+// element offset of level pixel (y, x) within a volume row
+__device__ __forceinline__ int lvl_off(int y, int x, int Hl, int Wl, int blk) {
+  return blk ? ((((x >> 4) * Hl + y) << 4) | (x & 15)) : y * Wl + x;
+}
 
 // One GEMM of the correlation path: C[b][m][n] (op)= alpha * sum_k A[b][m][k] * B[b][n][k]
 struct CorrGemmArgs {
@@ -65,6 +71,7 @@ struct UnpoolArgs {
   float* out;
   int B, H, W, C, nseg;
   int off[4], h[4], w[4];
+  int blk;  // level rows in 16-column block order (the dense pyramid's layout)
 };
 
 namespace {
@@ -252,7 +259,10 @@ __global__ __launch_bounds__(256) void pyramid_unpool_kernel(const UnpoolArgs u)
     float v = 0.f, s = 1.f;
     for (int l = 0; l < u.nseg; ++l, s *= 0.25f) {
       const int yl = y >> l, xl = x >> l;
-      if (yl < u.h[l] && xl < u.w[l]) v += s * G[(long)(u.off[l] + yl * u.w[l] + xl) * u.C + c];
+      if (yl < u.h[l] && xl < u.w[l]) {
+        const int r = u.blk ? ((((xl >> 4) * u.h[l] + yl) << 4) | (xl & 15)) : yl * u.w[l] + xl;
+        v += s * G[(long)(u.off[l] + r) * u.C + c];
+      }
     }
     u.out[i] = v;
   }
@@ -280,36 +290,53 @@ __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const floa
   const bool live = pix0 < (long)B * HW;  // no early exit: the block synchronises per level
   const long pix = live ? pix0 : 0;
   const int b = pix / HW, p = pix - (long)b * HW;
-  const int rd = 2 * r + 1, nd = rd + 1, win = rd * rd;
+  const int rd = 2 * r + 1, nd = rd + 1, win = rd * rd, nn = nd * nd;
   const float cx0 = coords[(long)b * 2 * HW + p], cy0 = coords[(long)b * 2 * HW + HW + p];
   const bool finite = isfinite(cx0) && isfinite(cy0);
   OutT* o = out + pix * out_ch;
-  for (int l = 0; l < pyr.levels; ++l) {
+  // software pipeline over the levels: the neighbourhood loads of level l+1 are in flight
+  // while level l is blended (the lookup is bound by the load round trips, not by bytes)
+  float fx = 0.f, fy = 0.f, nfx = 0.f, nfy = 0.f;
+  float v[4];
+  auto issue = [&](int l, float& fxo, float& fyo) __attribute__((always_inline)) {
     const float s = 1.0f / float(1 << l);
     const float cx = finite ? cx0 * s : 0.f, cy = finite ? cy0 * s : 0.f;
     const float fx0 = safe_floor(cx), fy0 = safe_floor(cy);
-    const float fx = cx - fx0, fy = cy - fy0;
+    fxo = cx - fx0;
+    fyo = cy - fy0;
     const int xb = (int)fx0 - r, yb = (int)fy0 - r;
     const int Hl = pyr.H[l], Wl = pyr.W[l];
     const long rbase = pix * pyr.ld[l];
     const float* row = pyr.ptr[l] + rbase;
     const __bf16* rowb = reinterpret_cast<const __bf16*>(pyr.ptr[l]) + rbase;
-    for (int e = lane; e < nd * nd; e += 64) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = lane + 64 * k;
       const int a = e / nd, c = e - a * nd;  // neighbour (y = yb + a, x = xb + c)
       const int y = yb + a, x = xb + c;
-      const bool in = live && finite && (unsigned)y < (unsigned)Hl && (unsigned)x < (unsigned)Wl;
-      nb[wave][e] = in ? (pyr.vbf16 ? static_cast<float>(rowb[y * Wl + x]) : row[y * Wl + x]) : 0.f;
+      const bool in = e < nn && live && finite && (unsigned)y < (unsigned)Hl && (unsigned)x < (unsigned)Wl;
+      const int off = in ? lvl_off(y, x, Hl, Wl, pyr.blk) : 0;
+      v[k] = in ? (pyr.vbf16 ? static_cast<float>(rowb[off]) : row[off]) : 0.f;
     }
+  };
+  issue(0, fx, fy);
+  for (int l = 0; l < pyr.levels; ++l) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (lane + 64 * k < nn) nb[wave][lane + 64 * k] = v[k];
     __syncthreads();
+    if (l + 1 < pyr.levels) issue(l + 1, nfx, nfy);
     if (live)
       for (int ch = lane; ch < win; ch += 64) {
         const int ix = ch / rd, iy = ch - ix * rd;  // x-offset-major window order
         const float* n0 = nb[wave] + iy * nd + ix;
-        const float v =
+        const float val =
             (1.f - fy) * ((1.f - fx) * n0[0] + fx * n0[1]) + fy * ((1.f - fx) * n0[nd] + fx * n0[nd + 1]);
-        o[l * win + ch] = from_f32<OutT>(v);
+        o[l * win + ch] = from_f32<OutT>(val);
       }
     __syncthreads();
+    fx = nfx;
+    fy = nfy;
   }
   if (live)
     for (int ch = pyr.levels * win + lane; ch < out_ch; ch += 64) o[ch] = from_f32<OutT>(0.f);
@@ -361,7 +388,7 @@ __global__ __launch_bounds__(256) void lookup_bwd_kernel(PyrDesc dpyr, const flo
         if (c < rd) v += (1.f - fx) * fy * gw[(a - 1) * rd + c];
         if (c > 0) v += fx * fy * gw[(a - 1) * rd + c - 1];
       }
-      row[y * Wl + x] += v;
+      row[lvl_off(y, x, Hl, Wl, dpyr.blk)] += v;
     }
     __syncthreads();
   }

@@ -31,7 +31,7 @@ def register() -> None:
         return A.new_empty((A.shape[0], A.shape[1], B.shape[1]), dtype=out_dtype)
 
     @fake(lib + "pyramid_unpool")
-    def _(G, H, W, segs):
+    def _(G, H, W, segs, blocked=False):
         return G.new_empty((G.shape[0], H * W, G.shape[2]))
 
     @fake(lib + "avgpool2x2")
@@ -110,8 +110,7 @@ def register() -> None:
         B, H, W, _ = x.shape
         N, _, KH, KW = w.shape
         Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
-        bm = 256 if N in (64, 96) else 128
-        T = -(-(Ho * Wo) // bm)
+        T = -(-(Ho * Wo) // 128)  # 128-pixel conv tiles (csrc/enc_bindings.cpp kBM)
         st = x.new_empty((B, T, 2, N), dtype=torch.float32) if stats else x.new_empty((0,), dtype=torch.float32)
         return x.new_empty((B, Ho, Wo, N)), st
 

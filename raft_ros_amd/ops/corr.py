@@ -21,8 +21,10 @@ Dense path on the GPU (kernels: csrc/corr_volume.hip):
   ``dF2 = sum_l unpool_l(dL_l^T . f1)`` as GEMMs straight from the level
   gradients -- no dense HW x HW ``dC`` / ``dC^T`` is ever formed.
 
-Level rows are padded to a multiple of 8 floats (16-byte aligned GEMM rows);
-the lookup kernels take the row pitch from the view's stride.
+Each level is stored in 16-column blocks (pixel (y, x) of a level at
+((x // 16) * Hl + y) * 16 + x % 16 of the query's row) by ordering the pooled-fmap2
+GEMM operand that way: a (2r+2)^2 lookup window is then 1-2 contiguous runs instead
+of 2r+2 rows, which is what the memory-bound lookup kernels pay for.
 """
 from __future__ import annotations
 
@@ -59,7 +61,10 @@ class _PyramidState:
         self.shape = None
 
     def views(self, buf: torch.Tensor) -> List[torch.Tensor]:
-        return [buf.as_strided((buf.shape[0], Hl, Wl), (self.ld, Wl, 1), buf.storage_offset() + off)
+        # 16-column blocks: level pixel (y, x) at ((x // 16) * Hl + y) * 16 + x % 16, so a lookup
+        # window is 1-2 contiguous runs instead of 2r+2 separate rows (cache lines touched)
+        return [buf.as_strided((buf.shape[0], -(-Wl // 16), Hl, 16), (self.ld, Hl * 16, 16, 1),
+                               buf.storage_offset() + off)
                 for Hl, Wl, off in self.sizes]
 
     def grad_buffers(self) -> List[torch.Tensor]:
@@ -89,16 +94,22 @@ def _pooled(f: torch.Tensor, levels: int) -> List[torch.Tensor]:
     return out
 
 
-def _concat_levels(fs: List[torch.Tensor], ld: int, offs: List[int], nchw: bool) -> torch.Tensor:
-    """Pooled fmaps -> one zero-padded operand: (B, ld, C) (NHWC rows q) or (B, C, ld)."""
+def _concat_levels(fs: List[torch.Tensor], ld: int, offs: List[int], nchw: bool, blocked: bool = False) -> torch.Tensor:
+    """Pooled fmaps -> one zero-padded operand: (B, ld, C) (NHWC rows q) or (B, C, ld).
+    ``blocked``: each level's pixels in 16-column block order (padding columns are zero rows,
+    so their correlations are 0 -- the zero padding of the reference's grid_sample)."""
     B, C = fs[0].shape[:2]
     out = fs[0].new_zeros((B, C, ld) if nchw else (B, ld, C))
     for f, off in zip(fs, offs):
-        n = f.shape[2] * f.shape[3]
+        if blocked:
+            Hl, Wl = f.shape[2:]
+            nb = -(-Wl // 16)
+            f = F.pad(f, (0, nb * 16 - Wl)).reshape(B, C, Hl, nb, 16).permute(0, 1, 3, 2, 4)
+        n = f.shape[2] * f.shape[3] * (f.shape[4] if f.dim() == 5 else 1)
         if nchw:
             out[:, :, off:off + n] = f.reshape(B, C, n)
         else:
-            out[:, off:off + n] = f.permute(0, 2, 3, 1).reshape(B, n, C)
+            out[:, off:off + n] = f.reshape(B, C, n).permute(0, 2, 1)
     return out
 
 
@@ -115,10 +126,10 @@ class _BuildPyramid(torch.autograd.Function):
         for f in f2s:
             Hl, Wl = f.shape[-2:]
             sizes.append((Hl, Wl, off))
-            off += _pad_to(Hl * Wl, 8)
+            off += -(-Wl // 16) * 16 * Hl  # 16-column blocks (see _PyramidState.views)
         ld = off
         state.sizes, state.ld = sizes, ld
-        f2cat = _concat_levels(f2s, ld, [o for _, _, o in sizes], nchw=False)  # (B, ld, C), pad rows 0
+        f2cat = _concat_levels(f2s, ld, [o for _, _, o in sizes], nchw=False, blocked=True)  # (B, ld, C)
         # AMP (not split): the volume is stored in bf16 -- its lookups feed bf16 convs, and the
         # lookup kernels are bound by the bytes they gather; split mode keeps it fp32-faithful
         buf = torch.empty(B * HW, ld, device=f1.device, dtype=torch.float32 if split else torch.bfloat16)
@@ -144,7 +155,7 @@ class _BuildPyramid(torch.autograd.Function):
         alpha = 1.0 / math.sqrt(C)
         split = ctx.split
         f2s = _pooled(fmap2.detach().float(), state.num_levels)
-        f2t = _concat_levels(f2s, ld, [o for _, _, o in state.sizes], nchw=True)  # (B, C, ld)
+        f2t = _concat_levels(f2s, ld, [o for _, _, o in state.sizes], nchw=True, blocked=True)  # (B, C, ld)
         f1t = fmap1.detach().float().new_zeros(B, C, _pad_to(HW, 8))
         f1t[:, :, :HW] = fmap1.detach().float().reshape(B, C, HW)
         d1 = torch.empty(B, HW, C, device=fmap1.device)
@@ -156,7 +167,7 @@ class _BuildPyramid(torch.autograd.Function):
         # dF2 = sum_l unpool_l(G_l)
         k.corr_gemm(dbuf, f1t, G, ld, C, HW, B, ld, HW * ld, f1t.shape[2], C * f1t.shape[2], C, ld * C, alpha,
                     True, split, 0)
-        d2 = k.pyramid_unpool(G, H, W, state.segments())
+        d2 = k.pyramid_unpool(G, H, W, state.segments(), True)
         state.release()
         g1 = d1.view(B, H, W, C).permute(0, 3, 1, 2)
         g2 = d2.view(B, H, W, C).permute(0, 3, 1, 2)

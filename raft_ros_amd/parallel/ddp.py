@@ -60,11 +60,14 @@ def init_distributed(backend: str | None = None, device_type: str | None = None)
     return DistInfo(rank, world, local, device)
 
 
-def wrap_model(model: torch.nn.Module, info: DistInfo, bucket_cap_mb: float = 32.0, static_graph: bool = True,
+def wrap_model(model: torch.nn.Module, info: DistInfo, bucket_cap_mb: float = 10.0, static_graph: bool = True,
                bf16_grads: bool = False):
-    """DDP wrapper sized for xGMI: the whole RAFT-base gradient (21 MB fp32) fits in one
-    32 MB bucket, i.e. one ring all-reduce per step, launched as soon as backward has
-    produced it (earlier buckets overlap with the rest of backward).
+    """DDP wrapper sized for xGMI.  RAFT-base's gradient is 21 MB fp32; the update block's
+    12.5 MB are complete first (its batched weight gradients run when the last refinement
+    step's backward is done, before the encoders backpropagate), so ~10 MB buckets let that
+    part of the ring all-reduce run over xGMI while the encoder backward computes
+    (``static_graph`` orders buckets by readiness after the first step); the encoder
+    gradients follow in the last bucket.
 
     ``bf16_grads``: register the bf16 compression hook -- buckets are cast to bf16 for the
     ring all-reduce and back to fp32 (halves the bytes over the per-link-bound xGMI ring;

@@ -68,7 +68,7 @@ def train(args: Namespace) -> str:
     model.train()
     if args.stage != "chairs":
         model.freeze_bn()
-    net = ddp.wrap_model(model, info, bucket_cap_mb=getattr(args, "bucket_mb", 32.0),
+    net = ddp.wrap_model(model, info, bucket_cap_mb=getattr(args, "bucket_mb", 10.0),
                          bf16_grads=getattr(args, "ddp_bf16_grads", False))
 
     args.device = str(dev)  # batched augmentation runs on the rank's device

@@ -19,7 +19,7 @@ def test_meta_shapes_of_tensor_returning_ops():
     x = torch.empty(4, 92, 124, 64, device=m, dtype=torch.bfloat16)
     w = torch.empty(96, 64, 3, 3, device=m)
     y, st = ops.enc_conv_fwd(x, w, None, 2, 1, True)
-    assert y.shape == (4, 46, 62, 96) and st.shape == (4, -(-46 * 62 // 256), 2, 96)
+    assert y.shape == (4, 46, 62, 96) and st.shape == (4, -(-46 * 62 // 128), 2, 96)
     assert ops.enc_conv_dgrad([y], [w], [2], [1], 92, 124, None, None).shape == x.shape
     img = torch.empty(2, 3, 368, 496, device=m)
     assert ops.enc_prep(img, img).shape == (4, 368, 496, 8)

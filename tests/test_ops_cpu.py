@@ -91,3 +91,29 @@ def test_flow_viz_matches_reference(reference_core):
     assert np.array_equal(flow_viz.make_colorwheel(), mod.make_colorwheel())
     for bgr in (False, True):
         assert np.array_equal(flow_viz.flow_to_image(flow, convert_to_bgr=bgr), mod.flow_to_image(flow, convert_to_bgr=bgr))
+
+
+def test_blocked_level_layout_matches_kernel_indexing():
+    """The dense pyramid stores each level in 16-column blocks; the GEMM operand built by
+    _concat_levels must put pixel (y, x) of level l at off_l + ((x//16)*Hl + y)*16 + x%16,
+    the index the lookup / unpool kernels use (csrc/corr_volume.hip lvl_off)."""
+    import torch
+    from raft_ros_amd.ops.corr import _concat_levels
+
+    B, C = 2, 3
+    fs = [torch.randn(B, C, 7, 37), torch.randn(B, C, 3, 18)]
+    offs, off = [], 0
+    for f in fs:
+        offs.append(off)
+        off += -(-f.shape[3] // 16) * 16 * f.shape[2]
+    rows = _concat_levels(fs, off, offs, nchw=False, blocked=True)  # (B, ld, C)
+    cols = _concat_levels(fs, off, offs, nchw=True, blocked=True)   # (B, C, ld)
+    assert torch.equal(rows, cols.permute(0, 2, 1))
+    for f, o in zip(fs, offs):
+        Hl, Wl = f.shape[2:]
+        nb = -(-Wl // 16)
+        for y in range(Hl):
+            for x in range(nb * 16):
+                idx = o + ((x // 16) * Hl + y) * 16 + x % 16
+                want = f[:, :, y, x] if x < Wl else torch.zeros(B, C)
+                assert torch.equal(rows[:, idx], want), (y, x)

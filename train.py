@@ -51,7 +51,9 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--ckpt_dir", default="checkpoints")
     g.add_argument("--log_dir", default="runs")
     g.add_argument("--dataset_root", default=None, help="directory holding Sintel/, KITTI/, ... (default ./datasets)")
-    g.add_argument("--bucket_mb", type=float, default=32.0, help="DDP gradient bucket size")
+    g.add_argument("--bucket_mb", type=float, default=10.0,
+                   help="DDP gradient bucket size (10 MB: the update-block gradients all-reduce while the "
+                        "encoders backpropagate)")
     g.add_argument("--seed", type=int, default=1234)
     g.add_argument("--deterministic", action="store_true",
                    help="bitwise-reproducible steps: torch.use_deterministic_algorithms + the native kernels' "
