@@ -126,8 +126,17 @@ class RAFT(nn.Module):
             image1 = (2 * (image1 / 255.0) - 1.0).contiguous(memory_format=fmt)
             image2 = (2 * (image2 / 255.0) - 1.0).contiguous(memory_format=fmt)
 
+        cnet_native = None
         if native:
-            # both encoders on the native HIP kernels (ops/encoder.py), input normalisation fused
+            # both encoders on the native HIP kernels (ops/encoder.py), input normalisation fused;
+            # the context encoder runs on a side stream concurrently with the feature encoder
+            # (autograd replays each node's backward on its forward stream, so the two backward
+            # passes overlap as well)
+            side = self._side_stream(raw1.device)
+            main = torch.cuda.current_stream(raw1.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                cnet_native = encoder_native.encode(self.cnet, raw1)
             fmap1, fmap2 = encoder_native.encode(self.fnet, raw1, raw2).split(raw1.shape[0], dim=0)
         else:
             with self._autocast(dev):
@@ -141,8 +150,11 @@ class RAFT(nn.Module):
             # computes it in fp32 in every mode (core/raft.py:102-103)
             corr_fn = CorrPyramid(fmap1, fmap2, radius=self.args.corr_radius, split=not bool(self.args.mixed_precision))
 
+        if native:  # join the context-encoder stream (the pyramid build above overlapped it)
+            main.wait_stream(side)
+            cnet_native.record_stream(main)
         with self._autocast(dev):
-            cnet = encoder_native.encode(self.cnet, raw1) if native else self.cnet(image1)
+            cnet = cnet_native if native else self.cnet(image1)
             net, inp = torch.split(cnet, [hdim, cdim], dim=1)
             net = torch.tanh(net)
             inp = torch.relu(inp)
@@ -176,6 +188,12 @@ class RAFT(nn.Module):
         return flow_predictions
 
     # ------------------------------------------------------------------ native encoders
+    def _side_stream(self, device) -> torch.cuda.Stream:
+        streams = self.__dict__.setdefault("_side_streams", {})
+        if device not in streams:
+            streams[device] = torch.cuda.Stream(device=device)
+        return streams[device]
+
     def _use_native_encoders(self, image1, amp: bool) -> bool:
         return (amp and self.amp_dtype == torch.bfloat16 and _arg(self.args, "native_encoder", True)
                 and encoder_native.supported(self.fnet, image1) and encoder_native.supported(self.cnet, image1))

@@ -134,6 +134,17 @@ class _Run:
         B, H, W = self.dims
         return C.geom(T * B, H, W, kh, kw, kh // 2, kw // 2)
 
+    def fork(self):
+        """Side stream for the independent conv branches of a step (it first waits for the
+        main stream; every buffer it touches is allocated on the main stream beforehand).
+        With ``CONCURRENT = False`` both branches run on the main stream."""
+        main = torch.cuda.current_stream()
+        if not CONCURRENT:
+            return main, main
+        side = _side_stream(main.device)
+        side.wait_stream(main)
+        return main, side
+
     def geom_d(self, kh, kw):
         B, H, W = self.dims
         return C.geom(B, H, W, kh, kw, kh - 1 - kh // 2, kw - 1 - kw // 2)
@@ -194,6 +205,16 @@ class _Run:
         return grads
 
 
+_SIDE = {}
+CONCURRENT = False  # run a step's independent conv branches on two streams (measured: no gain, 317.6 vs 315.3 pairs/s)
+
+
+def _side_stream(device) -> torch.cuda.Stream:
+    if device not in _SIDE:
+        _SIDE[device] = torch.cuda.Stream(device=device)
+    return _SIDE[device]
+
+
 class _PackWeights(torch.autograd.Function):
     """Token node: its backward (after every step's backward) runs the batched weight grads."""
 
@@ -237,12 +258,17 @@ class _Step(torch.autograd.Function):
         k.pack_flow(coords1, flow8, motion[:, 126:], True)
 
         c1 = ar.take("c1", t, 256)
-        C.conv_fwd([corr], run.wf["convc1"], g(1, 1), 256, c1, bias=run.bias["convc1"], act=1)
         cf = ar.take("cf", t, 256)
-        C.conv_fwd([c1], run.wf["convc2"], g(3, 3), 192, cf[:, :192], bias=run.bias["convc2"], act=1)
         f1 = ar.take("f1", t, 128)
-        C.conv_fwd([flow8], run.wf["convf1"], g(7, 7), 128, f1, bias=run.bias["convf1"], act=1)
-        C.conv_fwd([f1], run.wf["convf2"], g(3, 3), 64, cf[:, 192:], bias=run.bias["convf2"], act=1)
+        # the flow branch (convf1 -> convf2) runs beside the correlation branch (convc1 -> convc2):
+        # neither launch fills the 256 CUs on its own
+        main, side = run.fork()
+        with torch.cuda.stream(side):
+            C.conv_fwd([flow8], run.wf["convf1"], g(7, 7), 128, f1, bias=run.bias["convf1"], act=1)
+            C.conv_fwd([f1], run.wf["convf2"], g(3, 3), 64, cf[:, 192:], bias=run.bias["convf2"], act=1)
+        C.conv_fwd([corr], run.wf["convc1"], g(1, 1), 256, c1, bias=run.bias["convc1"], act=1)
+        C.conv_fwd([c1], run.wf["convc2"], g(3, 3), 192, cf[:, :192], bias=run.bias["convc2"], act=1)
+        main.wait_stream(side)
         C.conv_fwd([cf], run.wf["conv"], g(3, 3), 126, motion, bias=run.bias["conv"], act=1)
 
         inp = run.inp_bf
@@ -261,9 +287,12 @@ class _Step(torch.autograd.Function):
         hd = ar.take("hd", t, 512)
         C.conv_fwd([h], run.wf["heads"], g(3, 3), 512, hd, bias=run.bias["heads"], act=1)
         delta = torch.empty(P, 8, device=dev, dtype=torch.float32)
-        C.conv_fwd([hd[:, :256]], run.wf["fh2"], g(3, 3), 2, delta, bias=run.bias["fh2"])
         mask = ar.take("mask", t, 576)
+        main, side = run.fork()  # flow-head conv2 beside the mask head's 1x1
+        with torch.cuda.stream(side):
+            C.conv_fwd([hd[:, :256]], run.wf["fh2"], g(3, 3), 2, delta, bias=run.bias["fh2"])
         C.conv_fwd([hd[:, 256:]], run.wf["mask2"], g(1, 1), 576, mask, bias=run.bias["mask2"])
+        main.wait_stream(side)
 
         coords_out = torch.empty_like(coords1)
         flow = torch.empty_like(coords1)
@@ -307,8 +336,11 @@ class _Step(torch.autograd.Function):
             dmask.zero_()
             dd8.zero_()
         dhd = ar.take("dhd", t, 512)
+        main, side = run.fork()
+        with torch.cuda.stream(side):
+            dgrad("fh2", dd8, 3, 3, dhd[:, :256], 256, mask=hd[:, :256])
         dgrad("mask2", dmask, 1, 1, dhd[:, 256:], 256, mask=hd[:, 256:])
-        dgrad("fh2", dd8, 3, 3, dhd[:, :256], 256, mask=hd[:, :256])
+        main.wait_stream(side)
         dh = torch.empty(P, HID, device=dev, dtype=torch.float32)
         if g_net is not None:
             dh.copy_(_pm(g_net))
@@ -342,11 +374,14 @@ class _Step(torch.autograd.Function):
         dcf = ar.take("dcf", t, 256)
         dgrad("conv", dmo, 3, 3, dcf, 256, mask=cf)
         dc1 = ar.take("dc1", t, 256)
-        dgrad("convc2", dcf[:, :192], 3, 3, dc1, 256, mask=c1)
         dcorr = torch.empty(P, CORR_PAD, device=dev, dtype=bf)
-        dgrad("convc1", dc1, 1, 1, dcorr, CORR_PAD)
         df1 = ar.take("df1", t, 128)
-        dgrad("convf2", dcf[:, 192:], 3, 3, df1, 128, mask=f1)
+        main, side = run.fork()  # flow-branch dgrad beside the correlation-branch chain
+        with torch.cuda.stream(side):
+            dgrad("convf2", dcf[:, 192:], 3, 3, df1, 128, mask=f1)
+        dgrad("convc2", dcf[:, :192], 3, 3, dc1, 256, mask=c1)
+        dgrad("convc1", dc1, 1, 1, dcorr, CORR_PAD)
+        main.wait_stream(side)
         run.done.add(t)
 
         d_corr_in = None
