@@ -12,6 +12,7 @@ Rendezvous always uses 127.0.0.1 unless MASTER_ADDR says otherwise.
 """
 from __future__ import annotations
 
+import datetime
 import os
 import socket
 from dataclasses import dataclass
@@ -43,8 +44,19 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+DEFAULT_TIMEOUT_S = 600.0
+
+
+def collective_timeout() -> datetime.timedelta:
+    """Failure detection: a collective that does not complete within ``RAFT_DIST_TIMEOUT``
+    seconds (default 600) raises on the ranks that are still alive instead of hanging the
+    job forever (a dead or stuck peer; see utils/fault.py for the injection hooks)."""
+    return datetime.timedelta(seconds=float(os.environ.get("RAFT_DIST_TIMEOUT", DEFAULT_TIMEOUT_S)))
+
+
 def init_distributed(backend: str | None = None, device_type: str | None = None) -> DistInfo:
-    """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*)."""
+    """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*),
+    with the collective timeout of :func:`collective_timeout`."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -56,7 +68,7 @@ def init_distributed(backend: str | None = None, device_type: str | None = None)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = backend or ("nccl" if use_cuda else "gloo")
         kw = {"device_id": device} if use_cuda else {}
-        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+        dist.init_process_group(backend, rank=rank, world_size=world, timeout=collective_timeout(), **kw)
     return DistInfo(rank, world, local, device)
 
 

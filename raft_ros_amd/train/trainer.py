@@ -30,7 +30,7 @@ from ..data.datasets import fetch_dataloader
 from ..eval.validate import run_validation
 from ..models import RAFT
 from ..parallel import ddp
-from ..utils import checkpoint
+from ..utils import checkpoint, fault
 from ..utils.profiling import maybe_profiler, trace_range
 from .logger import Logger
 from .loss import sequence_loss
@@ -94,10 +94,12 @@ def train(args: Namespace) -> str:
     set_epoch = sampler.set_epoch if hasattr(sampler, "set_epoch") else None
     skipped = torch.zeros((), device=dev)
     fused_opt = bool(optimizer.defaults.get("fused"))
+    injector = fault.Injector.from_env(info.rank)  # RAFT_FAULT_INJECT (tests only)
     t0 = time.perf_counter()
     prof = maybe_profiler(getattr(args, "profile_dir", None))
     profiler = prof.__enter__()
     for data_blob in _infinite(train_loader, set_epoch):
+        injector.before_step(total_steps)
         optimizer.zero_grad(set_to_none=True)
         image1, image2, flow, valid = [x.to(dev, non_blocking=True) for x in data_blob]
         if args.add_noise:
@@ -108,6 +110,7 @@ def train(args: Namespace) -> str:
         with trace_range("forward"):
             flow_predictions = net(image1, image2, iters=args.iters)
             loss, metrics = sequence_loss(flow_predictions, flow, valid, args.gamma)
+            loss = injector.on_loss(total_steps, loss)
         with trace_range("backward"):
             scaler.scale(loss).backward()
         scaler.unscale_(optimizer)

@@ -33,7 +33,10 @@ if [ "${PROFILE:-1}" = "1" ]; then
   TAG=${TAG:-native}
   run rocprof_$TAG 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 bench.py --steps 4 --warmup 3 ${PROF_ARGS:-}
   python scripts/kernel_summary.py $OUT/prof_$TAG/run_kernel_trace.csv --boundary "${BOUNDARY:-seq_loss_fwd}" --every "${EVERY:-1}" --skip 3 --out $OUT/prof_$TAG/steady_summary.csv > $OUT/prof_$TAG/steady_summary.txt 2>&1
+  KPS=$(head -1 $OUT/prof_$TAG/steady_summary.txt | sed -n 's/.*kernels\/step=\([0-9]*\).*/\1/p')
+  [ -n "$KPS" ] && python scripts/kernel_timeline.py $OUT/prof_$TAG/run_kernel_trace.csv --per-step "$KPS" --list > $OUT/prof_$TAG/steady_timeline.txt 2>&1
+  python scripts/kernel_shapes.py $OUT/prof_$TAG/run_kernel_trace.csv --steps 4 --top 60 > $OUT/prof_$TAG/steady_shapes.txt 2>&1
   # keep only the summaries (the per-dispatch trace is too large to ship back)
-  find $OUT/prof_$TAG -type f ! -name '*stats*' ! -name 'steady_summary*' -delete
+  find $OUT/prof_$TAG -type f ! -name '*stats*' ! -name 'steady_*' -delete
 fi
 echo "done"
