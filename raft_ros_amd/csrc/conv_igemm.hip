@@ -435,10 +435,11 @@ __device__ __forceinline__ void fwd4_issue(const Fwd4Src& src, const __amdgpu_bu
 // Shared epilogue of the forward kernels: the fp32 accumulators go through an LDS tile
 // (et, BM x (BN+4) floats) so each thread finishes 8 consecutive output channels of one
 // pixel with 16-byte accesses; applies alpha/bias and the fused epilogue selected by a.epi.
-template <int BM, int BN, int TM, int TN>
+template <int BM, int BN, int TM, int TN, int NW = 4>
 __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f32x16 (&acc)[TM][TN], int m0,
                                              int n0, int P, int Nn) {
   constexpr int EPI_LD = BN + 4;  // fp32 epilogue tile row pitch
+  constexpr int NT = NW * 64;     // threads; waves are laid out (NW/2) x 2 over the tile
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
 #pragma unroll
@@ -447,14 +448,14 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int row = wm * (BM / (NW / 2)) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const int col = wn * (BN / 2) + j * 32 + (lane & 31);
         et[row * EPI_LD + col] = acc[i][j][r];
       }
   __syncthreads();
   constexpr int CPR = BN / 8;  // 8-channel chunks per tile row
-  static_assert(256 % CPR == 0, "a thread keeps one channel chunk across rows");
-  // every thread owns the same 8-channel chunk in all of its rows (256 % CPR == 0): the
+  static_assert(NT % CPR == 0, "a thread keeps one channel chunk across rows");
+  // every thread owns the same 8-channel chunk in all of its rows (NT % CPR == 0): the
   // bias is loaded once, before the row loop, instead of as a dependent load per row
   const int ch = tid % CPR;
   const int n = n0 + ch * 8;
@@ -465,7 +466,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
   for (int q = 0; q < 8; ++q) bia[q] = (a.bias && q < nv) ? a.bias[n + q] : 0.f;
   const float alpha = a.alpha;
 #pragma unroll 2
-  for (int row = tid / CPR; row < BM; row += 256 / CPR) {
+  for (int row = tid / CPR; row < BM; row += NT / CPR) {
     const long p = m0 + row;
     if (p >= P) break;
     const f32x4 lo = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8);
@@ -707,11 +708,16 @@ typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8;
 // 16-byte LDS read at a 32-bit LDS byte address
 __device__ __forceinline__ bf16x8 lds_read16(unsigned addr) { return *(const lds_bf16x8*)(uintptr_t)addr; }
 
-template <int BM, int BN>
-__global__ __launch_bounds__(256) void conv_fwd5_kernel(const ConvFwdArgs a, int strip_rows) {
+template <int BM, int BN, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void conv_fwd5_kernel(const ConvFwdArgs a, int strip_rows) {
   extern __shared__ __attribute__((aligned(1024))) __bf16 dsm[];
-  constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int BI = BN / 32;  // weight wave-instructions (8 rows each) per wave per step
+  // NW waves in an (NW/2) x 2 layout; NW = 8 puts two waves on every SIMD of the CU (one
+  // workgroup per CU when the strip ring fills the LDS), so one wave's LDS reads and waits
+  // overlap the other's MFMAs
+  constexpr int WGM = NW / 2;
+  constexpr int TM = BM / (32 * WGM), TN = BN / 64;
+  constexpr int BI = BN / (8 * NW);  // weight wave-instructions (8 rows each) per wave per step
+  static_assert(TM >= 1 && BI >= 1, "tile too small for the wave count");
   constexpr int BSTAGE = BN * 64;
   const int strip_elems = strip_rows * 64;
   __bf16* const strips = dsm;
@@ -751,7 +757,7 @@ __global__ __launch_bounds__(256) void conv_fwd5_kernel(const ConvFwdArgs a, int
   int frow[TM], fpy[TM], fpx[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    frow[i] = wm * (BM / 2) + i * 32 + fr;
+    frow[i] = wm * (BM / WGM) + i * 32 + fr;
     const int p = m0 + frow[i];
     if (p < P) {
       const int rem = p % (H * W);
@@ -795,7 +801,7 @@ __global__ __launch_bounds__(256) void conv_fwd5_kernel(const ConvFwdArgs a, int
         rs = r1; st = st1; soff = (unsigned)(c0 - sc0) * 2;
       }
       __bf16* sbuf = strips + (is_cc & 1) * strip_elems;
-      for (int q = wave; q < strip_instr; q += 4) {
+      for (int q = wave; q < strip_instr; q += NW) {
         const int row = q * 8 + lrow;
         const int p = m0 - halo_lo + row;
         const unsigned voff = (p >= 0 && p < P) ? (unsigned)p * st + (unsigned)(swz(row, lpc) * 16) : kOOB;
@@ -896,7 +902,7 @@ __global__ __launch_bounds__(256) void conv_fwd5_kernel(const ConvFwdArgs a, int
   wait_vmcnt<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  fwd_epilogue<BM, BN, TM, TN>(a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn);
+  fwd_epilogue<BM, BN, TM, TN, NW>(a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn);
 }
 
 // raise a kernel's dynamic-LDS limit once (it only ever grows)
@@ -1522,14 +1528,21 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   for (int i = 0; i < a.nsrc; ++i) ok5 = ok5 && a.src[i].C % 64 == 0;
   int v5 = cfg >= 20 ? cfg : 0;
   if (ok5 && v5 == 0 && cfg == 0) {
+    // 8-wave tiles (two waves per SIMD, no register spills) for every shape they win on
+    // (scripts/bench_convs.py, profiles/r2_bench_convs_nw.log): 3x3 with N >= 192 -> 256x128,
+    // 3x3 with 64 < N < 192 -> 128x128; 1x5/5x1: the 1x5 z||r forward (N = 256) -> 128x256,
+    // the 5x1 one (4-row halo), the q forwards and the z||r data gradients -> 128x128; the q
+    // data gradients (128 input channels) stay on v4
     const int taps = a.KH * a.KW;
-    if (taps == 9 && a.N >= 192) v5 = 23;
-    else if (taps == 9 && a.N > 64) v5 = 21;
-    else if (a.KH == 1 && a.KW == 5 && a.Cin >= 384 && a.N >= 256) v5 = 22;
+    if (taps == 9 && a.N >= 192) v5 = 24;
+    else if (taps == 9 && a.N > 64) v5 = 25;
+    else if (taps == 5 && a.KH == 1 && a.Cin >= 384 && a.N == 256) v5 = 26;
+    else if (taps == 5 && a.Cin >= 256) v5 = 25;
   }
   if (ok5 && v5 >= 20) {
-    auto bm_of = [](int v) { return v == 20 ? 64 : v == 23 ? 256 : 128; };
-    auto bn_of = [](int v) { return v == 22 ? 256 : 128; };
+    // 20..23: 4 waves per workgroup; 24..26: the 256x128 / 128x128 / 128x256 tiles with 8 waves
+    auto bm_of = [](int v) { return v == 20 ? 64 : (v == 23 || v == 24) ? 256 : 128; };
+    auto bn_of = [](int v) { return (v == 22 || v == 26) ? 256 : 128; };
     auto rows_of = [&](int v) { return (bm_of(v) + (a.KH - 1) * a.W + a.KW - 1 + 7) / 8 * 8; };
     long lds = fwd5_lds_bytes(bm_of(v5), bn_of(v5), rows_of(v5));
     if (lds == 0 && v5 != 21) {
@@ -1551,6 +1564,18 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
         case 22:
           set_lds_limit((const void*)conv_fwd5_kernel<128, 256>, (int)lds);
           hipLaunchKernelGGL((conv_fwd5_kernel<128, 256>), grid, dim3(256), lds, s, a, rows);
+          break;
+        case 24:
+          set_lds_limit((const void*)conv_fwd5_kernel<256, 128, 8>, (int)lds);
+          hipLaunchKernelGGL((conv_fwd5_kernel<256, 128, 8>), grid, dim3(512), lds, s, a, rows);
+          break;
+        case 25:
+          set_lds_limit((const void*)conv_fwd5_kernel<128, 128, 8>, (int)lds);
+          hipLaunchKernelGGL((conv_fwd5_kernel<128, 128, 8>), grid, dim3(512), lds, s, a, rows);
+          break;
+        case 26:
+          set_lds_limit((const void*)conv_fwd5_kernel<128, 256, 8>, (int)lds);
+          hipLaunchKernelGGL((conv_fwd5_kernel<128, 256, 8>), grid, dim3(512), lds, s, a, rows);
           break;
         default:
           set_lds_limit((const void*)conv_fwd5_kernel<128, 128>, (int)lds);

@@ -26,6 +26,8 @@ SHAPES = {
     "conv": ([(256, 256)], 126, 3, 3),
     "zr": ([(384, 384)], 256, 1, 5),
     "q": ([(384, 384)], 128, 5, 1),
+    "zr51": ([(384, 384)], 256, 5, 1),
+    "q15": ([(384, 384)], 128, 1, 5),
     "heads": ([(128, 128)], 512, 3, 3),
     "fh2": ([(256, 256)], 2, 3, 3),
     "mask2": ([(256, 256)], 576, 1, 1),
@@ -101,6 +103,11 @@ def main():
         gy = torch.randn_like(yt)
         tmb = timeit(lambda: torch.autograd.grad(yt, (xt, wtt, bt), gy, retain_graph=True))
         line.append(f"| miopen fwd {tmf:7.1f}us bwd(d+w) {tmb:7.1f}us")
+        # same-FLOP plain GEMM through hipBLASLt (torch.mm): what a tuned library reaches at this M,N,K
+        am = torch.randn(P, cin * kh * kw, device=dev).bfloat16()
+        bm = torch.randn(cin * kh * kw, cout, device=dev).bfloat16()
+        tg = timeit(lambda: torch.mm(am, bm))
+        line.append(f"| blas gemm {tg:7.1f}us ({2 * macs / tg / 1e6:5.0f}TF)")
         print("  ".join(line), flush=True)
         tot.setdefault("ours_fwd", 0.0)
         tot["ours_fwd"] = tot["ours_fwd"] + tf
