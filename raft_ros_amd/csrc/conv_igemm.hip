@@ -1195,7 +1195,7 @@ struct WG3Geo {
 };
 
 template <int KH, int KW, int TH, int TW, int MT, int S>
-__global__ __launch_bounds__(256) void conv_wgrad3_kernel(const ConvWgradArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv_wgrad3_kernel(const ConvWgradArgs a) {
   using G3 = WG3Geo<KH, KW, TH, TW>;
   static_assert(TH * TW == 64, "64-pixel tiles");
   static_assert(TW % 4 == 0, "4 consecutive tile pixels share a tile row (transposed-read rows)");
@@ -1615,10 +1615,10 @@ inline bool wgrad3_shape(int KH, int KW) {
 // Split count: ~one round of workgroups over the 256 CUs.  When a whole number of splits per
 // XCD fills >= 7/8 of its 32 CUs, every tile of a split runs on one XCD (its rows are fetched
 // into that XCD's L2 once); otherwise splits are interleaved over the chip.
-inline void choose_splits(long tiles, long work_units, long& splits, long& g) {
-  g = 32 / tiles;
-  if (g * tiles < 28) g = 0;
-  splits = g > 0 ? 8 * g : std::max(1L, (256 + tiles / 2) / tiles);
+inline void choose_splits(long tiles, long work_units, long& splits, long& g, long target = 256) {
+  g = (target / 8) / tiles;
+  if (g * tiles < (target / 8) * 7 / 8) g = 0;
+  splits = g > 0 ? 8 * g : std::max(1L, (target + tiles / 2) / tiles);
   if (splits > work_units) splits = work_units, g = 0;
   if (splits < 1) splits = 1;
 }
@@ -1627,7 +1627,11 @@ WgradPlan plan_conv_wgrad3(const ConvWgradArgs& a) {
   WgradPlan pl{};
   pl.kind = 3;
   const bool sq = a.KH == 3;
-  pl.BM = sq ? 64 : (a.N > 64 ? 128 : 64);
+  // 64 output channels per workgroup and ~2 workgroups per CU: the kernel is built for two
+  // waves per SIMD (amdgpu_waves_per_eu(2)), which hides the DMA / transposed-read latency
+  // that bound the one-wave 128-channel variant (scripts/bench_convs.py on MI355X: 3x3
+  // wgrads 1.2-1.3x faster, 1x5/5x1 1.05-1.1x)
+  pl.BM = 64;
   pl.BN = 64 * a.KH * a.KW;
   pl.tilesM = (a.N + pl.BM - 1) / pl.BM;
   pl.tilesN = a.Cin / 64;
@@ -1635,7 +1639,7 @@ WgradPlan plan_conv_wgrad3(const ConvWgradArgs& a) {
   const int TH = sq ? 8 : (a.KH == 5 ? 16 : 1), TW = 64 / TH;
   const long ntiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
   long splits, g;
-  choose_splits((long)pl.tilesM * pl.tilesN, ntiles, splits, g);
+  choose_splits((long)pl.tilesM * pl.tilesN, ntiles, splits, g, 512);
   long per = (ntiles + splits - 1) / splits;
   if ((ntiles + per - 1) / per != splits) g = 0;
   pl.nsplit = (int)((ntiles + per - 1) / per);
@@ -1677,12 +1681,8 @@ hipError_t launch_conv_wgrad(ConvWgradArgs a, const WgradPlan& pl, hipStream_t s
   if (pl.kind == 3) {
     if (a.KH == 3)
       hipLaunchKernelGGL((conv_wgrad3_kernel<3, 3, 8, 8, 1, 3>), grid, dim3(256), 0, s, a);
-    else if (a.KH == 5 && pl.BM == 128)
-      hipLaunchKernelGGL((conv_wgrad3_kernel<5, 1, 16, 4, 2, 3>), grid, dim3(256), 0, s, a);
     else if (a.KH == 5)
       hipLaunchKernelGGL((conv_wgrad3_kernel<5, 1, 16, 4, 1, 3>), grid, dim3(256), 0, s, a);
-    else if (pl.BM == 128)
-      hipLaunchKernelGGL((conv_wgrad3_kernel<1, 5, 1, 64, 2, 3>), grid, dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL((conv_wgrad3_kernel<1, 5, 1, 64, 1, 3>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
