@@ -153,6 +153,20 @@ struct ConvFwdArgs {
   long z_stride;
   void* out2;
   long out2_stride;
+  const void* g0;
+  long g0_stride;
+  float* carry;
+  long carry_stride;
+  void* out3;
+  long out3_stride;
+  int gru_cols;
+  const void* addsrc;
+  long addsrc_stride;
+  void* cout;
+  long cout_stride;
+  const void* cmask;
+  long cmask_stride;
+  int cm_c0, cm_valid;
   int cfg;
 };
 struct ConvWgradArgs {
@@ -758,7 +772,11 @@ int fill_srcs(at::TensorList srcs, long P, ConvSrc* out, bool allow_period) {
 void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, int64_t N, const c10::optional<at::Tensor>& bias,
               int64_t epi, int64_t act, double alpha, const at::Tensor& out, int64_t acc_c0,
               const c10::optional<at::Tensor>& mask, const c10::optional<at::Tensor>& h,
-              const c10::optional<at::Tensor>& z, const c10::optional<at::Tensor>& out2, int64_t cfg) {
+              const c10::optional<at::Tensor>& z, const c10::optional<at::Tensor>& out2, int64_t cfg,
+              const c10::optional<at::Tensor>& g0, const c10::optional<at::Tensor>& carry,
+              const c10::optional<at::Tensor>& out3, int64_t gru_cols, const c10::optional<at::Tensor>& addsrc,
+              const c10::optional<at::Tensor>& cout, const c10::optional<at::Tensor>& cmask, int64_t cm_c0,
+              int64_t cm_valid) {
   TORCH_CHECK(geom.size() == 7, "raft_amd conv_fwd: geom = (B, H, W, KH, KW, PH, PW)");
   ConvFwdArgs a{};
   a.B = geom[0]; a.H = geom[1]; a.W = geom[2]; a.KH = geom[3]; a.KW = geom[4]; a.PH = geom[5]; a.PW = geom[6];
@@ -789,7 +807,7 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
   a.out_stride = out.stride(0);
   a.out_f32 = out.scalar_type() == at::kFloat;
   TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "raft_amd conv_fwd: out dtype");
-  if (epi >= 2) TORCH_CHECK(!a.out_f32, "raft_amd conv_fwd: GRU epilogues write bf16");
+  if (epi == 2 || epi == 3) TORCH_CHECK(!a.out_f32, "raft_amd conv_fwd: GRU epilogues write bf16");
   if (mask) {
     check_pm(*mask, "mask", a.P);
     a.mask = mask->data_ptr();
@@ -812,6 +830,54 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
   }
   if (epi == 2) TORCH_CHECK(h && out2 && N % 2 == 0, "raft_amd conv_fwd: GRU z||r epilogue needs h, out2");
   if (epi == 3) TORCH_CHECK(h && z && out2, "raft_amd conv_fwd: GRU blend epilogue needs h, z, out2");
+  if (epi >= 4) {
+    // fused GRU backward: fp32 gradient rows, bf16 gate tensors, fp32 carry; every operand is
+    // accessed as 8 channels (16 or 32 bytes) per pixel
+    TORCH_CHECK(epi <= 6 && a.out_f32 && N % 8 == 0, "raft_amd conv_fwd: GRU backward epilogue needs fp32 out");
+    TORCH_CHECK(gru_cols > 0 && gru_cols % 8 == 0 && gru_cols <= N, "raft_amd conv_fwd: gru_cols");
+    auto al16 = [](const void* ptr) { return ptr == nullptr || reinterpret_cast<uintptr_t>(ptr) % 16 == 0; };
+    auto bf_rows = [&](const c10::optional<at::Tensor>& t, const char* what, const void*& ptr, long& stride) {
+      TORCH_CHECK(t.has_value(), "raft_amd conv_fwd: GRU backward epilogue needs ", what);
+      check_pm(*t, what, a.P);
+      TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->stride(0) % 8 == 0 && al16(t->data_ptr()),
+                  "raft_amd conv_fwd: ", what, " must be bf16 with 16-byte aligned rows");
+      ptr = t->data_ptr();
+      stride = t->stride(0);
+    };
+    const void* tmp = nullptr;
+    bf_rows(out3, "out3", tmp, a.out3_stride);
+    a.out3 = const_cast<void*>(tmp);
+    a.gru_cols = static_cast<int>(gru_cols);
+    if (epi == 4 || epi == 5) {
+      bf_rows(h, "h", a.h, a.h_stride);
+      bf_rows(g0, "g0", a.g0, a.g0_stride);
+      TORCH_CHECK(carry.has_value() && carry->scalar_type() == at::kFloat && carry->dim() == 2 &&
+                      carry->size(0) >= a.P && carry->size(1) >= gru_cols && carry->stride(1) == 1 &&
+                      carry->stride(0) % 4 == 0 && al16(carry->data_ptr()),
+                  "raft_amd conv_fwd: carry must be fp32 [P, >=gru_cols] with 16-byte aligned rows");
+      a.carry = carry->data_ptr<float>();
+      a.carry_stride = carry->stride(0);
+    }
+    if (epi == 4) {
+      bf_rows(z, "z", a.z, a.z_stride);
+      tmp = nullptr;
+      bf_rows(out2, "out2", tmp, a.out2_stride);
+      a.out2 = const_cast<void*>(tmp);
+      if (addsrc) bf_rows(addsrc, "addsrc", a.addsrc, a.addsrc_stride);
+    }
+    if (epi == 6) {
+      TORCH_CHECK(cm_c0 >= gru_cols && cm_c0 % 8 == 0 && cm_c0 <= N && cm_valid >= 0, "raft_amd conv_fwd: cm_c0");
+      tmp = nullptr;
+      bf_rows(cout, "cout", tmp, a.cout_stride);
+      a.cout = const_cast<void*>(tmp);
+      bf_rows(cmask, "cmask", a.cmask, a.cmask_stride);
+      const int64_t cw = std::min<int64_t>(N - cm_c0, (cm_valid + 7) / 8 * 8);  // columns stored / read
+      TORCH_CHECK(cout->size(1) >= cw && cmask->size(1) >= cw, "raft_amd conv_fwd: cout / cmask width");
+      a.cm_c0 = static_cast<int>(cm_c0);
+      a.cm_valid = static_cast<int>(cm_valid);
+    }
+    TORCH_CHECK(a.out_stride % 4 == 0 && al16(a.out), "raft_amd conv_fwd: out needs 16-byte aligned rows");
+  }
   const c10::DeviceGuard guard(wt.device());
   HIP_OK(launch_conv_fwd(a, cur_stream()));
 }
@@ -1109,7 +1175,9 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("instance_norm_bwd(Tensor x, Tensor dy, Tensor stats, bool relu) -> Tensor");
   m.def(
       "conv_fwd(Tensor[] srcs, Tensor wt, int[] geom, int N, Tensor? bias, int epi, int act, float alpha, "
-      "Tensor(a!) out, int acc_c0, Tensor? mask, Tensor? h, Tensor? z, Tensor(b!)? out2, int cfg=0) -> ()");
+      "Tensor(a!) out, int acc_c0, Tensor? mask, Tensor? h, Tensor? z, Tensor(b!)? out2, int cfg=0, "
+      "Tensor? g0=None, Tensor(c!)? carry=None, Tensor(d!)? out3=None, int gru_cols=0, Tensor? addsrc=None, "
+      "Tensor(e!)? cout=None, Tensor? cmask=None, int cm_c0=0, int cm_valid=0) -> ()");
   m.def("conv_wgrad(Tensor[] srcs, Tensor dy, int[] geom, int N, Tensor(a!) dw, Tensor(b!)? db, "
         "bool accumulate=True) -> ()");
   m.def("conv_wgrad_params(Tensor[] srcs, Tensor dy, int[] geom, Tensor(a!)[] wgrad, Tensor?[] bgrad, int[] segs, "

@@ -66,8 +66,30 @@ struct ConvFwdArgs {
   long h_stride;
   const __bf16* z;  // epi 3: update gate
   long z_stride;
-  __bf16* out2;  // epi 2: r*h, epi 3: tanh(q)
+  __bf16* out2;  // epi 2: r*h, epi 3: tanh(q), epi 4: dq
   long out2_stride;
+  // fused GRU backward (data-gradient launches of the update block): output channels
+  // [0, gru_cols) finish the gate math in the epilogue, the rest are stored as epi 1
+  //   epi 4 (after the dH-producing dgrad): g = dH; dq = g z (1 - q^2) -> out2,
+  //          dz = g (q - h) z (1 - z) -> out3, carry = g (1 - z)  (out not written)
+  //   epi 5 (the q dgrad, g = d(r*h)): dr = g h r (1 - r) -> out3, out = carry + g r
+  //   epi 6 (the last GRU dgrad): channels [0, gru_cols) -> bf16 out3 (d net), [gru_cols,
+  //          cm_c0) -> out as epi 1, [cm_c0, N) -> bf16 cout = (cmask > 0 ? g : 0), zero past
+  //          cm_valid (the ReLU' of the motion features; out not written)
+  const __bf16* g0;  // epi 4: q, epi 5: r
+  long g0_stride;
+  float* carry;
+  long carry_stride;
+  __bf16* out3;
+  long out3_stride;
+  int gru_cols;
+  const __bf16* addsrc;  // epi 4: incoming bf16 gradient added to g (null: none)
+  long addsrc_stride;
+  __bf16* cout;
+  long cout_stride;
+  const __bf16* cmask;
+  long cmask_stride;
+  int cm_c0, cm_valid;
   int cfg;  // kernel variant: 0 = automatic, otherwise forced (tests / microbenchmarks)
 };
 
@@ -465,6 +487,10 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
 #pragma unroll
   for (int q = 0; q < 8; ++q) bia[q] = (a.bias && q < nv) ? a.bias[n + q] : 0.f;
   const float alpha = a.alpha;
+  // this thread's 8 channels: the GRU-backward epilogues cover [0, gru_cols), epi 1 the rest
+  int epi = a.epi;
+  if (epi == 4 || epi == 5) epi = n < a.gru_cols ? epi : 1;
+  else if (epi == 6) epi = (n < a.gru_cols || n >= a.cm_c0) ? 6 : 1;
 #pragma unroll 2
   for (int row = tid / CPR; row < BM; row += NT / CPR) {
     const long p = m0 + row;
@@ -474,7 +500,79 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
     float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] = v[q] * alpha + bia[q];
-    if (a.epi == 0) {
+    if (epi == 4 || epi == 5) {
+      // fused GRU backward gate math (fp32 gradient rows; gru_cols is a multiple of 8)
+      float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
+      if (n >= a.acc_c0) {
+        const f32x4 o0 = *reinterpret_cast<const f32x4*>(o), o1 = *reinterpret_cast<const f32x4*>(o + 4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[q] += o0[q];
+          v[q + 4] += o1[q];
+        }
+      }
+      if (a.addsrc) {
+        const bf16x8 av = *reinterpret_cast<const bf16x8*>(a.addsrc + p * a.addsrc_stride + n);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] += static_cast<float>(av[q]);
+      }
+      const bf16x8 gv = *reinterpret_cast<const bf16x8*>(a.g0 + p * a.g0_stride + n);
+      const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + n);
+      float* cp = a.carry + p * a.carry_stride + n;
+      bf16x8 d3;
+      if (epi == 4) {
+        const bf16x8 zv = *reinterpret_cast<const bf16x8*>(a.z + p * a.z_stride + n);
+        bf16x8 dq;
+        float cr[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float zz = static_cast<float>(zv[q]), qq = static_cast<float>(gv[q]), hh = static_cast<float>(hv[q]);
+          dq[q] = static_cast<__bf16>(v[q] * zz * (1.f - qq * qq));
+          d3[q] = static_cast<__bf16>(v[q] * (qq - hh) * zz * (1.f - zz));
+          cr[q] = v[q] * (1.f - zz);
+        }
+        *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + n) = dq;
+        *reinterpret_cast<f32x4*>(cp) = f32x4{cr[0], cr[1], cr[2], cr[3]};
+        *reinterpret_cast<f32x4*>(cp + 4) = f32x4{cr[4], cr[5], cr[6], cr[7]};
+      } else {
+        const f32x4 c0 = *reinterpret_cast<const f32x4*>(cp), c1 = *reinterpret_cast<const f32x4*>(cp + 4);
+        const float cv[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+        float ov[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float rr = static_cast<float>(gv[q]), hh = static_cast<float>(hv[q]);
+          d3[q] = static_cast<__bf16>(v[q] * hh * rr * (1.f - rr));
+          ov[q] = cv[q] + v[q] * rr;
+        }
+        *reinterpret_cast<f32x4*>(o) = f32x4{ov[0], ov[1], ov[2], ov[3]};
+        *reinterpret_cast<f32x4*>(o + 4) = f32x4{ov[4], ov[5], ov[6], ov[7]};
+      }
+      *reinterpret_cast<bf16x8*>(a.out3 + p * a.out3_stride + n) = d3;
+    } else if (epi == 6) {
+      // last GRU data gradient: bf16 d net / fp32 d inp / masked bf16 d motion
+      const float* o = static_cast<const float*>(a.out) + p * a.out_stride + n;
+      const f32x4 o0 = *reinterpret_cast<const f32x4*>(o), o1 = *reinterpret_cast<const f32x4*>(o + 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[q] += o0[q];
+        v[q + 4] += o1[q];
+      }
+      bf16x8 w;
+      if (n < a.gru_cols) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(v[q]);
+        *reinterpret_cast<bf16x8*>(a.out3 + p * a.out3_stride + n) = w;
+      } else {
+        const int c = n - a.cm_c0;
+        if (c < a.cm_valid) {  // chunks wholly past cm_valid are not stored (cout may be narrower)
+          const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.cmask + p * a.cmask_stride + c);
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            w[q] = static_cast<__bf16>((c + q < a.cm_valid && static_cast<float>(m[q]) > 0.f) ? v[q] : 0.f);
+          *reinterpret_cast<bf16x8*>(a.cout + p * a.cout_stride + c) = w;
+        }
+      }
+    } else if (epi == 0) {
       if (a.act == 1)
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
@@ -501,7 +599,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
             if (q < nv) o[q] = static_cast<__bf16>(v[q]);
         }
       }
-    } else if (a.epi == 1) {
+    } else if (epi == 1) {
       if (a.mask) {
         const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.mask + p * a.mask_stride + n);
 #pragma unroll
@@ -538,7 +636,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
             if (q < nv) o[q] = static_cast<__bf16>(accum ? static_cast<float>(o[q]) + v[q] : v[q]);
         }
       }
-    } else if (a.epi == 2) {
+    } else if (epi == 2) {
       const int C = Nn >> 1;
       bf16x8 sg;
 #pragma unroll
@@ -1517,6 +1615,7 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   for (int i = 0; i < a.nsrc; ++i) maxbytes = std::max(maxbytes, a.P * a.src[i].stride * 2);
   const bool dma_ok = (uniform || a.nsrc == 1) && maxbytes < (1L << 31) && (long)a.N * a.Kpad * 2 < (1L << 31);
   if (!dma_ok || cfg == 1) {
+    if (a.epi >= 4) return hipErrorInvalidValue;  // the fused GRU epilogues live in the v4/v5 kernels
     hipLaunchKernelGGL((conv_fwd_kernel<64, 64>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
     return hipGetLastError();
   }

@@ -92,14 +92,26 @@ def geom(B: int, H: int, W: int, kh: int, kw: int, ph: int, pw: int) -> List[int
     return [B, H, W, kh, kw, ph, pw]
 
 
-EPI_STORE, EPI_GRAD, EPI_GRU_ZR, EPI_GRU_Q = 0, 1, 2, 3
+EPI_STORE, EPI_GRAD, EPI_GRU_ZR, EPI_GRU_Q, EPI_GRU_BWD_A, EPI_GRU_BWD_B, EPI_GRU_BWD_LAST = 0, 1, 2, 3, 4, 5, 6
 
 
 def conv_fwd(srcs, wt, g, N, out, bias=None, act=0, alpha=1.0, epi=EPI_STORE, acc_c0=1 << 30, mask=None,
-             h=None, z=None, out2=None, cfg: int = 0):
+             h=None, z=None, out2=None, cfg: int = 0, g0=None, carry=None, out3=None, gru_cols: int = 0,
+             addsrc=None, cout=None, cmask=None, cm_c0: int = 0, cm_valid: int = 0):
     """``cfg`` forces a kernel variant (0 = automatic; tests and microbenchmarks only):
-    1 generic, 8/9 v4 64x128/64x64, 20/21/22/23 v5 halo strip 64x128/128x128/128x256/256x128."""
-    ops().conv_fwd(list(srcs), wt, g, N, bias, epi, act, alpha, out, acc_c0, mask, h, z, out2, cfg)
+    1 generic, 8/9 v4 64x128/64x64, 20..23 v5 halo strip 64x128/128x128/128x256/256x128,
+    24..26 v5 with 8 waves 256x128/128x128/128x256.
+
+    Data-gradient launches of the GRU can finish the gate backward in the epilogue for the
+    output channels [0, gru_cols) (fp32 ``out``; the other channels behave as EPI_GRAD):
+      EPI_GRU_BWD_A: g = dH (+= out where acc): out2 = dq = g z (1 - q^2), out3 = dz =
+        g (q - h) z (1 - z), carry = g (1 - z); with z, g0 = q, h;
+        (+ ``addsrc``, an incoming bf16 gradient);
+      EPI_GRU_BWD_B: g = d(r h): out3 = dr = g h r (1 - r), out = carry + g r; g0 = r, h;
+      EPI_GRU_BWD_LAST: g = out + acc: [0, gru_cols) -> bf16 out3, [gru_cols, cm_c0) -> out,
+        [cm_c0, N) -> bf16 cout = g where cmask > 0 (zero past cm_valid)."""
+    ops().conv_fwd(list(srcs), wt, g, N, bias, epi, act, alpha, out, acc_c0, mask, h, z, out2, cfg, g0, carry,
+                   out3, gru_cols, addsrc, cout, cmask, cm_c0, cm_valid)
     return out
 
 

@@ -341,36 +341,48 @@ class _Step(torch.autograd.Function):
             dgrad("fh2", dd8, 3, 3, dhd[:, :256], 256, mask=hd[:, :256])
         dgrad("mask2", dmask, 1, 1, dhd[:, 256:], 256, mask=hd[:, 256:])
         main.wait_stream(side)
-        dh = torch.empty(P, HID, device=dev, dtype=torch.float32)
-        if g_net is not None:
-            dh.copy_(_pm(g_net))
-            acc = 0
-        else:
-            acc = 1 << 30
-        dgrad("heads", dhd, 3, 3, dh, HID, acc_c0=acc)
-
-        # ---- GRU stages (reverse order); G = [dh | d inp | d motion] accumulates over stages
-        G = torch.empty(P, 3 * HID, device=dev, dtype=torch.float32)
+        # ---- GRU stages (reverse order).  The gate backward runs in the epilogues of the data
+        # gradients: the conv producing a stage's dH finishes (dq, dz, carry) of that stage
+        # (EPI_GRU_BWD_A), the q conv's data gradient finishes dr and d h (EPI_GRU_BWD_B); the
+        # last one writes d net (bf16), d inp and the ReLU'-masked d motion (EPI_GRU_BWD_LAST).
+        # G = [d h | d inp | d motion] (fp32) accumulates over the stages.
+        stages = ((2, (5, 1)), (1, (1, 5)))
+        gates = {}
+        for stage, _ in stages:
+            gates[stage] = (ar.rows("h", t, t + 1) if stage == 1 else R("h1"), R(f"zr{stage}"), R(f"q{stage}"),
+                            ar.take(f"dq{stage}", t, HID), ar.take(f"dzr{stage}", t, 2 * HID))
         carry = torch.empty(P, HID, device=dev, dtype=torch.float32)
-        inp = run.inp_bf
-        first = True
-        for stage, (kh, kw) in ((2, (5, 1)), (1, (1, 5))):
-            h = ar.rows("h", t, t + 1) if stage == 1 else R("h1")
-            zr, rh, q = R(f"zr{stage}"), R(f"rh{stage}"), R(f"q{stage}")
-            dq = ar.take(f"dq{stage}", t, HID)
-            dzr = ar.take(f"dzr{stage}", t, 2 * HID)
-            dH = dh if stage == 2 else G[:, :HID]
-            k.gru_bwd_a(dH, zr[:, :HID], q, h, dq, dzr[:, :HID], carry)
-            # fresh write of d(rh); x part fresh on the first stage, accumulated afterwards
-            dgrad(f"q{stage}", dq, kh, kw, G, 3 * HID, acc_c0=(3 * HID if first else HID))
-            k.gru_bwd_b(G[:, :HID], zr[:, HID:], h, carry, dzr[:, HID:])
-            dgrad(f"zr{stage}", dzr, kh, kw, G, 3 * HID, acc_c0=0)
-            first = False
+
+        def gate_a(stage):
+            h, zr, q, dq, dzr = gates[stage]
+            return dict(epi=C.EPI_GRU_BWD_A, h=h, z=zr[:, :HID], g0=q, out2=dq, out3=dzr[:, :HID], carry=carry,
+                        gru_cols=HID)
+
+        # heads data gradient = dH of stage 2 (+ the incoming d net); `carry` stands in for the
+        # fp32 output, which this epilogue does not write
+        C.conv_fwd([dhd], run.wd["heads"], gd(3, 3), HID, carry,
+                   addsrc=_pm(g_net).to(bf).contiguous() if g_net is not None else None, **gate_a(2))
+
+        G = torch.empty(P, 3 * HID, device=dev, dtype=torch.float32)
+        motion = R("motion")
+        dmo = ar.take("dmo", t, HID)
+        d_net = torch.empty(P, HID, device=dev, dtype=bf)
+        for i, (stage, (kh, kw)) in enumerate(stages):
+            h, zr, q, dq, dzr = gates[stage]
+            # d(r h) -> dr and d h = carry + d(rh) r; the other channels fresh on the first stage,
+            # accumulated afterwards
+            C.conv_fwd([dq], run.wd[f"q{stage}"], gd(kh, kw), 3 * HID, G, epi=C.EPI_GRU_BWD_B,
+                       acc_c0=(3 * HID if i == 0 else HID), h=h, g0=zr[:, HID:], carry=carry, out3=dzr[:, HID:],
+                       gru_cols=HID)
+            if i + 1 < len(stages):  # -> dH of the next (earlier) stage
+                C.conv_fwd([dzr], run.wd[f"zr{stage}"], gd(kh, kw), 3 * HID, G, acc_c0=0,
+                           **gate_a(stages[i + 1][0]))
+            else:  # d net (bf16), d inp, d motion masked by the ReLU' (flow channels -> 0)
+                C.conv_fwd([dzr], run.wd[f"zr{stage}"], gd(kh, kw), 3 * HID, G, epi=C.EPI_GRU_BWD_LAST, acc_c0=0,
+                           out3=d_net, gru_cols=HID, cout=dmo, cmask=motion, cm_c0=2 * HID, cm_valid=126)
 
         # ---- motion encoder
-        motion, cf, c1, f1 = R("motion"), R("cf"), R("c1"), R("f1")
-        dmo = ar.take("dmo", t, HID)
-        k.masked_cast(G[:, 2 * HID:2 * HID + 126], motion, dmo)  # relu' ; flow channels -> 0
+        cf, c1, f1 = R("cf"), R("c1"), R("f1")
         dcf = ar.take("dcf", t, 256)
         dgrad("conv", dmo, 3, 3, dcf, 256, mask=cf)
         dc1 = ar.take("dc1", t, 256)
@@ -390,7 +402,7 @@ class _Step(torch.autograd.Function):
         elif run.pyr is not None and run.pyr.levels:
             k.corr_lookup_backward_(run.pyr.grad_buffers(), run.coords[t], dcorr.reshape(B, H, W, CORR_PAD),
                                     run.pyr.radius)
-        d_net = _nchw(G[:, :HID].to(ctx.net_dtype), B, H, W)
+        d_net = _nchw(d_net if ctx.net_dtype == bf else d_net.to(ctx.net_dtype), B, H, W)
         d_inp = _nchw(G[:, HID:2 * HID], B, H, W)
         zero = torch.zeros((), device=dev)
         return zero, zero, d_net, d_inp, d_corr_in, None, None, None

@@ -237,30 +237,28 @@ class _Step(torch.autograd.Function):
         hd = R("hd")
         dhd = ar.take("dhd", t, 128)
         dgrad("fh2", dd8, 3, 3, dhd, 128, mask=hd)
-        dh = torch.empty(P, HID, device=dev, dtype=torch.float32)
-        if g_net is not None:
-            dh.copy_(_pm(g_net))
-            acc = 0
-        else:
-            acc = 1 << 30
-        dgrad("fh1", dhd, 3, 3, dh, HID, acc_c0=acc)
-
-        # ConvGRU; G = [d h | d inp | d motion] (fp32)
+        # ConvGRU; the gate backward runs in the data-gradient epilogues (ops/update_fused.py):
+        # fh1's data gradient = dH (+ incoming d net) -> dq, dz, carry; q's -> dr, d h; z||r's ->
+        # bf16 d net, d inp, ReLU'-masked d motion.  G = [d h | d inp | d motion] (fp32)
         h = ar.rows("h", t, t + 1)
-        zr, rh, q = R("zr"), R("rh"), R("q")
+        zr, q = R("zr"), R("q")
         G = torch.empty(P, GX, device=dev, dtype=torch.float32)
         carry = torch.empty(P, HID, device=dev, dtype=torch.float32)
         dq = ar.take("dq", t, HID)
         dzr = ar.take("dzr", t, 2 * HID)
-        k.gru_bwd_a(dh, zr[:, :HID], q, h, dq, dzr[:, :HID], carry)
-        dgrad("q", dq, 3, 3, G, GX)
-        k.gru_bwd_b(G[:, :HID], zr[:, HID:], h, carry, dzr[:, HID:])
-        dgrad("zr", dzr, 3, 3, G, GX, acc_c0=0)
-
-        # motion encoder
+        C.conv_fwd([dhd], run.wd["fh1"], gd(3, 3), HID, carry, epi=C.EPI_GRU_BWD_A, h=h, z=zr[:, :HID], g0=q,
+                   out2=dq, out3=dzr[:, :HID], carry=carry, gru_cols=HID,
+                   addsrc=_pm(g_net).to(torch.bfloat16).contiguous() if g_net is not None else None)
+        C.conv_fwd([dq], run.wd["q"], gd(3, 3), GX, G, epi=C.EPI_GRU_BWD_B, h=h, g0=zr[:, HID:], carry=carry,
+                   out3=dzr[:, HID:], gru_cols=HID)
         motion, cf, f1 = R("motion"), R("cf"), R("f1")
         dmo = ar.take("dmo", t, 80)
-        k.masked_cast(G[:, HID + CTX:HID + CTX + 80], motion, dmo)  # relu' ; the flow channels -> coords (detached)
+        d_net = torch.empty(P, HID, device=dev, dtype=torch.bfloat16)
+        # relu' of the motion features; the flow channels -> coords (detached)
+        C.conv_fwd([dzr], run.wd["zr"], gd(3, 3), GX, G, epi=C.EPI_GRU_BWD_LAST, acc_c0=0, out3=d_net, gru_cols=HID,
+                   cout=dmo, cmask=motion, cm_c0=HID + CTX, cm_valid=80)
+
+        # motion encoder
         dcf = ar.take("dcf", t, 128)
         dgrad("conv", dmo, 3, 3, dcf, 128, mask=cf)
         dcorr = torch.empty(P, CORR_PAD, device=dev, dtype=torch.bfloat16)
@@ -275,7 +273,7 @@ class _Step(torch.autograd.Function):
         elif run.pyr is not None and run.pyr.levels:
             k.corr_lookup_backward_(run.pyr.grad_buffers(), run.coords[t], dcorr.reshape(B, H, W, CORR_PAD),
                                     run.pyr.radius)
-        d_net = _nchw(G[:, :HID].to(ctx.net_dtype), B, H, W)
+        d_net = _nchw(d_net if ctx.net_dtype == torch.bfloat16 else d_net.to(ctx.net_dtype), B, H, W)
         d_inp = _nchw(G[:, HID:HID + CTX], B, H, W)
         zero = torch.zeros((), device=dev)
         return zero, zero, d_net, d_inp, d_corr_in, None, None, None

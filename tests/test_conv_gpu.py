@@ -238,3 +238,77 @@ def test_wgrad_params_periodic_source_and_param_layout(cuda):
     gz2 = torch.empty_like(gz)
     C.conv_wgrad_params([hs, inp, mo], dy, C.geom(T * B, H, W, 1, 5, 0, 2), [gz2, gr], [bz, br], segs, scale=0.5)
     assert torch.equal(gz, gz2)
+
+
+@pytest.mark.parametrize("cfg", [0, 8, 25, 26])
+def test_gru_backward_epilogues_match_unfused(cuda, cfg):
+    """EPI_GRU_BWD_A / _B / _LAST (gate backward fused into the data-gradient epilogue) vs
+    the plain EPI_GRAD store followed by the separate gru_bwd_a / gru_bwd_b / masked_cast
+    kernels, on a 1x5 conv with 384 output channels (the GRU data-gradient shape)."""
+    from raft_ros_amd.ops._ext import ops
+
+    k = ops()
+    torch.manual_seed(11)
+    B, H, W, HID = 2, 23, 31, 128
+    P = B * H * W
+    dy = torch.randn(P, 256, device=cuda).bfloat16()
+    wt = C.pack_fwd(torch.randn(3 * HID, 256, 1, 5, device=cuda) * 0.05, [(256, 256)])
+    g = C.geom(B, H, W, 1, 5, 0, 2)
+    G0 = torch.randn(P, 3 * HID, device=cuda)
+    rnd = lambda: torch.rand(P, HID, device=cuda).bfloat16()  # noqa: E731
+    z, q, h, r = rnd(), (torch.rand(P, HID, device=cuda) * 2 - 1).bfloat16(), rnd(), rnd()
+    bf = torch.bfloat16
+
+    def plain(acc_c0):
+        out = G0.clone()
+        C.conv_fwd([dy], wt, g, 3 * HID, out, epi=C.EPI_GRAD, acc_c0=acc_c0, cfg=cfg)
+        return out
+
+    def close(a, b, tol=2e-2):
+        assert _rel(a.float(), b.float()) < tol
+
+    # A: dH accumulated into G, gate backward in the epilogue; channels >= 128 as EPI_GRAD
+    Gp = plain(0)
+    dq_r, dz_r, c_r = (torch.empty(P, HID, device=cuda, dtype=bf), torch.empty(P, HID, device=cuda, dtype=bf),
+                       torch.empty(P, HID, device=cuda))
+    k.gru_bwd_a(Gp[:, :HID], z, q, h, dq_r, dz_r, c_r)
+    Gf = G0.clone()
+    dq, dz, carry = torch.empty_like(dq_r), torch.empty_like(dz_r), torch.empty_like(c_r)
+    C.conv_fwd([dy], wt, g, 3 * HID, Gf, epi=C.EPI_GRU_BWD_A, acc_c0=0, h=h, z=z, g0=q, out2=dq, out3=dz,
+               carry=carry, gru_cols=HID, cfg=cfg)
+    close(dq, dq_r)
+    close(dz, dz_r)
+    close(carry, c_r, 1e-5)
+    assert torch.equal(Gf[:, HID:], Gp[:, HID:])
+    # A with an incoming bf16 gradient and no accumulation
+    add = torch.randn(P, HID, device=cuda).bfloat16()
+    Gq = G0.clone()
+    C.conv_fwd([dy], wt, g, 3 * HID, Gq, epi=C.EPI_GRU_BWD_A, acc_c0=1 << 30, h=h, z=z, g0=q, out2=dq, out3=dz,
+               carry=carry, gru_cols=HID, addsrc=add, cfg=cfg)
+    Gp2 = plain(1 << 30)
+    k.gru_bwd_a(Gp2[:, :HID] + add.float(), z, q, h, dq_r, dz_r, c_r)
+    close(dq, dq_r)
+    close(carry, c_r, 1e-5)
+    # B: d(r h) fresh in channels < 128, accumulated above
+    Gp = plain(HID)
+    dr_r = torch.empty(P, HID, device=cuda, dtype=bf)
+    c_in = torch.randn(P, HID, device=cuda)
+    k.gru_bwd_b(Gp[:, :HID], r, h, c_in, dr_r)
+    Gf = G0.clone()
+    dr = torch.empty_like(dr_r)
+    C.conv_fwd([dy], wt, g, 3 * HID, Gf, epi=C.EPI_GRU_BWD_B, acc_c0=HID, h=h, g0=r, carry=c_in, out3=dr,
+               gru_cols=HID, cfg=cfg)
+    close(dr, dr_r)
+    close(Gf, Gp, 1e-5)
+    # LAST: bf16 d net, fp32 d inp, masked bf16 d motion
+    Gp = plain(0)
+    motion = torch.randn(P, HID, device=cuda).bfloat16()
+    dmo_r = torch.empty(P, HID, device=cuda, dtype=bf)
+    k.masked_cast(Gp[:, 2 * HID:2 * HID + 126], motion, dmo_r)
+    Gf = G0.clone()
+    dnet, dmo = torch.empty(P, HID, device=cuda, dtype=bf), torch.full((P, HID), 7.0, device=cuda, dtype=bf)
+    C.conv_fwd([dy], wt, g, 3 * HID, Gf, epi=C.EPI_GRU_BWD_LAST, acc_c0=0, out3=dnet, gru_cols=HID, cout=dmo,
+               cmask=motion, cm_c0=2 * HID, cm_valid=126, cfg=cfg)
+    assert torch.equal(dnet, Gp[:, :HID].bfloat16())
+    assert torch.equal(Gf[:, HID:2 * HID], Gp[:, HID:2 * HID])
+    assert torch.equal(dmo, dmo_r)
