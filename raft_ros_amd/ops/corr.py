@@ -140,6 +140,7 @@ class _BuildPyramid(torch.autograd.Function):
         state.shape = (B, C, H, W)
         ctx.state, ctx.split = state, split
         ctx.save_for_backward(fmap1, fmap2)
+        ctx.set_materialize_grads(False)  # the token gradient is never used (may be None)
         return fmap1.new_zeros((), dtype=torch.float32)
 
     @staticmethod

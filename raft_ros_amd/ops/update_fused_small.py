@@ -146,6 +146,7 @@ class _PackWeights(torch.autograd.Function):
     @staticmethod
     def forward(ctx, run: _Run, *params):
         ctx.run = run
+        ctx.set_materialize_grads(False)  # the steps send no token gradient (None): no zero fills
         return params[0].new_zeros(())
 
     @staticmethod
@@ -275,8 +276,9 @@ class _Step(torch.autograd.Function):
                                     run.pyr.radius)
         d_net = _nchw(d_net if ctx.net_dtype == torch.bfloat16 else d_net.to(ctx.net_dtype), B, H, W)
         d_inp = _nchw(G[:, HID:HID + CTX], B, H, W)
-        zero = torch.zeros((), device=dev)
-        return zero, zero, d_net, d_inp, d_corr_in, None, None, None
+        # the tokens only order the autograd graph (their nodes run after every step's backward
+        # whatever they receive): no gradient, no fill / accumulate kernels
+        return None, None, d_net, d_inp, d_corr_in, None, None, None
 
 
 class FusedSmallUpdate:
