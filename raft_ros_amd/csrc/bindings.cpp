@@ -15,6 +15,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "kernel_abi.h"
+
 namespace raft_amd {
 
 struct PyrDesc {
@@ -126,89 +128,6 @@ hipError_t launch_gru_blend_fwd(int dtype, const void* z, const void* q, const v
 hipError_t launch_gru_blend_bwd(int dtype, const void* z, const void* q, const void* h, const void* g,
                                 void* dz, void* dq, void* dh, long numel, hipStream_t s);
 
-struct ConvSrc {
-  const void* ptr;
-  long stride;
-  int C;
-  int period;
-};
-struct ConvFwdArgs {
-  ConvSrc src[3];
-  int nsrc, Cin;
-  int B, H, W, KH, KW, PH, PW;
-  int K, Kpad;
-  const void* wt;
-  int N;
-  long P;
-  int epi, act, out_f32, acc_c0;
-  float alpha;
-  const float* bias;
-  void* out;
-  long out_stride;
-  const void* mask;
-  long mask_stride;
-  const void* h;
-  long h_stride;
-  const void* z;
-  long z_stride;
-  void* out2;
-  long out2_stride;
-  const void* g0;
-  long g0_stride;
-  float* carry;
-  long carry_stride;
-  void* out3;
-  long out3_stride;
-  int gru_cols;
-  const void* addsrc;
-  long addsrc_stride;
-  void* cout;
-  long cout_stride;
-  const void* cmask;
-  long cmask_stride;
-  int cm_c0, cm_valid;
-  int cfg;
-};
-struct ConvWgradArgs {
-  ConvSrc src[3];
-  int nsrc, Cin;
-  int B, H, W, KH, KW, PH, PW;
-  int K, Kpad;
-  const void* dy;
-  long dy_stride;
-  int N;
-  long P;
-  long pix_per_split;
-  float* slab;
-  float* dbslab;
-  int Npad;
-  int xcd_g;  // layouts must match conv_igemm.hip
-};
-struct WgradPlan {
-  int BM, BN, tilesM, tilesN, nsplit, Npad, xcd_g;
-  long pix_per_split;
-  int kind;
-};
-struct ConvParamDesc {
-  float* w[2];
-  long ws[2][4];
-  float* b[2];
-  int rows[2];
-  int nseg;
-  int seg_real[3], seg_pad[3];
-  int Cin, Cin_pad, KH, KW;
-  float scale;
-};
-hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s);
-bool wgrad_supported(const ConvWgradArgs& a);
-WgradPlan plan_conv_wgrad(const ConvWgradArgs& a);
-hipError_t launch_conv_wgrad(ConvWgradArgs a, const WgradPlan& pl, hipStream_t s);
-hipError_t launch_pack_conv_weights(const ConvParamDesc& d, int N, void* wf, int Kf, void* wd, int Kd, int Cout_pad,
-                                    float* bias, hipStream_t s);
-hipError_t launch_wgrad_reduce_params(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, int ndb,
-                                      const ConvParamDesc& d, int N, int accumulate, hipStream_t s);
-hipError_t launch_wgrad_reduce_packed(const float* slab, int nsplit, int Npad, int Kpad, int K, const float* dbslab,
-                                      int ndb, float* dw, long ldw, float* db, int N, int accumulate, hipStream_t s);
 
 int instance_norm_chunks(int HW);
 hipError_t launch_instance_norm_fwd(int dtype, const void* x, void* y, float* stats, float* part, int N, int HW,
@@ -762,7 +681,7 @@ int fill_srcs(at::TensorList srcs, long P, ConvSrc* out, bool allow_period) {
     check_pm(srcs[i], "src", periodic ? rows : P);
     TORCH_CHECK(srcs[i].scalar_type() == at::kBFloat16, "raft_amd conv: sources must be bf16");
     TORCH_CHECK(srcs[i].size(1) % 8 == 0, "raft_amd conv: source channels must be multiples of 8");
-    out[i] = ConvSrc{srcs[i].data_ptr(), srcs[i].stride(0), static_cast<int>(srcs[i].size(1)),
+    out[i] = ConvSrc{static_cast<const __bf16*>(srcs[i].data_ptr()), srcs[i].stride(0), static_cast<int>(srcs[i].size(1)),
                      periodic ? static_cast<int>(rows) : 0};
     Cin += static_cast<int>(srcs[i].size(1));
   }
@@ -790,7 +709,7 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
                   wt.size(1) >= a.K && wt.size(1) % 64 == 0,
               "raft_amd conv_fwd: wt must be contiguous bf16 [>=N][Kpad], Kpad % 64 == 0, Kpad >= K (", a.K, ")");
   a.Kpad = static_cast<int>(wt.size(1));
-  a.wt = wt.data_ptr();
+  a.wt = static_cast<const __bf16*>(wt.data_ptr());
   a.N = static_cast<int>(N);
   a.epi = static_cast<int>(epi);
   a.act = static_cast<int>(act);
@@ -810,22 +729,22 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
   if (epi == 2 || epi == 3) TORCH_CHECK(!a.out_f32, "raft_amd conv_fwd: GRU epilogues write bf16");
   if (mask) {
     check_pm(*mask, "mask", a.P);
-    a.mask = mask->data_ptr();
+    a.mask = static_cast<const __bf16*>(mask->data_ptr());
     a.mask_stride = mask->stride(0);
   }
   if (h) {
     check_pm(*h, "h", a.P);
-    a.h = h->data_ptr();
+    a.h = static_cast<const __bf16*>(h->data_ptr());
     a.h_stride = h->stride(0);
   }
   if (z) {
     check_pm(*z, "z", a.P);
-    a.z = z->data_ptr();
+    a.z = static_cast<const __bf16*>(z->data_ptr());
     a.z_stride = z->stride(0);
   }
   if (out2) {
     check_pm(*out2, "out2", a.P);
-    a.out2 = out2->data_ptr();
+    a.out2 = static_cast<__bf16*>(out2->data_ptr());
     a.out2_stride = out2->stride(0);
   }
   if (epi == 2) TORCH_CHECK(h && out2 && N % 2 == 0, "raft_amd conv_fwd: GRU z||r epilogue needs h, out2");
@@ -836,21 +755,21 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
     TORCH_CHECK(epi <= 6 && a.out_f32 && N % 8 == 0, "raft_amd conv_fwd: GRU backward epilogue needs fp32 out");
     TORCH_CHECK(gru_cols > 0 && gru_cols % 8 == 0 && gru_cols <= N, "raft_amd conv_fwd: gru_cols");
     auto al16 = [](const void* ptr) { return ptr == nullptr || reinterpret_cast<uintptr_t>(ptr) % 16 == 0; };
-    auto bf_rows = [&](const c10::optional<at::Tensor>& t, const char* what, const void*& ptr, long& stride) {
+    // bf16 rows of an epilogue operand: checked, returned as a writable pointer (the input
+    // operands convert to const on assignment)
+    auto bf_rows = [&](const c10::optional<at::Tensor>& t, const char* what, long& stride) -> __bf16* {
       TORCH_CHECK(t.has_value(), "raft_amd conv_fwd: GRU backward epilogue needs ", what);
       check_pm(*t, what, a.P);
       TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->stride(0) % 8 == 0 && al16(t->data_ptr()),
                   "raft_amd conv_fwd: ", what, " must be bf16 with 16-byte aligned rows");
-      ptr = t->data_ptr();
       stride = t->stride(0);
+      return static_cast<__bf16*>(t->data_ptr());
     };
-    const void* tmp = nullptr;
-    bf_rows(out3, "out3", tmp, a.out3_stride);
-    a.out3 = const_cast<void*>(tmp);
+    a.out3 = bf_rows(out3, "out3", a.out3_stride);
     a.gru_cols = static_cast<int>(gru_cols);
     if (epi == 4 || epi == 5) {
-      bf_rows(h, "h", a.h, a.h_stride);
-      bf_rows(g0, "g0", a.g0, a.g0_stride);
+      a.h = bf_rows(h, "h", a.h_stride);
+      a.g0 = bf_rows(g0, "g0", a.g0_stride);
       TORCH_CHECK(carry.has_value() && carry->scalar_type() == at::kFloat && carry->dim() == 2 &&
                       carry->size(0) >= a.P && carry->size(1) >= gru_cols && carry->stride(1) == 1 &&
                       carry->stride(0) % 4 == 0 && al16(carry->data_ptr()),
@@ -859,18 +778,14 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
       a.carry_stride = carry->stride(0);
     }
     if (epi == 4) {
-      bf_rows(z, "z", a.z, a.z_stride);
-      tmp = nullptr;
-      bf_rows(out2, "out2", tmp, a.out2_stride);
-      a.out2 = const_cast<void*>(tmp);
-      if (addsrc) bf_rows(addsrc, "addsrc", a.addsrc, a.addsrc_stride);
+      a.z = bf_rows(z, "z", a.z_stride);
+      a.out2 = bf_rows(out2, "out2", a.out2_stride);
+      if (addsrc) a.addsrc = bf_rows(addsrc, "addsrc", a.addsrc_stride);
     }
     if (epi == 6) {
       TORCH_CHECK(cm_c0 >= gru_cols && cm_c0 % 8 == 0 && cm_c0 <= N && cm_valid >= 0, "raft_amd conv_fwd: cm_c0");
-      tmp = nullptr;
-      bf_rows(cout, "cout", tmp, a.cout_stride);
-      a.cout = const_cast<void*>(tmp);
-      bf_rows(cmask, "cmask", a.cmask, a.cmask_stride);
+      a.cout = bf_rows(cout, "cout", a.cout_stride);
+      a.cmask = bf_rows(cmask, "cmask", a.cmask_stride);
       const int64_t cw = std::min<int64_t>(N - cm_c0, (cm_valid + 7) / 8 * 8);  // columns stored / read
       TORCH_CHECK(cout->size(1) >= cw && cmask->size(1) >= cw, "raft_amd conv_fwd: cout / cmask width");
       a.cm_c0 = static_cast<int>(cm_c0);
@@ -894,7 +809,7 @@ ConvWgradArgs wgrad_args(at::TensorList srcs, const at::Tensor& dy, at::IntArray
   check_pm(dy, "dy", a.P);
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16, "raft_amd conv_wgrad: dy must be bf16");
   TORCH_CHECK(dy.size(1) >= (N + 7) / 8 * 8, "raft_amd conv_wgrad: dy must hold N channels (rounded to 8)");
-  a.dy = dy.data_ptr();
+  a.dy = static_cast<const __bf16*>(dy.data_ptr());
   a.dy_stride = dy.stride(0);
   a.N = static_cast<int>(N);
   TORCH_CHECK(wgrad_supported(a), "raft_amd conv_wgrad: unsupported source layout (multi-source convs need "

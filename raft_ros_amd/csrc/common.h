@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "kernel_abi.h"  // shared argument structs, work mapping (xcd_remap)
+
 namespace raft_amd {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -42,12 +44,6 @@ __device__ __forceinline__ float wave_sum(float v) {
 // Bijective XCD-aware remap of a flat workgroup id (MI355X: 8 XCDs, blocks
 // b and b+8 share an XCD's L2).  Consecutive logical tiles land on the same
 // XCD so that tiles sharing an operand panel share that L2.
-__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
-  const int xcd = orig & 7;
-  const int q = nwg >> 3, r = nwg & 7;
-  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  return base + (orig >> 3);
-}
 
 inline int cdiv(long a, long b) { return static_cast<int>((a + b - 1) / b); }
 

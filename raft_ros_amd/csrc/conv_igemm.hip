@@ -31,93 +31,15 @@
 // Tiling: 256 threads = 4 wave64s in a 2x2 arrangement, v_mfma_f32_32x32x16_bf16,
 // BK = 64 per LDS stage, XCD-aware tile order.
 #include "common.h"
+#include "kernel_abi.h"
 
 #include <algorithm>
 
 namespace raft_amd {
 
-struct ConvSrc {
-  const __bf16* ptr;
-  long stride;  // elements between consecutive pixels
-  int C;        // channels taken from this source (multiple of 8)
-  int period;   // wgrad only: >0 -> pixel p reads row p % period (0: no wrap)
-};
 
-struct ConvFwdArgs {
-  ConvSrc src[3];
-  int nsrc, Cin;
-  int B, H, W, KH, KW, PH, PW;
-  int K, Kpad;
-  const __bf16* wt;  // packed weights [N][Kpad], k = tap*Cin + c
-  int N;
-  long P;
-  // epilogue
-  int epi;      // 0: bias+act store, 1: grad store, 2: GRU z||r, 3: GRU q+blend
-  int act;      // 0: none, 1: relu
-  int out_f32;  // output element type (epi 0/1)
-  int acc_c0;   // epi 1: accumulate (+=) into out for channels n >= acc_c0
-  float alpha;
-  const float* bias;
-  void* out;
-  long out_stride;
-  const __bf16* mask;  // epi 1: multiply by (mask[p][n] > 0) (ReLU' of the conv input)
-  long mask_stride;
-  const __bf16* h;  // epi 2/3: hidden state
-  long h_stride;
-  const __bf16* z;  // epi 3: update gate
-  long z_stride;
-  __bf16* out2;  // epi 2: r*h, epi 3: tanh(q), epi 4: dq
-  long out2_stride;
-  // fused GRU backward (data-gradient launches of the update block): output channels
-  // [0, gru_cols) finish the gate math in the epilogue, the rest are stored as epi 1
-  //   epi 4 (after the dH-producing dgrad): g = dH; dq = g z (1 - q^2) -> out2,
-  //          dz = g (q - h) z (1 - z) -> out3, carry = g (1 - z)  (out not written)
-  //   epi 5 (the q dgrad, g = d(r*h)): dr = g h r (1 - r) -> out3, out = carry + g r
-  //   epi 6 (the last GRU dgrad): channels [0, gru_cols) -> bf16 out3 (d net), [gru_cols,
-  //          cm_c0) -> out as epi 1, [cm_c0, N) -> bf16 cout = (cmask > 0 ? g : 0), zero past
-  //          cm_valid (the ReLU' of the motion features; out not written)
-  const __bf16* g0;  // epi 4: q, epi 5: r
-  long g0_stride;
-  float* carry;
-  long carry_stride;
-  __bf16* out3;
-  long out3_stride;
-  int gru_cols;
-  const __bf16* addsrc;  // epi 4: incoming bf16 gradient added to g (null: none)
-  long addsrc_stride;
-  __bf16* cout;
-  long cout_stride;
-  const __bf16* cmask;
-  long cmask_stride;
-  int cm_c0, cm_valid;
-  int cfg;  // kernel variant: 0 = automatic, otherwise forced (tests / microbenchmarks)
-};
 
-struct ConvWgradArgs {
-  ConvSrc src[3];
-  int nsrc, Cin;
-  int B, H, W, KH, KW, PH, PW;
-  int K, Kpad;
-  const __bf16* dy;  // [P][dy_stride], N channels used
-  long dy_stride;
-  int N;
-  long P;
-  long pix_per_split;
-  float* slab;    // [nsplit][Npad][Kpad] fp32: the split's partial dW (written, not accumulated)
-  float* dbslab;  // [nsplit][tilesN][Npad] fp32 bias partials (may be null)
-  int Npad;       // slab rows (N rounded up to the row tile)
-  int xcd_g;      // >0: XCD-grouped split mapping with xcd_g splits per XCD (set by the launcher)
-};
 
-// Plan of one weight-gradient launch (the caller sizes the slabs from it).
-//   kind 2: wgrad v2, tilesN = column tiles, pix_per_split = pixels per split
-//   kind 3: wgrad v3 (tap-batched), tilesN = 64-channel chunks, pix_per_split = pixel TILES per split
-// Bias partials: nsplit * tilesN rows of Npad floats.
-struct WgradPlan {
-  int BM, BN, tilesM, tilesN, nsplit, Npad, xcd_g;
-  long pix_per_split;
-  int kind;
-};
 
 namespace {
 
@@ -1027,7 +949,7 @@ inline long fwd5_lds_bytes(int BM, int BN, int strip_rows) {
 }
 
 // ============================================================================ wgrad helpers
-constexpr int WBK = 64;
+constexpr int WBK = kWgradBK;
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -1067,17 +989,7 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
   const int tilesN = (a.K + BN - 1) / BN;
   const int tiles = tilesM * tilesN;
   int split, t0;
-  if (a.xcd_g > 0) {
-    // workgroups are dealt round-robin to the 8 XCDs: keep every tile of a pixel split on
-    // one XCD so the split's dY / X rows are fetched into that XCD's L2 once
-    const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
-    const int si = local / tiles;
-    t0 = local - si * tiles;
-    split = xcd * a.xcd_g + si;
-  } else {
-    split = blockIdx.x / tiles;
-    t0 = blockIdx.x - split * tiles;
-  }
+  wgrad_block_map(blockIdx.x, tiles, a.xcd_g, split, t0);
   const int tm = t0 / tilesN, tn = t0 - (t0 / tilesN) * tilesN;
   const int m0 = tm * BM, n0 = tn * BN;
   const int P = (int)a.P;
@@ -1316,15 +1228,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   const int tilesM = (a.N + BM - 1) / BM;
   const int wtiles = tilesM * nchunk;
   int split, t0;
-  if (a.xcd_g > 0) {
-    const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
-    const int si = local / wtiles;
-    t0 = local - si * wtiles;
-    split = xcd * a.xcd_g + si;
-  } else {
-    split = blockIdx.x / wtiles;
-    t0 = blockIdx.x - split * wtiles;
-  }
+  wgrad_block_map(blockIdx.x, wtiles, a.xcd_g, split, t0);
   const int tm = t0 / nchunk, cc = t0 - tm * nchunk;
   const int m0 = tm * BM;
   const int tbeg = split * (int)a.pix_per_split;  // pix_per_split counts pixel TILES here
@@ -1690,84 +1594,6 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   else
     hipLaunchKernelGGL((conv_fwd4_kernel<64, 64, 4>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
   return hipGetLastError();
-}
-
-bool wgrad_supported(const ConvWgradArgs& a) {
-  bool seg_ok = a.nsrc == 1;
-  if (!seg_ok) {
-    seg_ok = a.Cin % 128 == 0;
-    for (int i = 0; i < a.nsrc; ++i) seg_ok = seg_ok && a.src[i].C % 128 == 0;
-  }
-  long maxbytes = 0;
-  for (int i = 0; i < a.nsrc; ++i) {
-    const long rows = a.src[i].period > 0 ? a.src[i].period : a.P;
-    maxbytes = std::max(maxbytes, rows * a.src[i].stride * 2);
-  }
-  return seg_ok && maxbytes < (1L << 31) && a.P * a.dy_stride * 2 < (1L << 31) && a.P < (1L << 30);
-}
-
-// wgrad v3 shapes: (KH, KW) -> pixel tile (TH x TW)
-inline bool wgrad3_shape(int KH, int KW) {
-  return (KH == 1 && KW == 5) || (KH == 5 && KW == 1) || (KH == 3 && KW == 3);
-}
-
-// Split count: ~one round of workgroups over the 256 CUs.  When a whole number of splits per
-// XCD fills >= 7/8 of its 32 CUs, every tile of a split runs on one XCD (its rows are fetched
-// into that XCD's L2 once); otherwise splits are interleaved over the chip.
-inline void choose_splits(long tiles, long work_units, long& splits, long& g, long target = 256) {
-  g = (target / 8) / tiles;
-  if (g * tiles < (target / 8) * 7 / 8) g = 0;
-  splits = g > 0 ? 8 * g : std::max(1L, (target + tiles / 2) / tiles);
-  if (splits > work_units) splits = work_units, g = 0;
-  if (splits < 1) splits = 1;
-}
-
-WgradPlan plan_conv_wgrad3(const ConvWgradArgs& a) {
-  WgradPlan pl{};
-  pl.kind = 3;
-  const bool sq = a.KH == 3;
-  // 64 output channels per workgroup and ~2 workgroups per CU: the kernel is built for two
-  // waves per SIMD (amdgpu_waves_per_eu(2)), which hides the DMA / transposed-read latency
-  // that bound the one-wave 128-channel variant (scripts/bench_convs.py on MI355X: 3x3
-  // wgrads 1.2-1.3x faster, 1x5/5x1 1.05-1.1x)
-  pl.BM = 64;
-  pl.BN = 64 * a.KH * a.KW;
-  pl.tilesM = (a.N + pl.BM - 1) / pl.BM;
-  pl.tilesN = a.Cin / 64;
-  pl.Npad = pl.tilesM * pl.BM;
-  const int TH = sq ? 8 : (a.KH == 5 ? 16 : 1), TW = 64 / TH;
-  const long ntiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
-  long splits, g;
-  choose_splits((long)pl.tilesM * pl.tilesN, ntiles, splits, g, 512);
-  long per = (ntiles + splits - 1) / splits;
-  if ((ntiles + per - 1) / per != splits) g = 0;
-  pl.nsplit = (int)((ntiles + per - 1) / per);
-  pl.pix_per_split = per;
-  pl.xcd_g = (int)g;
-  return pl;
-}
-
-WgradPlan plan_conv_wgrad(const ConvWgradArgs& a) {
-  bool v3 = wgrad3_shape(a.KH, a.KW) && a.Cin % 64 == 0;
-  for (int i = 0; i < a.nsrc; ++i) v3 = v3 && a.src[i].C % 64 == 0;
-  if (v3) return plan_conv_wgrad3(a);
-  WgradPlan pl{};
-  pl.kind = 2;
-  const bool big = a.N > 64;
-  pl.BM = big ? 128 : 64;
-  pl.BN = 128;
-  pl.tilesM = (a.N + pl.BM - 1) / pl.BM;
-  pl.tilesN = (a.K + pl.BN - 1) / pl.BN;
-  pl.Npad = pl.tilesM * pl.BM;
-  long splits, g;
-  choose_splits((long)pl.tilesM * pl.tilesN, (a.P + 255) / 256, splits, g);
-  long per = (a.P + splits - 1) / splits;
-  per = (per + WBK - 1) / WBK * WBK;
-  if ((a.P + per - 1) / per != splits) g = 0;  // rounding dropped a split: plain mapping
-  pl.nsplit = (int)((a.P + per - 1) / per);
-  pl.pix_per_split = per;
-  pl.xcd_g = (int)g;
-  return pl;
 }
 
 hipError_t launch_conv_wgrad(ConvWgradArgs a, const WgradPlan& pl, hipStream_t s) {

@@ -12,92 +12,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include "kernel_abi.h"
+
 namespace raft_amd {
 
-constexpr int kEncTab = 256;
-struct EncSrc {
-  const void* ptr;
-  int stride, C, H, W, is;
-};
-struct EncClass {
-  int t0, Gh, Gw, oy0, ox0, K, Kpad, tiles_img, blk0;
-  long wofs;
-};
-struct EncConvArgs {
-  EncSrc src[2];
-  int B;
-  int tab[kEncTab];
-  int ptab[kEncTab];
-  EncClass cls[4];
-  int ncls, N, tilesN;
-  const void* wt;
-  int Ho, Wo, os;
-  void* out;
-  int out_stride;
-  const float* bias;
-  const void* res;
-  int res_stride;
-  const void* mask;
-  int mask_stride;
-  float* stats;
-  const float* w[2];
-  long ws[2][4];
-  int wcin[2];
-  int pack_dgrad;
-};
-struct EncWgradArgs {
-  const void* x;
-  int xstride, Cx;
-  int B, Hx, Wx, Ho, Wo, KH, KW, stride, pad;
-  const void* dy;
-  int dy_stride, N;
-  int K, Kpad, Npad, tilesM, tilesN;
-  long P;
-  int pix_per_split, nsplit;
-  float* slab;
-  float* dbslab;
-};
-struct NormFinArgs {
-  const float* stats;
-  int B, T, BM, HW, N, kind;
-  const float* gamma;
-  const float* beta;
-  float* rmean;
-  float* rvar;
-  long long* nbt;
-  float momentum, eps;
-  float* coef;
-};
-struct NormBwdArgs {
-  const void* g;
-  const void* a0;
-  const float* c0;
-  int relu0;
-  const void* a1;
-  const float* c1;
-  float* part;
-  int B, HW, N, R, kind;
-  float* bcoef;
-  float* dgamma[2];
-  float* dbeta[2];
-  void* out0;
-  void* out1;
-};
-
-// launchers (encoder.hip); the device-side structs hold __bf16 pointers with the same layout
-int enc_tile_bn(int N);
-hipError_t launch_enc_pack(const EncConvArgs& a, int rows, void* out, hipStream_t s);
-hipError_t launch_enc_conv(const EncConvArgs& a, int nblocks, hipStream_t s);
-hipError_t launch_enc_wgrad(const EncWgradArgs& a, int BM, int BN, hipStream_t s);
-hipError_t launch_enc_wgrad_reduce(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, float* dw,
-                                   const long* ws, int Cout, int Cin, int Cx, int KH, int KW, float* db,
-                                   bool accumulate, hipStream_t s);
-hipError_t launch_enc_prep(const float* i0, const float* i1, const long* st, int B, int H, int W, int nimg,
-                           void* out, hipStream_t s);
-hipError_t launch_enc_norm_finalize(const NormFinArgs& a, hipStream_t s);
-hipError_t launch_enc_apply(const void* a, const float* ca, bool relu_a, const void* r, const float* cr,
-                            bool relu_out, void* out, int B, int HW, int N, hipStream_t s);
-hipError_t launch_enc_norm_bwd(const NormBwdArgs& a, hipStream_t s);
 
 namespace {
 
@@ -122,6 +40,10 @@ void check_w(const at::Tensor& w, const char* name) {
 }
 
 int round_up(long v, int m) { return (int)((v + m - 1) / m * m); }
+
+// typed views of bf16 tensor storage for the kernel argument structs
+const __bf16* cbf(const at::Tensor& t) { return static_cast<const __bf16*>(t.data_ptr()); }
+__bf16* mbf(const at::Tensor& t) { return static_cast<__bf16*>(t.data_ptr()); }
 
 int enc_tab_entry(int dy, int dx, int src, int c) {
   TORCH_CHECK(dy > -128 && dy < 128 && dx > -128 && dx < 128 && c < (1 << 14), "decode table range");
@@ -152,7 +74,7 @@ void run_conv(EncConvArgs& a, int rows, const at::TensorOptions& o) {
     blocks += a.B * cl.tiles_img * a.tilesN;
   }
   at::Tensor wt = at::empty({wtotal}, o.dtype(at::kBFloat16));
-  a.wt = wt.data_ptr();
+  a.wt = cbf(wt);
   check(launch_enc_pack(a, rows, wt.data_ptr(), stream()), "enc_pack");
   if (blocks > 0) check(launch_enc_conv(a, blocks, stream()), "enc_conv");
 }
@@ -177,7 +99,7 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
   const int Ho = (H + 2 * (int)pad - KH) / (int)stride + 1, Wo = (W + 2 * (int)pad - KW) / (int)stride + 1;
   EncConvArgs a;
   init_args(a);
-  a.src[0] = {x.data_ptr(), Cx, Cx, H, W, (int)stride};
+  a.src[0] = {cbf(x), Cx, Cx, H, W, (int)stride};
   a.B = B;
   a.N = N;
   int e = 0;
@@ -197,7 +119,7 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
   a.Ho = Ho;
   a.Wo = Wo;
   a.os = 1;
-  a.out = y.data_ptr();
+  a.out = mbf(y);
   a.out_stride = N;
   at::Tensor b;
   if (bias.has_value() && bias->defined()) {
@@ -241,7 +163,7 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
     const int Wo = ((int)W + 2 * (int)pads[j] - KW) / (int)strides[j] + 1;
     TORCH_CHECK(dys[j].size(1) == Ho && dys[j].size(2) == Wo, "dy spatial shape does not match the conv");
     const int C = (int)dys[j].size(3);
-    a.src[j] = {dys[j].data_ptr(), C, C, Ho, Wo, S / (int)strides[j]};
+    a.src[j] = {cbf(dys[j]), C, C, Ho, Wo, S / (int)strides[j]};
     set_weight(a, j, ws[j]);
   }
   int e = 0, ncls = 0;
@@ -278,18 +200,18 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
   a.Ho = (int)H;
   a.Wo = (int)W;
   a.os = S;
-  a.out = dx.data_ptr();
+  a.out = mbf(dx);
   a.out_stride = Cin;
   if (res.has_value() && res->defined()) {
     check_nhwc(*res, "res");
     TORCH_CHECK(res->sizes() == dx.sizes(), "res shape");
-    a.res = res->data_ptr();
+    a.res = cbf(*res);
     a.res_stride = Cin;
   }
   if (mask.has_value() && mask->defined()) {
     check_nhwc(*mask, "mask");
     TORCH_CHECK(mask->sizes() == dx.sizes(), "mask shape");
-    a.mask = mask->data_ptr();
+    a.mask = cbf(*mask);
     a.mask_stride = Cin;
   }
   a.pack_dgrad = 1;
@@ -310,7 +232,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
   TORCH_CHECK(Ho == (Hx + 2 * (int)pad - KH) / (int)stride + 1 && Wo == (Wx + 2 * (int)pad - KW) / (int)stride + 1,
               "wgrad spatial shapes");
   EncWgradArgs a{};
-  a.x = x.data_ptr();
+  a.x = cbf(x);
   a.xstride = Cx;
   a.Cx = Cx;
   a.B = B;
@@ -322,7 +244,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
   a.KW = KW;
   a.stride = (int)stride;
   a.pad = (int)pad;
-  a.dy = dy.data_ptr();
+  a.dy = cbf(dy);
   a.dy_stride = N;
   a.N = N;
   const int BM = (N % 128 == 0) ? 128 : 64;
@@ -460,15 +382,15 @@ std::vector<at::Tensor> enc_norm_bwd(const at::Tensor& g, const at::Tensor& a0, 
   const int B = (int)g.size(0), HW = (int)(g.size(1) * g.size(2)), N = (int)g.size(3);
   TORCH_CHECK(N <= 256, "norm backward: at most 256 channels");
   NormBwdArgs a{};
-  a.g = g.data_ptr();
-  a.a0 = a0.data_ptr();
+  a.g = cbf(g);
+  a.a0 = cbf(a0);
   a.c0 = c0.data_ptr<float>();
   a.relu0 = relu0 ? 1 : 0;
   const bool two = a1.has_value() && a1->defined();
   if (two) {
     check_nhwc(*a1, "a1");
     TORCH_CHECK(a1->sizes() == g.sizes(), "a1 shape");
-    a.a1 = a1->data_ptr();
+    a.a1 = cbf(*a1);
     a.c1 = c1->data_ptr<float>();
   }
   a.B = B;
@@ -482,8 +404,8 @@ std::vector<at::Tensor> enc_norm_bwd(const at::Tensor& g, const at::Tensor& a0, 
   a.part = part.data_ptr<float>();
   a.bcoef = bcoef.data_ptr<float>();
   at::Tensor da0 = at::empty_like(g), da1 = two ? at::empty_like(g) : at::Tensor();
-  a.out0 = da0.data_ptr();
-  a.out1 = two ? da1.data_ptr() : nullptr;
+  a.out0 = mbf(da0);
+  a.out1 = two ? mbf(da1) : nullptr;
   std::vector<at::Tensor> out{da0, da1, at::Tensor(), at::Tensor(), at::Tensor(), at::Tensor()};
   if (kind == 2 || kind == 3) {
     for (int j = 0; j < (two ? 2 : 1); ++j) {

@@ -28,97 +28,18 @@
 // 3-channel stem (padded to 8) and the small encoder's 8/16/24-channel bottlenecks, runs
 // through one kernel family.
 #include "common.h"
+#include "kernel_abi.h"
 
 #include <algorithm>
 
 namespace raft_amd {
 
-constexpr int kEncTab = 256;  // K/8 decode-table entries per launch (all classes)
 
-struct EncSrc {
-  const __bf16* ptr;
-  int stride;  // elements between consecutive pixels
-  int C;       // channels (multiple of 8)
-  int H, W;    // spatial dims
-  int is;      // source step per grid step
-};
 
-struct EncClass {
-  int t0;            // first decode-table entry
-  int Gh, Gw;        // pixel grid per image
-  int oy0, ox0;      // output coordinate = grid * os + o0
-  int K, Kpad;       // GEMM depth (Kpad: multiple of 64)
-  int tiles_img;     // BM-row tiles per image
-  int blk0;          // first workgroup of this class
-  long wofs;         // element offset of the class's packed weights [N][Kpad]
-};
 
-struct EncConvArgs {
-  EncSrc src[2];
-  int B;
-  // decode table: (dy+128) | (dx+128) << 8 | src << 16 | c << 17, -1 = zero columns
-  int tab[kEncTab];
-  // packing table: w | ky << 4 | kx << 8 | local << 12, -1 = zero columns
-  int ptab[kEncTab];
-  EncClass cls[4];
-  int ncls, N, tilesN;
-  const __bf16* wt;
-  int Ho, Wo, os;
-  __bf16* out;
-  int out_stride;
-  const float* bias;
-  const __bf16* res;
-  int res_stride;
-  const __bf16* mask;
-  int mask_stride;
-  float* stats;  // [B * tiles_img][2][N]: per tile column sum and M2
-  // weight packing
-  const float* w[2];
-  long ws[2][4];
-  int wcin[2];
-  int pack_dgrad;
-};
 
-struct EncWgradArgs {
-  const __bf16* x;
-  int xstride, Cx;
-  int B, Hx, Wx, Ho, Wo, KH, KW, stride, pad;
-  const __bf16* dy;
-  int dy_stride, N;
-  int K, Kpad, Npad, tilesM, tilesN;
-  long P;
-  int pix_per_split, nsplit;
-  float* slab;    // [nsplit][Npad][Kpad]
-  float* dbslab;  // [nsplit][Npad] or null
-};
 
-struct NormFinArgs {
-  const float* stats;  // conv epilogue tiles [B][T][2][N]
-  int B, T, BM, HW, N, kind;
-  const float* gamma;
-  const float* beta;
-  float* rmean;
-  float* rvar;
-  long long* nbt;
-  float momentum, eps;
-  float* coef;
-};
 
-struct NormBwdArgs {
-  const __bf16* g;
-  const __bf16* a0;
-  const float* c0;
-  int relu0;
-  const __bf16* a1;  // null: one branch
-  const float* c1;
-  float* part;
-  int B, HW, N, R, kind;
-  float* bcoef;  // [B][2][3][N]: da = k1 * dy + k2 * xhat + k3
-  float* dgamma[2];
-  float* dbeta[2];
-  __bf16* out0;
-  __bf16* out1;
-};
 
 namespace {
 

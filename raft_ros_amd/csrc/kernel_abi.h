@@ -1,0 +1,341 @@
+// Kernel ABI of the native extension: the argument structs shared by the HIP kernels
+// (csrc/*.hip, device side) and the torch bindings (csrc/*bindings.cpp, host side), their
+// launchers, and the host-only planning of the weight-gradient launches.  One definition
+// for both sides, so a field added for a kernel cannot silently shift the host layout.
+// Everything above the launcher section is plain C++ (the planning is unit-tested under
+// AddressSanitizer / UBSan on the host: tests/native/plan_test.cpp).
+#pragma once
+
+#include <algorithm>
+
+#if defined(__HIP__)
+#define RAFT_HD __host__ __device__
+#else
+#define RAFT_HD
+#endif
+
+namespace raft_amd {
+
+// ============================================================================ work mapping
+// Workgroups are dealt round-robin to the 8 XCDs (blockIdx % 8).  xcd_remap: contiguous
+// tile ranges per XCD (neighbouring tiles share operand rows in that XCD's L2); a bijection
+// of [0, nwg).
+RAFT_HD inline int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (orig >> 3);
+}
+
+// Weight-gradient launches: workgroup -> (pixel split, output tile).  With xcd_g > 0
+// (nsplit == 8 * xcd_g) every tile of a split runs on one XCD so the split's dY / X rows are
+// fetched into that XCD's L2 once; otherwise splits are laid out consecutively.
+RAFT_HD inline void wgrad_block_map(int bid, int tiles, int xcd_g, int& split, int& tile) {
+  if (xcd_g > 0) {
+    const int xcd = bid & 7, local = bid >> 3;
+    const int si = local / tiles;
+    tile = local - si * tiles;
+    split = xcd * xcd_g + si;
+  } else {
+    split = bid / tiles;
+    tile = bid - split * tiles;
+  }
+}
+
+// ============================================================================ update-block convs
+struct ConvSrc {
+  const __bf16* ptr;
+  long stride;  // elements between consecutive pixels
+  int C;        // channels taken from this source (multiple of 8)
+  int period;   // wgrad only: >0 -> pixel p reads row p % period (0: no wrap)
+};
+
+struct ConvFwdArgs {
+  ConvSrc src[3];
+  int nsrc, Cin;
+  int B, H, W, KH, KW, PH, PW;
+  int K, Kpad;
+  const __bf16* wt;  // packed weights [N][Kpad], k = tap*Cin + c
+  int N;
+  long P;
+  // epilogue
+  int epi;      // 0: bias+act store, 1: grad store, 2: GRU z||r, 3: GRU q+blend
+  int act;      // 0: none, 1: relu
+  int out_f32;  // output element type (epi 0/1)
+  int acc_c0;   // epi 1: accumulate (+=) into out for channels n >= acc_c0
+  float alpha;
+  const float* bias;
+  void* out;
+  long out_stride;
+  const __bf16* mask;  // epi 1: multiply by (mask[p][n] > 0) (ReLU' of the conv input)
+  long mask_stride;
+  const __bf16* h;  // epi 2/3: hidden state
+  long h_stride;
+  const __bf16* z;  // epi 3: update gate
+  long z_stride;
+  __bf16* out2;  // epi 2: r*h, epi 3: tanh(q), epi 4: dq
+  long out2_stride;
+  // fused GRU backward (data-gradient launches of the update block): output channels
+  // [0, gru_cols) finish the gate math in the epilogue, the rest are stored as epi 1
+  //   epi 4 (after the dH-producing dgrad): g = dH; dq = g z (1 - q^2) -> out2,
+  //          dz = g (q - h) z (1 - z) -> out3, carry = g (1 - z)  (out not written)
+  //   epi 5 (the q dgrad, g = d(r*h)): dr = g h r (1 - r) -> out3, out = carry + g r
+  //   epi 6 (the last GRU dgrad): channels [0, gru_cols) -> bf16 out3 (d net), [gru_cols,
+  //          cm_c0) -> out as epi 1, [cm_c0, N) -> bf16 cout = (cmask > 0 ? g : 0), zero past
+  //          cm_valid (the ReLU' of the motion features; out not written)
+  const __bf16* g0;  // epi 4: q, epi 5: r
+  long g0_stride;
+  float* carry;
+  long carry_stride;
+  __bf16* out3;
+  long out3_stride;
+  int gru_cols;
+  const __bf16* addsrc;  // epi 4: incoming bf16 gradient added to g (null: none)
+  long addsrc_stride;
+  __bf16* cout;
+  long cout_stride;
+  const __bf16* cmask;
+  long cmask_stride;
+  int cm_c0, cm_valid;
+  int cfg;  // kernel variant: 0 = automatic, otherwise forced (tests / microbenchmarks)
+};
+
+struct ConvWgradArgs {
+  ConvSrc src[3];
+  int nsrc, Cin;
+  int B, H, W, KH, KW, PH, PW;
+  int K, Kpad;
+  const __bf16* dy;  // [P][dy_stride], N channels used
+  long dy_stride;
+  int N;
+  long P;
+  long pix_per_split;
+  float* slab;    // [nsplit][Npad][Kpad] fp32: the split's partial dW (written, not accumulated)
+  float* dbslab;  // [nsplit][tilesN][Npad] fp32 bias partials (may be null)
+  int Npad;       // slab rows (N rounded up to the row tile)
+  int xcd_g;      // >0: XCD-grouped split mapping with xcd_g splits per XCD (set by the launcher)
+};
+
+// Plan of one weight-gradient launch (the caller sizes the slabs from it).
+//   kind 2: wgrad v2, tilesN = column tiles, pix_per_split = pixels per split
+//   kind 3: wgrad v3 (tap-batched), tilesN = 64-channel chunks, pix_per_split = pixel TILES per split
+// Bias partials: nsplit * tilesN rows of Npad floats.
+struct WgradPlan {
+  int BM, BN, tilesM, tilesN, nsplit, Npad, xcd_g;
+  long pix_per_split;
+  int kind;
+};
+
+struct ConvParamDesc {
+  float* w[2];     // parameter (pack: read) / gradient (reduce: written) tensors
+  long ws[2][4];   // strides (Cout, Cin, kh, kw) in elements
+  float* b[2];     // biases / bias gradients (may be null)
+  int rows[2];     // Cout of each stacked parameter (rows[1] = 0: single)
+  int nseg;
+  int seg_real[3], seg_pad[3];
+  int Cin, Cin_pad, KH, KW;
+  float scale;
+};
+
+// ============================================================================ encoder convs
+constexpr int kEncTab = 256;  // K/8 decode-table entries per launch (all classes)
+
+struct EncSrc {
+  const __bf16* ptr;
+  int stride;  // elements between consecutive pixels
+  int C;       // channels (multiple of 8)
+  int H, W;    // spatial dims
+  int is;      // source step per grid step
+};
+
+struct EncClass {
+  int t0;            // first decode-table entry
+  int Gh, Gw;        // pixel grid per image
+  int oy0, ox0;      // output coordinate = grid * os + o0
+  int K, Kpad;       // GEMM depth (Kpad: multiple of 64)
+  int tiles_img;     // BM-row tiles per image
+  int blk0;          // first workgroup of this class
+  long wofs;         // element offset of the class's packed weights [N][Kpad]
+};
+
+struct EncConvArgs {
+  EncSrc src[2];
+  int B;
+  // decode table: (dy+128) | (dx+128) << 8 | src << 16 | c << 17, -1 = zero columns
+  int tab[kEncTab];
+  // packing table: w | ky << 4 | kx << 8 | local << 12, -1 = zero columns
+  int ptab[kEncTab];
+  EncClass cls[4];
+  int ncls, N, tilesN;
+  const __bf16* wt;
+  int Ho, Wo, os;
+  __bf16* out;
+  int out_stride;
+  const float* bias;
+  const __bf16* res;
+  int res_stride;
+  const __bf16* mask;
+  int mask_stride;
+  float* stats;  // [B * tiles_img][2][N]: per tile column sum and M2
+  // weight packing
+  const float* w[2];
+  long ws[2][4];
+  int wcin[2];
+  int pack_dgrad;
+};
+
+struct EncWgradArgs {
+  const __bf16* x;
+  int xstride, Cx;
+  int B, Hx, Wx, Ho, Wo, KH, KW, stride, pad;
+  const __bf16* dy;
+  int dy_stride, N;
+  int K, Kpad, Npad, tilesM, tilesN;
+  long P;
+  int pix_per_split, nsplit;
+  float* slab;    // [nsplit][Npad][Kpad]
+  float* dbslab;  // [nsplit][Npad] or null
+};
+
+struct NormFinArgs {
+  const float* stats;  // conv epilogue tiles [B][T][2][N]
+  int B, T, BM, HW, N, kind;
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  long long* nbt;
+  float momentum, eps;
+  float* coef;
+};
+
+struct NormBwdArgs {
+  const __bf16* g;
+  const __bf16* a0;
+  const float* c0;
+  int relu0;
+  const __bf16* a1;  // null: one branch
+  const float* c1;
+  float* part;
+  int B, HW, N, R, kind;
+  float* bcoef;  // [B][2][3][N]: da = k1 * dy + k2 * xhat + k3
+  float* dgamma[2];
+  float* dbeta[2];
+  __bf16* out0;
+  __bf16* out1;
+};
+
+// ============================================================================ host-side planning
+constexpr int kWgradBK = 64;  // pixels per K step of wgrad v2 (conv_igemm.hip WBK)
+
+inline bool wgrad_supported(const ConvWgradArgs& a) {
+  bool seg_ok = a.nsrc == 1;
+  if (!seg_ok) {
+    seg_ok = a.Cin % 128 == 0;
+    for (int i = 0; i < a.nsrc; ++i) seg_ok = seg_ok && a.src[i].C % 128 == 0;
+  }
+  long maxbytes = 0;
+  for (int i = 0; i < a.nsrc; ++i) {
+    const long rows = a.src[i].period > 0 ? a.src[i].period : a.P;
+    maxbytes = std::max(maxbytes, rows * a.src[i].stride * 2);
+  }
+  return seg_ok && maxbytes < (1L << 31) && a.P * a.dy_stride * 2 < (1L << 31) && a.P < (1L << 30);
+}
+
+// wgrad v3 shapes: (KH, KW) -> pixel tile (TH x TW)
+inline bool wgrad3_shape(int KH, int KW) {
+  return (KH == 1 && KW == 5) || (KH == 5 && KW == 1) || (KH == 3 && KW == 3);
+}
+
+// Split count: ~one round of workgroups over the 256 CUs.  When a whole number of splits per
+// XCD fills >= 7/8 of its 32 CUs, every tile of a split runs on one XCD (its rows are fetched
+// into that XCD's L2 once); otherwise splits are interleaved over the chip.
+inline void choose_splits(long tiles, long work_units, long& splits, long& g, long target = 256) {
+  g = (target / 8) / tiles;
+  if (g * tiles < (target / 8) * 7 / 8) g = 0;
+  splits = g > 0 ? 8 * g : std::max(1L, (target + tiles / 2) / tiles);
+  if (splits > work_units) splits = work_units, g = 0;
+  if (splits < 1) splits = 1;
+}
+
+inline WgradPlan plan_conv_wgrad3(const ConvWgradArgs& a) {
+  WgradPlan pl{};
+  pl.kind = 3;
+  const bool sq = a.KH == 3;
+  // 64 output channels per workgroup and ~2 workgroups per CU: the kernel is built for two
+  // waves per SIMD (amdgpu_waves_per_eu(2)), which hides the DMA / transposed-read latency
+  // that bound the one-wave 128-channel variant (scripts/bench_convs.py on MI355X: 3x3
+  // wgrads 1.2-1.3x faster, 1x5/5x1 1.05-1.1x)
+  pl.BM = 64;
+  pl.BN = 64 * a.KH * a.KW;
+  pl.tilesM = (a.N + pl.BM - 1) / pl.BM;
+  pl.tilesN = a.Cin / 64;
+  pl.Npad = pl.tilesM * pl.BM;
+  const int TH = sq ? 8 : (a.KH == 5 ? 16 : 1), TW = 64 / TH;
+  const long ntiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
+  long splits, g;
+  choose_splits((long)pl.tilesM * pl.tilesN, ntiles, splits, g, 512);
+  long per = (ntiles + splits - 1) / splits;
+  if ((ntiles + per - 1) / per != splits) g = 0;
+  pl.nsplit = (int)((ntiles + per - 1) / per);
+  pl.pix_per_split = per;
+  pl.xcd_g = (int)g;
+  return pl;
+}
+
+inline WgradPlan plan_conv_wgrad(const ConvWgradArgs& a) {
+  bool v3 = wgrad3_shape(a.KH, a.KW) && a.Cin % 64 == 0;
+  for (int i = 0; i < a.nsrc; ++i) v3 = v3 && a.src[i].C % 64 == 0;
+  if (v3) return plan_conv_wgrad3(a);
+  WgradPlan pl{};
+  pl.kind = 2;
+  const bool big = a.N > 64;
+  pl.BM = big ? 128 : 64;
+  pl.BN = 128;
+  pl.tilesM = (a.N + pl.BM - 1) / pl.BM;
+  pl.tilesN = (a.K + pl.BN - 1) / pl.BN;
+  pl.Npad = pl.tilesM * pl.BM;
+  long splits, g;
+  choose_splits((long)pl.tilesM * pl.tilesN, (a.P + 255) / 256, splits, g);
+  long per = (a.P + splits - 1) / splits;
+  per = (per + kWgradBK - 1) / kWgradBK * kWgradBK;
+  if ((a.P + per - 1) / per != splits) g = 0;  // rounding dropped a split: plain mapping
+  pl.nsplit = (int)((a.P + per - 1) / per);
+  pl.pix_per_split = per;
+  pl.xcd_g = (int)g;
+  return pl;
+}
+
+
+}  // namespace raft_amd
+
+#ifndef RAFT_ABI_NO_HIP
+#include <hip/hip_runtime_api.h>
+
+namespace raft_amd {
+// conv_igemm.hip
+hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s);
+hipError_t launch_conv_wgrad(ConvWgradArgs a, const WgradPlan& pl, hipStream_t s);
+// weights.hip
+hipError_t launch_pack_conv_weights(const ConvParamDesc& d, int N, void* wf, int Kf, void* wd, int Kd, int Cout_pad,
+                                    float* bias, hipStream_t s);
+hipError_t launch_wgrad_reduce_params(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, int ndb,
+                                      const ConvParamDesc& d, int N, int accumulate, hipStream_t s);
+hipError_t launch_wgrad_reduce_packed(const float* slab, int nsplit, int Npad, int Kpad, int K, const float* dbslab,
+                                      int ndb, float* dw, long ldw, float* db, int N, int accumulate, hipStream_t s);
+// encoder.hip
+int enc_tile_bn(int N);
+hipError_t launch_enc_pack(const EncConvArgs& a, int rows, void* out, hipStream_t s);
+hipError_t launch_enc_conv(const EncConvArgs& a, int nblocks, hipStream_t s);
+hipError_t launch_enc_wgrad(const EncWgradArgs& a, int BM, int BN, hipStream_t s);
+hipError_t launch_enc_wgrad_reduce(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, float* dw,
+                                   const long* ws, int Cout, int Cin, int Cx, int KH, int KW, float* db,
+                                   bool accumulate, hipStream_t s);
+hipError_t launch_enc_prep(const float* i0, const float* i1, const long* st, int B, int H, int W, int nimg,
+                           void* out, hipStream_t s);
+hipError_t launch_enc_norm_finalize(const NormFinArgs& a, hipStream_t s);
+hipError_t launch_enc_apply(const void* a, const float* ca, bool relu_a, const void* r, const float* cr,
+                            bool relu_out, void* out, int B, int HW, int N, hipStream_t s);
+hipError_t launch_enc_norm_bwd(const NormBwdArgs& a, hipStream_t s);
+}  // namespace raft_amd
+#endif

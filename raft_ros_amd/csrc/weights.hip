@@ -16,19 +16,10 @@
 //     parameters, in the parameters' own strides -- straight into the
 //     parameter gradients, or accumulated into a packed fp32 [N][Kpad] buffer.
 #include "common.h"
+#include "kernel_abi.h"
 
 namespace raft_amd {
 
-struct ConvParamDesc {
-  float* w[2];     // parameter (pack: read) / gradient (reduce: written) tensors
-  long ws[2][4];   // strides (Cout, Cin, kh, kw) in elements
-  float* b[2];     // biases / bias gradients (may be null)
-  int rows[2];     // Cout of each stacked parameter (rows[1] = 0: single)
-  int nseg;
-  int seg_real[3], seg_pad[3];
-  int Cin, Cin_pad, KH, KW;
-  float scale;
-};
 
 namespace {
 

@@ -1,0 +1,138 @@
+// Host-side unit test of the kernel work planning in csrc/kernel_abi.h, built and run under
+// AddressSanitizer + UndefinedBehaviorSanitizer by tests/test_native_plan_cpu.py (no GPU):
+//   * xcd_remap is a bijection of [0, nwg) for every grid size;
+//   * every weight-gradient plan (v2 pixel splits, v3 tap-batched tile splits, with and
+//     without the XCD-grouped mapping) covers each (split, output tile) pair exactly once,
+//     has no empty split, pads N to whole row tiles and keeps the pixel ranges in bounds;
+//   * the slab sizes the bindings allocate from a plan stay addressable.
+#define RAFT_ABI_NO_HIP
+#include "kernel_abi.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace raft_amd;
+
+static int failures = 0;
+#define EXPECT(cond, ...)                                  \
+  do {                                                     \
+    if (!(cond)) {                                         \
+      ++failures;                                          \
+      if (failures < 20) {                                 \
+        std::fprintf(stderr, "FAIL %s:%d: %s | ", __FILE__, __LINE__, #cond); \
+        std::fprintf(stderr, __VA_ARGS__);                 \
+        std::fprintf(stderr, "\n");                        \
+      }                                                    \
+    }                                                      \
+  } while (0)
+
+static void test_xcd_remap() {
+  for (int nwg = 1; nwg <= 4099; nwg += (nwg < 64 ? 1 : 37)) {
+    std::vector<int> seen(nwg, 0);
+    for (int b = 0; b < nwg; ++b) {
+      const int w = xcd_remap(b, nwg);
+      EXPECT(w >= 0 && w < nwg, "nwg=%d b=%d -> %d", nwg, b, w);
+      if (w >= 0 && w < nwg) ++seen[w];
+    }
+    for (int w = 0; w < nwg; ++w) EXPECT(seen[w] == 1, "nwg=%d tile %d seen %d times", nwg, w, seen[w]);
+  }
+}
+
+static ConvWgradArgs make_args(int B, int H, int W, int KH, int KW, int Cin, int N, int nsrc) {
+  ConvWgradArgs a{};
+  a.B = B;
+  a.H = H;
+  a.W = W;
+  a.KH = KH;
+  a.KW = KW;
+  a.PH = KH / 2;
+  a.PW = KW / 2;
+  a.nsrc = nsrc;
+  a.Cin = Cin;
+  const int per = Cin / nsrc;
+  for (int i = 0; i < nsrc; ++i) {
+    a.src[i].C = per;
+    a.src[i].stride = per;
+    a.src[i].period = 0;
+  }
+  a.K = KH * KW * Cin;
+  a.Kpad = (a.K + 63) / 64 * 64;
+  a.N = N;
+  a.dy_stride = (N + 7) / 8 * 8;
+  a.P = (long)B * H * W;
+  return a;
+}
+
+static void check_plan(const ConvWgradArgs& a) {
+  const WgradPlan pl = plan_conv_wgrad(a);
+  EXPECT(pl.kind == 2 || pl.kind == 3, "kind %d", pl.kind);
+  EXPECT(pl.nsplit >= 1 && pl.tilesM >= 1 && pl.tilesN >= 1, "nsplit %d tiles %dx%d", pl.nsplit, pl.tilesM,
+         pl.tilesN);
+  EXPECT(pl.Npad == pl.tilesM * pl.BM && pl.Npad >= a.N && pl.Npad - a.N < pl.BM, "Npad %d N %d BM %d", pl.Npad,
+         a.N, pl.BM);
+  // work units split over the grid: pixels (v2) or 64-pixel tiles (v3)
+  long units;
+  if (pl.kind == 3) {
+    const int TH = a.KH == 3 ? 8 : (a.KH == 5 ? 16 : 1), TW = 64 / TH;
+    units = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
+    EXPECT(pl.tilesN == a.Cin / 64, "v3 chunks %d for Cin %d", pl.tilesN, a.Cin);
+  } else {
+    units = a.P;
+    EXPECT(pl.pix_per_split % kWgradBK == 0, "v2 split %ld not a multiple of the K step", pl.pix_per_split);
+    EXPECT(pl.tilesN * pl.BN >= a.K, "v2 column tiles %d x %d < K %d", pl.tilesN, pl.BN, a.K);
+  }
+  EXPECT(pl.pix_per_split >= 1, "pix_per_split %ld", pl.pix_per_split);
+  EXPECT((long)(pl.nsplit - 1) * pl.pix_per_split < units, "empty split: %d x %ld vs %ld", pl.nsplit,
+         pl.pix_per_split, units);
+  EXPECT((long)pl.nsplit * pl.pix_per_split >= units, "uncovered work: %d x %ld < %ld", pl.nsplit, pl.pix_per_split,
+         units);
+  if (pl.xcd_g > 0) EXPECT(pl.nsplit == 8 * pl.xcd_g, "xcd_g %d with nsplit %d", pl.xcd_g, pl.nsplit);
+  // the launch grid and its workgroup -> (split, tile) map
+  const int tiles = pl.tilesM * pl.tilesN;
+  const long grid = (long)tiles * pl.nsplit;
+  std::vector<int> seen(grid, 0);
+  for (long b = 0; b < grid; ++b) {
+    int split, tile;
+    wgrad_block_map((int)b, tiles, pl.xcd_g, split, tile);
+    EXPECT(split >= 0 && split < pl.nsplit && tile >= 0 && tile < tiles, "bid %ld -> split %d tile %d", b, split,
+           tile);
+    if (split >= 0 && split < pl.nsplit && tile >= 0 && tile < tiles) ++seen[(long)split * tiles + tile];
+  }
+  for (long i = 0; i < grid; ++i) EXPECT(seen[i] == 1, "(split, tile) %ld visited %d times", i, seen[i]);
+  // slabs the bindings allocate: [nsplit][Npad][Kpad] fp32 (+ bias partials)
+  const double slab_bytes = 4.0 * pl.nsplit * (double)pl.Npad * a.Kpad;
+  EXPECT(slab_bytes < 16e9, "slab %.1f GB", slab_bytes / 1e9);
+}
+
+static void test_wgrad_plans() {
+  const int shapes[][2] = {{1, 1}, {3, 3}, {1, 5}, {5, 1}, {7, 7}};
+  const int couts[] = {2, 8, 64, 96, 126, 128, 192, 256, 384, 512, 576};
+  const int cins[] = {64, 128, 256, 384};
+  const int dims[][3] = {{8, 46, 62}, {96, 46, 62}, {1, 16, 16}, {2, 55, 156}, {6, 135, 240}};
+  int n = 0;
+  for (auto& s : shapes)
+    for (int N : couts)
+      for (int Cin : cins)
+        for (auto& d : dims)
+          for (int nsrc = 1; nsrc <= 3; ++nsrc) {
+            if (Cin % nsrc || (Cin / nsrc) % (nsrc > 1 ? 128 : 8)) continue;
+            const ConvWgradArgs a = make_args(d[0], d[1], d[2], s[0], s[1], Cin, N, nsrc);
+            if (!wgrad_supported(a)) continue;
+            check_plan(a);
+            ++n;
+          }
+  EXPECT(n > 300, "only %d plans checked", n);
+  std::printf("checked %d weight-gradient plans\n", n);
+}
+
+int main() {
+  test_xcd_remap();
+  test_wgrad_plans();
+  if (failures) {
+    std::fprintf(stderr, "%d failures\n", failures);
+    return 1;
+  }
+  std::printf("ok\n");
+  return 0;
+}
