@@ -19,59 +19,11 @@
 
 namespace raft_amd {
 
-struct PyrDesc {
-  float* ptr[4];  // bf16 data when vbf16 (forward lookups of an AMP volume)
-  int H[4];
-  int W[4];
-  long ld[4];
-  int levels;
-  int vbf16;
-  int blk;
-};
-struct CorrGemmArgs {
-  const void* A;
-  long lda, sA;
-  const void* B;
-  long ldb, sB;
-  void* C;
-  long ldc, sC;
-  int M, N, K, batch;
-  float alpha;
-  int a_f32, b_f32, a_trans, split, c_bf16;
-  int epi;  // layouts must match corr_volume.hip
-};
-struct UnpoolArgs {
-  const float* G;
-  long sG;
-  float* out;
-  int B, H, W, C, nseg;
-  int off[4], h[4], w[4];
-  int blk;
-};
 
 enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 
 // launchers (defined in the .hip translation units)
 hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s);
-struct LocalCorrArgs {
-  const void* f1;
-  const void* f2;
-  long f2_bstride;
-  const float* coords;
-  int B, H, W, C, r, levels;
-  int off[4], h[4], w[4];
-  float scale;
-  void* out;
-  long ostride;
-  int out_f32;
-  int out_ch;
-  const void* gout;
-  long gstride;
-  int gout_bf16;
-  float* g1;
-  float* g2;  // layout must match local_corr_mfma.hip
-  long long* g2fix;
-};
 hipError_t launch_fixed_to_float(const long long* in, float* out, long n, hipStream_t s);
 hipError_t launch_local_corr_mfma(const LocalCorrArgs& a, bool backward, hipStream_t s);
 hipError_t launch_pyramid_unpool(const UnpoolArgs& u, hipStream_t s);
@@ -98,13 +50,6 @@ hipError_t launch_convex_up_bwd(const float* flow, const void* mask, int m_dtype
                                 long msH, long msW, const float* gout, void* dmask, long dsN, long dsC,
                                 long dsH, long dsW, float* part, float* dflow, void* rows, int rows_ld, int B,
                                 int H, int W, hipStream_t s);
-constexpr int kMaxPreds = 32;
-struct SeqPreds {
-  const float* p[kMaxPreds];
-};
-struct SeqGrads {
-  float* g[kMaxPreds];
-};
 int seq_loss_num_blocks(long P);
 hipError_t launch_seq_loss_fwd(const SeqPreds& preds, int n, const float* gt, const float* valid,
                                float gamma, float max_flow, long B, long HW, float* partial,
@@ -541,7 +486,7 @@ LocalCorrArgs local_mfma_args(const at::Tensor& f1, const at::Tensor& f2, const 
     TORCH_CHECK(a.off[l] >= 0 && a.h[l] > 0 && a.w[l] > 0 && (long)a.off[l] + (long)a.h[l] * a.w[l] <= f2.size(1),
                 "raft_amd::local_corr_mfma: level ", l, " exceeds fmap2");
   }
-  a.f1 = f1.data_ptr(); a.f2 = f2.data_ptr(); a.f2_bstride = f2.stride(0);
+  a.f1 = static_cast<const __bf16*>(f1.data_ptr()); a.f2 = static_cast<const __bf16*>(f2.data_ptr()); a.f2_bstride = f2.stride(0);
   a.coords = coords.data_ptr<float>();
   a.B = (int)B; a.H = (int)H; a.W = (int)W; a.C = (int)C; a.r = (int)radius;
   a.scale = (float)scale;

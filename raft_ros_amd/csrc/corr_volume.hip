@@ -32,47 +32,13 @@
 
 namespace raft_amd {
 
-struct PyrDesc {
-  float* ptr[4];
-  int H[4];
-  int W[4];
-  long ld[4];  // row pitch (elements) of level l: row `pix` starts at ptr[l] + pix * ld[l]
-  int levels;
-  int vbf16;   // levels hold bf16 (the AMP volume; forward lookups only -- gradients stay fp32)
-  int blk;     // levels stored in 16-column blocks [W/16][H][16] (W = blocks * 16)
-};
 
 // element offset of level pixel (y, x) within a volume row
 __device__ __forceinline__ int lvl_off(int y, int x, int Hl, int Wl, int blk) {
   return blk ? ((((x >> 4) * Hl + y) << 4) | (x & 15)) : y * Wl + x;
 }
 
-// One GEMM of the correlation path: C[b][m][n] (op)= alpha * sum_k A[b][m][k] * B[b][n][k]
-struct CorrGemmArgs {
-  const void* A;  // fp32 or bf16; a_trans: element (m, k) at A[k * lda + m]
-  long lda, sA;
-  const void* B;  // fp32 or bf16, element (n, k) at B[n * ldb + k]
-  long ldb, sB;
-  void* C;  // fp32 (or bf16 for epi 0)
-  long ldc, sC;
-  int M, N, K, batch;
-  float alpha;
-  int a_f32, b_f32, a_trans, split, c_bf16;
-  int epi;  // 0 store, 1 accumulate
-};
 
-// Adjoint of the pyramid pools: out[b][y][x][c] = sum_l G[b][off_l + (y>>l)*w_l + (x>>l)][c] / 4^l
-// over the levels whose (floor-sized) plane covers (y, x).  G holds the per-level gradients
-// of all levels (rows = concatenated levels), so each output element is one thread's sum:
-// deterministic, no read-modify-write races between levels.
-struct UnpoolArgs {
-  const float* G;
-  long sG;  // batch stride of G (elements); row pitch = C
-  float* out;
-  int B, H, W, C, nseg;
-  int off[4], h[4], w[4];
-  int blk;  // level rows in 16-column block order (the dense pyramid's layout)
-};
 
 namespace {
 

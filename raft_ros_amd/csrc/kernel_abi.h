@@ -225,6 +225,77 @@ struct NormBwdArgs {
   __bf16* out1;
 };
 
+// ============================================================================ correlation
+struct PyrDesc {
+  float* ptr[4];
+  int H[4];
+  int W[4];
+  long ld[4];  // row pitch (elements) of level l: row `pix` starts at ptr[l] + pix * ld[l]
+  int levels;
+  int vbf16;   // levels hold bf16 (the AMP volume; forward lookups only -- gradients stay fp32)
+  int blk;     // levels stored in 16-column blocks [W/16][H][16] (W = blocks * 16)
+};
+
+// One GEMM of the correlation path: C[b][m][n] (op)= alpha * sum_k A[b][m][k] * B[b][n][k]
+struct CorrGemmArgs {
+  const void* A;  // fp32 or bf16; a_trans: element (m, k) at A[k * lda + m]
+  long lda, sA;
+  const void* B;  // fp32 or bf16, element (n, k) at B[n * ldb + k]
+  long ldb, sB;
+  void* C;  // fp32 (or bf16 for epi 0)
+  long ldc, sC;
+  int M, N, K, batch;
+  float alpha;
+  int a_f32, b_f32, a_trans, split, c_bf16;
+  int epi;  // 0 store, 1 accumulate
+};
+
+// Adjoint of the pyramid pools: out[b][y][x][c] = sum_l G[b][off_l + (y>>l)*w_l + (x>>l)][c] / 4^l
+// over the levels whose (floor-sized) plane covers (y, x).  G holds the per-level gradients
+// of all levels (rows = concatenated levels), so each output element is one thread's sum:
+// deterministic, no read-modify-write races between levels.
+struct UnpoolArgs {
+  const float* G;
+  long sG;  // batch stride of G (elements); row pitch = C
+  float* out;
+  int B, H, W, C, nseg;
+  int off[4], h[4], w[4];
+  int blk;  // level rows in 16-column block order (the dense pyramid's layout)
+};
+
+struct LocalCorrArgs {
+  const __bf16* f1;   // (B*H*W, C) query features (NHWC rows)
+  const __bf16* f2;   // (B, R, C): pooled fmap2 levels, level l rows [off[l], off[l] + h[l]*w[l])
+  long f2_bstride;    // R * C
+  const float* coords;  // (B, 2, H, W) level-0 pixel coordinates
+  int B, H, W, C, r, levels;
+  int off[4], h[4], w[4];
+  float scale;
+  // forward
+  void* out;  // (B*H*W, ostride) features; level l taps at channel l*(2r+1)^2
+  long ostride;
+  int out_f32;
+  int out_ch;  // channels written per row: taps, then zeros up to out_ch (K padding of convc1)
+  // backward
+  const void* gout;  // (B*H*W, gstride) tap gradients (same layout as out), fp32 or bf16
+  long gstride;
+  int gout_bf16;
+  float* g1;  // (B*H*W, C) fp32
+  float* g2;  // (B, R, C) fp32, accumulated (atomics)
+  long long* g2fix;  // non-null: deterministic mode, 32.32 fixed-point accumulator like g2
+};
+
+// ============================================================================ sequence loss
+constexpr int kMaxPreds = 32;
+
+struct SeqPreds {
+  const float* p[kMaxPreds];
+};
+
+struct SeqGrads {
+  float* g[kMaxPreds];
+};
+
 // ============================================================================ host-side planning
 constexpr int kWgradBK = 64;  // pixels per K step of wgrad v2 (conv_igemm.hip WBK)
 

@@ -30,27 +30,6 @@
 
 namespace raft_amd {
 
-struct LocalCorrArgs {
-  const __bf16* f1;   // (B*H*W, C) query features (NHWC rows)
-  const __bf16* f2;   // (B, R, C): pooled fmap2 levels, level l rows [off[l], off[l] + h[l]*w[l])
-  long f2_bstride;    // R * C
-  const float* coords;  // (B, 2, H, W) level-0 pixel coordinates
-  int B, H, W, C, r, levels;
-  int off[4], h[4], w[4];
-  float scale;
-  // forward
-  void* out;  // (B*H*W, ostride) features; level l taps at channel l*(2r+1)^2
-  long ostride;
-  int out_f32;
-  int out_ch;  // channels written per row: taps, then zeros up to out_ch (K padding of convc1)
-  // backward
-  const void* gout;  // (B*H*W, gstride) tap gradients (same layout as out), fp32 or bf16
-  long gstride;
-  int gout_bf16;
-  float* g1;  // (B*H*W, C) fp32
-  float* g2;  // (B, R, C) fp32, accumulated (atomics)
-  long long* g2fix;  // non-null: deterministic mode, 32.32 fixed-point accumulator like g2
-};
 
 namespace {
 

@@ -19,15 +19,7 @@
 
 namespace raft_amd {
 
-constexpr int kMaxPreds = 32;
 
-struct SeqPreds {
-  const float* p[kMaxPreds];
-};
-
-struct SeqGrads {
-  float* g[kMaxPreds];
-};
 
 namespace {
 
