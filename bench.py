@@ -131,7 +131,10 @@ def run(args):
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
         if distributed:
-            dist.init_process_group("nccl", device_id=device)
+            from raft_ros_amd.parallel.ddp import process_group_kwargs
+
+            # high-priority RCCL stream: DDP's bucket all-reduces overtake queued backward kernels
+            dist.init_process_group("nccl", device_id=device, **process_group_kwargs("nccl"))
     else:
         device = torch.device("cpu")
         torch.set_num_threads(max(1, (os.cpu_count() or 2) // max(world, 1)))

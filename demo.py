@@ -74,6 +74,16 @@ def write_demo_frames(path, n_frames: int = 6):
 
 
 def demo(args):
+    rank = 0
+    if getattr(args, "query_shard", False):
+        # torchrun --nproc-per-node N demo.py --query_shard: every rank runs the same frames,
+        # each holding the correlation-volume rows of 1/N of the query pixels; rank 0 writes
+        from raft_ros_amd.parallel import ddp
+
+        info = ddp.init_distributed()
+        rank = info.rank
+        if info.device.type == "cuda":
+            args.device = str(info.device)
     model = RAFT(args)
     if args.model:
         checkpoint.load_weights(model, args.model)
@@ -91,7 +101,8 @@ def demo(args):
             image1, image2 = padder.pad(image1, image2)
             flow_low, flow_up = model(image1, image2, iters=args.iters, test_mode=True)
             out = os.path.join(args.output, "flow_%04d.png" % k)
-            viz(image1, flow_up, out, show=args.show)
+            if rank == 0:
+                viz(image1, flow_up, out, show=args.show)
             outs.append(out)
     return outs
 
@@ -109,6 +120,9 @@ def main(argv=None):
     p.add_argument("--iters", type=int, default=20)
     p.add_argument("--output", default="demo-output")
     p.add_argument("--show", action="store_true", help="also display with cv2 (if available)")
+    p.add_argument("--query_shard", action="store_true",
+                   help="under torchrun: shard the correlation volume over the ranks' query pixels "
+                        "(high-resolution inference; raft_ros_amd/parallel/query_shard.py)")
     args = p.parse_args(argv)
     return demo(args)
 

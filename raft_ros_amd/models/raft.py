@@ -19,7 +19,9 @@ Execution differences (GPU):
 * the lookup emits channels-last features already in the autocast dtype;
 * mixed precision uses ``args.amp_dtype`` (default bf16 on MI355X; 'fp16'
   reproduces the reference's fp16 autocast);
-* ``args.channels_last`` (default True on GPU) keeps every conv in NHWC.
+* ``args.channels_last`` (default True on GPU) keeps every conv in NHWC;
+* ``args.query_shard`` (inference in a process group): the correlation volume is sharded
+  over query pixels across the ranks (parallel/query_shard.py).
 """
 from __future__ import annotations
 
@@ -145,6 +147,13 @@ class RAFT(nn.Module):
         if self.args.alternate_corr:
             corr_fn = LocalCorrPyramid(fmap1, fmap2, radius=self.args.corr_radius,
                                        split=not (amp and dev == "cuda" and self.amp_dtype == torch.bfloat16))
+        elif _arg(self.args, "query_shard", False) and not torch.is_grad_enabled():
+            # inference over a process group: each rank holds the volume rows of its own query
+            # pixels (parallel/query_shard.py)
+            from ..parallel.query_shard import ShardedCorrPyramid
+
+            corr_fn = ShardedCorrPyramid(fmap1, fmap2, num_levels=self.args.corr_levels,
+                                         radius=self.args.corr_radius)
         else:
             # without AMP the volume stays fp32-faithful (split bf16 MFMA), as the reference
             # computes it in fp32 in every mode (core/raft.py:102-103)

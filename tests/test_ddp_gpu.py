@@ -105,3 +105,33 @@ def test_ddp_fused_native_grads_match_full_batch(cuda):
         assert err < max(3 * noise, 1e-2), (n, err, noise)
         n_checked += 1
     assert n_checked > 100, n_checked  # the update block, both encoders
+
+
+def _rccl_worker(rank, port, out):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, **ddp.process_group_kwargs("nccl"))
+    t = torch.arange(1024, device=dev, dtype=torch.float32)
+    dist.all_reduce(t)
+    net = torch.nn.parallel.DistributedDataParallel(torch.nn.Linear(64, 64).to(dev), device_ids=[0],
+                                                    bucket_cap_mb=10.0, gradient_as_bucket_view=True)
+    net(torch.randn(8, 64, device=dev)).square().sum().backward()
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(t, torch.arange(1024, device=dev, dtype=torch.float32)))
+    ok = ok and all(p.grad is not None and torch.isfinite(p.grad).all() for p in net.parameters())
+    dist.destroy_process_group()
+    torch.save({"ok": ok}, out)
+
+
+@pytest.mark.gpu
+def test_rccl_process_group_with_high_priority_stream(cuda):
+    """The RCCL process-group options used by train.py / bench.py (high-priority
+    communicator stream, collective timeout) initialise and run an all-reduce and a DDP
+    backward (one rank: the box has one GPU)."""
+    with tempfile.TemporaryDirectory() as tmp:
+        out = os.path.join(tmp, "r.pt")
+        mp.start_processes(_rccl_worker, args=(ddp.free_port(), out), nprocs=1, start_method="spawn")
+        assert torch.load(out, weights_only=True)["ok"]
