@@ -76,7 +76,11 @@ void run_conv(EncConvArgs& a, int rows, const at::TensorOptions& o) {
   at::Tensor wt = at::empty({wtotal}, o.dtype(at::kBFloat16));
   a.wt = cbf(wt);
   check(launch_enc_pack(a, rows, wt.data_ptr(), stream()), "enc_pack");
-  if (blocks > 0) check(launch_enc_conv(a, blocks, stream()), "enc_conv");
+  if (blocks == 0) return;
+  if (enc_conv3_eligible(a))
+    check(launch_enc_conv3(a, stream()), "enc_conv3");  // 3x3 64 -> 64: resident-weight kernel
+  else
+    check(launch_enc_conv(a, blocks, stream()), "enc_conv");
 }
 
 void init_args(EncConvArgs& a) {
@@ -126,8 +130,16 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
     b = bias->to(at::kFloat).contiguous();
     a.bias = b.data_ptr<float>();
   }
-  const int T = (Ho * Wo + kBM - 1) / kBM;
-  at::Tensor st = want_stats ? at::empty({B, T, 2, N}, x.options().dtype(at::kFloat)) : at::Tensor();
+  // tile statistics: [B, T, 2, N] over 128-pixel row tiles, or [B, Ty, Tx, 2, N] over the
+  // square tiles of the resident-weight 3x3 kernel (enc_norm_stats reads the layout from the rank)
+  at::Tensor st;
+  if (want_stats) {
+    const auto fo = x.options().dtype(at::kFloat);
+    if (enc_conv3_eligible(a))
+      st = at::empty({B, (Ho + kEnc3Tile - 1) / kEnc3Tile, (Wo + kEnc3Tile - 1) / kEnc3Tile, 2, N}, fo);
+    else
+      st = at::empty({B, (Ho * Wo + kBM - 1) / kBM, 2, N}, fo);
+  }
   if (want_stats) a.stats = st.data_ptr<float>();
   set_weight(a, 0, w);
   a.pack_dgrad = 0;
@@ -307,7 +319,7 @@ at::Tensor enc_prep(const at::Tensor& img0, const c10::optional<at::Tensor>& img
 at::Tensor enc_norm_stats(const c10::optional<at::Tensor>& stats, int64_t B, int64_t HW, int64_t N, int64_t kind,
                           const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
                           const c10::optional<at::Tensor>& rmean, const c10::optional<at::Tensor>& rvar,
-                          const c10::optional<at::Tensor>& nbt, double momentum, double eps) {
+                          const c10::optional<at::Tensor>& nbt, double momentum, double eps, int64_t W) {
   NormFinArgs a{};
   a.B = (int)B;
   a.HW = (int)HW;
@@ -318,9 +330,19 @@ at::Tensor enc_norm_stats(const c10::optional<at::Tensor>& stats, int64_t B, int
   TORCH_CHECK(!(kind == 1 || kind == 2) || has_stats, "training statistics need the conv tile statistics");
   at::TensorOptions o;
   if (has_stats) {
-    TORCH_CHECK(stats->dim() == 4 && stats->size(0) == B && stats->size(2) == 2 && stats->size(3) == N, "stats shape");
+    const int d = (int)stats->dim();
+    TORCH_CHECK((d == 4 || d == 5) && stats->size(0) == B && stats->size(d - 2) == 2 && stats->size(d - 1) == N &&
+                    stats->is_contiguous(),
+                "stats shape");
     a.stats = stats->data_ptr<float>();
-    a.T = (int)stats->size(1);
+    a.T = (int)(d == 5 ? stats->size(1) * stats->size(2) : stats->size(1));
+    if (d == 5) {  // square tiles of the 3x3 kernel: the tile pixel counts need the image width
+      TORCH_CHECK(W > 0 && HW % W == 0 && (W + kEnc3Tile - 1) / kEnc3Tile == stats->size(2) &&
+                      (HW / W + kEnc3Tile - 1) / kEnc3Tile == stats->size(1),
+                  "enc_norm_stats: square-tile statistics need the image width W");
+      a.tile_w = kEnc3Tile;
+      a.img_w = (int)W;
+    }
     o = stats->options();
   }
   auto fp = [](const c10::optional<at::Tensor>& t) -> float* {
@@ -431,7 +453,7 @@ TORCH_LIBRARY_FRAGMENT(raft_amd, m) {
   m.def("enc_prep(Tensor img0, Tensor? img1) -> Tensor");
   m.def(
       "enc_norm_stats(Tensor? stats, int B, int HW, int N, int kind, Tensor? gamma, Tensor? beta, Tensor(a!)? rmean, "
-      "Tensor(b!)? rvar, Tensor(c!)? nbt, float momentum, float eps) -> Tensor");
+      "Tensor(b!)? rvar, Tensor(c!)? nbt, float momentum, float eps, int W=0) -> Tensor");
   m.def("enc_apply(Tensor a, Tensor coef, bool relu_a, Tensor? r, Tensor? coef_r, bool relu_out) -> Tensor");
   m.def("enc_norm_bwd(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind) -> Tensor[]");
 }

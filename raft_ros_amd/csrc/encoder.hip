@@ -671,7 +671,13 @@ __global__ __launch_bounds__(256) void enc_norm_finalize_kernel(const NormFinArg
     float cn = 0.f, cm = 0.f, cM2 = 0.f;
     for (int e = tid; e < E; e += 256) {
       const int b = b0 + e / a.T, t = e - (e / a.T) * a.T;
-      const float nb = (float)min(a.BM, a.HW - t * a.BM);
+      float nb;
+      if (a.tile_w > 0) {  // square tiles, row-major over the image
+        const int tx_n = (a.img_w + a.tile_w - 1) / a.tile_w, ty = t / tx_n, tx = t - ty * tx_n;
+        nb = (float)(min(a.tile_w, a.HW / a.img_w - ty * a.tile_w) * min(a.tile_w, a.img_w - tx * a.tile_w));
+      } else {
+        nb = (float)min(a.BM, a.HW - t * a.BM);
+      }
       const float* st = a.stats + ((long)(b * a.T + t) * 2) * a.N;
       const float mb = st[n] / nb, M2b = st[a.N + n];
       const float nn = cn + nb, d = mb - cm;
@@ -959,6 +965,199 @@ int grid_for(long chunks) {
 // Tile configurations by output-channel count.
 enum EncTile : int { kT128x128 = 0, kT128x96 = 1, kT128x64 = 2, kT128x32 = 3 };
 
+// ============================================================================ 3x3 conv, resident weights
+// The 3x3 / stride-1 convs with 64 input and 64 output channels (stage 1 of both encoders,
+// at H/2 x W/2: the largest convs of a training step, forward and data gradient) on a
+// persistent workgroup per CU that keeps the whole packed weight matrix [64][576] in LDS
+// (73.7 KB, loaded once) and walks 16x16-pixel output tiles.  A tile's 18x18 halo block
+// (64 channels, 41 KB) is DMA'd (buffer_load ... lds; out-of-image pixels load as zeros, so
+// the padding needs no masking) into one of two LDS buffers while the previous tile
+// computes, and all 9 taps read their A fragments from it at a row shift: each input pixel
+// is fetched once per tile instead of once per tap (the register-staged kernel above
+// re-gathers the im2col rows of every tap: VALU-bound at ~18 VALU per MFMA).
+// 8 waves x (32 pixels x 64 channels), v_mfma_f32_32x32x16_bf16; 3 barriers per tile.
+// Epilogue as enc_conv_kernel: + bias, per-tile (sum, M2) statistics, + residual,
+// ReLU' mask, bf16 store (staged through the finished halo buffer).
+namespace {
+
+constexpr int C3_T = kEnc3Tile;           // output tile side
+constexpr int C3_B = C3_T + 2;            // halo block side
+constexpr int C3_ROWS = C3_B * C3_B;      // halo pixels (128-byte rows of 64 channels)
+constexpr int C3_PIECES = (C3_ROWS * 128 + 1023) / 1024;  // 1 KB DMA pieces per halo block
+constexpr int C3_HALO = C3_PIECES * 1024;  // halo buffer bytes (whole pieces)
+constexpr int C3_WB = 64 * 576 * 2;        // resident weights
+constexpr int C3_LDS = C3_WB + 2 * C3_HALO;
+constexpr int C3_SP = 72;                  // bf16 pitch of the staged output tile
+constexpr unsigned C3_OOB = 0x80000000u;
+static_assert(C3_T * C3_T * C3_SP * 2 + 2 * 8 * 64 * 4 <= C3_HALO, "epilogue staging must fit a halo buffer");
+static_assert(C3_LDS <= 160 * 1024, "LDS budget");
+
+typedef __attribute__((address_space(3))) void c3_lds_void;
+typedef __attribute__((address_space(3))) bf16x8 c3_lds_bf16x8;
+
+__device__ __forceinline__ int c3swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+__device__ __forceinline__ void c3_dma16(__amdgpu_buffer_rsrc_t r, unsigned lds_byte, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (c3_lds_void*)(uintptr_t)lds_byte, 16, voff, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 c3_read16(unsigned lds_byte) { return *(const c3_lds_bf16x8*)(uintptr_t)lds_byte; }
+
+__global__ __launch_bounds__(512) void enc_conv3_kernel(const EncConvArgs a, int ntiles, int tiles_x,
+                                                        int tiles_img) {
+  extern __shared__ __attribute__((aligned(1024))) char c3smem[];
+  const unsigned lds0 = (unsigned)(reinterpret_cast<uintptr_t>(c3smem) & 0xffffffffu);
+  const unsigned ldsW = lds0, ldsH = lds0 + C3_WB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.src[0].H, W = a.src[0].W;
+  const __amdgpu_buffer_rsrc_t rx = enc_rsrc(a.src[0].ptr, (unsigned)((long)a.B * H * W * 128));
+  const __amdgpu_buffer_rsrc_t rw = enc_rsrc(a.wt, (unsigned)C3_WB);
+  // halo-row shift of each tap (taps in decode-table order = packed-weight order)
+  int tshift[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int ent = a.tab[a.cls[0].t0 + t * 8];
+    tshift[t] = ((ent & 0xff) - 127) * C3_B + (((ent >> 8) & 0xff) - 127);
+  }
+
+  // weights -> LDS once: [64 rows][72 chunks], chunk index XOR-swizzled within each tap
+#pragma unroll 1
+  for (int q = wave; q < C3_WB / 1024; q += 8) {
+    const int pos = q * 1024 + lane * 16;
+    const int n = pos / 1152, pc = (pos - n * 1152) >> 4;
+    const int j = (pc & ~7) | c3swz(n, pc & 7);
+    c3_dma16(rw, ldsW + q * 1024, (unsigned)(n * 576 + j * 8) * 2u);
+  }
+  auto load_halo = [&](int tile, int buf) __attribute__((always_inline)) {
+    const int b = tile / tiles_img, tr = tile - b * tiles_img;
+    const int ty = tr / tiles_x;
+    const int y0 = ty * C3_T - 1, x0 = (tr - ty * tiles_x) * C3_T - 1;
+#pragma unroll 1
+    for (int q = wave; q < C3_PIECES; q += 8) {
+      const int pos = q * 1024 + lane * 16;
+      const int r = pos >> 7, pc = (pos >> 4) & 7;
+      const int hy = r / C3_B, hx = r - hy * C3_B;
+      const int y = y0 + hy, x = x0 + hx;
+      const bool ok = r < C3_ROWS && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+      const unsigned voff = ok ? (unsigned)((((b * H + y) * W + x) << 6) + c3swz(r, pc) * 8) * 2u : C3_OOB;
+      c3_dma16(rx, ldsH + buf * C3_HALO + q * 1024, voff);
+    }
+  };
+
+  // fragment geometry: this lane's pixel (py, px) of the tile and its 64-channel half
+  const int lh = lane >> 5;
+  const int py = 2 * wave + ((lane >> 4) & 1), px = lane & 15;
+  const int hb = py * C3_B + px;  // halo row of the pixel at tap (0, 0) offset (-1, -1)
+  const int n0 = lane & 31;       // B columns n0 and n0 + 32
+  const unsigned wrow = ldsW + n0 * 1152;
+  unsigned bsw[4];
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) bsw[s2] = (unsigned)(c3swz(n0, s2 * 2 + lh) << 4);
+  float bias[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bias[j] = a.bias ? a.bias[n0 + 32 * j] : 0.f;
+
+  int tile = blockIdx.x;
+  if (tile < ntiles) load_halo(tile, 0);
+#pragma unroll 1
+  for (int it = 0; tile < ntiles; tile += gridDim.x, ++it) {
+    const int cur = it & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // halo (+ weights) landed; the previous tile's epilogue is done with its buffer
+    if (tile + (int)gridDim.x < ntiles) load_halo(tile + gridDim.x, cur ^ 1);
+    const unsigned hbuf = ldsH + cur * C3_HALO;
+
+    f32x16 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int row = hb + tshift[t];
+      const unsigned abase = hbuf + (unsigned)row * 128u;
+      const int sw = (row >> 1) & 7;
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const bf16x8 fa = c3_read16(abase + (unsigned)(((s2 * 2 + lh) ^ sw) << 4));
+        const bf16x8 fb0 = c3_read16(wrow + t * 128 + bsw[s2]);
+        const bf16x8 fb1 = c3_read16(wrow + 32 * 1152 + t * 128 + bsw[s2]);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb0, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb1, acc[1], 0, 0, 0);
+      }
+    }
+
+    // ---- epilogue
+    const int b = tile / tiles_img, tr = tile - b * tiles_img;
+    const int ty = tr / tiles_x;
+    const int oy = ty * C3_T, ox = (tr - ty * tiles_x) * C3_T;
+    const int vh = min(C3_T, H - oy), vw = min(C3_T, W - ox);  // valid rows / columns of the tile
+    __syncthreads();  // every wave is done reading the halo buffer: reuse it for staging
+    __bf16* stg = reinterpret_cast<__bf16*>(c3smem + C3_WB + cur * C3_HALO);
+    float* sst = reinterpret_cast<float*>(c3smem + C3_WB + cur * C3_HALO + C3_T * C3_T * C3_SP * 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float sm = 0.f, sq = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;  // tile pixel of this element
+        const float v = acc[j][r] + bias[j];
+        const bool valid = (i >> 4) < vh && (i & 15) < vw;
+        sm += valid ? v : 0.f;
+        sq += valid ? v * v : 0.f;
+        stg[i * C3_SP + n0 + 32 * j] = static_cast<__bf16>(v);
+      }
+      if (a.stats) {
+        sm += __shfl_xor(sm, 32, 64);
+        sq += __shfl_xor(sq, 32, 64);
+        if (lane < 32) {
+          sst[wave * 64 + n0 + 32 * j] = sm;
+          sst[512 + wave * 64 + n0 + 32 * j] = sq;
+        }
+      }
+    }
+    __syncthreads();
+    if (a.stats && tid < 64) {
+      float sm = 0.f, sq = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        sm += sst[w * 64 + tid];
+        sq += sst[512 + w * 64 + tid];
+      }
+      float* st = a.stats + ((long)(b * tiles_img + tr) * 2) * 64;
+      st[tid] = sm;
+      st[64 + tid] = fmaxf(sq - sm * sm / (float)(vh * vw), 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = tid + 512 * k;
+      const int i = idx >> 3, c8 = (idx & 7) * 8;
+      const int yy = i >> 4, xx = i & 15;
+      if (yy >= vh || xx >= vw) continue;
+      const long pix = ((long)b * a.Ho + oy + yy) * a.Wo + ox + xx;
+      const bf16x8 sv = *reinterpret_cast<const bf16x8*>(stg + i * C3_SP + c8);
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = static_cast<float>(sv[e]);
+      if (a.res) {
+        float r8[8];
+        load8(a.res + pix * a.res_stride + c8, r8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += r8[e];
+      }
+      if (a.mask) {
+        float m8[8];
+        load8(a.mask + pix * a.mask_stride + c8, m8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = m8[e] > 0.f ? v[e] : 0.f;
+      }
+      store8(a.out + pix * a.out_stride + c8, v);
+    }
+  }
+}
+
+}  // namespace
+
 int enc_tile_bn(int N) {
   if (N % 128 == 0) return 128;
   if (N == 96) return 96;
@@ -989,6 +1188,27 @@ void launch_enc_conv_n(const EncConvArgs& a, int nblocks, hipStream_t s) {
       hipLaunchKernelGGL((enc_conv_kernel<128, 32, 4, 1, NSRC>), dim3(nblocks), dim3(256), 0, s, a);
       break;
   }
+}
+
+hipError_t launch_enc_conv3(const EncConvArgs& a, hipStream_t s) {
+  static int num_cu = 0;
+  static bool lds_set = false;
+  if (!num_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&num_cu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || num_cu <= 0)
+      num_cu = 256;
+  }
+  if (!lds_set) {
+    (void)hipFuncSetAttribute((const void*)enc_conv3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, C3_LDS);
+    lds_set = true;
+  }
+  const int tiles_x = (a.Wo + C3_T - 1) / C3_T, tiles_img = tiles_x * ((a.Ho + C3_T - 1) / C3_T);
+  const int ntiles = a.B * tiles_img;
+  if (ntiles == 0) return hipSuccess;
+  const int grid = std::min(ntiles, num_cu);
+  hipLaunchKernelGGL(enc_conv3_kernel, dim3(grid), dim3(512), C3_LDS, s, a, ntiles, tiles_x, tiles_img);
+  return hipGetLastError();
 }
 
 hipError_t launch_enc_conv(const EncConvArgs& a, int nblocks, hipStream_t s) {

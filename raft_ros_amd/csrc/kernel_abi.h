@@ -200,6 +200,8 @@ struct EncWgradArgs {
 struct NormFinArgs {
   const float* stats;  // conv epilogue tiles [B][T][2][N]
   int B, T, BM, HW, N, kind;
+  int tile_w, img_w;   // tile_w > 0: T = square tile_w x tile_w tiles in row-major order of an
+                       // img_w-wide image (the 3x3 resident-weight conv); else BM-pixel row tiles
   const float* gamma;
   const float* beta;
   float* rmean;
@@ -224,6 +226,31 @@ struct NormBwdArgs {
   __bf16* out0;
   __bf16* out1;
 };
+
+// 3x3 / stride-1 encoder convs with 64 input and 64 output channels (both encoders' stage-1
+// residual convs and their data gradients) run on a resident-weight kernel over square
+// output tiles (encoder.hip enc_conv3_kernel).
+constexpr int kEnc3Tile = 16;
+
+// Host check: can enc_conv3_kernel run this planned launch?  (one class, one source of
+// exactly 64 channels, 64 outputs, the 9 taps of a 3x3 window at offsets in [-1, 1], output
+// grid = input grid.)
+inline bool enc_conv3_eligible(const EncConvArgs& a) {
+  if (a.ncls != 1 || a.src[1].ptr != nullptr || a.N != 64 || a.os != 1) return false;
+  const EncSrc& s = a.src[0];
+  const EncClass& c = a.cls[0];
+  if (s.C != 64 || s.stride != 64 || s.is != 1 || c.K != 576 || c.Kpad != 576 || c.oy0 || c.ox0) return false;
+  if (c.Gh != a.Ho || c.Gw != a.Wo || s.H != a.Ho || s.W != a.Wo) return false;
+  for (int t = 0; t < 9; ++t)
+    for (int e = 0; e < 8; ++e) {
+      const int ent = a.tab[c.t0 + t * 8 + e];
+      if (ent < 0) return false;
+      const int dy = (ent & 0xff) - 128, dx = ((ent >> 8) & 0xff) - 128, src = (ent >> 16) & 1, ch = ent >> 17;
+      const int dy0 = (a.tab[c.t0 + t * 8] & 0xff) - 128, dx0 = ((a.tab[c.t0 + t * 8] >> 8) & 0xff) - 128;
+      if (src != 0 || ch != e * 8 || dy != dy0 || dx != dx0 || dy < -1 || dy > 1 || dx < -1 || dx > 1) return false;
+    }
+  return true;
+}
 
 // ============================================================================ correlation
 struct PyrDesc {
@@ -398,6 +425,7 @@ hipError_t launch_wgrad_reduce_packed(const float* slab, int nsplit, int Npad, i
 int enc_tile_bn(int N);
 hipError_t launch_enc_pack(const EncConvArgs& a, int rows, void* out, hipStream_t s);
 hipError_t launch_enc_conv(const EncConvArgs& a, int nblocks, hipStream_t s);
+hipError_t launch_enc_conv3(const EncConvArgs& a, hipStream_t s);
 hipError_t launch_enc_wgrad(const EncWgradArgs& a, int BM, int BN, hipStream_t s);
 hipError_t launch_enc_wgrad_reduce(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, float* dw,
                                    const long* ws, int Cout, int Cin, int Cx, int KH, int KW, float* db,

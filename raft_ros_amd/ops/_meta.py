@@ -107,11 +107,17 @@ def register() -> None:
 
     @fake(lib + "enc_conv_fwd")
     def _(x, w, bias, stride, pad, stats):
-        B, H, W, _ = x.shape
-        N, _, KH, KW = w.shape
+        B, H, W, Cx = x.shape
+        N, Cin, KH, KW = w.shape
         Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
-        T = -(-(Ho * Wo) // 128)  # 128-pixel conv tiles (csrc/enc_bindings.cpp kBM)
-        st = x.new_empty((B, T, 2, N), dtype=torch.float32) if stats else x.new_empty((0,), dtype=torch.float32)
+        if not stats:
+            st = x.new_empty((0,), dtype=torch.float32)
+        elif (Cx, Cin, N, KH, KW, stride, pad) == (64, 64, 64, 3, 3, 1, 1):
+            # resident-weight 3x3 kernel: 16x16 tiles (csrc/kernel_abi.h enc_conv3_eligible)
+            st = x.new_empty((B, -(-Ho // 16), -(-Wo // 16), 2, N), dtype=torch.float32)
+        else:
+            T = -(-(Ho * Wo) // 128)  # 128-pixel conv tiles (csrc/enc_bindings.cpp kBM)
+            st = x.new_empty((B, T, 2, N), dtype=torch.float32)
         return x.new_empty((B, Ho, Wo, N)), st
 
     @fake(lib + "enc_conv_dgrad")
@@ -124,7 +130,7 @@ def register() -> None:
         return img0.new_empty((n, img0.shape[2], img0.shape[3], 8), dtype=torch.bfloat16)
 
     @fake(lib + "enc_norm_stats")
-    def _(stats, B, HW, N, kind, gamma, beta, rmean, rvar, nbt, momentum, eps):
+    def _(stats, B, HW, N, kind, gamma, beta, rmean, rvar, nbt, momentum, eps, W=0):
         like = stats if stats is not None else rmean
         return like.new_empty((B, 4, N), dtype=torch.float32)
 

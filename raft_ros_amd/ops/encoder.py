@@ -111,9 +111,9 @@ def _stats(a, st, nd, P):
         return ops().enc_norm_stats(st if k == _BATCH_TRAIN else None, B, H * W, N, k, P[nd["g"]], P[nd["bt"]],
                                     m.running_mean, m.running_var,
                                     m.num_batches_tracked if k == _BATCH_TRAIN else None,
-                                    m.momentum if m.momentum is not None else 0.1, m.eps)
+                                    m.momentum if m.momentum is not None else 0.1, m.eps, W)
     eps = getattr(m, "eps", 1e-5)
-    return ops().enc_norm_stats(st, B, H * W, N, k, None, None, None, None, None, 0.0, eps)
+    return ops().enc_norm_stats(st, B, H * W, N, k, None, None, None, None, None, 0.0, eps, W)
 
 
 def _conv(x, cd, P, stats):

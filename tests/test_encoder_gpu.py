@@ -35,7 +35,9 @@ def _nchw(t):
 
 CONVS = [  # (B, Cin, Cx, H, W, Cout, k, stride, pad)
     (2, 3, 8, 64, 80, 64, 7, 2, 3),
-    (2, 64, 64, 48, 40, 64, 3, 1, 1),
+    (2, 64, 64, 48, 40, 64, 3, 1, 1),   # resident-weight 3x3 kernel (16x16 tiles, partial last column)
+    (3, 64, 64, 37, 45, 64, 3, 1, 1),   # partial tiles on both edges
+    (1, 64, 64, 9, 200, 64, 3, 1, 1),   # image shorter than a tile
     (2, 64, 64, 48, 40, 96, 3, 2, 1),
     (2, 96, 96, 24, 20, 128, 3, 2, 1),
     (2, 64, 64, 48, 40, 96, 1, 2, 0),
@@ -65,8 +67,15 @@ def test_conv_fwd_stats_dgrad_wgrad(cfg):
     assert y.shape == (B, ref.shape[2], ref.shape[3], Cout)
     assert _rel(_nchw(y), ref) < 1e-2
     # tile statistics -> per-image mean / variance
-    HW = ref.shape[2] * ref.shape[3]
-    tile_n = torch.tensor([min(128, HW - t * 128) for t in range(st.shape[1])], device=cuda, dtype=torch.float32)
+    Ho, Wo = ref.shape[2], ref.shape[3]
+    HW = Ho * Wo
+    if st.dim() == 5:  # square 16x16 tiles of the resident-weight 3x3 kernel, row-major
+        assert st.shape[1:3] == (-(-Ho // 16), -(-Wo // 16))
+        tile_n = torch.tensor([min(16, Ho - ty * 16) * min(16, Wo - tx * 16) for ty in range(st.shape[1])
+                               for tx in range(st.shape[2])], device=cuda, dtype=torch.float32)
+        st = st.reshape(B, -1, 2, Cout)
+    else:
+        tile_n = torch.tensor([min(128, HW - t * 128) for t in range(st.shape[1])], device=cuda, dtype=torch.float32)
     sums, m2 = st[:, :, 0], st[:, :, 1]
     mean = sums.sum(1) / HW
     tmean = sums / tile_n[None, :, None]
