@@ -243,6 +243,59 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
   TORCH_CHECK(dy.size(0) == B && dy.size(3) == N && Cin <= Cx, "wgrad shapes");
   TORCH_CHECK(Ho == (Hx + 2 * (int)pad - KH) / (int)stride + 1 && Wo == (Wx + 2 * (int)pad - KW) / (int)stride + 1,
               "wgrad spatial shapes");
+  const bool want_db = db.has_value() && db->defined();
+  if (want_db) {
+    TORCH_CHECK(db->scalar_type() == at::kFloat && db->numel() == N && db->is_contiguous(), "db: fp32 [N]");
+  }
+  // 3x3 / stride-1 convs on 64 channels (stage 1 at H/2): the tap-batched halo-block weight
+  // gradient of the update block (conv_igemm.hip conv_wgrad3_kernel: every tap from one DMA'd
+  // halo block, two waves per SIMD) instead of the per-tap im2col kernel below, reduced
+  // straight into the fp32 parameter layout (weights.hip).  scripts/bench_enc.py on MI355X:
+  // 158 -> 122 us at 16 x 184 x 248; the 128-channel stage-3 conv is faster below (47 vs 55 us)
+  if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && Cin == Cx && Cin == 64 && N % 8 == 0) {
+    ConvWgradArgs w{};
+    w.src[0] = ConvSrc{cbf(x), (long)Cx, Cin, 0};
+    w.nsrc = 1;
+    w.Cin = Cin;
+    w.B = B;
+    w.H = Hx;
+    w.W = Wx;
+    w.KH = 3;
+    w.KW = 3;
+    w.PH = 1;
+    w.PW = 1;
+    w.K = 9 * Cin;
+    w.Kpad = round_up(w.K, 64);
+    w.dy = cbf(dy);
+    w.dy_stride = N;
+    w.N = N;
+    w.P = (long)B * Hx * Wx;
+    if (wgrad_supported(w)) {
+      const WgradPlan pl = plan_conv_wgrad(w);
+      const bool with_b = want_db && !db_zero;
+      auto fo = x.options().dtype(at::kFloat);
+      at::Tensor slab = at::empty({(long)pl.nsplit * pl.Npad * w.Kpad}, fo);
+      at::Tensor dbslab = with_b ? at::empty({(long)pl.nsplit * pl.tilesN * pl.Npad}, fo) : at::Tensor();
+      w.slab = slab.data_ptr<float>();
+      w.dbslab = with_b ? dbslab.data_ptr<float>() : nullptr;
+      check(launch_conv_wgrad(w, pl, stream()), "conv_wgrad (encoder)");
+      ConvParamDesc d{};
+      d.w[0] = dw.data_ptr<float>();
+      for (int k = 0; k < 4; ++k) d.ws[0][k] = dw.stride(k);
+      d.b[0] = with_b ? db->data_ptr<float>() : nullptr;
+      d.rows[0] = N;
+      d.nseg = 1;
+      d.seg_real[0] = d.seg_pad[0] = Cin;
+      d.Cin = d.Cin_pad = Cin;
+      d.KH = d.KW = 3;
+      d.scale = 1.f;
+      check(launch_wgrad_reduce_params(w.slab, pl.nsplit, pl.Npad, w.Kpad, w.dbslab, pl.nsplit * pl.tilesN, d, N,
+                                       accumulate ? 1 : 0, stream()),
+            "wgrad_reduce_params (encoder)");
+      if (want_db && db_zero && !accumulate) db->zero_();  // exact zero in front of IN / BN-train
+      return;
+    }
+  }
   EncWgradArgs a{};
   a.x = cbf(x);
   a.xstride = Cx;
@@ -278,11 +331,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
   a.nsplit = (int)((a.P + pps - 1) / pps);
   at::Tensor slab = at::empty({(long)a.nsplit * a.Npad * a.Kpad}, x.options().dtype(at::kFloat));
   a.slab = slab.data_ptr<float>();
-  const bool want_db = db.has_value() && db->defined();
   at::Tensor dbslab;
-  if (want_db) {
-    TORCH_CHECK(db->scalar_type() == at::kFloat && db->numel() == N && db->is_contiguous(), "db: fp32 [N]");
-  }
   if (want_db && !db_zero) {
     dbslab = at::empty({(long)a.nsplit * a.Npad}, x.options().dtype(at::kFloat));
     a.dbslab = dbslab.data_ptr<float>();

@@ -38,6 +38,7 @@ CONVS = [  # (B, Cin, Cx, H, W, Cout, k, stride, pad)
     (2, 64, 64, 48, 40, 64, 3, 1, 1),   # resident-weight 3x3 kernel (16x16 tiles, partial last column)
     (3, 64, 64, 37, 45, 64, 3, 1, 1),   # partial tiles on both edges
     (1, 64, 64, 9, 200, 64, 3, 1, 1),   # image shorter than a tile
+    (2, 128, 128, 20, 18, 128, 3, 1, 1),  # tap-batched halo-block weight gradient, 2 chunks
     (2, 64, 64, 48, 40, 96, 3, 2, 1),
     (2, 96, 96, 24, 20, 128, 3, 2, 1),
     (2, 64, 64, 48, 40, 96, 1, 2, 0),
