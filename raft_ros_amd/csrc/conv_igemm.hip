@@ -1587,8 +1587,9 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
       return hipGetLastError();
     }
   }
-  // v4 (scripts/bench_convs.py on MI355X): 64x128 tiles for 64 < N <= 512, 64x64 otherwise
-  const bool wide = cfg == 8 || (cfg != 9 && a.N > 64 && a.N <= 512);
+  // v4 (scripts/bench_convs.py on MI355X): 64x128 tiles for N > 64 (the 576-wide mask-head 1x1:
+  // 34.3 -> 30.0 us, profiles/r2_bench_convs_cfg8.log), 64x64 otherwise
+  const bool wide = cfg == 8 || (cfg != 9 && a.N > 64);
   if (wide)
     hipLaunchKernelGGL((conv_fwd4_kernel<64, 128, 3>), dim3(tiles(64, 128)), dim3(256), 0, s, a);
   else

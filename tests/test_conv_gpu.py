@@ -30,6 +30,7 @@ CASES = [
     ([(2, 8)], 128, 7, 7, 1),
     ([(324, 328)], 256, 1, 1, 1),
     ([(256, 256)], 2, 3, 3, 0),
+    ([(128, 128)], 2, 3, 3, 0),
     ([(256, 256)], 576, 1, 1, 0),
 ]
 
