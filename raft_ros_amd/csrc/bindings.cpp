@@ -29,7 +29,8 @@ hipError_t launch_local_corr_mfma(const LocalCorrArgs& a, bool backward, hipStre
 hipError_t launch_pyramid_unpool(const UnpoolArgs& u, hipStream_t s);
 hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int W, hipStream_t s);
 hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void* out, int out_dtype,
-                                  int B, int H, int W, int r, int out_ch, hipStream_t s);
+                                  int B, int H, int W, int r, int out_ch, hipStream_t s, void* flow8 = nullptr,
+                                  void* motion = nullptr, long smo = 0);
 hipError_t launch_corr_lookup_bwd(const PyrDesc& dpyr, const float* coords, const void* gout,
                                   int g_dtype, int B, int H, int W, int r, int gstride, hipStream_t s);
 hipError_t launch_gru_bwd_a(const float* dH, long sdh, const void* z, long sz, const void* q, long sq,
@@ -976,7 +977,10 @@ void apply_delta(const at::Tensor& coords1, const at::Tensor& delta, const at::T
 }
 
 // corr_lookup into a caller buffer (B, H, W, och) with och >= L*(2r+1)^2 (zero padded)
-void corr_lookup_into(at::TensorList pyramid, const at::Tensor& coords, int64_t radius, const at::Tensor& out) {
+// flow8 / motion (optional): the step's packed flow operand, written by the same launch
+// (pack_flow(coords, flow8, motion, from_coords=true) folded into the lookup)
+void corr_lookup_into(at::TensorList pyramid, const at::Tensor& coords, int64_t radius, const at::Tensor& out,
+                      const c10::optional<at::Tensor>& flow8, const c10::optional<at::Tensor>& motion) {
   check_coords(coords);
   const long B = coords.size(0), H = coords.size(2), W = coords.size(3);
   std::vector<at::Tensor> lv(pyramid.begin(), pyramid.end());
@@ -986,9 +990,23 @@ void corr_lookup_into(at::TensorList pyramid, const at::Tensor& coords, int64_t 
   TORCH_CHECK(out.dim() == 4 && out.is_contiguous() && out.size(0) == B && out.size(1) == H && out.size(2) == W &&
                   out.size(3) >= d.levels * win,
               "raft_amd::corr_lookup_into: out must be contiguous (B, H, W, >= L*(2r+1)^2)");
+  void* f8 = nullptr;
+  void* mo = nullptr;
+  long smo = 0;
+  if (flow8) {
+    TORCH_CHECK(flow8->is_contiguous() && flow8->scalar_type() == at::kBFloat16 && flow8->numel() == B * H * W * 8,
+                "raft_amd::corr_lookup_into: flow8 must be contiguous bf16 (P, 8)");
+    f8 = flow8->data_ptr();
+    if (motion) {
+      pm_any(*motion, "motion", B * H * W, at::kBFloat16);
+      TORCH_CHECK(motion->size(1) >= 2, "raft_amd::corr_lookup_into: motion slice needs 2 channels");
+      mo = motion->data_ptr();
+      smo = motion->stride(0);
+    }
+  }
   const c10::DeviceGuard guard(coords.device());
   HIP_OK(launch_corr_lookup_fwd(d, coords.data_ptr<float>(), out.data_ptr(), dtype_code(out.scalar_type()), B, H, W,
-                                static_cast<int>(radius), static_cast<int>(out.size(3)), cur_stream()));
+                                static_cast<int>(radius), static_cast<int>(out.size(3)), cur_stream(), f8, mo, smo));
 }
 
 // ---------------------------------------------------------------- NHWC instance norm
@@ -1057,7 +1075,9 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("masked_cast(Tensor src, Tensor? mask, Tensor(a!) out) -> ()");
   m.def("pack_flow(Tensor flow, Tensor(a!) flow8, Tensor(b!)? motion, bool from_coords=False) -> ()");
   m.def("apply_delta(Tensor coords1, Tensor delta, Tensor(a!) coords_out, Tensor(b!) flow_out) -> ()");
-  m.def("corr_lookup_into(Tensor[] pyramid, Tensor coords, int radius, Tensor(a!) out) -> ()");
+  m.def(
+      "corr_lookup_into(Tensor[] pyramid, Tensor coords, int radius, Tensor(a!) out, Tensor(b!)? flow8=None, "
+      "Tensor(c!)? motion=None) -> ()");
   m.def("convex_upsample_backward_into(Tensor flow, Tensor mask, Tensor grad, Tensor(a!) dmask, Tensor(b!) rows) -> ()");
   m.def("corr_lookup_backward_(Tensor(a!)[] dpyramid, Tensor coords, Tensor grad, int radius) -> ()");
   m.def(

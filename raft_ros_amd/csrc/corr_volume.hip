@@ -245,10 +245,19 @@ __device__ __forceinline__ float safe_floor(float v) {
 // the (2r+2)^2 neighbourhood (<= 14 x 14 for r <= 6) as fp32.
 constexpr int NBMAX = 14 * 14;
 
+// Optionally also packs the step's flow operand (the pack_flow op, folded in: the wave
+// already holds the query's coordinates): flow8[pix] = bf16 [u, v, 0 x 6] and
+// motion[pix * smo + {0, 1}] = bf16 [u, v], with (u, v) = coords - (x, y).
+struct FlowPack {
+  __bf16* flow8;
+  __bf16* motion;
+  long smo;
+};
+
 template <typename OutT>
 __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const float* __restrict__ coords,
                                                          OutT* __restrict__ out, int B, int H, int W, int r,
-                                                         int out_ch) {
+                                                         int out_ch, const FlowPack fp) {
   __shared__ float nb[4][NBMAX];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
@@ -259,6 +268,13 @@ __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const floa
   const int rd = 2 * r + 1, nd = rd + 1, win = rd * rd, nn = nd * nd;
   const float cx0 = coords[(long)b * 2 * HW + p], cy0 = coords[(long)b * 2 * HW + HW + p];
   const bool finite = isfinite(cx0) && isfinite(cy0);
+  if (fp.flow8 && live && lane < 8) {
+    const int py = p / W;
+    const float u = cx0 - (float)(p - py * W), v = cy0 - (float)py;
+    const __bf16 f = static_cast<__bf16>(lane == 0 ? u : (lane == 1 ? v : 0.f));
+    fp.flow8[pix * 8 + lane] = f;
+    if (fp.motion && lane < 2) fp.motion[pix * fp.smo + lane] = f;
+  }
   OutT* o = out + pix * out_ch;
   // software pipeline over the levels: the neighbourhood loads of level l+1 are in flight
   // while level l is blended (the lookup is bound by the load round trips, not by bytes)
@@ -409,20 +425,21 @@ hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int 
 }
 
 hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void* out, int out_dtype, int B, int H,
-                                  int W, int r, int out_ch, hipStream_t s) {
+                                  int W, int r, int out_ch, hipStream_t s, void* flow8, void* motion, long smo) {
+  const FlowPack fp{static_cast<__bf16*>(flow8), static_cast<__bf16*>(motion), smo};
   const long npix = (long)B * H * W;
   if (npix == 0) return hipSuccess;
   if (r > 6) return hipErrorInvalidValue;
   const dim3 g((unsigned)((npix + 3) / 4)), blk(256);
   if (out_dtype == kBF16)
     hipLaunchKernelGGL(lookup_fwd_kernel<__bf16>, g, blk, 0, s, pyr, coords, static_cast<__bf16*>(out), B, H, W, r,
-                       out_ch);
+                       out_ch, fp);
   else if (out_dtype == kF16)
     hipLaunchKernelGGL(lookup_fwd_kernel<_Float16>, g, blk, 0, s, pyr, coords, static_cast<_Float16*>(out), B, H, W,
-                       r, out_ch);
+                       r, out_ch, fp);
   else
     hipLaunchKernelGGL(lookup_fwd_kernel<float>, g, blk, 0, s, pyr, coords, static_cast<float*>(out), B, H, W, r,
-                       out_ch);
+                       out_ch, fp);
   return hipGetLastError();
 }
 

@@ -5,8 +5,8 @@ corr lookup -> BasicMotionEncoder -> SepConvGRU -> FlowHead + mask head ->
 coords update -> convex upsampling) is ONE autograd node, ``_Step``, whose
 forward runs 16 HIP launches:
 
-  lookup (4 levels x 81 taps)          -> corr (P, 328)             [corr_lookup_into]
-  coords1 - grid                       -> flow8 (P, 8), motion[:, 126:]   [pack_flow]
+  lookup (4 levels x 81 taps)          -> corr (P, 328)             [corr_lookup_into, which also
+  coords1 - grid                       -> flow8 (P, 8), motion[:, 126:]   packs the flow operand]
   corr --convc1 1x1+relu--> c1 --convc2 3x3+relu--> cf[:, :192]
   flow8 --convf1 7x7+relu--> f1 --convf2 3x3+relu--> cf[:, 192:]
   cf --conv 3x3+relu--> motion[:, :126]
@@ -250,13 +250,14 @@ class _Step(torch.autograd.Function):
             h0.copy_(net_pm)
         # correlation features
         corr = ar.take("corr", t, CORR_PAD)
-        if run.pyr is not None:
-            k.corr_lookup_into(run.pyr.levels, coords1, run.pyr.radius, corr.view(B, H, W, CORR_PAD))
-        else:
-            corr.copy_(corr_in.reshape(P, CORR_PAD))
         flow8 = ar.take("flow8", t, 8)
         motion = ar.take("motion", t, HID)
-        k.pack_flow(coords1, flow8, motion[:, 126:], True)
+        if run.pyr is not None:  # the lookup launch also packs the flow operand (flow8, motion[:, 126:])
+            k.corr_lookup_into(run.pyr.levels, coords1, run.pyr.radius, corr.view(B, H, W, CORR_PAD), flow8,
+                               motion[:, 126:])
+        else:
+            corr.copy_(corr_in.reshape(P, CORR_PAD))
+            k.pack_flow(coords1, flow8, motion[:, 126:], True)
 
         c1 = ar.take("c1", t, 256)
         cf = ar.take("cf", t, 256)
@@ -306,6 +307,8 @@ class _Step(torch.autograd.Function):
         run.coords[t] = coords1
         run.flows[t] = flow
         ctx.mark_non_differentiable(coords_out)
+        # no zero fills for the gradients that never arrive (coords_out; the last step's net)
+        ctx.set_materialize_grads(False)
         return _nchw(h, B, H, W), flow_up, coords_out
 
     @staticmethod

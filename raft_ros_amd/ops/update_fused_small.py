@@ -5,8 +5,8 @@ batched over all iterations by a token node), for the small update operator
 (reference core/update.py:16-31 ConvGRU, :62-77 SmallMotionEncoder, :99-112
 SmallUpdateBlock; core/raft.py:131-134 upflow8):
 
-  lookup (4 levels x 49 taps, radius 3)   -> corr (P, 200)                [corr_lookup_into]
-  coords1 - grid                          -> flow8 (P, 8), motion[:, 80:82]      [pack_flow]
+  lookup (4 levels x 49 taps, radius 3)   -> corr (P, 200)                [corr_lookup_into, which also
+  coords1 - grid                          -> flow8 (P, 8), motion[:, 80:82]      packs the flow operand]
   corr --convc1 1x1+relu--> cf[:, :96]
   flow8 --convf1 7x7+relu--> f1 --convf2 3x3+relu--> cf[:, 96:]
   cf --conv 3x3+relu--> motion[:, :80]           (motion = 88 channels, 82..87 zero)
@@ -171,13 +171,14 @@ class _Step(torch.autograd.Function):
         if net_pm.data_ptr() != h0.data_ptr():
             h0.copy_(net_pm)
         corr = ar.take("corr", t, CORR_PAD)
-        if run.pyr is not None:
-            k.corr_lookup_into(run.pyr.levels, coords1, run.pyr.radius, corr.view(B, H, W, CORR_PAD))
-        else:
-            corr.copy_(corr_in.reshape(P, CORR_PAD))
         flow8 = ar.take("flow8", t, 8)
         motion = run.motion(t)
-        k.pack_flow(coords1, flow8, motion[:, 80:82], True)
+        if run.pyr is not None:  # the lookup launch also packs the flow operand
+            k.corr_lookup_into(run.pyr.levels, coords1, run.pyr.radius, corr.view(B, H, W, CORR_PAD), flow8,
+                               motion[:, 80:82])
+        else:
+            corr.copy_(corr_in.reshape(P, CORR_PAD))
+            k.pack_flow(coords1, flow8, motion[:, 80:82], True)
 
         cf = ar.take("cf", t, 128)
         C.conv_fwd([corr], run.wf["convc1"], g(1, 1), 96, cf[:, :96], bias=run.bias["convc1"], act=1)
@@ -211,6 +212,8 @@ class _Step(torch.autograd.Function):
         ctx.has_corr_in = corr_in is not None
         run.coords[t] = coords1
         ctx.mark_non_differentiable(coords_out)
+        # no zero fills for the gradients that never arrive (coords_out; the last step's net)
+        ctx.set_materialize_grads(False)
         return _nchw(hn, B, H, W), flow_up, coords_out
 
     @staticmethod

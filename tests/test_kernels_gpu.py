@@ -122,6 +122,25 @@ def test_corr_lookup_fwd(cuda, radius, shape):
     torch.testing.assert_close(got16.permute(0, 3, 1, 2).float(), want, rtol=2e-2, atol=2e-2)
 
 
+def test_corr_lookup_into_packs_flow_like_pack_flow(cuda):
+    """The lookup launch's folded flow packing == the standalone pack_flow op, bit for bit."""
+    torch.manual_seed(7)
+    B, H, W, r = 2, 13, 17, 4
+    _, _, pyr = _pyramid(B, 64, H, W, cuda)
+    levels = [p[:, 0].contiguous() for p in pyr]
+    coords = (ref.coords_grid(B, H, W, cuda) + 5 * torch.randn(B, 2, H, W, device=cuda)).contiguous()
+    P = B * H * W
+    out = torch.empty(B, H, W, 328, device=cuda, dtype=torch.bfloat16)
+    flow8, motion = torch.full((P, 8), 7.0, device=cuda).bfloat16(), torch.zeros(P, 128, device=cuda).bfloat16()
+    _ops().corr_lookup_into(levels, coords, r, out, flow8, motion[:, 126:])
+    f8_ref, mo_ref = torch.empty_like(flow8), torch.zeros_like(motion)
+    _ops().pack_flow(coords, f8_ref, mo_ref[:, 126:], True)
+    assert torch.equal(flow8, f8_ref) and torch.equal(motion, mo_ref)
+    # the correlation features are unchanged by the extra outputs
+    want = _ops().corr_lookup(levels, coords, r, torch.bfloat16)
+    torch.testing.assert_close(out[..., :324], want, rtol=0, atol=0)
+
+
 def test_corr_lookup_window_order_is_x_major(cuda):
     # a volume that is a pure ramp in x: tap channel ix*(2r+1)+iy must move x with ix
     B, H, W, r = 1, 16, 16, 2
