@@ -27,6 +27,7 @@ hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s);
 hipError_t launch_fixed_to_float(const long long* in, float* out, long n, hipStream_t s);
 hipError_t launch_local_corr_mfma(const LocalCorrArgs& a, bool backward, hipStream_t s);
 hipError_t launch_pyramid_unpool(const UnpoolArgs& u, hipStream_t s);
+hipError_t launch_pyramid_operand(const PyrOperandArgs& a, hipStream_t s);
 hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int W, hipStream_t s);
 hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void* out, int out_dtype,
                                   int B, int H, int W, int r, int out_ch, hipStream_t s, void* flow8 = nullptr,
@@ -231,6 +232,38 @@ at::Tensor pyramid_unpool(const at::Tensor& G, int64_t H, int64_t W, at::IntArra
   auto out = at::empty({G.size(0), H * W, G.size(2)}, G.options());
   u.out = out.data_ptr<float>();
   HIP_OK(launch_pyramid_unpool(u, cur_stream()));
+  return out;
+}
+
+// Dense-pyramid GEMM operand straight from a feature map (B, C, H, W) of any strides, bf16 or
+// fp32: levels [off, h, w] (2x2 average pools, floor), fp32 (B, ld, C) or (B, C, ld) (nchw).
+at::Tensor pyramid_operand(const at::Tensor& fmap, at::IntArrayRef segs, int64_t ld, bool blocked, bool nchw) {
+  check_gpu(fmap, "fmap");
+  TORCH_CHECK(fmap.dim() == 4 && (fmap.scalar_type() == at::kFloat || fmap.scalar_type() == at::kBFloat16),
+              "raft_amd::pyramid_operand: fmap must be (B, C, H, W) fp32 or bf16");
+  TORCH_CHECK(segs.size() % 3 == 0 && segs.size() >= 3 && segs.size() <= 12, "raft_amd::pyramid_operand: 1..4 levels");
+  PyrOperandArgs a{};
+  a.B = (int)fmap.size(0); a.C = (int)fmap.size(1); a.H = (int)fmap.size(2); a.W = (int)fmap.size(3);
+  TORCH_CHECK(nchw || a.C % 4 == 0, "raft_amd::pyramid_operand: channels must be a multiple of 4");
+  a.nseg = (int)(segs.size() / 3);
+  a.blk = blocked ? 1 : 0;
+  a.nchw = nchw ? 1 : 0;
+  a.ld = ld;
+  for (int l = 0; l < a.nseg; ++l) {
+    a.off[l] = (int)segs[3 * l]; a.h[l] = (int)segs[3 * l + 1]; a.w[l] = (int)segs[3 * l + 2];
+    const long span = blocked ? (long)((a.w[l] + 15) / 16) * a.h[l] * 16 : (long)a.h[l] * a.w[l];
+    TORCH_CHECK(a.off[l] >= 0 && (l == 0 || a.off[l] >= a.off[l - 1]) && a.h[l] <= (a.H >> l) &&
+                    a.w[l] <= (a.W >> l) && (long)a.off[l] + span <= ld,
+                "raft_amd::pyramid_operand: level ", l, " does not fit");
+  }
+  a.src = fmap.data_ptr();
+  a.src_bf16 = fmap.scalar_type() == at::kBFloat16 ? 1 : 0;
+  a.sB = fmap.stride(0); a.sC = fmap.stride(1); a.sH = fmap.stride(2); a.sW = fmap.stride(3);
+  const c10::DeviceGuard guard(fmap.device());
+  auto out = nchw ? at::empty({a.B, a.C, ld}, fmap.options().dtype(at::kFloat))
+                  : at::empty({a.B, ld, a.C}, fmap.options().dtype(at::kFloat));
+  a.out = out.data_ptr<float>();
+  HIP_OK(launch_pyramid_operand(a, cur_stream()));
   return out;
 }
 
@@ -1084,6 +1117,7 @@ TORCH_LIBRARY(raft_amd, m) {
       "corr_gemm(Tensor A, Tensor B, Tensor(a!) C, int M, int N, int K, int batch, int lda, int sA, int ldb, int sB, "
       "int ldc, int sC, float alpha, bool a_trans, bool split, int epi) -> ()");
   m.def("pyramid_unpool(Tensor G, int H, int W, int[] segs, bool blocked=False) -> Tensor");
+  m.def("pyramid_operand(Tensor fmap, int[] segs, int ld, bool blocked, bool nchw) -> Tensor");
   m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");
   m.def("convex_upsample_backward(Tensor flow, Tensor mask, Tensor grad) -> (Tensor, Tensor)");
   m.def("seq_loss(Tensor[] preds, Tensor gt, Tensor valid, float gamma, float max_flow) -> Tensor");
@@ -1108,6 +1142,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("corr_gemm", &raft_amd::corr_gemm);
   m.impl("pyramid_unpool", &raft_amd::pyramid_unpool);
   m.impl("convex_upsample", &raft_amd::convex_upsample);
+  m.impl("pyramid_operand", &raft_amd::pyramid_operand);
   m.impl("convex_upsample_backward", &raft_amd::convex_upsample_backward);
   m.impl("seq_loss", &raft_amd::seq_loss);
   m.impl("seq_loss_backward", &raft_amd::seq_loss_backward);

@@ -234,6 +234,80 @@ __global__ __launch_bounds__(256) void pyramid_unpool_kernel(const UnpoolArgs u)
   }
 }
 
+// ---------------------------------------------------------------------------- pyramid operand
+__device__ __forceinline__ float pyr_src(const PyrOperandArgs& a, int b, int c, int y, int x) {
+  const long i = b * a.sB + c * a.sC + y * a.sH + x * a.sW;
+  return a.src_bf16 ? static_cast<float>(static_cast<const __bf16*>(a.src)[i]) : static_cast<const float*>(a.src)[i];
+}
+
+// level-L pixel (y, x): 2x2 average of level L-1, summed in F.avg_pool2d's order
+template <int L>
+__device__ float pyr_pool(const PyrOperandArgs& a, int b, int c, int y, int x) {
+  if constexpr (L == 0) {
+    return pyr_src(a, b, c, y, x);
+  } else {
+    float s = 0.f;
+    s += pyr_pool<L - 1>(a, b, c, 2 * y, 2 * x);
+    s += pyr_pool<L - 1>(a, b, c, 2 * y, 2 * x + 1);
+    s += pyr_pool<L - 1>(a, b, c, 2 * y + 1, 2 * x);
+    s += pyr_pool<L - 1>(a, b, c, 2 * y + 1, 2 * x + 1);
+    return s / 4.f;
+  }
+}
+
+__device__ __forceinline__ float pyr_value(const PyrOperandArgs& a, int l, int b, int c, int y, int x) {
+  switch (l) {
+    case 0: return pyr_pool<0>(a, b, c, y, x);
+    case 1: return pyr_pool<1>(a, b, c, y, x);
+    case 2: return pyr_pool<2>(a, b, c, y, x);
+    default: return pyr_pool<3>(a, b, c, y, x);
+  }
+}
+
+// column q of the operand -> (level, y, x); false for padding columns
+__device__ __forceinline__ bool pyr_column(const PyrOperandArgs& a, long q, int& l, int& y, int& x) {
+  for (l = a.nseg - 1; l > 0 && q < a.off[l]; --l) {
+  }
+  if (q < a.off[l]) return false;
+  const long j = q - a.off[l];
+  const int Hl = a.h[l], Wl = a.w[l];
+  if (a.blk) {
+    const long blk = j / (16L * Hl), rem = j - blk * 16L * Hl;
+    y = (int)(rem / 16);
+    x = (int)(blk * 16 + rem % 16);
+    return y < Hl && x < Wl;
+  }
+  if (j >= (long)Hl * Wl) return false;
+  y = (int)(j / Wl);
+  x = (int)(j - (long)y * Wl);
+  return true;
+}
+
+__global__ __launch_bounds__(256) void pyramid_operand_kernel(const PyrOperandArgs a) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (a.nchw) {  // (B, C, ld): consecutive threads walk the pixel axis
+    const long total = (long)a.B * a.C * a.ld;
+    if (i >= total) return;
+    const long q = i % a.ld, bc = i / a.ld;
+    const int c = (int)(bc % a.C), b = (int)(bc / a.C);
+    int l, y, x;
+    a.out[i] = pyr_column(a, q, l, y, x) ? pyr_value(a, l, b, c, y, x) : 0.f;
+  } else {  // (B, ld, C): 4 channels per thread
+    const int C4 = a.C / 4;
+    const long total = (long)a.B * a.ld * C4;
+    if (i >= total) return;
+    const int c = (int)(i % C4) * 4;
+    const long bq = i / C4, q = bq % a.ld;
+    const int b = (int)(bq / a.ld);
+    int l, y, x;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (pyr_column(a, q, l, y, x))
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = pyr_value(a, l, b, c + e, y, x);
+    *reinterpret_cast<f32x4*>(a.out + (bq * a.C + c)) = v;
+  }
+}
+
 __device__ __forceinline__ float safe_floor(float v) {
   // keep far-out-of-range / non-finite coordinates from overflowing int math
   v = fminf(fmaxf(v, -1.0e6f), 1.0e6f);
@@ -413,6 +487,13 @@ hipError_t launch_pyramid_unpool(const UnpoolArgs& u, hipStream_t s) {
   const long total = (long)u.B * u.H * u.W * u.C;
   if (total == 0) return hipSuccess;
   hipLaunchKernelGGL(pyramid_unpool_kernel, dim3(grid_for(total)), dim3(256), 0, s, u);
+  return hipGetLastError();
+}
+
+hipError_t launch_pyramid_operand(const PyrOperandArgs& a, hipStream_t s) {
+  const long total = a.nchw ? (long)a.B * a.C * a.ld : (long)a.B * a.ld * (a.C / 4);
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(pyramid_operand_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

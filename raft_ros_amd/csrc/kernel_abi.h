@@ -290,6 +290,22 @@ struct UnpoolArgs {
   int blk;  // level rows in 16-column block order (the dense pyramid's layout)
 };
 
+// GEMM operand of the dense pyramid: the 2x2 average-pooled levels of a feature map
+// (any strides, bf16 or fp32), every level at column offset off[l] of a ld-long pixel
+// axis (16-column block order when blk), zero rows/columns in the padding; written as
+// fp32 (B, ld, C) rows (nchw = 0) or (B, C, ld) (nchw = 1).  Pool sums follow
+// F.avg_pool2d's order, so the operand is bitwise equal to the torch op sequence.
+struct PyrOperandArgs {
+  const void* src;
+  int src_bf16;
+  long sB, sC, sH, sW;  // element strides of src viewed as (B, C, H, W)
+  int B, C, H, W, nseg;
+  int off[4], h[4], w[4];
+  int blk, nchw;
+  long ld;
+  float* out;
+};
+
 struct LocalCorrArgs {
   const __bf16* f1;   // (B*H*W, C) query features (NHWC rows)
   const __bf16* f2;   // (B, R, C): pooled fmap2 levels, level l rows [off[l], off[l] + h[l]*w[l])

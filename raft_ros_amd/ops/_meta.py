@@ -45,6 +45,11 @@ def register() -> None:
         B, _, H, W = coords.shape
         return coords.new_empty((B, H, W, och), dtype=out_dtype)
 
+    @fake(lib + "pyramid_operand")
+    def _(fmap, segs, ld, blocked, nchw):
+        B, C = fmap.shape[:2]
+        return fmap.new_empty((B, C, ld) if nchw else (B, ld, C), dtype=torch.float32)
+
     @fake(lib + "convex_upsample")
     def _(flow, mask):
         B, _, H, W = flow.shape

@@ -121,15 +121,15 @@ class _BuildPyramid(torch.autograd.Function):
         k = ops()
         alpha = 1.0 / math.sqrt(C)
         f1 = fmap1.detach().float().permute(0, 2, 3, 1).reshape(B, HW, C).contiguous()
-        f2s = _pooled(fmap2.detach().float(), state.num_levels)
         sizes, off = [], 0
-        for f in f2s:
-            Hl, Wl = f.shape[-2:]
+        for l in range(state.num_levels):
+            Hl, Wl = H >> l, W >> l  # repeated 2x2 floor pooling
             sizes.append((Hl, Wl, off))
             off += -(-Wl // 16) * 16 * Hl  # 16-column blocks (see _PyramidState.views)
         ld = off
         state.sizes, state.ld = sizes, ld
-        f2cat = _concat_levels(f2s, ld, [o for _, _, o in sizes], nchw=False, blocked=True)  # (B, ld, C)
+        # pooled fmap2 levels in blocked order, (B, ld, C): one HIP launch (== _concat_levels(_pooled))
+        f2cat = k.pyramid_operand(fmap2.detach(), state.segments(), ld, True, False)
         # AMP (not split): the volume is stored in bf16 -- its lookups feed bf16 convs, and the
         # lookup kernels are bound by the bytes they gather; split mode keeps it fp32-faithful
         buf = torch.empty(B * HW, ld, device=f1.device, dtype=torch.float32 if split else torch.bfloat16)
@@ -155,10 +155,8 @@ class _BuildPyramid(torch.autograd.Function):
         k = ops()
         alpha = 1.0 / math.sqrt(C)
         split = ctx.split
-        f2s = _pooled(fmap2.detach().float(), state.num_levels)
-        f2t = _concat_levels(f2s, ld, [o for _, _, o in state.sizes], nchw=True, blocked=True)  # (B, C, ld)
-        f1t = fmap1.detach().float().new_zeros(B, C, _pad_to(HW, 8))
-        f1t[:, :, :HW] = fmap1.detach().float().reshape(B, C, HW)
+        f2t = k.pyramid_operand(fmap2.detach(), state.segments(), ld, True, True)  # (B, C, ld)
+        f1t = k.pyramid_operand(fmap1.detach(), [0, H, W], _pad_to(HW, 8), False, True)  # (B, C, HW + pad)
         d1 = torch.empty(B, HW, C, device=fmap1.device)
         G = torch.empty(B, ld, C, device=fmap1.device)
         dbuf = state.dbuf
@@ -302,14 +300,14 @@ class LocalCorrPyramid:
         self.fmap1, self.fmap2 = fmap1, fmap2
         if self.mfma:
             self.f1 = fmap1.detach().permute(0, 2, 3, 1).reshape(B * H * W, C).to(torch.bfloat16).contiguous()
-            f2s = _pooled(fmap2.detach().float(), num_levels)
             segs, off = [], 0
-            for f in f2s:
-                Hl, Wl = f.shape[-2:]
+            for l in range(num_levels):
+                Hl, Wl = H >> l, W >> l  # repeated 2x2 floor pooling
                 segs += [off, Hl, Wl]
                 off += _pad_to(Hl * Wl, 8)
             self.segs = segs
-            self.f2cat = _concat_levels(f2s, off, segs[0::3], nchw=False).to(torch.bfloat16)
+            # pooled fmap2 levels, (B, rows, C): one HIP launch (== _concat_levels(_pooled))
+            self.f2cat = ops().pyramid_operand(fmap2.detach(), segs, off, False, False).to(torch.bfloat16)
         elif self.native:
             dt = feature_dtype or torch.float32
             self.f1 = fmap1.permute(0, 2, 3, 1).to(dt).contiguous()

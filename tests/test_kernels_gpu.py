@@ -122,6 +122,30 @@ def test_corr_lookup_fwd(cuda, radius, shape):
     torch.testing.assert_close(got16.permute(0, 3, 1, 2).float(), want, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("blocked", [True, False])
+def test_pyramid_operand_matches_torch_ops(cuda, dtype, blocked):
+    """The one-launch pyramid GEMM operand == F.avg_pool2d levels + pad/permute copies, bit for bit."""
+    from raft_ros_amd.ops.corr import _concat_levels, _pad_to, _pooled
+
+    torch.manual_seed(8)
+    B, C, H, W = 2, 64, 27, 45  # odd sizes: floor pooling, partial 16-column blocks
+    fmap = torch.randn(B, C, H, W, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    fs = _pooled(fmap.float(), 4)
+    segs, off = [], 0
+    for f in fs:
+        Hl, Wl = f.shape[-2:]
+        segs += [off, Hl, Wl]
+        off += -(-Wl // 16) * 16 * Hl if blocked else _pad_to(Hl * Wl, 8)
+    for nchw in (False, True):
+        want = _concat_levels(fs, off, segs[0::3], nchw=nchw, blocked=blocked)
+        got = _ops().pyramid_operand(fmap, segs, off, blocked, nchw)
+        assert torch.equal(got, want), (nchw, (got - want).abs().max().item())
+    # level 0 only, transposed and zero-padded: the dF2 GEMM's f1 operand
+    f1t = _ops().pyramid_operand(fmap, [0, H, W], _pad_to(H * W, 8), False, True)
+    assert torch.equal(f1t[:, :, :H * W], fmap.float().reshape(B, C, H * W)) and not f1t[:, :, H * W:].any()
+
+
 def test_corr_lookup_into_packs_flow_like_pack_flow(cuda):
     """The lookup launch's folded flow packing == the standalone pack_flow op, bit for bit."""
     torch.manual_seed(7)
