@@ -177,7 +177,7 @@ class RAFT(nn.Module):
         flow_up = None
         if self._use_fused(image1, amp):
             return self._forward_fused(corr_fn, net, inp, coords0, coords1, iters, test_mode)
-        for _ in range(iters):
+        for it in range(iters):
             coords1 = coords1.detach()
             corr = corr_fn(coords1, out_dtype=corr_dtype)
             flow = coords1 - coords0
@@ -186,6 +186,8 @@ class RAFT(nn.Module):
             with self._autocast(dev):
                 net, up_mask, delta_flow = self.update_block(net, inp, corr, flow)
             coords1 = coords1 + delta_flow.float()
+            if test_mode and it + 1 < iters:  # only the last upsampled flow is returned
+                continue
             if up_mask is None:
                 flow_up = upflow8(coords1 - coords0)
             else:
@@ -226,15 +228,18 @@ class RAFT(nn.Module):
         flow_predictions = []
         flow_up = None
         for t in range(iters):
+            # test_mode returns only the last upsampled flow: earlier steps skip the mask head
+            # and the upsampling (honoured only without autograd; results are unchanged)
+            up = not test_mode or t == iters - 1
             if dense:
-                net, flow_up, coords1 = upd.step(t, net, coords1, ptoken=corr_fn.token)
+                net, flow_up, coords1 = upd.step(t, net, coords1, ptoken=corr_fn.token, upsample=up)
             elif getattr(corr_fn, "mfma", False):  # features already in the fused layout
                 corr = corr_fn.lookup_padded(coords1.detach(), pad)
-                net, flow_up, coords1 = upd.step(t, net, coords1, corr=corr)
+                net, flow_up, coords1 = upd.step(t, net, coords1, corr=corr, upsample=up)
             else:
                 c = corr_fn(coords1.detach(), out_dtype=torch.bfloat16).permute(0, 2, 3, 1)
                 corr = torch.nn.functional.pad(c, (0, pad - c.shape[-1]))
-                net, flow_up, coords1 = upd.step(t, net, coords1, corr=corr)
+                net, flow_up, coords1 = upd.step(t, net, coords1, corr=corr, upsample=up)
             flow_predictions.append(flow_up)
         if test_mode:
             return coords1 - coords0, flow_up

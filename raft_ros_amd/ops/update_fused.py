@@ -234,7 +234,7 @@ class _PackWeights(torch.autograd.Function):
 
 class _Step(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, wtoken, ptoken, net, inp32, corr_in, coords1, run: _Run, t: int):
+    def forward(ctx, wtoken, ptoken, net, inp32, corr_in, coords1, run: _Run, t: int, up: bool = True):
         B, H, W = run.dims
         P = run.P
         dev = net.device
@@ -287,8 +287,18 @@ class _Step(torch.autograd.Function):
             h = hn
 
         hd = ar.take("hd", t, 512)
-        C.conv_fwd([h], run.wf["heads"], g(3, 3), 512, hd, bias=run.bias["heads"], act=1)
         delta = torch.empty(P, 8, device=dev, dtype=torch.float32)
+        coords_out = torch.empty_like(coords1)
+        flow = torch.empty_like(coords1)
+        if not up:
+            # inference step whose upsampled flow nobody reads (test_mode keeps only the last):
+            # the flow head alone -- the first 256 rows of the fused heads weight -- no mask
+            # head, no convex upsampling
+            C.conv_fwd([h], run.wf["heads"], g(3, 3), 256, hd, bias=run.bias["heads"], act=1)
+            C.conv_fwd([hd[:, :256]], run.wf["fh2"], g(3, 3), 2, delta, bias=run.bias["fh2"])
+            k.apply_delta(coords1, delta, coords_out, flow)
+            return _nchw(h, B, H, W), None, coords_out
+        C.conv_fwd([h], run.wf["heads"], g(3, 3), 512, hd, bias=run.bias["heads"], act=1)
         mask = ar.take("mask", t, 576)
         main, side = run.fork()  # flow-head conv2 beside the mask head's 1x1
         with torch.cuda.stream(side):
@@ -296,8 +306,6 @@ class _Step(torch.autograd.Function):
         C.conv_fwd([hd[:, 256:]], run.wf["mask2"], g(1, 1), 576, mask, bias=run.bias["mask2"])
         main.wait_stream(side)
 
-        coords_out = torch.empty_like(coords1)
-        flow = torch.empty_like(coords1)
         k.apply_delta(coords1, delta, coords_out, flow)
         flow_up = k.convex_upsample(flow, _nchw(mask, B, H, W))
 
@@ -410,7 +418,7 @@ class _Step(torch.autograd.Function):
         d_inp = _nchw(G[:, HID:2 * HID], B, H, W)
         # the tokens only order the autograd graph (their nodes run after every step's backward
         # whatever they receive): no gradient, no fill / accumulate kernels
-        return None, None, d_net, d_inp, d_corr_in, None, None, None
+        return None, None, d_net, d_inp, d_corr_in, None, None, None, None
 
 
 class FusedBasicUpdate:
@@ -423,14 +431,17 @@ class FusedBasicUpdate:
         # the fp32 ``inp`` keeps autograd's cross-iteration gradient sum in fp32
         self.inp32 = inp.float().contiguous(memory_format=torch.channels_last)
 
-    def step(self, t: int, net, coords1, ptoken=None, corr=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    def step(self, t: int, net, coords1, ptoken=None, corr=None,
+             upsample: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor], torch.Tensor]:
         """One refinement iteration -> (net, flow_up (B, 2, 8H, 8W) fp32, coords1 after the
         update (no grad)).  ``ptoken``: the correlation pyramid's autograd token (dense path);
-        ``corr``: (B, H, W, 328) bf16 features (local-correlation path)."""
+        ``corr``: (B, H, W, 328) bf16 features (local-correlation path).  ``upsample=False``
+        (honoured without autograd only): flow_up is None and the mask head is skipped."""
         if ptoken is None:
             ptoken = self.token.new_zeros(())
+        up = upsample or torch.is_grad_enabled()  # skipping needs a forward nobody backpropagates
         return _Step.apply(self.token, ptoken, net, self.inp32, corr, coords1.detach().float().contiguous(),
-                           self.run, t)
+                           self.run, t, up)
 
 
 def supported(block) -> bool:

@@ -159,7 +159,7 @@ class _PackWeights(torch.autograd.Function):
 
 class _Step(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, wtoken, ptoken, net, inp32, corr_in, coords1, run: _Run, t: int):
+    def forward(ctx, wtoken, ptoken, net, inp32, corr_in, coords1, run: _Run, t: int, up: bool = True):
         B, H, W = run.dims
         P = run.P
         k = ops()
@@ -205,7 +205,7 @@ class _Step(torch.autograd.Function):
         coords_out = torch.empty_like(coords1)
         flow = torch.empty_like(coords1)
         k.apply_delta(coords1, delta, coords_out, flow)
-        flow_up = k.upflow8(flow)
+        flow_up = k.upflow8(flow) if up else None  # inference: only the last step's is read
 
         ctx.run, ctx.t = run, t
         ctx.net_dtype = net.dtype
@@ -281,7 +281,7 @@ class _Step(torch.autograd.Function):
         d_inp = _nchw(G[:, HID:HID + CTX], B, H, W)
         # the tokens only order the autograd graph (their nodes run after every step's backward
         # whatever they receive): no gradient, no fill / accumulate kernels
-        return None, None, d_net, d_inp, d_corr_in, None, None, None
+        return None, None, d_net, d_inp, d_corr_in, None, None, None, None
 
 
 class FusedSmallUpdate:
@@ -295,11 +295,13 @@ class FusedSmallUpdate:
         self.token = _PackWeights.apply(self.run, *_params(block))
         self.inp32 = inp.float().contiguous(memory_format=torch.channels_last)
 
-    def step(self, t: int, net, coords1, ptoken=None, corr=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    def step(self, t: int, net, coords1, ptoken=None, corr=None,
+             upsample: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor], torch.Tensor]:
         if ptoken is None:
             ptoken = self.token.new_zeros(())
+        up = upsample or torch.is_grad_enabled()  # skipping needs a forward nobody backpropagates
         return _Step.apply(self.token, ptoken, net, self.inp32, corr, coords1.detach().float().contiguous(),
-                           self.run, t)
+                           self.run, t, up)
 
 
 def supported(block) -> bool:

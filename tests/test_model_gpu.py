@@ -54,6 +54,24 @@ def test_training_step_runs_and_decreases_loss(cuda):
     assert losses[-1] < losses[0]
 
 
+@pytest.mark.parametrize("small,amp", [(False, True), (False, False), (True, True)])
+def test_test_mode_skips_intermediate_upsampling_bitwise(cuda, small, amp):
+    """test_mode without autograd skips the mask head / upsampling of all but the last step:
+    the returned flows equal the last of the full per-step predictions (bit for bit on the
+    bf16 fused path; the fp32 path's library convs may pick other algorithms per call)."""
+    torch.manual_seed(0)
+    model = RAFT(Namespace(small=small, mixed_precision=amp, amp_dtype="bf16")).to(cuda).eval()
+    i1, i2, _, _ = _pair(cuda, B=2)
+    with torch.no_grad():
+        lo, up = model(i1, i2, iters=5, test_mode=True)
+        preds = model(i1, i2, iters=5, test_mode=False)
+    if amp:
+        assert torch.equal(up, preds[-1])
+    else:
+        torch.testing.assert_close(up, preds[-1], rtol=1e-5, atol=1e-5)
+    assert lo.shape[-2:] == (up.shape[-2] // 8, up.shape[-1] // 8) and torch.isfinite(lo).all()
+
+
 def test_alternate_corr_inference(cuda):
     torch.manual_seed(0)
     model = RAFT(Namespace(small=False, mixed_precision=False)).to(cuda).eval()
