@@ -1534,10 +1534,13 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
     // 8-wave tiles (two waves per SIMD, no register spills) for every shape they win on
     // (scripts/bench_convs.py, profiles/r2_bench_convs_nw.log): 3x3 with N >= 192 -> 256x128,
     // 3x3 with 64 < N < 192 -> 128x128; 1x5/5x1: the 1x5 z||r forward (N = 256) -> 128x256,
-    // the 5x1 one (4-row halo), the q forwards and the z||r data gradients -> 128x128; the q
-    // data gradients (128 input channels) stay on v4
+    // the 5x1 one (4-row halo), the q forwards and the 5x1 z||r data gradient -> 128x128; the
+    // 1x5 data gradients (N = 384: d[h | inp | motion]) -> 64x128 with 4 waves (2x the
+    // workgroups: z||r 52.3 -> 45.7 us, q 33.3 -> 29.9 us, profiles/r2_bench_convs_v5_all.log);
+    // the 5x1 q data gradient (128 input channels) stays on v4
     const int taps = a.KH * a.KW;
-    if (taps == 9 && a.N >= 192) v5 = 24;
+    if (taps == 5 && a.KH == 1 && a.N == 384) v5 = 20;
+    else if (taps == 9 && a.N >= 192) v5 = 24;
     else if (taps == 9 && a.N > 64) v5 = 25;
     else if (taps == 5 && a.KH == 1 && a.Cin >= 384 && a.N == 256) v5 = 26;
     else if (taps == 5 && a.Cin >= 256) v5 = 25;
