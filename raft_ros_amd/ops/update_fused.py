@@ -116,6 +116,7 @@ class _Run:
         self.pyr = pyramid  # ops.corr._PyramidState or None (local correlation supplies corr)
         self.arena = _Arena(iters, P, inp.device, keep)
         self.done = set()  # steps whose backward stored their dY
+        self.g_all: Optional[torch.Tensor] = None  # [iters, P, 3*HID] data-gradient rows (backward)
         self.coords: Dict[int, torch.Tensor] = {}
         self.flows: Dict[int, torch.Tensor] = {}
         self.wf: Dict[str, torch.Tensor] = {}
@@ -375,7 +376,12 @@ class _Step(torch.autograd.Function):
         C.conv_fwd([dhd], run.wd["heads"], gd(3, 3), HID, carry,
                    addsrc=_pm(g_net).to(bf).contiguous() if g_net is not None else None, **gate_a(2))
 
-        G = torch.empty(P, 3 * HID, device=dev, dtype=torch.float32)
+        # this step's slot of a per-forward [iters, P, 3*HID] buffer: the d inp columns of every
+        # step stay there and are summed once by the last backward (step 0) -- no per-step
+        # gradient copy / add kernels for the iteration-shared context features
+        if run.g_all is None:
+            run.g_all = torch.empty(run.iters, P, 3 * HID, device=dev, dtype=torch.float32)
+        G = run.g_all[t]
         motion = R("motion")
         dmo = ar.take("dmo", t, HID)
         d_net = torch.empty(P, HID, device=dev, dtype=bf)
@@ -415,7 +421,12 @@ class _Step(torch.autograd.Function):
             k.corr_lookup_backward_(run.pyr.grad_buffers(), run.coords[t], dcorr.reshape(B, H, W, CORR_PAD),
                                     run.pyr.radius)
         d_net = _nchw(d_net if ctx.net_dtype == bf else d_net.to(ctx.net_dtype), B, H, W)
-        d_inp = _nchw(G[:, HID:2 * HID], B, H, W)
+        d_inp = None
+        if t == 0:  # the last step backward to run (every other step's d net feeds it)
+            done = sorted(run.done)
+            gi = run.g_all[:, :, HID:2 * HID] if len(done) == run.iters else run.g_all[done][:, :, HID:2 * HID]
+            d_inp = _nchw(gi.sum(0), B, H, W)
+            run.g_all = None
         # the tokens only order the autograd graph (their nodes run after every step's backward
         # whatever they receive): no gradient, no fill / accumulate kernels
         return None, None, d_net, d_inp, d_corr_in, None, None, None, None

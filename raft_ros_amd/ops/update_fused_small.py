@@ -65,6 +65,7 @@ class _Run:
         self.pyr = pyramid
         self.arena = _Arena(iters, self.P, inp.device, keep)
         self.done = set()
+        self.g_all: Optional[torch.Tensor] = None  # [iters, P, GX] data-gradient rows (backward)
         self.coords = {}
         self.wf, self.wd, self.bias = {}, {}, {}
         for name, mods, segs, dgrad in _LAYERS:
@@ -246,7 +247,10 @@ class _Step(torch.autograd.Function):
         # bf16 d net, d inp, ReLU'-masked d motion.  G = [d h | d inp | d motion] (fp32)
         h = ar.rows("h", t, t + 1)
         zr, q = R("zr"), R("q")
-        G = torch.empty(P, GX, device=dev, dtype=torch.float32)
+        # per-forward [iters, P, GX] rows: the d inp columns are summed once by step 0's backward
+        if run.g_all is None:
+            run.g_all = torch.empty(run.iters, P, GX, device=dev, dtype=torch.float32)
+        G = run.g_all[t]
         carry = torch.empty(P, HID, device=dev, dtype=torch.float32)
         dq = ar.take("dq", t, HID)
         dzr = ar.take("dzr", t, 2 * HID)
@@ -278,7 +282,12 @@ class _Step(torch.autograd.Function):
             k.corr_lookup_backward_(run.pyr.grad_buffers(), run.coords[t], dcorr.reshape(B, H, W, CORR_PAD),
                                     run.pyr.radius)
         d_net = _nchw(d_net if ctx.net_dtype == torch.bfloat16 else d_net.to(ctx.net_dtype), B, H, W)
-        d_inp = _nchw(G[:, HID:HID + CTX], B, H, W)
+        d_inp = None
+        if t == 0:  # the last step backward to run (every other step's d net feeds it)
+            done = sorted(run.done)
+            gall = run.g_all if len(done) == run.iters else run.g_all[done]
+            d_inp = _nchw(gall[:, :, HID:HID + CTX].sum(0), B, H, W)
+            run.g_all = None
         # the tokens only order the autograd graph (their nodes run after every step's backward
         # whatever they receive): no gradient, no fill / accumulate kernels
         return None, None, d_net, d_inp, d_corr_in, None, None, None, None
