@@ -283,16 +283,40 @@ __device__ __forceinline__ bool pyr_column(const PyrOperandArgs& a, long q, int&
   return true;
 }
 
+// (B, C, ld) layout: a block computes a 64-column x 64-channel tile with channel-contiguous
+// reads (4 channels per thread, as the row layout) and writes it transposed through LDS, so
+// both the NHWC source reads and the column-contiguous stores are coalesced.
+__global__ __launch_bounds__(256) void pyramid_operand_t_kernel(const PyrOperandArgs a) {
+  __shared__ float tile[64][65];
+  const int tid = threadIdx.x;
+  const long q0 = (long)blockIdx.x * 64;
+  const int c0 = blockIdx.y * 64, b = blockIdx.z;
+  const int c4 = (tid & 15) * 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int qq = (tid >> 4) + 16 * k;
+    const long q = q0 + qq;
+    int l, y, x;
+    const bool live = q < a.ld && pyr_column(a, q, l, y, x);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = c0 + c4 + e;
+      tile[c4 + e][qq] = (live && c < a.C) ? pyr_value(a, l, b, c, y, x) : 0.f;
+    }
+  }
+  __syncthreads();
+  const int cl = tid >> 2, qs = (tid & 3) * 16;
+  const int c = c0 + cl;
+  if (c >= a.C) return;
+  float* o = a.out + ((long)b * a.C + c) * a.ld + q0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    if (q0 + qs + j < a.ld) o[qs + j] = tile[cl][qs + j];
+}
+
 __global__ __launch_bounds__(256) void pyramid_operand_kernel(const PyrOperandArgs a) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (a.nchw) {  // (B, C, ld): consecutive threads walk the pixel axis
-    const long total = (long)a.B * a.C * a.ld;
-    if (i >= total) return;
-    const long q = i % a.ld, bc = i / a.ld;
-    const int c = (int)(bc % a.C), b = (int)(bc / a.C);
-    int l, y, x;
-    a.out[i] = pyr_column(a, q, l, y, x) ? pyr_value(a, l, b, c, y, x) : 0.f;
-  } else {  // (B, ld, C): 4 channels per thread
+  {  // (B, ld, C): 4 channels per thread
     const int C4 = a.C / 4;
     const long total = (long)a.B * a.ld * C4;
     if (i >= total) return;
@@ -491,8 +515,13 @@ hipError_t launch_pyramid_unpool(const UnpoolArgs& u, hipStream_t s) {
 }
 
 hipError_t launch_pyramid_operand(const PyrOperandArgs& a, hipStream_t s) {
-  const long total = a.nchw ? (long)a.B * a.C * a.ld : (long)a.B * a.ld * (a.C / 4);
-  if (total == 0) return hipSuccess;
+  if ((long)a.B * a.C * a.ld == 0) return hipSuccess;
+  if (a.nchw) {
+    const dim3 grid((unsigned)((a.ld + 63) / 64), (unsigned)((a.C + 63) / 64), (unsigned)a.B);
+    hipLaunchKernelGGL(pyramid_operand_t_kernel, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
+  const long total = (long)a.B * a.ld * (a.C / 4);
   hipLaunchKernelGGL(pyramid_operand_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
