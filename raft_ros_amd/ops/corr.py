@@ -57,6 +57,7 @@ class _PyramidState:
         self.dbuf: Optional[torch.Tensor] = None
         self.dlevels: Optional[List[torch.Tensor]] = None
         self.sizes = []                        # (Hl, Wl, off) per level
+        self.tail = None                       # stream of fused-step lookup backwards (to join)
         self.ld = 0
         self.shape = None
 
@@ -147,6 +148,12 @@ class _BuildPyramid(torch.autograd.Function):
     def backward(ctx, gtoken):
         state: _PyramidState = ctx.state
         fmap1, fmap2 = ctx.saved_tensors
+        tail = getattr(state, "tail", None)
+        if tail is not None:  # lookups' backward ran on the fused step's tail stream
+            torch.cuda.current_stream().wait_stream(tail)
+            state.tail = None
+            if state.dbuf is not None:
+                state.dbuf.record_stream(tail)
         if state.dbuf is None:
             state.release()
             return None, None, None, None

@@ -31,6 +31,7 @@ HIP launch per conv per RAFT forward (``ops.conv.pack_weights``).
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -117,6 +118,7 @@ class _Run:
         self.arena = _Arena(iters, P, inp.device, keep)
         self.done = set()  # steps whose backward stored their dY
         self.g_all: Optional[torch.Tensor] = None  # [iters, P, 3*HID] data-gradient rows (backward)
+        self.tail: Optional[torch.cuda.Stream] = None  # stream of the motion-encoder backward
         self.coords: Dict[int, torch.Tensor] = {}
         self.flows: Dict[int, torch.Tensor] = {}
         self.wf: Dict[str, torch.Tensor] = {}
@@ -207,6 +209,14 @@ class _Run:
 
 
 _SIDE = {}
+_TAIL = {}
+TAIL_STREAM = True  # motion-encoder backward on its own stream (see _Step.backward)
+
+
+def _tail_stream(device) -> torch.cuda.Stream:
+    if device not in _TAIL:
+        _TAIL[device] = torch.cuda.Stream(device=device)
+    return _TAIL[device]
 CONCURRENT = False  # run a step's independent conv branches on two streams (measured: no gain, 317.6 vs 315.3 pairs/s)
 
 
@@ -228,6 +238,8 @@ class _PackWeights(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gtoken):
         run: _Run = ctx.run
+        if run.tail is not None:  # the steps' motion-encoder backward wrote dY on the tail stream
+            torch.cuda.current_stream().wait_stream(run.tail)
         grads = run.weight_grads()
         run.arena.bufs.clear()
         return (None, *grads)
@@ -399,27 +411,32 @@ class _Step(torch.autograd.Function):
                 C.conv_fwd([dzr], run.wd[f"zr{stage}"], gd(kh, kw), 3 * HID, G, epi=C.EPI_GRU_BWD_LAST, acc_c0=0,
                            out3=d_net, gru_cols=HID, cout=dmo, cmask=motion, cm_c0=2 * HID, cm_valid=126)
 
-        # ---- motion encoder
+        # ---- motion encoder.  With the dense pyramid its backward is a side branch: it feeds only
+        # the pyramid gradient and the batched weight gradients, not the d net the next (earlier)
+        # step waits for.  It runs on the tail stream, beside that step's head / GRU backward;
+        # the pyramid and weight-gradient backward join the tail stream before they read.
         cf, c1, f1 = R("cf"), R("c1"), R("f1")
         dcf = ar.take("dcf", t, 256)
-        dgrad("conv", dmo, 3, 3, dcf, 256, mask=cf)
         dc1 = ar.take("dc1", t, 256)
-        dcorr = torch.empty(P, CORR_PAD, device=dev, dtype=bf)
         df1 = ar.take("df1", t, 128)
-        main, side = run.fork()  # flow-branch dgrad beside the correlation-branch chain
-        with torch.cuda.stream(side):
+        dcorr = torch.empty(P, CORR_PAD, device=dev, dtype=bf)
+        dense = not ctx.has_corr_in and run.pyr is not None and bool(run.pyr.levels)
+        pgrad = run.pyr.grad_buffers() if dense else None  # allocated (zeroed) on the main stream
+        tail = _tail_stream(dev) if dense and TAIL_STREAM and dev.type == "cuda" else None
+        if tail is not None:
+            tail.wait_stream(torch.cuda.current_stream(dev))
+            dcorr.record_stream(tail)
+            run.tail = run.pyr.tail = tail
+        with torch.cuda.stream(tail) if tail is not None else contextlib.nullcontext():
+            dgrad("conv", dmo, 3, 3, dcf, 256, mask=cf)
             dgrad("convf2", dcf[:, 192:], 3, 3, df1, 128, mask=f1)
-        dgrad("convc2", dcf[:, :192], 3, 3, dc1, 256, mask=c1)
-        dgrad("convc1", dc1, 1, 1, dcorr, CORR_PAD)
-        main.wait_stream(side)
+            dgrad("convc2", dcf[:, :192], 3, 3, dc1, 256, mask=c1)
+            dgrad("convc1", dc1, 1, 1, dcorr, CORR_PAD)
+            if dense:
+                k.corr_lookup_backward_(pgrad, run.coords[t], dcorr.reshape(B, H, W, CORR_PAD), run.pyr.radius)
         run.done.add(t)
 
-        d_corr_in = None
-        if ctx.has_corr_in:
-            d_corr_in = dcorr.reshape(B, H, W, CORR_PAD)
-        elif run.pyr is not None and run.pyr.levels:
-            k.corr_lookup_backward_(run.pyr.grad_buffers(), run.coords[t], dcorr.reshape(B, H, W, CORR_PAD),
-                                    run.pyr.radius)
+        d_corr_in = dcorr.reshape(B, H, W, CORR_PAD) if ctx.has_corr_in else None
         d_net = _nchw(d_net if ctx.net_dtype == bf else d_net.to(ctx.net_dtype), B, H, W)
         d_inp = None
         if t == 0:  # the last step backward to run (every other step's d net feeds it)
