@@ -241,6 +241,8 @@ class RAFT(nn.Module):
                 corr = torch.nn.functional.pad(c, (0, pad - c.shape[-1]))
                 net, flow_up, coords1 = upd.step(t, net, coords1, corr=corr, upsample=up)
             flow_predictions.append(flow_up)
+        if hasattr(upd, "join"):
+            upd.join()  # upsampled flows computed on the fused step's tail stream
         if test_mode:
             return coords1 - coords0, flow_up
         return flow_predictions

@@ -213,6 +213,11 @@ _TAIL = {}
 TAIL_STREAM = True  # motion-encoder backward on its own stream (see _Step.backward)
 
 
+def keep_tail(run) -> bool:
+    """Forward tail work needs a caller that joins the tail stream (FusedBasicUpdate.join)."""
+    return run.arena.keep
+
+
 def _tail_stream(device) -> torch.cuda.Stream:
     if device not in _TAIL:
         _TAIL[device] = torch.cuda.Stream(device=device)
@@ -313,14 +318,20 @@ class _Step(torch.autograd.Function):
             return _nchw(h, B, H, W), None, coords_out
         C.conv_fwd([h], run.wf["heads"], g(3, 3), 512, hd, bias=run.bias["heads"], act=1)
         mask = ar.take("mask", t, 576)
-        main, side = run.fork()  # flow-head conv2 beside the mask head's 1x1
-        with torch.cuda.stream(side):
-            C.conv_fwd([hd[:, :256]], run.wf["fh2"], g(3, 3), 2, delta, bias=run.bias["fh2"])
-        C.conv_fwd([hd[:, 256:]], run.wf["mask2"], g(1, 1), 576, mask, bias=run.bias["mask2"])
-        main.wait_stream(side)
-
+        C.conv_fwd([hd[:, :256]], run.wf["fh2"], g(3, 3), 2, delta, bias=run.bias["fh2"])
         k.apply_delta(coords1, delta, coords_out, flow)
-        flow_up = k.convex_upsample(flow, _nchw(mask, B, H, W))
+        # the mask head's 1x1 and the convex upsampling feed only the loss, not the next step:
+        # they run on the tail stream beside the next step's lookup / motion encoder / GRU
+        # (the caller joins the tail stream before the loss reads the flows)
+        tail = _tail_stream(dev) if TAIL_STREAM and dev.type == "cuda" and keep_tail(run) else None
+        if tail is not None:
+            tail.wait_stream(torch.cuda.current_stream(dev))
+            run.tail = tail
+        with torch.cuda.stream(tail) if tail is not None else contextlib.nullcontext():
+            C.conv_fwd([hd[:, 256:]], run.wf["mask2"], g(1, 1), 576, mask, bias=run.bias["mask2"])
+            flow_up = k.convex_upsample(flow, _nchw(mask, B, H, W))
+        if tail is not None:
+            flow_up.record_stream(torch.cuda.current_stream(dev))
 
         ctx.run, ctx.t = run, t
         ctx.net_dtype = net.dtype
@@ -458,6 +469,11 @@ class FusedBasicUpdate:
         self.token = _PackWeights.apply(self.run, *_params(block))
         # the fp32 ``inp`` keeps autograd's cross-iteration gradient sum in fp32
         self.inp32 = inp.float().contiguous(memory_format=torch.channels_last)
+
+    def join(self):
+        """Make the current stream wait for the steps' tail-stream work (their upsampled flows)."""
+        if self.run.tail is not None:
+            torch.cuda.current_stream().wait_stream(self.run.tail)
 
     def step(self, t: int, net, coords1, ptoken=None, corr=None,
              upsample: bool = True) -> Tuple[torch.Tensor, Optional[torch.Tensor], torch.Tensor]:
