@@ -211,6 +211,14 @@ class _Run:
 _SIDE = {}
 _TAIL = {}
 TAIL_STREAM = True  # motion-encoder backward on its own stream (see _Step.backward)
+HEAD_STREAM = True  # upsampler / head backward ahead of the d-net chain (see _Step.backward)
+_HEAD = {}
+
+
+def _head_stream(device) -> torch.cuda.Stream:
+    if device not in _HEAD:
+        _HEAD[device] = torch.cuda.Stream(device=device)
+    return _HEAD[device]
 
 
 def keep_tail(run) -> bool:
@@ -362,21 +370,34 @@ class _Step(torch.autograd.Function):
             C.conv_fwd([dy], run.wd[name], gd(kh, kw), n, out, epi=C.EPI_GRAD, mask=mask, acc_c0=acc_c0)
 
         hd, mask = R("hd"), R("mask")
-        # ---- upsampler + heads
         dmask = ar.take("dmask", t, 576)
         dd8 = ar.take("dd8", t, 8)
-        if g_flow_up is not None:
-            k.convex_upsample_backward_into(run.flows[t], _nchw(mask, B, H, W), g_flow_up,
-                                            _nchw(dmask, B, H, W), dd8)
-        else:
-            dmask.zero_()
-            dd8.zero_()
         dhd = ar.take("dhd", t, 512)
-        main, side = run.fork()
-        with torch.cuda.stream(side):
+        # ---- upsampler + head data gradients.  They need only this step's loss gradient and
+        # forward activations, not the d net of the later step: on the head stream they start
+        # from the loss gradient's ready event while the main stream still runs the later
+        # step's GRU backward (without such an event: after everything queued so far)
+        main = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+        head = _head_stream(dev) if HEAD_STREAM and main is not None and ar.keep else None
+        if head is not None:
+            ready = getattr(g_flow_up, "_raft_ready", None) if g_flow_up is not None else None
+            if ready is not None:
+                head.wait_event(ready)
+            else:
+                head.wait_stream(main)
+            if g_flow_up is not None:
+                g_flow_up.record_stream(head)
+        with torch.cuda.stream(head) if head is not None else contextlib.nullcontext():
+            if g_flow_up is not None:
+                k.convex_upsample_backward_into(run.flows[t], _nchw(mask, B, H, W), g_flow_up,
+                                                _nchw(dmask, B, H, W), dd8)
+            else:
+                dmask.zero_()
+                dd8.zero_()
             dgrad("fh2", dd8, 3, 3, dhd[:, :256], 256, mask=hd[:, :256])
-        dgrad("mask2", dmask, 1, 1, dhd[:, 256:], 256, mask=hd[:, 256:])
-        main.wait_stream(side)
+            dgrad("mask2", dmask, 1, 1, dhd[:, 256:], 256, mask=hd[:, 256:])
+        if head is not None:
+            main.wait_stream(head)
         # ---- GRU stages (reverse order).  The gate backward runs in the epilogues of the data
         # gradients: the conv producing a stage's dH finishes (dq, dz, carry) of that stage
         # (EPI_GRU_BWD_A), the q conv's data gradient finishes dr and d h (EPI_GRU_BWD_B); the

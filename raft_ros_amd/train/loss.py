@@ -35,6 +35,13 @@ class _FusedSeqLoss(torch.autograd.Function):
         flow_gt, valid, *preds = ctx.saved_tensors
         grads = ops().seq_loss_backward(preds, flow_gt, valid, gloss.float().reshape(1), ctx.gamma,
                                         ctx.max_flow)
+        if grads and grads[0].is_cuda:
+            # when the gradients are ready: the fused refinement steps start their upsampler /
+            # head backward on a side stream from this event (ops/update_fused.py)
+            ready = torch.cuda.Event()
+            ready.record()
+            for g in grads:
+                g._raft_ready = ready
         return (None, None, None, None, *grads)
 
 
