@@ -324,18 +324,23 @@ class _Step(torch.autograd.Function):
             C.conv_fwd([hd[:, :256]], run.wf["fh2"], g(3, 3), 2, delta, bias=run.bias["fh2"])
             k.apply_delta(coords1, delta, coords_out, flow)
             return _nchw(h, B, H, W), None, coords_out
-        C.conv_fwd([h], run.wf["heads"], g(3, 3), 512, hd, bias=run.bias["heads"], act=1)
         mask = ar.take("mask", t, 576)
+        # the mask head (its 3x3 half of the fused heads conv, the 1x1) and the convex upsampling
+        # feed only the loss, not the next step: they run on the tail stream beside the next
+        # step's lookup / motion encoder / GRU (the caller joins the tail stream before the loss
+        # reads the flows); the main stream keeps the flow head alone
+        tail = _tail_stream(dev) if TAIL_STREAM and dev.type == "cuda" and keep_tail(run) else None
+        C.conv_fwd([h], run.wf["heads"], g(3, 3), 256 if tail is not None else 512, hd, bias=run.bias["heads"],
+                   act=1)
         C.conv_fwd([hd[:, :256]], run.wf["fh2"], g(3, 3), 2, delta, bias=run.bias["fh2"])
         k.apply_delta(coords1, delta, coords_out, flow)
-        # the mask head's 1x1 and the convex upsampling feed only the loss, not the next step:
-        # they run on the tail stream beside the next step's lookup / motion encoder / GRU
-        # (the caller joins the tail stream before the loss reads the flows)
-        tail = _tail_stream(dev) if TAIL_STREAM and dev.type == "cuda" and keep_tail(run) else None
         if tail is not None:
             tail.wait_stream(torch.cuda.current_stream(dev))
             run.tail = tail
         with torch.cuda.stream(tail) if tail is not None else contextlib.nullcontext():
+            if tail is not None:  # mask.0: rows [256, 512) of the fused heads weight
+                C.conv_fwd([h], run.wf["heads"][256:], g(3, 3), 256, hd[:, 256:], bias=run.bias["heads"][256:],
+                           act=1)
             C.conv_fwd([hd[:, 256:]], run.wf["mask2"], g(1, 1), 576, mask, bias=run.bias["mask2"])
             flow_up = k.convex_upsample(flow, _nchw(mask, B, H, W))
         if tail is not None:
