@@ -200,10 +200,9 @@ class RAFT(nn.Module):
 
     # ------------------------------------------------------------------ native encoders
     def _side_stream(self, device) -> torch.cuda.Stream:
-        streams = self.__dict__.setdefault("_side_streams", {})
-        if device not in streams:
-            streams[device] = torch.cuda.Stream(device=device)
-        return streams[device]
+        from ..ops.streams import aux_stream
+
+        return aux_stream(device, "side")
 
     def _use_native_encoders(self, image1, amp: bool) -> bool:
         return (amp and self.amp_dtype == torch.bfloat16 and _arg(self.args, "native_encoder", True)

@@ -37,6 +37,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from . import conv as C
+from .streams import aux_stream
 from ._ext import ops
 
 HID = 128
@@ -208,17 +209,12 @@ class _Run:
         return grads
 
 
-_SIDE = {}
-_TAIL = {}
 TAIL_STREAM = True  # motion-encoder backward on its own stream (see _Step.backward)
 HEAD_STREAM = True  # upsampler / head backward ahead of the d-net chain (see _Step.backward)
-_HEAD = {}
 
 
 def _head_stream(device) -> torch.cuda.Stream:
-    if device not in _HEAD:
-        _HEAD[device] = torch.cuda.Stream(device=device)
-    return _HEAD[device]
+    return aux_stream(device, "side")  # idle during the loop's backward (ops/streams.py)
 
 
 def keep_tail(run) -> bool:
@@ -227,16 +223,12 @@ def keep_tail(run) -> bool:
 
 
 def _tail_stream(device) -> torch.cuda.Stream:
-    if device not in _TAIL:
-        _TAIL[device] = torch.cuda.Stream(device=device)
-    return _TAIL[device]
+    return aux_stream(device, "tail")
 CONCURRENT = False  # run a step's independent conv branches on two streams (measured: no gain, 317.6 vs 315.3 pairs/s)
 
 
 def _side_stream(device) -> torch.cuda.Stream:
-    if device not in _SIDE:
-        _SIDE[device] = torch.cuda.Stream(device=device)
-    return _SIDE[device]
+    return aux_stream(device, "side")
 
 
 class _PackWeights(torch.autograd.Function):
