@@ -224,7 +224,10 @@ def keep_tail(run) -> bool:
 
 def _tail_stream(device) -> torch.cuda.Stream:
     return aux_stream(device, "tail")
-CONCURRENT = False  # run a step's independent conv branches on two streams (measured: no gain, 317.6 vs 315.3 pairs/s)
+# the step's flow / correlation conv branches on the side and main streams (+0.7 %,
+# profiles/r2_concurrent_branches_ab.log; it lost while the process used more streams than
+# hardware queues)
+CONCURRENT = True
 
 
 def _side_stream(device) -> torch.cuda.Stream:
