@@ -63,7 +63,8 @@ def parse():
     ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=None,
                     help="replay the step as captured HIP graph(s) (train: fwd+loss+bwd+clip+AdamW, grads "
                          "all-reduced between two graphs when N>1; infer: the forward). Default: on for infer; "
-                         "off for train, where the step is GPU-bound (graph 223 vs eager 224 pairs/s on MI355X)")
+                         "off for train, where the step is GPU-bound and eager keeps more of the multi-stream overlap "
+                         "(graph 372 vs eager 386 pairs/s on MI355X, profiles/r2_graph_vs_eager_final.log)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: gloo-backend plumbing check of the launch path only (tests), never a measurement")
     return ap.parse_args()
