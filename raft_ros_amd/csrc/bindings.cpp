@@ -11,6 +11,7 @@
 #include <c10/core/DeviceGuard.h>
 
 #include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -24,7 +25,7 @@ enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 
 // launchers (defined in the .hip translation units)
 hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s);
-hipError_t launch_fixed_to_float(const long long* in, float* out, long n, hipStream_t s);
+hipError_t launch_fixed_to_float(const long long* in, float* out, long n, const float* fix_scale, hipStream_t s);
 hipError_t launch_local_corr_mfma(const LocalCorrArgs& a, bool backward, hipStream_t s);
 hipError_t launch_pyramid_unpool(const UnpoolArgs& u, hipStream_t s);
 hipError_t launch_pyramid_operand(const PyrOperandArgs& a, hipStream_t s);
@@ -63,7 +64,8 @@ hipError_t launch_local_corr_fwd(const void* f1, const void* f2, int dtype, cons
                                  float* out, int B, int H1, int W1, int H2, int W2, int C, int r,
                                  float scale, hipStream_t s);
 hipError_t launch_local_corr_bwd(const void* f1, const void* f2, int dtype, const float* coords,
-                                 const float* gout, float* g1, float* g2, long long* g2fix, int B, int H1, int W1,
+                                 const float* gout, float* g1, float* g2, long long* g2fix, const float* fix_scale,
+                                 int B, int H1, int W1,
                                  int H2, int W2, int C, int r, float scale, hipStream_t s);
 
 hipError_t launch_gru_gates_fwd(int dtype, const void* zr, const void* h, void* z, void* rh, long npix,
@@ -473,6 +475,17 @@ at::Tensor local_corr(const at::Tensor& f1, const at::Tensor& f2, const at::Tens
   return out;
 }
 
+// Per-tensor scale of the deterministic fixed-point gradient accumulators (common.h
+// fixed_atomic_add): the power of two that maps the largest possible accumulated value,
+// nterms * max|g| * max|f1| * |scale|, to 2^62.  A device scalar, computed without a host
+// sync (reductions are deterministic, so the scale is too).
+at::Tensor fixed_point_scale(const at::Tensor& g, const at::Tensor& f1, double scale, double nterms) {
+  auto bound = g.abs().amax().to(at::kFloat) * f1.abs().amax().to(at::kFloat) *
+               static_cast<float>(std::abs(scale) * nterms);
+  auto e = at::floor(62.0 - at::log2(bound.clamp_min(1e-30f))).clamp(-60.0, 120.0);
+  return at::exp2(e).reshape({1}).contiguous();
+}
+
 std::tuple<at::Tensor, at::Tensor> local_corr_backward(const at::Tensor& f1, const at::Tensor& f2,
                                                        const at::Tensor& coords,
                                                        const at::Tensor& grad, int64_t radius,
@@ -489,11 +502,16 @@ std::tuple<at::Tensor, at::Tensor> local_corr_backward(const at::Tensor& f1, con
   auto g2 = at::zeros({B, H2, W2, C}, f1.options().dtype(at::kFloat));
   at::Tensor fix = deterministic ? at::zeros({B, H2, W2, C}, f1.options().dtype(at::kLong)) : at::Tensor();
   long long* fp = deterministic ? reinterpret_cast<long long*>(fix.data_ptr<int64_t>()) : nullptr;
+  // one level per call: a level-0 pixel of f2 takes at most (2r+2)^2 window corners of each of
+  // the queries that map onto it (H1*W1 / (H2*W2) of them, rounded up)
+  const double per_px = std::ceil((double)(H1 * W1) / (double)(H2 * W2));
+  at::Tensor fs = deterministic ? fixed_point_scale(g, f1, scale, per_px * 4.0 * (rd + 1) * (rd + 1)) : at::Tensor();
   HIP_OK(launch_local_corr_bwd(f1.data_ptr(), f2.data_ptr(), dtype_code(f1.scalar_type()),
                                coords.data_ptr<float>(), g.data_ptr<float>(), g1.data_ptr<float>(),
-                               g2.data_ptr<float>(), fp, B, H1, W1, H2, W2, C, static_cast<int>(radius),
-                               static_cast<float>(scale), cur_stream()));
-  if (deterministic) HIP_OK(launch_fixed_to_float(fp, g2.data_ptr<float>(), g2.numel(), cur_stream()));
+                               g2.data_ptr<float>(), fp, deterministic ? fs.data_ptr<float>() : nullptr, B, H1, W1,
+                               H2, W2, C, static_cast<int>(radius), static_cast<float>(scale), cur_stream()));
+  if (deterministic)
+    HIP_OK(launch_fixed_to_float(fp, g2.data_ptr<float>(), g2.numel(), fs.data_ptr<float>(), cur_stream()));
   return {g1, g2};
 }
 
@@ -560,8 +578,15 @@ void local_corr_mfma_backward(const at::Tensor& f1, const at::Tensor& f2, const 
   // deterministic: 32.32 fixed-point integer atomics (order-independent), then added into g2
   at::Tensor fix = deterministic ? at::zeros(g2.sizes(), g2.options().dtype(at::kLong)) : at::Tensor();
   a.g2fix = deterministic ? reinterpret_cast<long long*>(fix.data_ptr<int64_t>()) : nullptr;
+  at::Tensor fs;
+  if (deterministic) {
+    // the coarsest level gathers the most queries per pixel: 4^(L-1) of them, each touching it
+    // through up to (2r+2)^2 window corners
+    fs = fixed_point_scale(gout, f1, scale, std::pow(4.0, a.levels - 1) * 4.0 * (2 * radius + 2) * (2 * radius + 2));
+    a.fix_scale = fs.data_ptr<float>();
+  }
   HIP_OK(launch_local_corr_mfma(a, true, cur_stream()));
-  if (deterministic) HIP_OK(launch_fixed_to_float(a.g2fix, a.g2, g2.numel(), cur_stream()));
+  if (deterministic) HIP_OK(launch_fixed_to_float(a.g2fix, a.g2, g2.numel(), a.fix_scale, cur_stream()));
 }
 
 // ---------------------------------------------------------------- fused GRU gates

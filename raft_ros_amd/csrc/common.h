@@ -47,13 +47,16 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 inline int cdiv(long a, long b) { return static_cast<int>((a + b - 1) / b); }
 
-// Deterministic scatter-add: contributions are rounded to 32.32 fixed point and added with
-// 64-bit integer atomics, which are associative -- the sum no longer depends on the order the
-// waves arrive in (torch.use_deterministic_algorithms).  Resolution 2^-32, range +-2^31.
-constexpr double kFixScale = 4294967296.0;
-__device__ __forceinline__ void fixed_atomic_add(long long* p, float v) {
+// Deterministic scatter-add: contributions are rounded to fixed point and added with 64-bit
+// integer atomics, which are associative -- the sum no longer depends on the order the waves
+// arrive in (torch.use_deterministic_algorithms).  The scale ``fs`` is a power of two chosen
+// per tensor by the host wrapper (bindings.cpp fixed_point_scale) from a bound of the largest
+// possible sum, so the accumulator spends its 63 bits on the actual value range: realistic
+// loss gradients (~1e-8 per contribution) keep ~40 significant bits instead of being
+// quantised by a fixed 2^-32 step.
+__device__ __forceinline__ void fixed_atomic_add(long long* p, float v, float fs) {
   atomicAdd(reinterpret_cast<unsigned long long*>(p),
-            static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v) * kFixScale)));
+            static_cast<unsigned long long>(__double2ll_rn(static_cast<double>(v) * static_cast<double>(fs))));
 }
 
 }  // namespace raft_amd

@@ -1546,9 +1546,11 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
     else if (taps == 5 && a.Cin >= 256) v5 = 25;
   }
   if (ok5 && v5 >= 20) {
-    // 20..23: 4 waves per workgroup; 24..26: the 256x128 / 128x128 / 128x256 tiles with 8 waves
-    auto bm_of = [](int v) { return v == 20 ? 64 : (v == 23 || v == 24) ? 256 : 128; };
-    auto bn_of = [](int v) { return (v == 22 || v == 26) ? 256 : 128; };
+    // 20 / 21: 64x128 / 128x128 with 4 waves per workgroup; 24..26: the 256x128 / 128x128 /
+    // 128x256 tiles with 8 waves
+    if (v5 == 22 || v5 == 23 || v5 > 26) return hipErrorInvalidValue;
+    auto bm_of = [](int v) { return v == 20 ? 64 : v == 24 ? 256 : 128; };
+    auto bn_of = [](int v) { return v == 26 ? 256 : 128; };
     auto rows_of = [&](int v) { return (bm_of(v) + (a.KH - 1) * a.W + a.KW - 1 + 7) / 8 * 8; };
     long lds = fwd5_lds_bytes(bm_of(v5), bn_of(v5), rows_of(v5));
     if (lds == 0 && v5 != 21) {
@@ -1559,17 +1561,9 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
     if (lds > 0) {
       const dim3 grid(tiles(bm_of(v5), bn_of(v5)));
       switch (v5) {
-        case 23:
-          set_lds_limit((const void*)conv_fwd5_kernel<256, 128>, (int)lds);
-          hipLaunchKernelGGL((conv_fwd5_kernel<256, 128>), grid, dim3(256), lds, s, a, rows);
-          break;
         case 20:
           set_lds_limit((const void*)conv_fwd5_kernel<64, 128>, (int)lds);
           hipLaunchKernelGGL((conv_fwd5_kernel<64, 128>), grid, dim3(256), lds, s, a, rows);
-          break;
-        case 22:
-          set_lds_limit((const void*)conv_fwd5_kernel<128, 256>, (int)lds);
-          hipLaunchKernelGGL((conv_fwd5_kernel<128, 256>), grid, dim3(256), lds, s, a, rows);
           break;
         case 24:
           set_lds_limit((const void*)conv_fwd5_kernel<256, 128, 8>, (int)lds);

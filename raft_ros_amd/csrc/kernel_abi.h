@@ -325,7 +325,8 @@ struct LocalCorrArgs {
   int gout_bf16;
   float* g1;  // (B*H*W, C) fp32
   float* g2;  // (B, R, C) fp32, accumulated (atomics)
-  long long* g2fix;  // non-null: deterministic mode, 32.32 fixed-point accumulator like g2
+  long long* g2fix;  // non-null: deterministic mode, fixed-point accumulator like g2
+  const float* fix_scale;  // deterministic mode: device scalar, the power-of-two fixed-point scale
 };
 
 // ============================================================================ sequence loss

@@ -108,7 +108,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void local_corr_bwd_kernel(
     const T* __restrict__ f1, const T* __restrict__ f2, const float* __restrict__ coords,
     const float* __restrict__ gout, float* __restrict__ g1, float* __restrict__ g2, long long* __restrict__ g2fix,
-    int B, int H1, int W1, int H2, int W2, int C, int r, float scale) {
+    const float* __restrict__ fix_scale, int B, int H1, int W1, int H2, int W2, int C, int r, float scale) {
   __shared__ float gn[4][kMaxNb];
   __shared__ int pos[4][kMaxNb];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -150,6 +150,7 @@ __global__ __launch_bounds__(256) void local_corr_bwd_kernel(
   const T* a = f1 + pix * C;
   const T* f2b = f2 + (long)b * H2 * W2 * C;
   float* g2b = g2 + (long)b * H2 * W2 * C;
+  const float fs = g2fix != nullptr ? *fix_scale : 0.f;
   for (int c0 = lane; c0 < C; c0 += 64) {
     const float av = to_f32(a[c0]);
     float acc = 0.f;
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(256) void local_corr_bwd_kernel(
       const float gv = gn[w][n];
       acc += gv * to_f32(f2b[(long)q * C + c0]);
       if (g2fix != nullptr)
-        fixed_atomic_add(g2fix + (g2b - g2) + (long)q * C + c0, gv * av);
+        fixed_atomic_add(g2fix + (g2b - g2) + (long)q * C + c0, gv * av, fs);
       else
         atomicAdd(g2b + (long)q * C + c0, gv * av);
     }
@@ -188,19 +189,19 @@ hipError_t launch_local_corr_fwd(const void* f1, const void* f2, int dtype, cons
 }
 
 hipError_t launch_local_corr_bwd(const void* f1, const void* f2, int dtype, const float* coords,
-                                 const float* gout, float* g1, float* g2, long long* g2fix, int B, int H1, int W1,
-                                 int H2, int W2, int C, int r, float scale, hipStream_t s) {
+                                 const float* gout, float* g1, float* g2, long long* g2fix, const float* fix_scale,
+                                 int B, int H1, int W1, int H2, int W2, int C, int r, float scale, hipStream_t s) {
   if ((2 * r + 2) * (2 * r + 2) > kMaxNb) return hipErrorInvalidValue;
   const long npix = (long)B * H1 * W1;
   if (npix == 0) return hipSuccess;
   const dim3 g((npix + 3) / 4), blk(256);
   if (dtype == kBF16)
     hipLaunchKernelGGL(local_corr_bwd_kernel<__bf16>, g, blk, 0, s, static_cast<const __bf16*>(f1),
-                       static_cast<const __bf16*>(f2), coords, gout, g1, g2, g2fix, B, H1, W1, H2, W2, C, r,
+                       static_cast<const __bf16*>(f2), coords, gout, g1, g2, g2fix, fix_scale, B, H1, W1, H2, W2, C, r,
                        scale);
   else if (dtype == kF32)
     hipLaunchKernelGGL(local_corr_bwd_kernel<float>, g, blk, 0, s, static_cast<const float*>(f1),
-                       static_cast<const float*>(f2), coords, gout, g1, g2, g2fix, B, H1, W1, H2, W2, C, r,
+                       static_cast<const float*>(f2), coords, gout, g1, g2, g2fix, fix_scale, B, H1, W1, H2, W2, C, r,
                        scale);
   else
     return hipErrorInvalidValue;

@@ -244,6 +244,7 @@ __global__ __launch_bounds__(256) void local_corr_mfma_bwd_kernel(const LocalCor
   __syncthreads();
   const int rd = 2 * a.r + 1, nd = rd + 1, win = rd * rd;
   const int nkc = a.C / KC;  // <= 4 (C <= 256)
+  const float fs = a.g2fix != nullptr ? *a.fix_scale : 0.f;  // fixed-point scale (deterministic mode)
   // dF1 accumulators: MFMA 16x16x32, wave w owns channels [16w, 16w + 16) of every 64-slice,
   // 2 M-tiles of 16 queries, 4 slices -> acc1[slice][mtile]
   f32x4 acc1[4][2];
@@ -357,7 +358,7 @@ __global__ __launch_bounds__(256) void local_corr_mfma_bwd_kernel(const LocalCor
             if (a.g2fix != nullptr) {
               long long* dst = a.g2fix + (g2l - a.g2) + di;
 #pragma unroll
-              for (int j = 0; j < 2; ++j) fixed_atomic_add(dst + j * 32, acc2[i][j][e]);
+              for (int j = 0; j < 2; ++j) fixed_atomic_add(dst + j * 32, acc2[i][j][e], fs);
             } else {
               float* dst = g2l + di;
 #pragma unroll
@@ -384,17 +385,18 @@ __global__ __launch_bounds__(256) void local_corr_mfma_bwd_kernel(const LocalCor
 }
 
 __global__ __launch_bounds__(256) void fixed_to_float_kernel(const long long* __restrict__ in, float* __restrict__ out,
-                                                             long n) {
+                                                             long n, const float* __restrict__ fix_scale) {
+  const double inv = 1.0 / static_cast<double>(*fix_scale);
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
-    out[i] += static_cast<float>(static_cast<double>(in[i]) / kFixScale);
+    out[i] += static_cast<float>(static_cast<double>(in[i]) * inv);
 }
 
 }  // namespace
 
-hipError_t launch_fixed_to_float(const long long* in, float* out, long n, hipStream_t s) {
+hipError_t launch_fixed_to_float(const long long* in, float* out, long n, const float* fix_scale, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const long blocks = std::min<long>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(fixed_to_float_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, out, n);
+  hipLaunchKernelGGL(fixed_to_float_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, out, n, fix_scale);
   return hipGetLastError();
 }
 

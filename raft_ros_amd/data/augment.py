@@ -288,9 +288,16 @@ class BatchAugmentor:
         keep = (valid >= 1) & inside & (cx >= 0) & (cx < cw) & (cy >= 0) & (cy < ch)
         b = torch.arange(B, device=dev).view(B, 1, 1).expand_as(cx)
         idx = ((b * ch + cy) * cw + cx)[keep]
+        # below scale 1 several samples round onto one target pixel; the reference's numpy
+        # assignment keeps the LAST one in row-major source order, so keep the largest source
+        # index per target explicitly (a plain indexed write leaves the winner unspecified on
+        # the GPU)
+        src = (ys * Wm + xs).long()[keep]
+        win = torch.full((B * ch * cw,), -1, device=dev, dtype=torch.long).scatter_reduce(0, idx, src, "amax")
+        last = win[idx] == src
         out_f = torch.zeros(B * ch * cw, 2, device=dev)
         out_v = torch.zeros(B * ch * cw, device=dev)
-        out_f[idx] = fv.permute(0, 2, 3, 1)[keep]
+        out_f[idx[last]] = fv.permute(0, 2, 3, 1)[keep][last]
         out_v[idx] = 1.0
         return out_f.view(B, ch, cw, 2).permute(0, 3, 1, 2), out_v.view(B, ch, cw)
 

@@ -7,9 +7,12 @@ Architecture and parameter names match the reference encoders so that
   128/s2) -> 1x1 conv to ``output_dim``;
 * ``SmallEncoder``: same topology with ``BottleneckBlock`` (32, 64/s2, 96/s2).
 
-Encoders run on PyTorch-ROCm (MIOpen convs; channels-last + bf16 autocast in
-the training/benchmark path).  Passing a list/tuple ``[img1, img2]`` runs both
-frames as one batch (core/extractor.py:170-174).
+On the GPU the RAFT orchestrator runs both encoders on the hand-written HIP
+kernels of ``ops/encoder.py`` / ``csrc/encoder.hip`` (one autograd node per
+encoder, NHWC, fused norm statistics); the ``forward`` methods here are the
+module path (CPU runs, and the reference op path the GPU tests compare
+against).  Passing a list/tuple ``[img1, img2]`` runs both frames as one batch
+(core/extractor.py:170-174).
 """
 from __future__ import annotations
 

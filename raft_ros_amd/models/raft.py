@@ -138,15 +138,18 @@ class RAFT(nn.Module):
             main = torch.cuda.current_stream(raw1.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                cnet_native = encoder_native.encode(self.cnet, raw1)
+                cnet_native = encoder_native.encode(self.cnet, raw1, join_stream=main)
             fmap1, fmap2 = encoder_native.encode(self.fnet, raw1, raw2).split(raw1.shape[0], dim=0)
         else:
             with self._autocast(dev):
                 fmap1, fmap2 = self.fnet([image1, image2])
         fmap1, fmap2 = fmap1.float(), fmap2.float()
+        # the correlation keeps fp32 numerics (split-bf16 MFMA) except under bf16 AMP: the
+        # reference builds it in fp32 outside autocast in every mode (core/raft.py:102-103),
+        # so fp16 AMP and fp32 runs both get the fp32-faithful volume
+        split = not (amp and dev == "cuda" and self.amp_dtype == torch.bfloat16)
         if self.args.alternate_corr:
-            corr_fn = LocalCorrPyramid(fmap1, fmap2, radius=self.args.corr_radius,
-                                       split=not (amp and dev == "cuda" and self.amp_dtype == torch.bfloat16))
+            corr_fn = LocalCorrPyramid(fmap1, fmap2, radius=self.args.corr_radius, split=split)
         elif _arg(self.args, "query_shard", False) and not torch.is_grad_enabled():
             # inference over a process group: each rank holds the volume rows of its own query
             # pixels (parallel/query_shard.py)
@@ -155,9 +158,7 @@ class RAFT(nn.Module):
             corr_fn = ShardedCorrPyramid(fmap1, fmap2, num_levels=self.args.corr_levels,
                                          radius=self.args.corr_radius)
         else:
-            # without AMP the volume stays fp32-faithful (split bf16 MFMA), as the reference
-            # computes it in fp32 in every mode (core/raft.py:102-103)
-            corr_fn = CorrPyramid(fmap1, fmap2, radius=self.args.corr_radius, split=not bool(self.args.mixed_precision))
+            corr_fn = CorrPyramid(fmap1, fmap2, radius=self.args.corr_radius, split=split)
 
         if native:  # join the context-encoder stream (the pyramid build above overlapped it)
             main.wait_stream(side)

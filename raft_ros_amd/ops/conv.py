@@ -99,7 +99,7 @@ def conv_fwd(srcs, wt, g, N, out, bias=None, act=0, alpha=1.0, epi=EPI_STORE, ac
              h=None, z=None, out2=None, cfg: int = 0, g0=None, carry=None, out3=None, gru_cols: int = 0,
              addsrc=None, cout=None, cmask=None, cm_c0: int = 0, cm_valid: int = 0):
     """``cfg`` forces a kernel variant (0 = automatic; tests and microbenchmarks only):
-    1 generic, 8/9 v4 64x128/64x64, 20..23 v5 halo strip 64x128/128x128/128x256/256x128,
+    1 generic, 8/9 v4 64x128/64x64, 20/21 v5 halo strip 64x128/128x128 (4 waves),
     24..26 v5 with 8 waves 256x128/128x128/128x256.
 
     Data-gradient launches of the GRU can finish the gate backward in the epilogue for the

@@ -225,10 +225,11 @@ def _backward(L, P, gy, stem_rec, recs):
 
 class _EncoderFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, layout, x0, *params):
+    def forward(ctx, layout, x0, join, *params):
         y, stem_rec, recs = _forward(layout, x0, params)
         ctx.layout = layout
         ctx.params = params
+        ctx.join = join
         # records hold only tensors created here (activations, statistics coefficients)
         ctx.stem_rec, ctx.recs = stem_rec, recs
         return y
@@ -238,7 +239,19 @@ class _EncoderFn(torch.autograd.Function):
         gy = gy.contiguous().to(torch.bfloat16)
         grads = _backward(ctx.layout, ctx.params, gy, ctx.stem_rec, ctx.recs)
         ctx.stem_rec = ctx.recs = None
-        return (None, None, *grads)
+        if ctx.join is not None:
+            # the forward ran on a side stream, so autograd ran this backward there too: make
+            # the join stream (the model's main stream) wait for the parameter gradients before
+            # anything else reads them -- DDP starts a bucket's all-reduce from whichever
+            # gradient hook fires last and orders it only after THAT hook's stream, so a bucket
+            # shared with main-stream gradients must not see these still in flight
+            cur = torch.cuda.current_stream(gy.device)
+            if cur != ctx.join:
+                ctx.join.wait_stream(cur)
+                for g in grads:
+                    if g is not None:
+                        g.record_stream(ctx.join)
+        return (None, None, None, *grads)
 
 
 def _layout(enc):
@@ -252,11 +265,13 @@ def _layout(enc):
     return cached[1]
 
 
-def encode(enc, image1: torch.Tensor, image2: torch.Tensor | None = None) -> torch.Tensor:
+def encode(enc, image1: torch.Tensor, image2: torch.Tensor | None = None,
+           join_stream: torch.cuda.Stream | None = None) -> torch.Tensor:
     """Run ``enc`` natively on raw 0..255 fp32 images (``image2``: second frame of a
     paired batch).  Returns the (n, C, H/8, W/8) bf16 feature map in channels-last
-    layout (``n`` = 2B when paired)."""
+    layout (``n`` = 2B when paired).  ``join_stream``: when this runs on a side stream,
+    the stream that must see the parameter gradients complete (see ``_EncoderFn.backward``)."""
     L = _layout(enc)
     x0 = ops().enc_prep(image1.float(), image2.float() if image2 is not None else None)
-    y = _EncoderFn.apply(L, x0, *L.params)
+    y = _EncoderFn.apply(L, x0, join_stream, *L.params)
     return y.permute(0, 3, 1, 2)

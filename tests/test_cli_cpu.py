@@ -70,3 +70,20 @@ def test_demo_sequence_shape_and_motion():
     fr = demo_sequence(3, 96, 128)
     assert len(fr) == 3 and fr[0].shape == (3, 96, 128) and fr[0].dtype == torch.uint8
     assert (fr[0].float() - fr[1].float()).abs().mean() > 1.0  # frames actually move
+
+
+def test_train_refuses_gpu_ids_the_node_does_not_have(monkeypatch):
+    """Reference default --gpus 0 1 on a 1-GPU node: a clear error, not a dead rank on cuda:1."""
+    import pytest
+
+    import train
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    with pytest.raises(SystemExit, match="1 visible GPU"):
+        train.check_gpus([0, 1], ndev=1)
+    with pytest.raises(SystemExit):
+        train.check_gpus([0, 0], ndev=2)
+    train.check_gpus([0, 1], ndev=2)
+    train.check_gpus([0, 1], ndev=0)  # CPU-only host: not checked
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    train.check_gpus([0, 1], ndev=1)  # torchrun decides the ranks

@@ -94,6 +94,48 @@ def test_sparse_scatter_keeps_samples_on_rounded_positions():
     assert (f.permute(0, 2, 3, 1)[~on] == 0).all()
 
 
+def _numpy_sparse_resize(flow, valid, fx, fy):
+    """Oracle with the semantics of core/utils/augmentor.py:161-193 (resize_sparse_flow_map):
+    valid samples in row-major order, scaled and rounded, strictly-inside filter, then one
+    numpy fancy-index assignment -- duplicates resolve to the LAST sample."""
+    ht, wd = flow.shape[:2]
+    yy, xx = np.meshgrid(np.arange(ht), np.arange(wd), indexing="ij")
+    coords = np.stack([xx, yy], -1).reshape(-1, 2).astype(np.float32)
+    f = flow.reshape(-1, 2).astype(np.float32)
+    v = valid.reshape(-1) >= 1
+    c0, f0 = coords[v] * [fx, fy], f[v] * [fx, fy]
+    ht1, wd1 = int(round(ht * fy)), int(round(wd * fx))
+    xn = np.round(c0[:, 0]).astype(np.int32)
+    yn = np.round(c0[:, 1]).astype(np.int32)
+    keep = (xn > 0) & (xn < wd1) & (yn > 0) & (yn < ht1)
+    out = np.zeros([ht1, wd1, 2], dtype=np.float32)
+    ov = np.zeros([ht1, wd1], dtype=np.int32)
+    out[yn[keep], xn[keep]] = f0[keep]
+    ov[yn[keep], xn[keep]] = 1
+    return out, ov
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_sparse_downscale_duplicates_resolve_like_numpy_last_write(device):
+    """Scale < 1 (HD1K min_scale -0.5): several samples round onto one target pixel; the
+    batched scatter must keep the reference's last-write-wins winner -- on the
+    GPU too, where a plain indexed write with duplicates has no defined winner."""
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    h, w, s = 24, 32, 0.5
+    g = torch.Generator().manual_seed(7)
+    flow = torch.randn(h, w, 2, generator=g) * 3
+    valid = (torch.rand(h, w, generator=g) > 0.3).float()
+    ref_f, ref_v = _numpy_sparse_resize(flow.numpy(), valid.numpy(), s, s)
+    rh, rw = ref_f.shape[:2]
+    aug = A.BatchAugmentor([A.AugSpec((rh, rw), 0.0, 0.0, False, True)], seed=0, device=device)
+    one = lambda v: torch.tensor([v], device=device)  # noqa: E731
+    sf, sv = aug._sparse_flow(flow.permute(2, 0, 1)[None].to(device), valid[None].to(device), one(s), one(s),
+                              one(True), one(False), one(0), one(0), one(rh), one(rw), h, w)
+    assert torch.equal(sv[0].cpu(), torch.from_numpy(ref_v).float())
+    assert torch.allclose(sf[0].permute(1, 2, 0).cpu(), torch.from_numpy(ref_f), atol=1e-6)
+
+
 def test_color_jitter_identity_and_ranges():
     img = torch.rand(2, 3, 16, 16) * 255
     img = img.round()

@@ -54,8 +54,11 @@ def _worker(rank, world, port, tmpdir):
     assert _ext.is_loaded(), _ext.load_error()
     dist.init_process_group("gloo", rank=rank, world_size=world)
     model = _model(dev)
-    net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[0], bucket_cap_mb=32,
-                                                    gradient_as_bucket_view=True)
+    # the trainer's wrapper with its defaults (10 MB buckets, static graph, bucket views): the
+    # context encoder's gradients come from the side stream it ran on (models/raft.py) and
+    # share buckets with main-stream gradients
+    net = ddp.wrap_model(model, ddp.DistInfo(rank, world, 0, dev))
+    assert isinstance(net, torch.nn.parallel.DistributedDataParallel)
     i1, i2, flow, valid = _batch(dev)
     h = SHAPE[0] // world
     sl = slice(rank * h, rank * h + h)

@@ -82,10 +82,28 @@ def _spawned(rank: int, args) -> None:
     _main(args)
 
 
+def check_gpus(gpus, ndev=None) -> None:
+    """Refuse ``--gpus`` ids the node does not have (the reference default ``--gpus 0 1``,
+    train.py:229, would otherwise start a rank that dies on ``cuda:1`` of a 1-GPU box).
+    ``torch.cuda.device_count()`` does not initialise HIP, so this is safe before spawning.
+    Without a GPU (CPU runs, tests) the ids are not checked.  Under torchrun the world size,
+    not ``--gpus``, decides the ranks."""
+    if "WORLD_SIZE" in os.environ:
+        return
+    ndev = torch.cuda.device_count() if ndev is None else ndev
+    if ndev == 0:
+        return
+    bad = [g for g in gpus if not 0 <= g < ndev]
+    if bad or len(set(gpus)) != len(gpus):
+        raise SystemExit(f"train.py: --gpus {' '.join(map(str, gpus))} but this node has {ndev} visible GPU(s) "
+                         f"(ids 0..{ndev - 1}); pass e.g. --gpus {' '.join(map(str, range(min(len(gpus), ndev))))}")
+
+
 def main(argv=None):
     args = build_parser().parse_args(argv)
     if args.dataset_root:
         os.environ["RAFT_DATASET_ROOT"] = args.dataset_root
+    check_gpus(args.gpus)
     if "WORLD_SIZE" not in os.environ and len(args.gpus) > 1 and torch.cuda.is_available():
         from raft_ros_amd.parallel.ddp import spawn
 
