@@ -444,9 +444,15 @@ at::Tensor enc_apply(const at::Tensor& x, const at::Tensor& coef, bool relu_a, c
 }
 
 // returns [da0, da1 | empty, dgamma0, dbeta0, dgamma1, dbeta1] (BatchNorm kinds; empty otherwise)
-std::vector<at::Tensor> enc_norm_bwd(const at::Tensor& g, const at::Tensor& a0, const at::Tensor& c0, bool relu0,
-                                     const c10::optional<at::Tensor>& a1, const c10::optional<at::Tensor>& c1,
-                                     int64_t kind) {
+//
+// ``stage``: 0 = all three passes; 1 = reduce only, returns [part] ([B][R][4][N] fp32
+// partial sums of this rank's images); 2 = finalize + apply from ``part`` holding the
+// partials of ``b_fin`` images -- every rank's, gathered rank-major (synchronized BatchNorm:
+// parallel/sync_bn.py) -- dgamma / dbeta then come out as the sums over those b_fin images.
+std::vector<at::Tensor> enc_norm_bwd_impl(const at::Tensor& g, const at::Tensor& a0, const at::Tensor& c0, bool relu0,
+                                          const c10::optional<at::Tensor>& a1, const c10::optional<at::Tensor>& c1,
+                                          int64_t kind, int stage, const c10::optional<at::Tensor>& part_in,
+                                          int64_t b_fin) {
   check_nhwc(g, "g");
   check_nhwc(a0, "a0");
   TORCH_CHECK(a0.sizes() == g.sizes(), "a0 shape");
@@ -470,9 +476,18 @@ std::vector<at::Tensor> enc_norm_bwd(const at::Tensor& g, const at::Tensor& a0, 
   a.R = std::min(kNormChunks, std::max(1, HW / 256));
   a.kind = (int)kind;
   auto fo = g.options().dtype(at::kFloat);
-  at::Tensor part = at::empty({(long)B * a.R * 4 * N}, fo);
-  at::Tensor bcoef = at::empty({(long)B * 2 * 3 * N}, fo);
+  const long bf = stage == 2 ? (long)b_fin : (long)B;
+  TORCH_CHECK(stage != 2 || (kind == 2 && bf >= B && part_in.has_value() && part_in->defined() &&
+                             part_in->scalar_type() == at::kFloat && part_in->is_contiguous() &&
+                             part_in->numel() == bf * a.R * 4 * N),
+              "enc_norm_bwd_finish: training BatchNorm and [b_fin, R, 4, N] fp32 partials");
+  at::Tensor part = stage == 2 ? *part_in : at::empty({(long)B, (long)a.R, 4L, (long)N}, fo);
   a.part = part.data_ptr<float>();
+  if (stage == 1) {
+    check(launch_enc_norm_bwd_stages(a, 1, 0, stream()), "enc_norm_bwd_part");
+    return {part};
+  }
+  at::Tensor bcoef = at::empty({bf * 2 * 3 * N}, fo);
   a.bcoef = bcoef.data_ptr<float>();
   at::Tensor da0 = at::empty_like(g), da1 = two ? at::empty_like(g) : at::Tensor();
   a.out0 = mbf(da0);
@@ -486,8 +501,29 @@ std::vector<at::Tensor> enc_norm_bwd(const at::Tensor& g, const at::Tensor& a0, 
       a.dbeta[j] = out[3 + 2 * j].data_ptr<float>();
     }
   }
-  check(launch_enc_norm_bwd(a, stream()), "enc_norm_bwd");
+  if (stage == 2)
+    check(launch_enc_norm_bwd_stages(a, 6, (int)bf, stream()), "enc_norm_bwd_finish");
+  else
+    check(launch_enc_norm_bwd(a, stream()), "enc_norm_bwd");
   return out;
+}
+
+std::vector<at::Tensor> enc_norm_bwd(const at::Tensor& g, const at::Tensor& a0, const at::Tensor& c0, bool relu0,
+                                     const c10::optional<at::Tensor>& a1, const c10::optional<at::Tensor>& c1,
+                                     int64_t kind) {
+  return enc_norm_bwd_impl(g, a0, c0, relu0, a1, c1, kind, 0, c10::nullopt, 0);
+}
+
+at::Tensor enc_norm_bwd_part(const at::Tensor& g, const at::Tensor& a0, const at::Tensor& c0, bool relu0,
+                             const c10::optional<at::Tensor>& a1, const c10::optional<at::Tensor>& c1, int64_t kind) {
+  return enc_norm_bwd_impl(g, a0, c0, relu0, a1, c1, kind, 1, c10::nullopt, 0)[0];
+}
+
+std::vector<at::Tensor> enc_norm_bwd_finish(const at::Tensor& g, const at::Tensor& a0, const at::Tensor& c0,
+                                            bool relu0, const c10::optional<at::Tensor>& a1,
+                                            const c10::optional<at::Tensor>& c1, int64_t kind, const at::Tensor& part,
+                                            int64_t b_fin) {
+  return enc_norm_bwd_impl(g, a0, c0, relu0, a1, c1, kind, 2, part, b_fin);
 }
 
 }  // namespace raft_amd
@@ -505,6 +541,10 @@ TORCH_LIBRARY_FRAGMENT(raft_amd, m) {
       "Tensor(b!)? rvar, Tensor(c!)? nbt, float momentum, float eps, int W=0) -> Tensor");
   m.def("enc_apply(Tensor a, Tensor coef, bool relu_a, Tensor? r, Tensor? coef_r, bool relu_out) -> Tensor");
   m.def("enc_norm_bwd(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind) -> Tensor[]");
+  m.def("enc_norm_bwd_part(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind) -> Tensor");
+  m.def(
+      "enc_norm_bwd_finish(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind, Tensor part, "
+      "int b_fin) -> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
@@ -515,4 +555,6 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("enc_norm_stats", &raft_amd::enc_norm_stats);
   m.impl("enc_apply", &raft_amd::enc_apply);
   m.impl("enc_norm_bwd", &raft_amd::enc_norm_bwd);
+  m.impl("enc_norm_bwd_part", &raft_amd::enc_norm_bwd_part);
+  m.impl("enc_norm_bwd_finish", &raft_amd::enc_norm_bwd_finish);
 }

@@ -1265,15 +1265,28 @@ hipError_t launch_enc_apply(const void* a, const float* ca, bool relu_a, const v
   return hipGetLastError();
 }
 
-hipError_t launch_enc_norm_bwd(const NormBwdArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(enc_norm_bwd_reduce_kernel, dim3(a.R, a.B), dim3(256), 0, s, a);
-  RAFT_HIP_CHECK(hipGetLastError());
-  const int groups = a.kind == 1 ? a.B : 1;
-  hipLaunchKernelGGL(enc_norm_bwd_finalize_kernel, dim3(groups, (a.N + 15) / 16), dim3(256), 0, s, a);
-  RAFT_HIP_CHECK(hipGetLastError());
-  const long chunks = (long)a.B * a.HW * (a.N / 8);
-  hipLaunchKernelGGL(enc_norm_bwd_apply_kernel, dim3(grid_for(chunks)), dim3(256), 0, s, a);
-  return hipGetLastError();
+hipError_t launch_enc_norm_bwd_stages(const NormBwdArgs& a, int stages, int b_fin, hipStream_t s) {
+  if (stages & 1) {
+    hipLaunchKernelGGL(enc_norm_bwd_reduce_kernel, dim3(a.R, a.B), dim3(256), 0, s, a);
+    RAFT_HIP_CHECK(hipGetLastError());
+  }
+  if (stages & 2) {
+    // synchronized BatchNorm: the finalize runs over the partial sums of every rank's images
+    // (a.part holds b_fin images' partials, bcoef b_fin rows); the apply below uses a.B
+    NormBwdArgs f = a;
+    if (b_fin > 0) f.B = b_fin;
+    const int groups = f.kind == 1 ? f.B : 1;
+    hipLaunchKernelGGL(enc_norm_bwd_finalize_kernel, dim3(groups, (f.N + 15) / 16), dim3(256), 0, s, f);
+    RAFT_HIP_CHECK(hipGetLastError());
+  }
+  if (stages & 4) {
+    const long chunks = (long)a.B * a.HW * (a.N / 8);
+    hipLaunchKernelGGL(enc_norm_bwd_apply_kernel, dim3(grid_for(chunks)), dim3(256), 0, s, a);
+    RAFT_HIP_CHECK(hipGetLastError());
+  }
+  return hipSuccess;
 }
+
+hipError_t launch_enc_norm_bwd(const NormBwdArgs& a, hipStream_t s) { return launch_enc_norm_bwd_stages(a, 7, 0, s); }
 
 }  // namespace raft_amd

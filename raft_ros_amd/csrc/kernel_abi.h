@@ -453,5 +453,8 @@ hipError_t launch_enc_norm_finalize(const NormFinArgs& a, hipStream_t s);
 hipError_t launch_enc_apply(const void* a, const float* ca, bool relu_a, const void* r, const float* cr,
                             bool relu_out, void* out, int B, int HW, int N, hipStream_t s);
 hipError_t launch_enc_norm_bwd(const NormBwdArgs& a, hipStream_t s);
+// stages: bit 0 reduce (partials of a.B images), bit 1 finalize (over b_fin > 0 images'
+// partials when given: synchronized BatchNorm), bit 2 apply
+hipError_t launch_enc_norm_bwd_stages(const NormBwdArgs& a, int stages, int b_fin, hipStream_t s);
 }  // namespace raft_amd
 #endif

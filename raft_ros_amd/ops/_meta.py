@@ -153,6 +153,20 @@ def register() -> None:
                 f() if bn else g.new_empty((0,)), f() if bn else g.new_empty((0,)),
                 f() if bn and two else g.new_empty((0,)), f() if bn and two else g.new_empty((0,))]
 
+    @fake(lib + "enc_norm_bwd_part")
+    def _(g, a0, c0, relu0, a1, c1, kind):
+        B, H, W, N = g.shape
+        R = min(64, max(1, H * W // 256))  # csrc kNormChunks
+        return g.new_empty((B, R, 4, N), dtype=torch.float32)
+
+    @fake(lib + "enc_norm_bwd_finish")
+    def _(g, a0, c0, relu0, a1, c1, kind, part, b_fin):
+        N = g.shape[3]
+        two = a1 is not None
+        f = lambda: g.new_empty((N,), dtype=torch.float32)  # noqa: E731
+        return [torch.empty_like(g), torch.empty_like(g) if two else g.new_empty((0,)), f(), f(),
+                f() if two else g.new_empty((0,)), f() if two else g.new_empty((0,))]
+
     @fake(lib + "upflow8")
     def _(flow):
         B, _, H, W = flow.shape

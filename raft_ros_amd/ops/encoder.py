@@ -25,6 +25,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from ..parallel import sync_bn
 from ._ext import ops, use_native
 from .norm import InstanceNorm2dNHWC
 
@@ -108,10 +109,14 @@ def _stats(a, st, nd, P):
     B, H, W, N = a.shape
     k = nd["kind"]
     if k in (_BATCH_TRAIN, _BATCH_EVAL):
-        return ops().enc_norm_stats(st if k == _BATCH_TRAIN else None, B, H * W, N, k, P[nd["g"]], P[nd["bt"]],
+        Bs = B
+        if k == _BATCH_TRAIN and sync_bn.is_synced(m):  # --sync_bn: every rank's images (parallel/sync_bn.py)
+            st, Bs = sync_bn.native_norm_stats(st, m.process_group)
+        coef = ops().enc_norm_stats(st if k == _BATCH_TRAIN else None, Bs, H * W, N, k, P[nd["g"]], P[nd["bt"]],
                                     m.running_mean, m.running_var,
                                     m.num_batches_tracked if k == _BATCH_TRAIN else None,
                                     m.momentum if m.momentum is not None else 0.1, m.eps, W)
+        return coef[:B] if Bs != B else coef
     eps = getattr(m, "eps", 1e-5)
     return ops().enc_norm_stats(st, B, H * W, N, k, None, None, None, None, None, 0.0, eps, W)
 
@@ -177,6 +182,14 @@ def _norm_grads(nd, dg, dbt, grads):
         grads[nd["bt"]] = dbt
 
 
+def _norm_bwd(o, nd, g, a0, c0, relu0, a1, c1):
+    """Norm backward of one conv tail (optionally both tail branches of a block)."""
+    m = nd["module"]
+    if nd["kind"] == _BATCH_TRAIN and sync_bn.is_synced(m):
+        return sync_bn.native_norm_bwd(o, g, a0, c0, relu0, a1, c1, nd["kind"], m.process_group)
+    return o.enc_norm_bwd(g, a0, c0, relu0, a1, c1, nd["kind"])
+
+
 def _backward(L, P, gy, stem_rec, recs):
     o = ops()
     grads = [None] * len(P)
@@ -187,8 +200,8 @@ def _backward(L, P, gy, stem_rec, recs):
                          None, last_h)
     for (units, down), (ins, acts, coefs, drec, _h) in zip(reversed(L.blocks), reversed(recs)):
         dnd = down[1] if down is not None else None
-        kind = units[-1][1]["kind"]
-        r = o.enc_norm_bwd(g, acts[-1], coefs[-1], True, drec[0] if drec else None, drec[1] if drec else None, kind)
+        r = _norm_bwd(o, units[-1][1], g, acts[-1], coefs[-1], True, drec[0] if drec else None,
+                      drec[1] if drec else None)
         # both tail norms of a block share a kind (one norm_fn per encoder)
         da, dad = r[0], r[1] if drec else None
         _norm_grads(units[-1][1], r[2], r[3], grads)
@@ -202,7 +215,7 @@ def _backward(L, P, gy, stem_rec, recs):
                 dh = o.enc_conv_dgrad([da], [P[cd["w"]]], [cd["stride"]], [cd["pad"]], x.shape[1], x.shape[2],
                                       None, x)
                 pnd = units[u - 1][1]
-                r = o.enc_norm_bwd(dh, acts[u - 1], coefs[u - 1], False, None, None, pnd["kind"])
+                r = _norm_bwd(o, pnd, dh, acts[u - 1], coefs[u - 1], False, None, None)
                 da = r[0]
                 _norm_grads(pnd, r[2], r[3], grads)
             else:
@@ -217,7 +230,7 @@ def _backward(L, P, gy, stem_rec, recs):
                 g = o.enc_conv_dgrad(dys, ws, ss, ps, x.shape[1], x.shape[2], None if down is not None else g, x)
     x0, a0, c0, _h0 = stem_rec
     sc, sn = L.stem
-    r = o.enc_norm_bwd(g, a0, c0, False, None, None, sn["kind"])
+    r = _norm_bwd(o, sn, g, a0, c0, False, None, None)
     _norm_grads(sn, r[2], r[3], grads)
     _wgrad(x0, r[0], sc, P, grads, sn)
     return grads

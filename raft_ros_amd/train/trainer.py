@@ -66,6 +66,12 @@ def train(args: Namespace) -> str:
     if dev.type == "cuda" and getattr(args, "channels_last", True):
         model = model.to(memory_format=torch.channels_last)
     model.train()
+    if getattr(args, "sync_bn", False) and info.distributed:
+        # global-batch BatchNorm statistics for the context encoder (parallel/sync_bn.py); the
+        # default keeps the reference's per-replica statistics (DataParallel, train.py:138)
+        from ..parallel.sync_bn import convert_sync_bn
+
+        convert_sync_bn(model.cnet)
     if args.stage != "chairs":
         model.freeze_bn()
     net = ddp.wrap_model(model, info, bucket_cap_mb=getattr(args, "bucket_mb", 10.0),

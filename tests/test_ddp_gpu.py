@@ -138,3 +138,73 @@ def test_rccl_process_group_with_high_priority_stream(cuda):
         out = os.path.join(tmp, "r.pt")
         mp.start_processes(_rccl_worker, args=(ddp.free_port(), out), nprocs=1, start_method="spawn")
         assert torch.load(out, weights_only=True)["ok"]
+
+
+def _sync_bn_worker(rank, world, port, tmpdir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from raft_ros_amd.parallel.sync_bn import convert_sync_bn
+    from raft_ros_amd.ops import encoder as E
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cnet, img, G = _sync_bn_setup(dev)
+    convert_sync_bn(cnet)
+    h = img.shape[0] // world
+    sl = slice(rank * h, rank * h + h)
+    assert E.supported(cnet, img)
+    y = E.encode(cnet, img[sl])
+    (y.float() * G[sl]).sum().backward()
+    torch.cuda.synchronize()
+    torch.save({"y": y.detach().float().cpu(),
+                "g": {n: p.grad.float().cpu() for n, p in cnet.named_parameters() if p.grad is not None},
+                "rm": cnet.norm1.running_mean.cpu(), "rv": cnet.norm1.running_var.cpu()},
+               os.path.join(tmpdir, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _sync_bn_setup(dev):
+    from raft_ros_amd.models.extractor import BasicEncoder
+
+    torch.manual_seed(0)
+    cnet = BasicEncoder(output_dim=256, norm_fn="batch").to(dev).to(memory_format=torch.channels_last).train()
+    g = torch.Generator(device=dev).manual_seed(1)
+    img = torch.rand(4, 3, 128, 160, device=dev, generator=g) * 255
+    G = torch.randn(4, 256, 16, 20, device=dev, generator=g)
+    return cnet, img, G
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_native_encoder_sync_bn_matches_full_batch(cuda):
+    """--sync_bn on the native (HIP) encoder: 2 ranks (gloo, sharing cuda:0) each encode half of
+    the batch; the all-gathered conv statistics / norm-backward partial sums must reproduce the
+    single-process full-batch BatchNorm -- outputs, summed parameter gradients, running stats."""
+    from raft_ros_amd.ops import encoder as E
+
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_sync_bn_worker, args=(2, ddp.free_port(), tmp), nprocs=2, start_method="spawn")
+        r = [torch.load(os.path.join(tmp, f"r{k}.pt"), weights_only=True) for k in range(2)]
+    cnet, img, G = _sync_bn_setup(cuda)
+    y = E.encode(cnet, img)
+    (y.float() * G).sum().backward()
+    torch.cuda.synchronize()
+    yr = torch.cat([r[0]["y"], r[1]["y"]])
+    rel = lambda a, b: float((a - b).norm() / (b.norm() + 1e-12))  # noqa: E731
+    assert rel(yr, y.detach().float().cpu()) < 1e-2
+    top = max(float(p.grad.norm()) for p in cnet.parameters() if p.grad is not None)
+    n_checked = 0
+    for n, p in cnet.named_parameters():
+        if p.grad is None or float(p.grad.norm()) < 1e-4 * top:
+            continue
+        err = rel(r[0]["g"][n] + r[1]["g"][n], p.grad.float().cpu())
+        assert err < 5e-2, (n, err)
+        n_checked += 1
+    assert n_checked > 20
+    for k in range(2):
+        torch.testing.assert_close(r[k]["rm"], cnet.norm1.running_mean.cpu(), rtol=1e-3, atol=1e-3)
+        torch.testing.assert_close(r[k]["rv"], cnet.norm1.running_var.cpu(), rtol=1e-3, atol=1e-3)

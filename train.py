@@ -58,6 +58,9 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--deterministic", action="store_true",
                    help="bitwise-reproducible steps: torch.use_deterministic_algorithms + the native kernels' "
                         "atomic-free / fixed-point-atomic backward paths")
+    g.add_argument("--sync_bn", action="store_true",
+                   help="synchronize the context encoder's BatchNorm statistics over the DDP ranks (default: "
+                        "per-rank statistics, like the reference's DataParallel replicas)")
     g.add_argument("--ddp_bf16_grads", action="store_true",
                    help="all-reduce gradients in bf16 (DDP compression hook; halves xGMI traffic)")
     g.add_argument("--profile_dir", default=None, help="capture a torch.profiler trace of steps 5-7 here")
