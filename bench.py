@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--impl", choices=["native", "reference"], default="native")
     ap.add_argument("--small", action="store_true")
     ap.add_argument("--amp_dtype", default="bf16", choices=["bf16", "fp16"])
+    ap.add_argument("--fp32", action="store_true",
+                    help="no autocast (mixed_precision=False): the reference's default for demo.py / evaluate.py / "
+                         "the ROS node and train_standard.sh")
     ap.add_argument("--lr", type=float, default=4e-4)
     # ~10 MB buckets: the update-block gradients (12.5 MB, ready first -- batched wgrads run
     # before the encoders' backward) all-reduce over xGMI while the encoders backpropagate
@@ -151,7 +154,7 @@ def run(args):
     _ext.set_backend(args.impl)
     torch.backends.cudnn.benchmark = True
     torch.manual_seed(1234 + rank)
-    margs = Namespace(small=args.small, mixed_precision=True, amp_dtype=args.amp_dtype,
+    margs = Namespace(small=args.small, mixed_precision=not args.fp32, amp_dtype=args.amp_dtype,
                       alternate_corr=args.alternate_corr,
                       dropout=0.0, channels_last=args.impl == "native",
                       fused_update=not args.no_fused)
@@ -160,7 +163,8 @@ def run(args):
         model = model.to(memory_format=torch.channels_last)
     model.train()
     oargs = Namespace(lr=args.lr, wdecay=1e-4, epsilon=1e-8, num_steps=100000)
-    train_graph = bool(args.graph) and args.mode == "train" and args.impl == "native" and args.amp_dtype == "bf16"
+    train_graph = (bool(args.graph) and args.mode == "train" and args.impl == "native" and args.amp_dtype == "bf16"
+                   and not args.fp32)
     if distributed and not train_graph:
         ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local] if device.type == "cuda" else None,
                                                         bucket_cap_mb=args.bucket_mb,
@@ -168,7 +172,7 @@ def run(args):
     else:
         ddp = model
     optimizer, scheduler = fetch_optimizer(oargs, model, capturable=train_graph)
-    scaler = torch.amp.GradScaler("cuda", enabled=args.amp_dtype == "fp16" and device.type == "cuda")
+    scaler = torch.amp.GradScaler("cuda", enabled=args.amp_dtype == "fp16" and not args.fp32 and device.type == "cuda")
 
     H, W = args.image_size
     pool = [synthetic_batch(args.batch, H, W, seed=rank * 97 + i, device=device) for i in range(2 if H * W > 1e6 else 4)]
@@ -246,10 +250,10 @@ def run(args):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(value / (BASELINE_PAIRS_PER_SEC * world), 3)
-                            if BASELINE_PAIRS_PER_SEC and args.impl == "native" and args.mode == "train"
+                            if BASELINE_PAIRS_PER_SEC and args.impl == "native" and args.mode == "train" and not args.fp32
                             and not args.small and not args.alternate_corr and (H, W) == (368, 496)
                             and args.iters == 12 and args.batch == 8 else None),
-            "dtype": args.amp_dtype if device.type == "cuda" else "fp32",
+            "dtype": args.amp_dtype if device.type == "cuda" and not args.fp32 else "fp32",
             "data": "synthetic (textured pairs warped by known smooth flow; random-init weights)",
             "config": {
                 "model": "RAFT-small" if args.small else "RAFT-base",

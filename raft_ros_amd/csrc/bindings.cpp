@@ -43,6 +43,8 @@ hipError_t launch_gru_bwd_b(float* drh, long sd, const void* r, long sr, const v
                             hipStream_t s);
 hipError_t launch_masked_cast(const float* src, long ss, const void* mask, long sm, void* out, long so,
                               long P, int C, int Cvalid, hipStream_t s);
+hipError_t launch_split_pack(const float* src, long ss, int C, int Cpad, void* dst, long sd, int G, int c0, long P,
+                             hipStream_t s);
 hipError_t launch_pack_flow(const float* flow, void* flow8, void* motion, long smo, int B, int HW, int W,
                             int from_coords, hipStream_t s);
 hipError_t launch_apply_delta(const float* coords1, const float* delta, long sd, float* coords_out,
@@ -699,9 +701,21 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
               const c10::optional<at::Tensor>& g0, const c10::optional<at::Tensor>& carry,
               const c10::optional<at::Tensor>& out3, int64_t gru_cols, const c10::optional<at::Tensor>& addsrc,
               const c10::optional<at::Tensor>& cout, const c10::optional<at::Tensor>& cmask, int64_t cm_c0,
-              int64_t cm_valid) {
+              int64_t cm_valid, at::IntArrayRef split) {
   TORCH_CHECK(geom.size() == 7, "raft_amd conv_fwd: geom = (B, H, W, KH, KW, PH, PW)");
   ConvFwdArgs a{};
+  if (!split.empty()) {
+    // split-bf16 epilogues (kernel_abi.h ConvFwdArgs::split_g): [G_out, G_out2, S_h, S_z]
+    TORCH_CHECK(split.size() == 4 && (epi == 0 || epi == 2 || epi == 3) && split[0] > 0 && split[0] % 8 == 0,
+                "raft_amd conv_fwd: split = [G_out, G_out2, S_h, S_z] with epilogue 0, 2 or 3");
+    for (int i = 1; i < 4; ++i) TORCH_CHECK(split[i] >= 0 && split[i] % 8 == 0, "raft_amd conv_fwd: split");
+    a.split_g = (int)split[0];
+    a.split_g2 = (int)split[1];
+    a.split_h = (int)split[2];
+    a.split_z = (int)split[3];
+    TORCH_CHECK(epi != 2 || (a.split_g2 > 0 && a.split_h > 0), "raft_amd conv_fwd: split z||r needs G_out2 and S_h");
+    TORCH_CHECK(epi != 3 || (a.split_h > 0 && a.split_z > 0), "raft_amd conv_fwd: split blend needs S_h and S_z");
+  }
   a.B = geom[0]; a.H = geom[1]; a.W = geom[2]; a.KH = geom[3]; a.KW = geom[4]; a.PH = geom[5]; a.PW = geom[6];
   a.P = (long)a.B * a.H * a.W;
   a.nsrc = static_cast<int>(srcs.size());
@@ -752,7 +766,8 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
     a.out2_stride = out2->stride(0);
   }
   if (epi == 2) TORCH_CHECK(h && out2 && N % 2 == 0, "raft_amd conv_fwd: GRU z||r epilogue needs h, out2");
-  if (epi == 3) TORCH_CHECK(h && z && out2, "raft_amd conv_fwd: GRU blend epilogue needs h, z, out2");
+  if (epi == 3) TORCH_CHECK(h && z && (out2 || a.split_g > 0), "raft_amd conv_fwd: GRU blend epilogue needs h, z, out2");
+  TORCH_CHECK(a.split_g == 0 || !a.out_f32, "raft_amd conv_fwd: a split output is bf16 (its planes)");
   if (epi >= 4) {
     // fused GRU backward: fp32 gradient rows, bf16 gate tensors, fp32 carry; every operand is
     // accessed as 8 channels (16 or 32 bytes) per pixel
@@ -1017,6 +1032,25 @@ void pack_flow(const at::Tensor& flow, const at::Tensor& flow8, const c10::optio
                           from_coords ? 1 : 0, cur_stream()));
 }
 
+// fp32 (P, C) rows -> split-bf16 planes of group width G in dst (P, *) bf16 rows, channels
+// [c0, c0 + Cpad) (zero past C); see kernel_abi.h ConvFwdArgs::split_g
+void split_pack(const at::Tensor& src, const at::Tensor& dst, int64_t G, int64_t c0, int64_t Cpad) {
+  check_gpu(src, "src");
+  check_gpu(dst, "dst");
+  TORCH_CHECK(src.dim() == 2 && src.scalar_type() == at::kFloat && src.stride(1) == 1,
+              "raft_amd split_pack: src must be fp32 (P, C) rows");
+  TORCH_CHECK(dst.dim() == 2 && dst.scalar_type() == at::kBFloat16 && dst.stride(1) == 1 && dst.size(0) == src.size(0),
+              "raft_amd split_pack: dst must be bf16 (P, *) rows");
+  const long C = src.size(1);
+  TORCH_CHECK(G > 0 && c0 >= 0 && Cpad >= C, "raft_amd split_pack: G, c0, Cpad");
+  const long last = c0 + Cpad - 1;  // highest output channel: its hi-again plane must fit in the row
+  TORCH_CHECK((last / G) * 3 * G + 2 * G + last % G < dst.size(1) || dst.size(0) == 0,
+              "raft_amd split_pack: dst rows too narrow for the split planes");
+  const c10::DeviceGuard guard(src.device());
+  HIP_OK(launch_split_pack(src.data_ptr<float>(), src.stride(0), (int)C, (int)Cpad, dst.data_ptr(), dst.stride(0),
+                           (int)G, (int)c0, src.size(0), cur_stream()));
+}
+
 // coords_out = coords1 + delta[:, :2] (delta: (P, >=2) fp32 rows), flow_out = coords_out - grid
 void apply_delta(const at::Tensor& coords1, const at::Tensor& delta, const at::Tensor& coords_out,
                  const at::Tensor& flow_out) {
@@ -1113,7 +1147,8 @@ TORCH_LIBRARY(raft_amd, m) {
       "conv_fwd(Tensor[] srcs, Tensor wt, int[] geom, int N, Tensor? bias, int epi, int act, float alpha, "
       "Tensor(a!) out, int acc_c0, Tensor? mask, Tensor? h, Tensor? z, Tensor(b!)? out2, int cfg=0, "
       "Tensor? g0=None, Tensor(c!)? carry=None, Tensor(d!)? out3=None, int gru_cols=0, Tensor? addsrc=None, "
-      "Tensor(e!)? cout=None, Tensor? cmask=None, int cm_c0=0, int cm_valid=0) -> ()");
+      "Tensor(e!)? cout=None, Tensor? cmask=None, int cm_c0=0, int cm_valid=0, int[] split=[]) -> ()");
+  m.def("split_pack(Tensor src, Tensor(a!) dst, int G, int c0, int Cpad) -> ()");
   m.def("conv_wgrad(Tensor[] srcs, Tensor dy, int[] geom, int N, Tensor(a!) dw, Tensor(b!)? db, "
         "bool accumulate=True) -> ()");
   m.def("conv_wgrad_params(Tensor[] srcs, Tensor dy, int[] geom, Tensor(a!)[] wgrad, Tensor?[] bgrad, int[] segs, "
@@ -1182,6 +1217,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("gru_bwd_b", &raft_amd::gru_bwd_b);
   m.impl("masked_cast", &raft_amd::masked_cast);
   m.impl("pack_flow", &raft_amd::pack_flow);
+  m.impl("split_pack", &raft_amd::split_pack);
   m.impl("apply_delta", &raft_amd::apply_delta);
   m.impl("corr_lookup_into", &raft_amd::corr_lookup_into);
   m.impl("convex_upsample_backward_into", &raft_amd::convex_upsample_backward_into);

@@ -376,6 +376,42 @@ __device__ __forceinline__ void fwd4_issue(const Fwd4Src& src, const __amdgpu_bu
   for (int i = 0; i < BI; ++i) bload16(rw, sB + (wave * BI + i) * 512, bvoff[i], (unsigned)k0 * 2);
 }
 
+// split-bf16 planes (see ConvFwdArgs::split_g): store 8 consecutive channels [n, n + nv) of one
+// pixel row as hi / lo / hi planes of group width G; read hi + lo of 8 channels at plane offset S
+__device__ __forceinline__ void split_store8(__bf16* row, int G, int n, int nv, const float (&v)[8]) {
+  __bf16* o = row + (long)(n / G) * 3 * G + n % G;
+  bf16x8 hi, lo;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    hi[q] = static_cast<__bf16>(v[q]);
+    lo[q] = static_cast<__bf16>(v[q] - static_cast<float>(hi[q]));
+  }
+  if (nv == 8) {
+    *reinterpret_cast<bf16x8*>(o) = hi;
+    *reinterpret_cast<bf16x8*>(o + G) = lo;
+    *reinterpret_cast<bf16x8*>(o + 2 * G) = hi;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < nv) {
+        o[q] = hi[q];
+        o[G + q] = lo[q];
+        o[2 * G + q] = hi[q];
+      }
+  }
+}
+
+__device__ __forceinline__ void load8(const __bf16* row, int S, float (&x)[8]) {
+  const bf16x8 hv = *reinterpret_cast<const bf16x8*>(row);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) x[q] = static_cast<float>(hv[q]);
+  if (S > 0) {
+    const bf16x8 lv = *reinterpret_cast<const bf16x8*>(row + S);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] += static_cast<float>(lv[q]);
+  }
+}
+
 // Shared epilogue of the forward kernels: the fp32 accumulators go through an LDS tile
 // (et, BM x (BN+4) floats) so each thread finishes 8 consecutive output channels of one
 // pixel with 16-byte accesses; applies alpha/bias and the fused epilogue selected by a.epi.
@@ -498,7 +534,9 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
       if (a.act == 1)
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
-      if (a.out_f32) {
+      if (a.split_g > 0 && !a.out_f32) {
+        split_store8(static_cast<__bf16*>(a.out) + p * a.out_stride, a.split_g, n, nv, v);
+      } else if (a.out_f32) {
         float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
         if (nv == 8 && (a.out_stride & 3) == 0) {
           *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
@@ -558,6 +596,32 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
             if (q < nv) o[q] = static_cast<__bf16>(accum ? static_cast<float>(o[q]) + v[q] : v[q]);
         }
       }
+    } else if (epi == 2 && a.split_g > 0) {
+      // split mode: sigmoid in fp32, r * h from the fp32-faithful h (hi + lo planes)
+      const int C = Nn >> 1;
+      float sg[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) sg[q] = sigmoidf_(v[q]);
+      split_store8(static_cast<__bf16*>(a.out) + p * a.out_stride, a.split_g, n, 8, sg);
+      if (n >= C) {
+        float hv[8];
+        load8(a.h + p * a.h_stride + (n - C), a.split_h, hv);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) hv[q] *= sg[q];
+        split_store8(a.out2 + p * a.out2_stride, a.split_g2, n - C, 8, hv);
+      }
+    } else if (epi == 3 && a.split_g > 0) {
+      float zv[8], hv[8], hn[8];
+      load8(a.z + p * a.z_stride + n, a.split_z, zv);
+      load8(a.h + p * a.h_stride + n, a.split_h, hv);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float qq = tanhf_(v[q]);
+        hn[q] = (1.f - zv[q]) * hv[q] + zv[q] * qq;
+        v[q] = qq;
+      }
+      split_store8(static_cast<__bf16*>(a.out) + p * a.out_stride, a.split_g, n, 8, hn);
+      if (a.out2) split_store8(a.out2 + p * a.out2_stride, a.split_g2 > 0 ? a.split_g2 : a.split_g, n, 8, v);
     } else if (epi == 2) {
       const int C = Nn >> 1;
       bf16x8 sg;
@@ -1519,7 +1583,8 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   for (int i = 0; i < a.nsrc; ++i) maxbytes = std::max(maxbytes, a.P * a.src[i].stride * 2);
   const bool dma_ok = (uniform || a.nsrc == 1) && maxbytes < (1L << 31) && (long)a.N * a.Kpad * 2 < (1L << 31);
   if (!dma_ok || cfg == 1) {
-    if (a.epi >= 4) return hipErrorInvalidValue;  // the fused GRU epilogues live in the v4/v5 kernels
+    // the fused GRU epilogues and the split-bf16 stores live in the v4/v5 kernels
+    if (a.epi >= 4 || a.split_g > 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL((conv_fwd_kernel<64, 64>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
     return hipGetLastError();
   }

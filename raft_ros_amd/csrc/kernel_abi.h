@@ -98,6 +98,17 @@ struct ConvFwdArgs {
   long cmask_stride;
   int cm_c0, cm_valid;
   int cfg;  // kernel variant: 0 = automatic, otherwise forced (tests / microbenchmarks)
+  // split-bf16 ("fp32-faithful") mode of epilogues 0 / 2 / 3 (inference without AMP): a bf16
+  // output value x is stored as three planes hi = bf16(x), lo = bf16(x - hi), hi again, in
+  // groups of G channels: channel n of an output lives at (n / G) * 3G + plane * G + n % G.
+  // A consumer conv reads a group as ONE source of 3G channels [hi | lo | hi] against packed
+  // weights [W_hi | W_hi | W_lo], so its bf16 MFMAs compute x_hi W_hi + x_lo W_hi + x_hi W_lo
+  // (fp32 accumulate): the fp32 product up to the dropped x_lo * W_lo term (~2^-16 relative).
+  // Epilogue operands read from such tensors (h, z) add their hi and lo planes.
+  int split_g;   // > 0: out is split with group width G = split_g
+  int split_g2;  // > 0: out2 is split with group width split_g2
+  int split_h;   // > 0: h is split; its lo plane is split_h channels after the hi plane
+  int split_z;   // > 0: z is split (lo plane offset)
 };
 
 struct ConvWgradArgs {

@@ -117,9 +117,34 @@ __global__ __launch_bounds__(256) void apply_delta_kernel(const float* __restric
   flow_out[i1] = cy - (float)y;
 }
 
+// fp32 rows -> split-bf16 planes (kernel_abi.h ConvFwdArgs::split_g): channel c of src row p
+// (zero for C <= c < Cpad) goes to output channel n = c0 + c of a group-G split row of dst
+__global__ __launch_bounds__(256) void split_pack_kernel(const float* __restrict__ src, long ss, int C, int Cpad,
+                                                         __bf16* __restrict__ dst, long sd, int G, int c0, long P) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= P * Cpad) return;
+  const long p = i / Cpad;
+  const int c = (int)(i - p * Cpad);
+  const float x = c < C ? src[p * ss + c] : 0.f;
+  const __bf16 hi = static_cast<__bf16>(x), lo = static_cast<__bf16>(x - static_cast<float>(hi));
+  const int n = c0 + c;
+  __bf16* o = dst + p * sd + (long)(n / G) * 3 * G + n % G;
+  o[0] = hi;
+  o[G] = lo;
+  o[2 * G] = hi;
+}
+
 inline dim3 grid1(long n) { return dim3((unsigned)((n + 255) / 256)); }
 
 }  // namespace
+
+hipError_t launch_split_pack(const float* src, long ss, int C, int Cpad, void* dst, long sd, int G, int c0, long P,
+                             hipStream_t s) {
+  if (P * Cpad == 0) return hipSuccess;
+  hipLaunchKernelGGL(split_pack_kernel, grid1(P * Cpad), dim3(256), 0, s, src, ss, C, Cpad, static_cast<__bf16*>(dst),
+                     sd, G, c0, P);
+  return hipGetLastError();
+}
 
 hipError_t launch_gru_bwd_a(const float* dH, long sdh, const void* z, long sz, const void* q, long sq,
                             const void* h, long sh, void* dq, long sdq, void* dz, long sdz, float* carry,

@@ -178,6 +178,8 @@ class RAFT(nn.Module):
         flow_up = None
         if self._use_fused(image1, amp):
             return self._forward_fused(corr_fn, net, inp, coords0, coords1, iters, test_mode)
+        if self._use_split(image1, amp):
+            return self._forward_split(corr_fn, net, inp, coords0, coords1, iters, test_mode)
         for it in range(iters):
             coords1 = coords1.detach()
             corr = corr_fn(coords1, out_dtype=corr_dtype)
@@ -214,6 +216,31 @@ class RAFT(nn.Module):
         return (amp and self.amp_dtype == torch.bfloat16 and _arg(self.args, "fused_update", True)
                 and (update_fused.supported(self.update_block) or update_fused_small.supported(self.update_block))
                 and use_native(image1))
+
+    def _use_split(self, image1, amp: bool) -> bool:
+        """fp32 inference (no AMP, no autograd) on the fused HIP step in split-bf16 mode."""
+        return (not amp and not torch.is_grad_enabled() and _arg(self.args, "fused_update", True)
+                and update_fused.supported(self.update_block) and use_native(image1))
+
+    def _forward_split(self, corr_fn, net, inp, coords0, coords1, iters: int, test_mode: bool):
+        """fp32-faithful refinement loop (ops/update_fused.py SplitBasicUpdate): same math as
+        the module loop above, every conv on the hand-written kernels."""
+        dense = isinstance(corr_fn, CorrPyramid)
+        upd = update_fused.SplitBasicUpdate(self.update_block, inp, iters, pyramid=corr_fn.state if dense else None)
+        flow_predictions = []
+        flow_up = None
+        for t in range(iters):
+            up = not test_mode or t == iters - 1
+            corr = None
+            if not dense:
+                c = corr_fn(coords1, out_dtype=torch.float32)
+                corr = c.permute(0, 2, 3, 1).reshape(-1, c.shape[1])
+            _, flow_up, coords1 = upd.step(t, net if t == 0 else None, coords1, coords0, corr=corr, upsample=up)
+            if up:
+                flow_predictions.append(flow_up)
+        if test_mode:
+            return coords1 - coords0, flow_up
+        return flow_predictions
 
     def _forward_fused(self, corr_fn, net, inp, coords0, coords1, iters: int, test_mode: bool):
         """Refinement loop on the fused HIP step (raft_ros_amd/ops/update_fused.py): lookup,

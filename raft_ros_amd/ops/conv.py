@@ -97,7 +97,7 @@ EPI_STORE, EPI_GRAD, EPI_GRU_ZR, EPI_GRU_Q, EPI_GRU_BWD_A, EPI_GRU_BWD_B, EPI_GR
 
 def conv_fwd(srcs, wt, g, N, out, bias=None, act=0, alpha=1.0, epi=EPI_STORE, acc_c0=1 << 30, mask=None,
              h=None, z=None, out2=None, cfg: int = 0, g0=None, carry=None, out3=None, gru_cols: int = 0,
-             addsrc=None, cout=None, cmask=None, cm_c0: int = 0, cm_valid: int = 0):
+             addsrc=None, cout=None, cmask=None, cm_c0: int = 0, cm_valid: int = 0, split=None):
     """``cfg`` forces a kernel variant (0 = automatic; tests and microbenchmarks only):
     1 generic, 8/9 v4 64x128/64x64, 20/21 v5 halo strip 64x128/128x128 (4 waves),
     24..26 v5 with 8 waves 256x128/128x128/128x256.
@@ -109,9 +109,12 @@ def conv_fwd(srcs, wt, g, N, out, bias=None, act=0, alpha=1.0, epi=EPI_STORE, ac
         (+ ``addsrc``, an incoming bf16 gradient);
       EPI_GRU_BWD_B: g = d(r h): out3 = dr = g h r (1 - r), out = carry + g r; g0 = r, h;
       EPI_GRU_BWD_LAST: g = out + acc: [0, gru_cols) -> bf16 out3, [gru_cols, cm_c0) -> out,
-        [cm_c0, N) -> bf16 cout = g where cmask > 0 (zero past cm_valid)."""
+        [cm_c0, N) -> bf16 cout = g where cmask > 0 (zero past cm_valid).
+
+    ``split = (G_out, G_out2, S_h, S_z)``: split-bf16 (fp32-faithful) epilogues 0 / 2 / 3, see
+    ``split_pack`` and csrc/kernel_abi.h ``ConvFwdArgs::split_g``."""
     ops().conv_fwd(list(srcs), wt, g, N, bias, epi, act, alpha, out, acc_c0, mask, h, z, out2, cfg, g0, carry,
-                   out3, gru_cols, addsrc, cout, cmask, cm_c0, cm_valid)
+                   out3, gru_cols, addsrc, cout, cmask, cm_c0, cm_valid, list(split) if split else [])
     return out
 
 
@@ -131,6 +134,52 @@ def conv_wgrad_params(srcs, dy, g, wgrads, bgrads, segments, scale: float = 1.0,
     every refinement iteration of a batched update-block weight gradient."""
     ops().conv_wgrad_params(list(srcs), dy, g, list(wgrads), list(bgrads), flat_segments(segments), scale,
                             accumulate)
+
+
+def split_planes(n: int, G: int) -> int:
+    """Channels of a split-bf16 row holding ``n`` channels in groups of ``G`` (hi, lo, hi planes)."""
+    return -(-n // G) * 3 * G
+
+
+def split_pack(src: torch.Tensor, dst: torch.Tensor, G: int, c0: int = 0, cpad: Optional[int] = None):
+    """fp32 (P, C) rows -> split-bf16 planes (hi, lo, hi) of group width ``G`` in ``dst`` at
+    output channels [c0, c0 + cpad) (zeros past C)."""
+    ops().split_pack(src, dst, G, c0, cpad if cpad is not None else src.shape[1])
+    return dst
+
+
+def pack_weights_split(weights, biases, source_segments, scale: float = 1.0):
+    """Forward weights of a conv over split-bf16 operands (no data-gradient operand).
+
+    ``source_segments``: one list of (real, padded) segments per SOURCE tensor (a source is one
+    split operand [hi | lo | hi] of its padded width).  The packed K runs over each source's
+    planes against [W_hi | W_hi | W_lo], so x_hi W_hi + x_lo W_hi + x_hi W_lo is one GEMM."""
+    w = torch.cat([t.detach() for t in weights], 0).float() * scale
+    parts, c = [], 0
+    for segs in source_segments:
+        r = sum(rr for rr, _ in segs)
+        ws = w[:, c:c + r]
+        hi = ws.to(torch.bfloat16).float()
+        parts += [hi, hi, ws - hi]
+        c += r
+    assert c == w.shape[1], (c, w.shape)
+    b = [None if t is None else t.detach().float() * scale for t in biases]
+    wf, _, bias = pack_weights([torch.cat(parts, 1)], [torch.cat(b) if all(x is not None for x in b) else None],
+                               split_segments_by_source(source_segments), 1.0, dgrad=False)
+    return wf, bias
+
+
+def split_segments_by_source(source_segments) -> List[Tuple[int, int]]:
+    """Segments of the expanded weight [W_hi | W_hi | W_lo] per source, in K order (every
+    source's (real, padded) channel groups appear three times: its hi, lo and hi planes)."""
+    out: List[Tuple[int, int]] = []
+    for segs in source_segments:
+        for r, p in list(segs) * 3:
+            if out and r == p and out[-1][0] == out[-1][1]:  # unpadded neighbours merge (<= 3 segments)
+                out[-1] = (out[-1][0] + r, out[-1][1] + p)
+            else:
+                out.append((r, p))
+    return out
 
 
 def pack_weights(weights, biases, segments, scale: float = 1.0, dgrad: bool = True):

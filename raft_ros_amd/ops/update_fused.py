@@ -513,3 +513,111 @@ def supported(block) -> bool:
     from ..models.update import BasicUpdateBlock
 
     return isinstance(block, BasicUpdateBlock)
+
+
+# ------------------------------------------------------------------ fp32-faithful inference
+# Without AMP (the reference's default for demo.py / evaluate.py / the ROS node) the
+# refinement step runs on the same HIP kernels in split-bf16 mode: every activation is
+# stored as hi / lo / hi bf16 planes and every conv packs [W_hi | W_hi | W_lo], so each
+# bf16 MFMA GEMM computes x_hi W_hi + x_lo W_hi + x_hi W_lo with fp32 accumulation -- the
+# fp32 product up to the dropped x_lo W_lo term (~2^-16 relative); gates, GRU blend and
+# coordinates stay fp32 (csrc/kernel_abi.h ConvFwdArgs::split_g).  Inference only.
+
+# name -> input segments per SOURCE operand (each a split [hi | lo | hi] tensor)
+_SPLIT_SOURCES = {
+    "convc1": [[(324, CORR_PAD)]],
+    "convc2": [[(256, 256)]],
+    "convf1": [[(2, 8)]],
+    "convf2": [[(128, 128)]],
+    "conv": [[(256, 256)]],
+    "zr1": [[(128, 128)]] * 3,
+    "q1": [[(128, 128)]] * 3,
+    "zr2": [[(128, 128)]] * 3,
+    "q2": [[(128, 128)]] * 3,
+    "heads": [[(128, 128)]],
+    "fh2": [[(256, 256)]],
+    "mask2": [[(256, 256)]],
+}
+
+
+class SplitBasicUpdate:
+    """Per-forward driver of the fp32-faithful (split-bf16) fused refinement step."""
+
+    def __init__(self, block, inp: torch.Tensor, iters: int, pyramid=None):
+        B, _, H, W = inp.shape
+        self.dims = (B, H, W)
+        self.P = P = B * H * W
+        self.pyr = pyramid
+        dev = inp.device
+        self.wf, self.bias = {}, {}
+        for name, mods, _, scale, _ in _LAYERS:
+            ms = mods(block)
+            self.wf[name], self.bias[name] = C.pack_weights_split([m.weight for m in ms], [m.bias for m in ms],
+                                                                  _SPLIT_SOURCES[name], scale)
+        bf = torch.bfloat16
+        e = lambda n: torch.empty(P, n, device=dev, dtype=bf)  # noqa: E731
+        self.inp = C.split_pack(_pm(inp.float()), e(384), HID)
+        self.h = [e(384), e(384), e(384)]  # h (in), h1, h (out) ping-pong
+        self.corr, self.flow8, self.motion = e(3 * CORR_PAD), e(24), e(384)
+        self.c1, self.cf, self.f1 = e(768), e(768), e(384)
+        self.zr, self.rh, self.hd = e(768), e(384), e(1536)
+        self.delta = torch.empty(P, 8, device=dev, dtype=torch.float32)
+        self.mask = torch.empty(P, 576, device=dev, dtype=torch.float32)
+
+    def geom(self, kh, kw):
+        B, H, W = self.dims
+        return C.geom(B, H, W, kh, kw, kh // 2, kw // 2)
+
+    def step(self, t: int, net, coords1, coords0, corr=None, upsample: bool = True):
+        """-> (net (B, 128, H, W) fp32 channels-last, flow_up or None, coords1 after the update).
+        ``corr``: (P, >=324) fp32 lookup rows (local correlation); else the dense pyramid."""
+        B, H, W = self.dims
+        P, g, k = self.P, self.geom, ops()
+        h0 = self.h[0]
+        if t == 0 or net is not None:
+            C.split_pack(_pm(net.float()), h0, HID)
+        if corr is None:
+            st = self.pyr
+            corr = k.corr_lookup(st.levels, coords1.contiguous(), st.radius, torch.float32, CORR_PAD).view(P, CORR_PAD)
+        C.split_pack(corr, self.corr, CORR_PAD, 0, CORR_PAD)
+        flow = (coords1 - coords0).permute(0, 2, 3, 1).reshape(P, 2).contiguous()
+        C.split_pack(flow, self.flow8, 8, 0, 8)
+        C.split_pack(flow, self.motion, HID, 126, 2)
+        S1 = lambda G: [G, 0, 0, 0]  # noqa: E731
+        C.conv_fwd([self.flow8], self.wf["convf1"], g(7, 7), 128, self.f1, bias=self.bias["convf1"], act=1,
+                   split=S1(128))
+        C.conv_fwd([self.f1], self.wf["convf2"], g(3, 3), 64, self.cf[:, 192:], bias=self.bias["convf2"], act=1,
+                   split=S1(256))
+        C.conv_fwd([self.corr], self.wf["convc1"], g(1, 1), 256, self.c1, bias=self.bias["convc1"], act=1,
+                   split=S1(256))
+        C.conv_fwd([self.c1], self.wf["convc2"], g(3, 3), 192, self.cf, bias=self.bias["convc2"], act=1,
+                   split=S1(256))
+        C.conv_fwd([self.cf], self.wf["conv"], g(3, 3), 126, self.motion, bias=self.bias["conv"], act=1,
+                   split=S1(128))
+        h = h0
+        for stage, (kh, kw) in ((1, (1, 5)), (2, (5, 1))):
+            C.conv_fwd([h, self.inp, self.motion], self.wf[f"zr{stage}"], g(kh, kw), 2 * HID, self.zr,
+                       bias=self.bias[f"zr{stage}"], epi=C.EPI_GRU_ZR, h=h, out2=self.rh, split=[HID, HID, HID, 0])
+            hn = self.h[1] if stage == 1 else self.h[2]
+            C.conv_fwd([self.rh, self.inp, self.motion], self.wf[f"q{stage}"], g(kh, kw), HID, hn,
+                       bias=self.bias[f"q{stage}"], epi=C.EPI_GRU_Q, h=h, z=self.zr, split=[HID, 0, HID, HID])
+            h = hn
+        self.h[0], self.h[2] = self.h[2], self.h[0]  # the next step's input
+        nh = 512 if upsample else 256
+        C.conv_fwd([h], self.wf["heads"][:nh], g(3, 3), nh, self.hd, bias=self.bias["heads"][:nh], act=1,
+                   split=S1(256))
+        C.conv_fwd([self.hd[:, :768]], self.wf["fh2"], g(3, 3), 2, self.delta, bias=self.bias["fh2"])
+        coords_out = torch.empty_like(coords1)
+        flow_lo = torch.empty_like(coords1)
+        k.apply_delta(coords1, self.delta, coords_out, flow_lo)
+        flow_up = None
+        if upsample:
+            C.conv_fwd([self.hd[:, 768:]], self.wf["mask2"], g(1, 1), 576, self.mask, bias=self.bias["mask2"])
+            flow_up = k.convex_upsample(flow_lo, _nchw(self.mask, B, H, W))
+        return None, flow_up, coords_out
+
+    def net(self) -> torch.Tensor:
+        """The current hidden state as fp32 (B, 128, H, W) (hi + lo planes)."""
+        B, H, W = self.dims
+        h = self.h[0]
+        return _nchw((h[:, :HID].float() + h[:, HID:2 * HID].float()), B, H, W)

@@ -313,3 +313,77 @@ def test_gru_backward_epilogues_match_unfused(cuda, cfg):
     assert torch.equal(dnet, Gp[:, :HID].bfloat16())
     assert torch.equal(Gf[:, HID:2 * HID], Gp[:, HID:2 * HID])
     assert torch.equal(dmo, dmo_r)
+
+
+def _split_read(buf, G, n):
+    """hi + lo planes of channels [0, n) of a group-G split row buffer -> fp32 (P, n)."""
+    parts = []
+    for g0 in range(0, n, G):
+        base = (g0 // G) * 3 * G
+        w = min(G, n - g0)
+        parts.append(buf[:, base:base + w].float() + buf[:, base + G:base + G + w].float())
+    return torch.cat(parts, 1)
+
+
+@pytest.mark.parametrize("segs,cout,kh,kw,act,G", [
+    ([(256, 256)], 192, 3, 3, 1, 256),   # convc2 into a 256-wide group
+    ([(2, 8)], 128, 7, 7, 1, 128),       # convf1 on the padded flow operand
+    ([(324, 328)], 256, 1, 1, 1, 256),   # convc1 on the correlation features
+    ([(128, 128)], 512, 3, 3, 1, 256),   # the fused heads conv, two 256-groups
+])
+def test_split_conv_is_fp32_faithful(cuda, segs, cout, kh, kw, act, G):
+    """Split-bf16 mode (fp32 inference): a conv over [hi | lo | hi] operands against
+    [W_hi | W_hi | W_lo] equals the fp32 conv to ~1e-5 relative (vs ~4e-3 for plain bf16)."""
+    torch.manual_seed(0)
+    B, H, W = 2, 13, 19
+    P = B * H * W
+    cin = sum(r for r, _ in segs)
+    cpad = sum(p for _, p in segs)
+    x = torch.randn(B, cin, H, W, device=cuda)
+    w = torch.randn(cout, cin, kh, kw, device=cuda) / (cin * kh * kw) ** 0.5
+    bias = torch.randn(cout, device=cuda)
+    ref = F.conv2d(x, w, bias, padding=(kh // 2, kw // 2))
+    if act:
+        ref = F.relu(ref)
+    xs = torch.zeros(P, 3 * cpad, device=cuda, dtype=torch.bfloat16)
+    C.split_pack(x.permute(0, 2, 3, 1).reshape(P, cin).contiguous(), xs, cpad, 0, cpad)
+    wf, b = C.pack_weights_split([w], [bias], [segs])
+    out = torch.zeros(P, C.split_planes(cout, G), device=cuda, dtype=torch.bfloat16)
+    C.conv_fwd([xs], wf, C.geom(B, H, W, kh, kw, kh // 2, kw // 2), cout, out, bias=b, act=act, split=[G, 0, 0, 0])
+    got = _from_pm(_split_read(out, G, cout), B, H, W)
+    err = _rel(got, ref)
+    assert err < 3e-5, err
+
+
+def test_split_gru_stage_is_fp32_faithful(cuda):
+    """One SepConvGRU stage (z||r 1x5 with sigmoid / r*h epilogue, q 1x5 with tanh + blend)
+    in split-bf16 mode vs the fp32 module math (core/update.py:33-60)."""
+    torch.manual_seed(1)
+    B, H, W, Hd = 2, 11, 23, 128
+    P = B * H * W
+    h, inp, mo = (torch.randn(B, Hd, H, W, device=cuda) * s for s in (0.5, 1.0, 1.0))
+    wz, wr, wq = (torch.randn(Hd, 3 * Hd, 1, 5, device=cuda) * 0.03 for _ in range(3))
+    bz, br, bq = (torch.randn(Hd, device=cuda) * 0.1 for _ in range(3))
+    hx = torch.cat([h, inp, mo], 1)
+    z = torch.sigmoid(F.conv2d(hx, wz, bz, padding=(0, 2)))
+    r = torch.sigmoid(F.conv2d(hx, wr, br, padding=(0, 2)))
+    q = torch.tanh(F.conv2d(torch.cat([r * h, inp, mo], 1), wq, bq, padding=(0, 2)))
+    ref = (1 - z) * h + z * q
+
+    def sp(t):
+        buf = torch.empty(P, 3 * Hd, device=cuda, dtype=torch.bfloat16)
+        return C.split_pack(t.permute(0, 2, 3, 1).reshape(P, Hd).contiguous(), buf, Hd)
+
+    hs, ins, ms = sp(h), sp(inp), sp(mo)
+    src = [[(Hd, Hd)]] * 3
+    wzr, bzr = C.pack_weights_split([wz, wr], [bz, br], src)
+    wqp, bqp = C.pack_weights_split([wq], [bq], src)
+    g = C.geom(B, H, W, 1, 5, 0, 2)
+    zr = torch.empty(P, 6 * Hd, device=cuda, dtype=torch.bfloat16)
+    rh = torch.empty(P, 3 * Hd, device=cuda, dtype=torch.bfloat16)
+    hn = torch.empty(P, 3 * Hd, device=cuda, dtype=torch.bfloat16)
+    C.conv_fwd([hs, ins, ms], wzr, g, 2 * Hd, zr, bias=bzr, epi=C.EPI_GRU_ZR, h=hs, out2=rh, split=[Hd, Hd, Hd, 0])
+    C.conv_fwd([rh, ins, ms], wqp, g, Hd, hn, bias=bqp, epi=C.EPI_GRU_Q, h=hs, z=zr, split=[Hd, 0, Hd, Hd])
+    got = _from_pm(_split_read(hn, Hd, Hd), B, H, W)
+    assert (got - ref).abs().max().item() < 5e-5, (got - ref).abs().max().item()
+    assert _rel(_from_pm(_split_read(zr, Hd, 2 * Hd), B, H, W), torch.cat([z, r], 1)) < 3e-5
