@@ -7,7 +7,10 @@
 #include <c10/hip/HIPStream.h>
 
 #include <algorithm>
+#include <array>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -83,6 +86,24 @@ void run_conv(EncConvArgs& a, int rows, const at::TensorOptions& o) {
     check(launch_enc_conv(a, blocks, stream()), "enc_conv");
 }
 
+// Decode / packing tables too deep for the kernel arguments (the split-bf16 layout's 3x
+// channels): one device copy per conv geometry, built on first use (so a HIP-graph capture
+// must follow a warm-up forward, as GraphedRAFT's does).
+const int* device_tables(const std::vector<int>& tab, const std::vector<int>& ptab, std::array<int, 5> key,
+                         const at::TensorOptions& o) {
+  static std::map<std::array<int, 5>, at::Tensor> cache;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it == cache.end()) {
+    std::vector<int> both(tab);
+    both.insert(both.end(), ptab.begin(), ptab.end());
+    at::Tensor host = at::from_blob(both.data(), {(long)both.size()}, at::TensorOptions().dtype(at::kInt)).clone();
+    it = cache.emplace(key, host.to(o.dtype(at::kInt))).first;
+  }
+  return it->second.data_ptr<int>();
+}
+
 void init_args(EncConvArgs& a) {
   std::memset(&a, 0, sizeof(a));
   for (int i = 0; i < kEncTab; ++i) a.tab[i] = a.ptab[i] = -1;
@@ -93,7 +114,7 @@ void init_args(EncConvArgs& a) {
 // y[B,Ho,Wo,N] = conv(x[B,H,W,Cx], w[N,Cin,KH,KW]) + bias; stats [B, T, 2, N] (column sum, M2 per 128-pixel tile)
 std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::Tensor& w,
                                                 const c10::optional<at::Tensor>& bias, int64_t stride, int64_t pad,
-                                                bool want_stats) {
+                                                bool want_stats, bool split) {
   check_nhwc(x, "x");
   check_w(w, "w");
   const int B = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), Cx = (int)x.size(3);
@@ -106,25 +127,35 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
   a.src[0] = {cbf(x), Cx, Cx, H, W, (int)stride};
   a.B = B;
   a.N = N;
+  std::vector<int> tab(kEncTabMax, -1), ptab(kEncTabMax, -1);
   int e = 0;
   for (int ky = 0; ky < KH; ++ky)
     for (int kx = 0; kx < KW; ++kx)
       for (int c = 0; c < Cx; c += 8) {
-        TORCH_CHECK(e < kEncTab, "conv too deep for the decode table");
-        a.tab[e] = enc_tab_entry(ky - (int)pad, kx - (int)pad, 0, c);
-        a.ptab[e] = enc_ptab_entry(0, ky, kx, c);
+        TORCH_CHECK(e < kEncTabMax, "conv too deep for the decode table");
+        tab[e] = enc_tab_entry(ky - (int)pad, kx - (int)pad, 0, c);
+        ptab[e] = enc_ptab_entry(0, ky, kx, c);
         ++e;
       }
   const int K = e * 8, Kpad = round_up(K, 64);
-  TORCH_CHECK(Kpad / 8 <= kEncTab, "conv too deep for the decode table");
+  TORCH_CHECK(Kpad / 8 <= kEncTabMax, "conv too deep for the decode table");
+  if (Kpad / 8 <= kEncTab) {
+    std::copy(tab.begin(), tab.begin() + kEncTab, a.tab);
+    std::copy(ptab.begin(), ptab.begin() + kEncTab, a.ptab);
+  } else {
+    const int* dt = device_tables(tab, ptab, {x.get_device(), KH, KW, (int)pad, Cx}, x.options());
+    a.tab_ptr = dt;
+    a.ptab_ptr = dt + kEncTabMax;
+  }
   a.cls[0] = EncClass{0, Ho, Wo, 0, 0, K, Kpad, 0, 0, 0};
   a.ncls = 1;
-  at::Tensor y = at::empty({B, Ho, Wo, N}, x.options());
+  at::Tensor y = at::empty({B, Ho, Wo, split ? 3 * N : N}, x.options());
   a.Ho = Ho;
   a.Wo = Wo;
   a.os = 1;
   a.out = mbf(y);
-  a.out_stride = N;
+  a.out_stride = split ? 3 * N : N;
+  a.split = split ? 1 : 0;
   at::Tensor b;
   if (bias.has_value() && bias->defined()) {
     b = bias->to(at::kFloat).contiguous();
@@ -345,7 +376,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
 }
 
 // [img0; img1] (fp32 0..255, [B,3,H,W] any strides) -> [nimg, H, W, 8] bf16 in [-1, 1]
-at::Tensor enc_prep(const at::Tensor& img0, const c10::optional<at::Tensor>& img1) {
+at::Tensor enc_prep(const at::Tensor& img0, const c10::optional<at::Tensor>& img1, bool split) {
   TORCH_CHECK(img0.is_cuda() && img0.scalar_type() == at::kFloat && img0.dim() == 4 && img0.size(1) == 3,
               "images: fp32 [B, 3, H, W]");
   const int B = (int)img0.size(0), H = (int)img0.size(2), W = (int)img0.size(3);
@@ -356,10 +387,10 @@ at::Tensor enc_prep(const at::Tensor& img0, const c10::optional<at::Tensor>& img
                 "paired images must match");
     nimg = 2 * B;
   }
-  at::Tensor out = at::empty({nimg, H, W, 8}, img0.options().dtype(at::kBFloat16));
+  at::Tensor out = at::empty({nimg, H, W, split ? 24 : 8}, img0.options().dtype(at::kBFloat16));
   long st[4] = {img0.stride(0), img0.stride(1), img0.stride(2), img0.stride(3)};
   check(launch_enc_prep(img0.data_ptr<float>(), nimg > B ? img1->data_ptr<float>() : nullptr, st, B, H, W, nimg,
-                        out.data_ptr(), stream()),
+                        out.data_ptr(), split ? 1 : 0, stream()),
         "enc_prep");
   return out;
 }
@@ -421,9 +452,10 @@ at::Tensor enc_norm_stats(const c10::optional<at::Tensor>& stats, int64_t B, int
 }
 
 at::Tensor enc_apply(const at::Tensor& x, const at::Tensor& coef, bool relu_a, const c10::optional<at::Tensor>& r,
-                     const c10::optional<at::Tensor>& coef_r, bool relu_out) {
+                     const c10::optional<at::Tensor>& coef_r, bool relu_out, bool split) {
   check_nhwc(x, "a");
-  const int B = (int)x.size(0), HW = (int)(x.size(1) * x.size(2)), N = (int)x.size(3);
+  TORCH_CHECK(!split || x.size(3) % 24 == 0, "enc_apply: split rows hold 3 planes of a multiple of 8 channels");
+  const int B = (int)x.size(0), HW = (int)(x.size(1) * x.size(2)), N = (int)x.size(3) / (split ? 3 : 1);
   TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() == (long)B * 4 * N, "coef");
   const void* rp = nullptr;
   const float* crp = nullptr;
@@ -438,7 +470,7 @@ at::Tensor enc_apply(const at::Tensor& x, const at::Tensor& coef, bool relu_a, c
   }
   at::Tensor out = at::empty_like(x);
   check(launch_enc_apply(x.data_ptr(), coef.data_ptr<float>(), relu_a, rp, crp, relu_out, out.data_ptr(), B, HW, N,
-                         stream()),
+                         split ? 1 : 0, stream()),
         "enc_apply");
   return out;
 }
@@ -529,17 +561,19 @@ std::vector<at::Tensor> enc_norm_bwd_finish(const at::Tensor& g, const at::Tenso
 }  // namespace raft_amd
 
 TORCH_LIBRARY_FRAGMENT(raft_amd, m) {
-  m.def("enc_conv_fwd(Tensor x, Tensor w, Tensor? bias, int stride, int pad, bool stats) -> (Tensor, Tensor)");
+  m.def("enc_conv_fwd(Tensor x, Tensor w, Tensor? bias, int stride, int pad, bool stats, bool split=False) -> "
+        "(Tensor, Tensor)");
   m.def(
       "enc_conv_dgrad(Tensor[] dys, Tensor[] ws, int[] strides, int[] pads, int H, int W, Tensor? res, Tensor? mask) "
       "-> Tensor");
   m.def("enc_conv_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, Tensor(b!)? db, int stride, int pad, bool accumulate, "
         "bool db_zero=False) -> ()");
-  m.def("enc_prep(Tensor img0, Tensor? img1) -> Tensor");
+  m.def("enc_prep(Tensor img0, Tensor? img1, bool split=False) -> Tensor");
   m.def(
       "enc_norm_stats(Tensor? stats, int B, int HW, int N, int kind, Tensor? gamma, Tensor? beta, Tensor(a!)? rmean, "
       "Tensor(b!)? rvar, Tensor(c!)? nbt, float momentum, float eps, int W=0) -> Tensor");
-  m.def("enc_apply(Tensor a, Tensor coef, bool relu_a, Tensor? r, Tensor? coef_r, bool relu_out) -> Tensor");
+  m.def("enc_apply(Tensor a, Tensor coef, bool relu_a, Tensor? r, Tensor? coef_r, bool relu_out, bool split=False) "
+        "-> Tensor");
   m.def("enc_norm_bwd(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind) -> Tensor[]");
   m.def("enc_norm_bwd_part(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind) -> Tensor");
   m.def(

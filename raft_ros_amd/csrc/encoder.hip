@@ -56,6 +56,23 @@ __device__ __forceinline__ void store8(__bf16* p, const float* v) {
   for (int i = 0; i < 8; ++i) x[i] = static_cast<__bf16>(v[i]);
   *reinterpret_cast<bf16x8*>(p) = x;
 }
+// split-bf16 planes (kernel_abi.h EncConvArgs::split): hi at p, lo at p + S, hi again at p + 2S
+__device__ __forceinline__ void store8_split(__bf16* p, int S, const float* v) {
+  bf16x8 hi, lo;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    hi[i] = static_cast<__bf16>(v[i]);
+    lo[i] = static_cast<__bf16>(v[i] - static_cast<float>(hi[i]));
+  }
+  *reinterpret_cast<bf16x8*>(p) = hi;
+  *reinterpret_cast<bf16x8*>(p + S) = lo;
+  *reinterpret_cast<bf16x8*>(p + 2 * S) = hi;
+}
+__device__ __forceinline__ void load8_split(const __bf16* p, int S, float* v) {
+  const bf16x8 hi = *reinterpret_cast<const bf16x8*>(p), lo = *reinterpret_cast<const bf16x8*>(p + S);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = static_cast<float>(hi[i]) + static_cast<float>(lo[i]);
+}
 __device__ __forceinline__ void loadf8(const float* p, float* v) {
   const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
 #pragma unroll
@@ -107,12 +124,15 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
   using C = EncCfg<BM, BN, WM, WN>;
   constexpr int TM = C::TM, TN = C::TN, ACH = C::ACH, BCH = C::BCH, STAGE = C::STAGE;
   __shared__ __attribute__((aligned(16))) char smem_raw[C::SMEM];
-  __shared__ int s_tab[kEncTab];
+  __shared__ int s_tab[kEncTabMax];
   __shared__ int s_out[BM];  // output pixel offset of each tile row (-1: past the grid)
   __bf16* smem = reinterpret_cast<__bf16*>(smem_raw);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int e = tid; e < kEncTab; e += 256) s_tab[e] = a.tab[e];
+  if (a.tab_ptr)
+    for (int e = tid; e < kEncTabMax; e += 256) s_tab[e] = a.tab_ptr[e];
+  else
+    for (int e = tid; e < kEncTab; e += 256) s_tab[e] = a.tab[e];
 
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   int ci;
@@ -357,7 +377,10 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = m[e] > 0.f ? v[e] : 0.f;
     }
-    store8(a.out + pix * a.out_stride + n, v);
+    if (a.split)
+      store8_split(a.out + pix * a.out_stride + n, a.N, v);
+    else
+      store8(a.out + pix * a.out_stride + n, v);
   }
 }
 
@@ -372,8 +395,9 @@ __global__ __launch_bounds__(256) void enc_pack_kernel(const EncConvArgs a, __bf
   if (ci == 2) cl = a.cls[2];
   if (ci == 3) cl = a.cls[3];
   const int row = blockIdx.x;
+  const int* ptab = a.ptab_ptr ? a.ptab_ptr : a.ptab;
   for (int k = threadIdx.x; k < cl.Kpad; k += 256) {
-    const int ent = (k < cl.K) ? a.ptab[cl.t0 + (k >> 3)] : -1;
+    const int ent = (k < cl.K) ? ptab[cl.t0 + (k >> 3)] : -1;
     float v = 0.f;
     if (ent >= 0) {
       const int w = ent & 15, ky = (ent >> 4) & 15, kx = (ent >> 8) & 15, loc = (ent >> 12) + (k & 7);
@@ -638,7 +662,7 @@ __global__ __launch_bounds__(256) void enc_wgrad_reduce_kernel(const float* __re
 // fp32, b < B from img0, b >= B from img1 (the feature encoder's paired batch).
 __global__ __launch_bounds__(256) void enc_prep_kernel(const float* __restrict__ i0, const float* __restrict__ i1,
                                                        long sb, long sc, long sh, long sw, int B, int H, int W,
-                                                       int nimg, __bf16* __restrict__ out) {
+                                                       int nimg, __bf16* __restrict__ out, int split) {
   const long p = (long)blockIdx.x * 256 + threadIdx.x;
   const long total = (long)nimg * H * W;
   if (p >= total) return;
@@ -652,7 +676,10 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const float* __restrict__
   for (int c = 0; c < 3; ++c) v[c] = 2.f * (src[o + c * sc] / 255.f) - 1.f;
 #pragma unroll
   for (int c = 3; c < 8; ++c) v[c] = 0.f;
-  store8(out + p * 8, v);
+  if (split)
+    store8_split(out + p * 24, 8, v);
+  else
+    store8(out + p * 8, v);
 }
 
 // ============================================================================ norms
@@ -738,15 +765,19 @@ __global__ __launch_bounds__(256) void enc_norm_finalize_kernel(const NormFinArg
 __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict__ a, const float* __restrict__ ca,
                                                         int relu_a, const __bf16* __restrict__ r,
                                                         const float* __restrict__ cr, int relu_out,
-                                                        __bf16* __restrict__ out, int B, int HW, int N) {
+                                                        __bf16* __restrict__ out, int B, int HW, int N, int split) {
   const int G = N / 8;
+  const int rs = split ? 3 * N : N;  // row stride: split rows hold hi / lo / hi planes
   const long total = (long)B * HW * G;
   for (long ch = (long)blockIdx.x * 256 + threadIdx.x; ch < total; ch += (long)gridDim.x * 256) {
     const long p = ch / G;
     const int n = (int)(ch - p * G) * 8;
     const int b = (int)(p / HW);
     float v[8], s[8], t[8];
-    load8(a + p * N + n, v);
+    if (split)
+      load8_split(a + p * rs + n, N, v);
+    else
+      load8(a + p * N + n, v);
     loadf8(ca + (long)b * 4 * N + n, s);
     loadf8(ca + (long)b * 4 * N + N + n, t);
 #pragma unroll
@@ -756,7 +787,10 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
     }
     if (r) {
       float rv[8];
-      load8(r + p * N + n, rv);
+      if (split)
+        load8_split(r + p * rs + n, N, rv);
+      else
+        load8(r + p * N + n, rv);
       if (cr) {
         loadf8(cr + (long)b * 4 * N + n, s);
         loadf8(cr + (long)b * 4 * N + N + n, t);
@@ -769,7 +803,10 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
     if (relu_out)
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-    store8(out + p * N + n, v);
+    if (split)
+      store8_split(out + p * rs + n, N, v);
+    else
+      store8(out + p * N + n, v);
   }
 }
 
@@ -1243,10 +1280,10 @@ hipError_t launch_enc_wgrad_reduce(const float* slab, int nsplit, int Npad, int 
 }
 
 hipError_t launch_enc_prep(const float* i0, const float* i1, const long* st, int B, int H, int W, int nimg,
-                           void* out, hipStream_t s) {
+                           void* out, int split, hipStream_t s) {
   const long total = (long)nimg * H * W;
   hipLaunchKernelGGL(enc_prep_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, i0, i1, st[0], st[1],
-                     st[2], st[3], B, H, W, nimg, static_cast<__bf16*>(out));
+                     st[2], st[3], B, H, W, nimg, static_cast<__bf16*>(out), split);
   return hipGetLastError();
 }
 
@@ -1257,11 +1294,11 @@ hipError_t launch_enc_norm_finalize(const NormFinArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_enc_apply(const void* a, const float* ca, bool relu_a, const void* r, const float* cr,
-                            bool relu_out, void* out, int B, int HW, int N, hipStream_t s) {
+                            bool relu_out, void* out, int B, int HW, int N, int split, hipStream_t s) {
   const long chunks = (long)B * HW * (N / 8);
   hipLaunchKernelGGL(enc_apply_kernel, dim3(grid_for(chunks)), dim3(256), 0, s, static_cast<const __bf16*>(a), ca,
                      relu_a ? 1 : 0, static_cast<const __bf16*>(r), cr, relu_out ? 1 : 0, static_cast<__bf16*>(out), B,
-                     HW, N);
+                     HW, N, split);
   return hipGetLastError();
 }
 

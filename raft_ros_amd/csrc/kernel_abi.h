@@ -149,7 +149,9 @@ struct ConvParamDesc {
 };
 
 // ============================================================================ encoder convs
-constexpr int kEncTab = 256;  // K/8 decode-table entries per launch (all classes)
+constexpr int kEncTab = 256;  // K/8 decode-table entries per launch (all classes) held in the arguments
+// deeper convs (the split-bf16 layout's 3x channels) read their tables from device memory
+constexpr int kEncTabMax = 512;
 
 struct EncSrc {
   const __bf16* ptr;
@@ -193,6 +195,12 @@ struct EncConvArgs {
   long ws[2][4];
   int wcin[2];
   int pack_dgrad;
+  // tables of more than kEncTab entries: device copies [kEncTabMax] (null: the arrays above)
+  const int* tab_ptr;
+  const int* ptab_ptr;
+  // split-bf16 output (fp32-faithful inference, see ConvFwdArgs::split_g): out rows hold
+  // [hi | lo | hi] planes of N channels each (out_stride = 3N)
+  int split;
 };
 
 struct EncWgradArgs {
@@ -459,10 +467,10 @@ hipError_t launch_enc_wgrad_reduce(const float* slab, int nsplit, int Npad, int 
                                    const long* ws, int Cout, int Cin, int Cx, int KH, int KW, float* db,
                                    bool accumulate, hipStream_t s);
 hipError_t launch_enc_prep(const float* i0, const float* i1, const long* st, int B, int H, int W, int nimg,
-                           void* out, hipStream_t s);
+                           void* out, int split, hipStream_t s);
 hipError_t launch_enc_norm_finalize(const NormFinArgs& a, hipStream_t s);
 hipError_t launch_enc_apply(const void* a, const float* ca, bool relu_a, const void* r, const float* cr,
-                            bool relu_out, void* out, int B, int HW, int N, hipStream_t s);
+                            bool relu_out, void* out, int B, int HW, int N, int split, hipStream_t s);
 hipError_t launch_enc_norm_bwd(const NormBwdArgs& a, hipStream_t s);
 // stages: bit 0 reduce (partials of a.B images), bit 1 finalize (over b_fin > 0 images'
 // partials when given: synchronized BatchNorm), bit 2 apply

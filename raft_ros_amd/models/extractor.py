@@ -9,9 +9,10 @@ Architecture and parameter names match the reference encoders so that
 
 On the GPU the RAFT orchestrator runs both encoders on the hand-written HIP
 kernels of ``ops/encoder.py`` / ``csrc/encoder.hip`` (one autograd node per
-encoder, NHWC, fused norm statistics); the ``forward`` methods here are the
-module path (CPU runs, and the reference op path the GPU tests compare
-against).  Passing a list/tuple ``[img1, img2]`` runs both frames as one batch
+encoder, NHWC, fused norm statistics) under bf16 AMP, and for fp32 inference in
+their split-bf16 (fp32-faithful) mode; the ``forward`` methods here are the
+module path (CPU runs, fp32 training, and the reference op path the GPU tests
+compare against).  Passing a list/tuple ``[img1, img2]`` runs both frames as one batch
 (core/extractor.py:170-174).
 """
 from __future__ import annotations

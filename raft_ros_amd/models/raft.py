@@ -16,6 +16,9 @@ Execution differences (GPU):
   the GRU gate math are native HIP kernels (``raft_ros_amd.ops``);
 * under bf16 AMP both encoders run on native HIP kernels as one autograd node
   each (``ops/encoder.py``; ``args.native_encoder=False`` selects the module path);
+* fp32 inference (no AMP, no autograd: the demo / evaluate / ROS default) runs the
+  encoders and the refinement step on the same kernels in split-bf16 mode (hi / lo
+  bf16 planes, 3 MFMA products per GEMM: fp32-faithful), so no MIOpen kernel runs;
 * the lookup emits channels-last features already in the autocast dtype;
 * mixed precision uses ``args.amp_dtype`` (default bf16 on MI355X; 'fp16'
   reproduces the reference's fp16 autocast);
@@ -137,9 +140,10 @@ class RAFT(nn.Module):
             side = self._side_stream(raw1.device)
             main = torch.cuda.current_stream(raw1.device)
             side.wait_stream(main)
+            split = not amp  # fp32 inference: split-bf16 (fp32-faithful) encoder kernels
             with torch.cuda.stream(side):
-                cnet_native = encoder_native.encode(self.cnet, raw1, join_stream=main)
-            fmap1, fmap2 = encoder_native.encode(self.fnet, raw1, raw2).split(raw1.shape[0], dim=0)
+                cnet_native = encoder_native.encode(self.cnet, raw1, join_stream=main, split=split)
+            fmap1, fmap2 = encoder_native.encode(self.fnet, raw1, raw2, split=split).split(raw1.shape[0], dim=0)
         else:
             with self._autocast(dev):
                 fmap1, fmap2 = self.fnet([image1, image2])
@@ -208,7 +212,9 @@ class RAFT(nn.Module):
         return aux_stream(device, "side")
 
     def _use_native_encoders(self, image1, amp: bool) -> bool:
-        return (amp and self.amp_dtype == torch.bfloat16 and _arg(self.args, "native_encoder", True)
+        """bf16 AMP (training and inference), or fp32 inference on the split-bf16 kernels."""
+        mode_ok = (self.amp_dtype == torch.bfloat16) if amp else not torch.is_grad_enabled()
+        return (mode_ok and _arg(self.args, "native_encoder", True)
                 and encoder_native.supported(self.fnet, image1) and encoder_native.supported(self.cnet, image1))
 
     # ------------------------------------------------------------------ fused (HIP) update path

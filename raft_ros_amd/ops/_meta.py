@@ -111,10 +111,14 @@ def register() -> None:
         return wf, wd, w[0].new_empty((n,))
 
     @fake(lib + "enc_conv_fwd")
-    def _(x, w, bias, stride, pad, stats):
+    def _(x, w, bias, stride, pad, stats, split=False):
         B, H, W, Cx = x.shape
         N, Cin, KH, KW = w.shape
         Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+        if split:
+            T = -(-(Ho * Wo) // 128)
+            st = x.new_empty((B, T, 2, N), dtype=torch.float32) if stats else x.new_empty((0,), dtype=torch.float32)
+            return x.new_empty((B, Ho, Wo, 3 * N)), st
         if not stats:
             st = x.new_empty((0,), dtype=torch.float32)
         elif (Cx, Cin, N, KH, KW, stride, pad) == (64, 64, 64, 3, 3, 1, 1):
@@ -130,9 +134,9 @@ def register() -> None:
         return dys[0].new_empty((dys[0].shape[0], H, W, ws[0].shape[1]))
 
     @fake(lib + "enc_prep")
-    def _(img0, img1):
+    def _(img0, img1, split=False):
         n = img0.shape[0] * (2 if img1 is not None else 1)
-        return img0.new_empty((n, img0.shape[2], img0.shape[3], 8), dtype=torch.bfloat16)
+        return img0.new_empty((n, img0.shape[2], img0.shape[3], 24 if split else 8), dtype=torch.bfloat16)
 
     @fake(lib + "enc_norm_stats")
     def _(stats, B, HW, N, kind, gamma, beta, rmean, rvar, nbt, momentum, eps, W=0):
@@ -140,7 +144,7 @@ def register() -> None:
         return like.new_empty((B, 4, N), dtype=torch.float32)
 
     @fake(lib + "enc_apply")
-    def _(a, coef, relu_a, r, coef_r, relu_out):
+    def _(a, coef, relu_a, r, coef_r, relu_out, split=False):
         return torch.empty_like(a)
 
     @fake(lib + "enc_norm_bwd")

@@ -103,10 +103,11 @@ class _Layout:
         self.out = conv(enc.conv2)
 
 
-def _stats(a, st, nd, P):
+def _stats(a, st, nd, P, split: bool = False):
     """coef [B, 4, N] of the norm ``nd`` for the conv output ``a``."""
     m = nd["module"]
     B, H, W, N = a.shape
+    N = N // 3 if split else N
     k = nd["kind"]
     if k in (_BATCH_TRAIN, _BATCH_EVAL):
         Bs = B
@@ -159,6 +160,60 @@ def _forward(L, x0, P):
         recs.append((ins, acts, coefs, drec, h))
     y, _ = _conv(h, L.out, P, False)
     return y, stem_rec, recs
+
+
+# ------------------------------------------------------------------ fp32-faithful inference
+# Without AMP (demo.py / evaluate.py / the ROS node default) the encoders run on the same
+# kernels in split-bf16 mode: activations are stored as [hi | lo | hi] bf16 planes and each
+# conv packs [W_hi | W_hi | W_lo], so a bf16 MFMA GEMM computes x_hi W_hi + x_lo W_hi + x_hi W_lo
+# with fp32 accumulation; norm statistics come from the fp32 accumulators and the norm /
+# residual / ReLU apply pass reads and writes the planes in fp32 (csrc/encoder.hip).
+
+def _split_weight(L, w: torch.Tensor, cx: int) -> torch.Tensor:
+    """(N, Cin, kh, kw) fp32 -> (N, 3 cx, kh, kw) [W_hi | W_hi | W_lo], each plane zero-padded
+    from Cin to the input planes' cx channels (cached per parameter version)."""
+    key = (id(w), w._version, cx)
+    cache = L.__dict__.setdefault("split_w", {})
+    hit = cache.get(key)
+    if hit is not None:
+        return hit
+    wf = w.detach().float()
+    hi = wf.to(torch.bfloat16).float()
+    pad = cx - wf.shape[1]
+    pd = (lambda t: torch.nn.functional.pad(t, (0, 0, 0, 0, 0, pad))) if pad else (lambda t: t)  # noqa: E731
+    out = torch.cat([pd(hi), pd(hi), pd(wf - hi)], 1).contiguous()
+    cache.clear() if len(cache) > 64 else None
+    cache[key] = out
+    return out
+
+
+def _conv_split(L, x, cd, P, stats):
+    b = P[cd["b"]] if cd["b"] >= 0 else None
+    return ops().enc_conv_fwd(x, _split_weight(L, P[cd["w"]], x.shape[3] // 3), b, cd["stride"], cd["pad"], stats, True)
+
+
+def _forward_split(L, x0, P):
+    """``_forward`` on split-bf16 planes (inference only); returns the split output rows."""
+    o = ops()
+    sc, sn = L.stem
+    a0, st = _conv_split(L, x0, sc, P, True)
+    h = o.enc_apply(a0, _stats(a0, st, sn, P, True), True, None, None, False, True)
+    for units, down in L.blocks:
+        hin = h
+        cur = hin
+        for ui, (cd, nd) in enumerate(units):
+            a, st = _conv_split(L, cur, cd, P, nd["kind"] != _BATCH_EVAL)
+            c = _stats(a, st, nd, P, True)
+            if ui + 1 < len(units):
+                cur = o.enc_apply(a, c, True, None, None, False, True)
+        if down is not None:
+            dcd, dnd = down
+            ad, st = _conv_split(L, hin, dcd, P, dnd["kind"] != _BATCH_EVAL)
+            h = o.enc_apply(a, c, True, ad, _stats(ad, st, dnd, P, True), True, True)
+        else:
+            h = o.enc_apply(a, c, True, hin, None, True, True)
+    y, _ = _conv_split(L, h, L.out, P, False)
+    return y
 
 
 def _wgrad(x, dy, cd, P, grads, nd=None):
@@ -279,12 +334,19 @@ def _layout(enc):
 
 
 def encode(enc, image1: torch.Tensor, image2: torch.Tensor | None = None,
-           join_stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+           join_stream: torch.cuda.Stream | None = None, split: bool = False) -> torch.Tensor:
     """Run ``enc`` natively on raw 0..255 fp32 images (``image2``: second frame of a
     paired batch).  Returns the (n, C, H/8, W/8) bf16 feature map in channels-last
     layout (``n`` = 2B when paired).  ``join_stream``: when this runs on a side stream,
-    the stream that must see the parameter gradients complete (see ``_EncoderFn.backward``)."""
+    the stream that must see the parameter gradients complete (see ``_EncoderFn.backward``).
+    ``split``: fp32-faithful inference (no autograd): the fp32 feature map."""
     L = _layout(enc)
+    if split:
+        assert not torch.is_grad_enabled(), "the split-bf16 encoder is inference-only"
+        x0 = ops().enc_prep(image1.float(), image2.float() if image2 is not None else None, True)
+        y = _forward_split(L, x0, L.params)
+        N = y.shape[3] // 3
+        return (y[..., :N].float() + y[..., N:2 * N].float()).permute(0, 3, 1, 2)
     x0 = ops().enc_prep(image1.float(), image2.float() if image2 is not None else None)
     y = _EncoderFn.apply(L, x0, join_stream, *L.params)
     return y.permute(0, 3, 1, 2)
