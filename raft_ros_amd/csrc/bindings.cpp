@@ -160,7 +160,7 @@ long elem_span(const at::Tensor& t) {  // elements addressable from data_ptr()
 // transposed A, epilogues store (epi 0) / accumulate (epi 1, fp32).
 void corr_gemm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, int64_t M, int64_t N, int64_t K,
                int64_t batch, int64_t lda, int64_t sA, int64_t ldb, int64_t sB, int64_t ldc, int64_t sC, double alpha,
-               bool a_trans, bool split, int64_t epi) {
+               bool a_trans, bool split, int64_t epi, int64_t cfg) {
   check_gpu(A, "A");
   check_gpu(B, "B");
   check_gpu(C, "C");
@@ -193,6 +193,7 @@ void corr_gemm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, in
   g.split = split;
   g.c_bf16 = C.scalar_type() == at::kBFloat16;
   g.epi = (int)epi;
+  g.cfg = (int)cfg;
   const c10::DeviceGuard guard(A.device());
   HIP_OK(launch_corr_gemm(g, cur_stream()));
 }
@@ -209,7 +210,7 @@ at::Tensor gemm_nt(const at::Tensor& A, const at::Tensor& B, double alpha, at::S
   auto C = at::empty({batch, M, N}, A.options().dtype(out_dtype));
   if (batch == 0 || M == 0 || N == 0) return C;
   corr_gemm(A, B, C, M, N, K, batch, A.stride(1), A.stride(0), B.stride(1), B.stride(0), N, M * N, alpha, false,
-            false, 0);
+            false, 0, 0);
   return C;
 }
 
@@ -1175,7 +1176,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_lookup_backward_(Tensor(a!)[] dpyramid, Tensor coords, Tensor grad, int radius) -> ()");
   m.def(
       "corr_gemm(Tensor A, Tensor B, Tensor(a!) C, int M, int N, int K, int batch, int lda, int sA, int ldb, int sB, "
-      "int ldc, int sC, float alpha, bool a_trans, bool split, int epi) -> ()");
+      "int ldc, int sC, float alpha, bool a_trans, bool split, int epi, int cfg=0) -> ()");
   m.def("pyramid_unpool(Tensor G, int H, int W, int[] segs, bool blocked=False) -> Tensor");
   m.def("pyramid_operand(Tensor fmap, int[] segs, int ld, bool blocked, bool nchw) -> Tensor");
   m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");

@@ -212,6 +212,150 @@ __global__ __launch_bounds__(256) void corr_gemm_kernel(const CorrGemmArgs g) {
     }
 }
 
+// ---------------------------------------------------------------------------- volume build v2
+// C[b][m][n] = bf16(alpha * sum_k A[b][m][k] * B[b][n][k]): bf16 operands (rows of K), fp32
+// accumulation, bf16 output -- the dense correlation volume under AMP (K = C = 256 / 128,
+// N = every pyramid level's pixels).  With K this short the kernel is bound by WRITING the
+// volume (B * HW * ld bf16: 173 MB at 8 x 368x496, 2.8 GB at 1080p), so it is built around
+// the stores:
+//   * 128x128 tile, 4 waves as 2x2, each 64x64 = 2x2 v_mfma_f32_32x32x16_bf16 per 16-deep k;
+//   * both operand tiles are DMA'd (buffer_load ... lds) into a 2-stage LDS ring in 64-deep
+//     K steps; 128-B rows with the 16-B chunk index XOR-swizzled by (row >> 1) & 7 through
+//     the SOURCE address (the lane-linear DMA image stays contiguous, and each 16-lane group
+//     of a fragment ds_read_b128 hits 16 distinct bank slots); rows past M / N load zeros;
+//   * the epilogue stages the bf16 tile in LDS and writes 16-byte row-contiguous chunks
+//     (one wave instruction = 4 rows x 256 B), not 2-byte scattered stores;
+//   * 64 KB of LDS per workgroup: two per CU, so one's stores overlap the other's MFMAs.
+constexpr int VBM = 128, VBN = 128, VBK = 64;
+constexpr int VSTAGE = (VBM + VBN) * VBK;  // bf16 elements per ring stage
+constexpr int VCP = VBN + 8;               // epilogue tile pitch (bf16)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t vrsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+typedef __attribute__((address_space(3))) void vlds_void;
+typedef __attribute__((address_space(3))) bf16x8 vlds_bf16x8;
+__device__ __forceinline__ void vbload16(__amdgpu_buffer_rsrc_t r, const __bf16* lds_wave_base, unsigned voff,
+                                         unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      r, (vlds_void*)(reinterpret_cast<uintptr_t>(lds_wave_base) & 0xffffffffu), 16, voff, soff, 0, 0);
+}
+constexpr unsigned kVOOB = 0x80000000u;
+
+__global__ __launch_bounds__(256, 2) void corr_volume_bf16_kernel(const CorrGemmArgs g) {
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[2 * VSTAGE];
+  const int tilesM = (g.M + VBM - 1) / VBM, tilesN = (g.N + VBN - 1) / VBN;
+  const int per_b = tilesM * tilesN;
+  const int wg = xcd_remap(blockIdx.x, per_b * g.batch);
+  const int b = wg / per_b, t = wg - b * per_b;
+  const int m0 = (t / tilesN) * VBM, n0 = (t - (t / tilesN) * tilesN) * VBN;
+  const __bf16* A = static_cast<const __bf16*>(g.A) + (long)b * g.sA;
+  const __bf16* B = static_cast<const __bf16*>(g.B) + (long)b * g.sB;
+  const __amdgpu_buffer_rsrc_t ra = vrsrc(A, (unsigned)((long)g.M * g.lda * 2));
+  const __amdgpu_buffer_rsrc_t rb = vrsrc(B, (unsigned)((long)g.N * g.ldb * 2));
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // DMA: wave-instruction q (of 16 per operand) fills tile rows 8q .. 8q+7; lane -> row
+  // 8q + lane/8, LDS chunk slot lane%8 <- source chunk slot ^ ((row >> 1) & 7)
+  const int lr = lane >> 3, lc = lane & 7;
+  unsigned avoff[4], bvoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wave * 4 + i) * 8 + lr;
+    const int src_chunk = lc ^ ((row >> 1) & 7);
+    avoff[i] = m0 + row < g.M ? (unsigned)((long)(m0 + row) * g.lda * 2 + src_chunk * 16) : kVOOB;
+    bvoff[i] = n0 + row < g.N ? (unsigned)((long)(n0 + row) * g.ldb * 2 + src_chunk * 16) : kVOOB;
+  }
+  auto issue = [&](int k0, int stage) __attribute__((always_inline)) {
+    const __bf16* sA = smem + stage * VSTAGE;
+    const __bf16* sB = sA + VBM * VBK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) vbload16(ra, sA + (wave * 4 + i) * 512, avoff[i], (unsigned)k0 * 2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) vbload16(rb, sB + (wave * 4 + i) * 512, bvoff[i], (unsigned)k0 * 2);
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // fragment rows of this lane and their swizzle
+  const int fr = lane & 31, fh = lane >> 5;
+  int arow[2], brow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    arow[i] = wm * 64 + i * 32 + fr;
+    brow[i] = wn * 64 + i * 32 + fr;
+  }
+  const unsigned lds0 = (unsigned)(reinterpret_cast<uintptr_t>(smem) & 0xffffffffu);
+  auto frag = [&](unsigned base, int row, int s) __attribute__((always_inline)) {
+    const int chunk = (2 * s + fh) ^ ((row >> 1) & 7);
+    return *(const vlds_bf16x8*)(uintptr_t)(base + (unsigned)(row * VBK * 2 + chunk * 16));
+  };
+
+  const int nk = (g.K + VBK - 1) / VBK;
+  issue(0, 0);
+  if (nk > 1) issue(VBK, 1);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this stage landed, next in flight
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const unsigned sa = lds0 + (unsigned)((kt & 1) * VSTAGE * 2), sb = sa + VBM * VBK * 2;
+#pragma unroll
+    for (int s = 0; s < VBK / 16; ++s) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        af[i] = frag(sa, arow[i], s);
+        bfr[i] = frag(sb, brow[i], s);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading this stage
+    if (kt + 2 < nk) issue((kt + 2) * VBK, kt & 1);
+  }
+
+  // ---- epilogue: bf16 tile through LDS, 16-byte row-contiguous stores
+  __bf16* ct = smem;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        const int col = wn * 64 + j * 32 + fr;
+        ct[row * VCP + col] = static_cast<__bf16>(g.alpha * acc[i][j][r]);
+      }
+  __syncthreads();
+  __bf16* C = static_cast<__bf16*>(g.C) + (long)b * g.sC;
+#pragma unroll
+  for (int i = 0; i < (VBM * VBN / 8) / 256; ++i) {
+    const int id = tid + 256 * i;
+    const int row = id >> 4, c8 = (id & 15) * 8;
+    const int m = m0 + row, n = n0 + c8;
+    if (m >= g.M || n >= g.N) continue;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(ct + row * VCP + c8);
+    __bf16* dst = C + (long)m * g.ldc + n;
+    if (n + 8 <= g.N) {
+      *reinterpret_cast<bf16x8*>(dst) = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (n + e < g.N) dst[e] = v[e];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void pyramid_unpool_kernel(const UnpoolArgs u) {
   const long total = (long)u.B * u.H * u.W * u.C;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -496,6 +640,17 @@ inline int grid_for(long total) {
 
 hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s) {
   if (g.M == 0 || g.N == 0 || g.batch == 0) return hipSuccess;
+  // bf16 x bf16 -> bf16 store (the AMP volume build): the store-oriented v2 kernel, when its
+  // 16-byte DMA / store granules and 32-bit buffer offsets fit
+  const bool v2 = !g.split && !g.a_trans && !g.a_f32 && !g.b_f32 && g.c_bf16 && g.epi == 0 && g.K % VBK == 0 &&
+                  g.lda % 8 == 0 && g.ldb % 8 == 0 && g.ldc % 8 == 0 && g.sC % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(g.C) % 16 == 0 && (long)g.M * g.lda * 2 < (1L << 31) &&
+                  (long)g.N * g.ldb * 2 < (1L << 31) && g.cfg != 1;
+  if (v2) {
+    const long tiles = (long)((g.M + VBM - 1) / VBM) * ((g.N + VBN - 1) / VBN) * g.batch;
+    hipLaunchKernelGGL(corr_volume_bf16_kernel, dim3((unsigned)tiles), dim3(256), 0, s, g);
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)(((g.M + GBM - 1) / GBM) * ((g.N + GBN - 1) / GBN) * g.batch)), blk(256);
   if (g.split) {
     if (g.a_trans) hipLaunchKernelGGL((corr_gemm_kernel<true, true>), grid, blk, 0, s, g);

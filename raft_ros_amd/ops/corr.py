@@ -121,7 +121,9 @@ class _BuildPyramid(torch.autograd.Function):
         HW = H * W
         k = ops()
         alpha = 1.0 / math.sqrt(C)
-        f1 = fmap1.detach().float().permute(0, 2, 3, 1).reshape(B, HW, C).contiguous()
+        # bf16 operands for the AMP volume (the store-bound v2 kernel); fp32 for split mode
+        op_dt = torch.float32 if split else torch.bfloat16
+        f1 = fmap1.detach().permute(0, 2, 3, 1).reshape(B, HW, C).to(op_dt).contiguous()
         sizes, off = [], 0
         for l in range(state.num_levels):
             Hl, Wl = H >> l, W >> l  # repeated 2x2 floor pooling
@@ -130,7 +132,7 @@ class _BuildPyramid(torch.autograd.Function):
         ld = off
         state.sizes, state.ld = sizes, ld
         # pooled fmap2 levels in blocked order, (B, ld, C): one HIP launch (== _concat_levels(_pooled))
-        f2cat = k.pyramid_operand(fmap2.detach(), state.segments(), ld, True, False)
+        f2cat = k.pyramid_operand(fmap2.detach(), state.segments(), ld, True, False).to(op_dt)
         # AMP (not split): the volume is stored in bf16 -- its lookups feed bf16 convs, and the
         # lookup kernels are bound by the bytes they gather; split mode keeps it fp32-faithful
         buf = torch.empty(B * HW, ld, device=f1.device, dtype=torch.float32 if split else torch.bfloat16)

@@ -9,7 +9,11 @@ compute streams, leaving a queue for the RCCL communicator under DDP:
   the refinement loop's backward each step's upsampler / head data gradients (the context
   encoder is idle then);
 * ``tail``: the refinement loop's work nobody waits for until the end -- the mask head and
-  the upsampling in the forward, the motion-encoder and lookup backward.
+  the upsampling in the forward, the motion-encoder and lookup backward;
+* ``wgrad``: the batched update-block weight gradients of the iterations whose backward is
+  complete, beside the remaining iterations' backward (ops/update_fused.py ``WGRAD_SPLIT``).
+  Under DDP this fourth compute stream shares a hardware queue with the communicator's
+  stream; the gradients it computes are what that communicator waits for anyway.
 """
 from __future__ import annotations
 
@@ -22,7 +26,7 @@ _STREAMS: Dict[Tuple[torch.device, str], torch.cuda.Stream] = {}
 
 def aux_stream(device, name: str) -> torch.cuda.Stream:
     """The process-wide ``name`` ('side' or 'tail') stream of ``device``."""
-    if name not in ("side", "tail"):
+    if name not in ("side", "tail", "wgrad"):
         raise ValueError(f"unknown auxiliary stream {name!r}")
     key = (torch.device(device), name)
     if key not in _STREAMS:

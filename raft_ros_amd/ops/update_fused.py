@@ -32,6 +32,7 @@ HIP launch per conv per RAFT forward (``ops.conv.pack_weights``).
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -120,6 +121,8 @@ class _Run:
         self.done = set()  # steps whose backward stored their dY
         self.g_all: Optional[torch.Tensor] = None  # [iters, P, 3*HID] data-gradient rows (backward)
         self.tail: Optional[torch.cuda.Stream] = None  # stream of the motion-encoder backward
+        self.wgrads: Optional[List[torch.Tensor]] = None  # weight gradients of iterations [wg_lo, iters)
+        self.wg_lo = iters
         self.coords: Dict[int, torch.Tensor] = {}
         self.flows: Dict[int, torch.Tensor] = {}
         self.wf: Dict[str, torch.Tensor] = {}
@@ -154,9 +157,13 @@ class _Run:
         return C.geom(B, H, W, kh, kw, kh - 1 - kh // 2, kw - 1 - kw // 2)
 
     # ------------------------------------------------------------ batched weight gradients
-    def weight_grads(self) -> List[Optional[torch.Tensor]]:
+    def weight_grads(self, t_lo: int = 0, t_hi: Optional[int] = None,
+                     grads: Optional[List[torch.Tensor]] = None) -> List[Optional[torch.Tensor]]:
+        """Parameter gradients summed over iterations [t_lo, t_hi); ``grads``: the tensors of an
+        earlier range to accumulate into (None: fresh ones)."""
         T, P, ar = self.iters, self.P, self.arena
-        for t in range(T):  # steps whose outputs fed no loss: zero dY
+        t_hi = T if t_hi is None else t_hi
+        for t in range(t_lo, t_hi):  # steps whose outputs fed no loss: zero dY
             if t not in self.done:
                 for name in ("dmask", "dd8", "dhd", "dq1", "dq2", "dzr1", "dzr2", "dmo", "dcf", "dc1", "df1"):
                     if name in ar.bufs:
@@ -189,27 +196,58 @@ class _Run:
                 return [r("hd")[:, :256]], r("dd8")
             return [r("hd")[:, 256:]], r("dmask")  # mask2
 
-        grads: List[Optional[torch.Tensor]] = []
+        out: List[Optional[torch.Tensor]] = []
+        gi = 0
         for name, mods, segs, scale, _ in _LAYERS:
             ms = mods(self.block)
-            wg = [torch.empty_like(m.weight) for m in ms]
-            bg = [torch.empty_like(m.bias) for m in ms]
+            if grads is None:
+                wg = [torch.empty_like(m.weight) for m in ms]
+                bg = [torch.empty_like(m.bias) for m in ms]
+            else:
+                wg = [grads[gi + 2 * i] for i in range(len(ms))]
+                bg = [grads[gi + 2 * i + 1] for i in range(len(ms))]
+            gi += 2 * len(ms)
             kh, kw = ms[0].weight.shape[2:]
-            # one launch over all iterations, unless an operand would exceed the kernels'
-            # 32-bit byte offsets (very large batches / resolutions): then chunks of iterations
-            srcs, dy = srcs_dy(name, 0, T)
+            # one launch over the range, unless an operand would exceed the kernels' 32-bit
+            # byte offsets (very large batches / resolutions): then chunks of iterations
+            srcs, dy = srcs_dy(name, t_lo, t_hi)
             per_iter = max([s.stride(0) * 2 * P for s in srcs] + [dy.stride(0) * 2 * P])
-            chunk = max(1, min(T, _I32 // max(per_iter, 1)))
-            for t0 in range(0, T, chunk):
-                t1 = min(T, t0 + chunk)
+            chunk = max(1, min(t_hi - t_lo, _I32 // max(per_iter, 1)))
+            for t0 in range(t_lo, t_hi, chunk):
+                t1 = min(t_hi, t0 + chunk)
                 srcs, dy = srcs_dy(name, t0, t1)
-                C.conv_wgrad_params(srcs, dy, self.geom(kh, kw, t1 - t0), wg, bg, segs, scale, accumulate=t0 > 0)
+                C.conv_wgrad_params(srcs, dy, self.geom(kh, kw, t1 - t0), wg, bg, segs, scale,
+                                    accumulate=t0 > t_lo or grads is not None)
             for w, b in zip(wg, bg):
-                grads += [w, b]
-        return grads
+                out += [w, b]
+        return out
+
+    def early_weight_grads(self, t: int) -> None:
+        """Called once step ``t``'s backward has stored its dY: when [t, t_hi) is a complete
+        range of WGRAD_SPLIT, queue its weight gradients on the ``wgrad`` stream, where they
+        run beside the backward of the earlier iterations (the data-gradient chain is serial
+        and leaves most of the GPU idle)."""
+        if WGRAD_SPLIT <= 1 or not self.arena.keep or t == 0:
+            return
+        T = self.iters
+        bounds = [T * k // WGRAD_SPLIT for k in range(1, WGRAD_SPLIT)]
+        if t not in bounds:
+            return
+        t_hi = min([b for b in bounds if b > t], default=T)
+        dev = self.inp_bf.device
+        ws = aux_stream(dev, "wgrad")
+        ws.wait_stream(torch.cuda.current_stream(dev))
+        if self.tail is not None:  # the motion-encoder backward wrote its dY there
+            ws.wait_stream(self.tail)
+        with torch.cuda.stream(ws):
+            self.wgrads = self.weight_grads(t, t_hi, self.wgrads)
+        self.wg_lo = t
 
 
 TAIL_STREAM = True  # motion-encoder backward on its own stream (see _Step.backward)
+# the batched weight gradients in WGRAD_SPLIT iteration ranges: all but the first start on the
+# wgrad stream as soon as their iterations' backward is done (_Run.early_weight_grads)
+WGRAD_SPLIT = int(os.environ.get("RAFT_WGRAD_SPLIT", "1"))  # 2: -1.5 % (gpurun_out r3 A/B), kept off
 HEAD_STREAM = True  # upsampler / head backward ahead of the d-net chain (see _Step.backward)
 
 
@@ -246,10 +284,26 @@ class _PackWeights(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gtoken):
         run: _Run = ctx.run
+        cur = torch.cuda.current_stream() if run.inp_bf.is_cuda else None
         if run.tail is not None:  # the steps' motion-encoder backward wrote dY on the tail stream
-            torch.cuda.current_stream().wait_stream(run.tail)
-        grads = run.weight_grads()
+            cur.wait_stream(run.tail)
+        if run.wgrads is not None:
+            # the later iterations' gradients were computed on the wgrad stream during the
+            # loop's backward (_Run.early_weight_grads): add the remaining iterations there too
+            # (same stream: ordered after them), then join
+            ws = aux_stream(cur.device, "wgrad")
+            ws.wait_stream(cur)
+            with torch.cuda.stream(ws):
+                grads = run.weight_grads(0, run.wg_lo, run.wgrads)
+            cur.wait_stream(ws)
+            for g in grads:
+                g.record_stream(cur)
+            for b in run.arena.bufs.values():
+                b.record_stream(ws)
+        else:
+            grads = run.weight_grads()
         run.arena.bufs.clear()
+        run.wgrads = None
         return (None, *grads)
 
 
@@ -467,6 +521,7 @@ class _Step(torch.autograd.Function):
             if dense:
                 k.corr_lookup_backward_(pgrad, run.coords[t], dcorr.reshape(B, H, W, CORR_PAD), run.pyr.radius)
         run.done.add(t)
+        run.early_weight_grads(t)
 
         d_corr_in = dcorr.reshape(B, H, W, CORR_PAD) if ctx.has_corr_in else None
         d_net = _nchw(d_net if ctx.net_dtype == bf else d_net.to(ctx.net_dtype), B, H, W)

@@ -29,6 +29,26 @@ def test_gemm_nt_bf16(cuda, M, N, K, batch):
     torch.testing.assert_close(Cb.float(), 2 * R, rtol=2e-2, atol=5e-2)
 
 
+@pytest.mark.parametrize("M,N,K,batch", [(2852, 3808, 256, 2), (300, 1000, 128, 3), (64, 8, 64, 1)])
+def test_corr_volume_v2_matches_generic(cuda, M, N, K, batch):
+    """The store-oriented bf16 volume kernel (corr_volume_bf16_kernel: DMA ring, swizzled
+    LDS, LDS-staged 16-byte stores) vs the generic kernel (cfg=1) and an fp32 matmul: partial
+    tiles in M and N, odd N (partial 16-byte chunks at the row end)."""
+    torch.manual_seed(3)
+    ops = _ops()
+    A = torch.randn(batch, M, K, device=cuda).bfloat16()
+    B = torch.randn(batch, N, K, device=cuda).bfloat16()
+    outs = []
+    for cfg in (0, 1):
+        C = torch.full((batch, M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+        ops.corr_gemm(A, B, C, M, N, K, batch, K, M * K, K, N * K, N, M * N, 0.0625, False, False, 0, cfg)
+        outs.append(C.float())
+    want = 0.0625 * torch.matmul(A.float(), B.float().transpose(1, 2))
+    assert torch.isfinite(outs[0]).all()
+    torch.testing.assert_close(outs[0], want, rtol=1e-2, atol=1e-2)
+    assert (outs[0] - outs[1]).abs().max().item() <= 2 * want.abs().max().item() * 2 ** -8
+
+
 def test_gemm_nt_identity_asymmetric(cuda):
     M, K = 128, 128
     A = torch.eye(M, K, device=cuda).bfloat16()[None]
