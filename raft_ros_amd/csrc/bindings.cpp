@@ -35,6 +35,7 @@ hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void*
                                   void* motion = nullptr, long smo = 0);
 hipError_t launch_corr_lookup_bwd(const PyrDesc& dpyr, const float* coords, const void* gout,
                                   int g_dtype, int B, int H, int W, int r, int gstride, hipStream_t s);
+hipError_t launch_lookup_grad_rows(const GradRowsArgs& a, int g_dtype, hipStream_t s);
 hipError_t launch_gru_bwd_a(const float* dH, long sdh, const void* z, long sz, const void* q, long sq,
                             const void* h, long sh, void* dq, long sdq, void* dz, long sdz, float* carry,
                             long sc, long P, int C, hipStream_t s);
@@ -127,11 +128,13 @@ PyrDesc make_desc(const std::vector<at::Tensor>& levels, long rows, bool allow_b
     TORCH_CHECK(t.scalar_type() == at::kFloat || (allow_bf16 && bf),
                 "raft_amd: pyramid levels must be fp32 (bf16: forward lookups only)");
     if (blk) {
-      TORCH_CHECK(t.size(3) == 16 && t.stride(3) == 1 && t.stride(2) == 16 && t.stride(1) == t.size(2) * 16 &&
-                      t.stride(0) >= t.size(1) * t.size(2) * 16,
+      // (strides of size-1 dims are free: torch reports such views contiguous as they are)
+      TORCH_CHECK(t.size(3) == 16 && t.stride(3) == 1 && (t.size(2) == 1 || t.stride(2) == 16) &&
+                      (t.size(1) == 1 || t.stride(1) == t.size(2) * 16) && t.stride(0) >= t.size(1) * t.size(2) * 16,
                   "raft_amd: blocked pyramid levels must be (rows, W/16, H, 16) views");
     } else {
-      TORCH_CHECK(t.dim() == 3 && t.stride(2) == 1 && t.stride(1) == t.size(2) && t.stride(0) >= t.size(1) * t.size(2),
+      TORCH_CHECK(t.dim() == 3 && (t.size(2) == 1 || t.stride(2) == 1) && (t.size(1) == 1 || t.stride(1) == t.size(2)) &&
+                      t.stride(0) >= t.size(1) * t.size(2),
                   "raft_amd: pyramid levels must be (B*H*W, Hl, Wl) row views");
     }
     TORCH_CHECK(l == 0 || ((bf ? 1 : 0) == d.vbf16 && (blk ? 1 : 0) == d.blk),
@@ -323,6 +326,62 @@ void corr_lookup_backward_(at::TensorList dpyr, const at::Tensor& coords, const 
   HIP_OK(launch_corr_lookup_bwd(d, coords.data_ptr<float>(), g.data_ptr(),
                                 dtype_code(g.scalar_type()), B, H, W, static_cast<int>(radius),
                                 static_cast<int>(g.size(3)), cur_stream()));
+}
+
+// Deferred lookup backward: out (B*H*W, ld) bf16 / fp32 rows of 16-column-blocked level
+// gradients (segments: off, Hl, Wl per level) from the window gradients grads[t] (B, H, W,
+// >= L*(2r+1)^2) of the lookups at coords[t]; accumulate: add to out instead of overwriting.
+void corr_lookup_grad_rows(const at::Tensor& out, at::TensorList coords, at::TensorList grads,
+                           at::IntArrayRef segments, int64_t radius, bool accumulate) {
+  TORCH_CHECK(coords.size() == grads.size() && !coords.empty() && (long)coords.size() <= kGradRowsMaxT,
+              "raft_amd::corr_lookup_grad_rows: 1..32 (coords, grad) pairs");
+  TORCH_CHECK(segments.size() % 3 == 0 && segments.size() >= 3 && segments.size() <= 12,
+              "raft_amd::corr_lookup_grad_rows: segments = (off, Hl, Wl) per level, 1..4 levels");
+  TORCH_CHECK(radius >= 0 && radius <= 6, "raft_amd::corr_lookup_grad_rows: radius <= 6");
+  check_coords(coords[0]);
+  const long B = coords[0].size(0), H = coords[0].size(2), W = coords[0].size(3);
+  check_gpu(out, "out");
+  TORCH_CHECK(out.dim() == 2 && out.is_contiguous() && out.size(0) == B * H * W &&
+                  (out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16),
+              "raft_amd::corr_lookup_grad_rows: out must be contiguous (B*H*W, ld) fp32 / bf16");
+  GradRowsArgs a{};
+  a.ld = out.size(1);
+  TORCH_CHECK(a.ld % 16 == 0 && a.ld <= kGradRowsMaxLd, "raft_amd::corr_lookup_grad_rows: ld");
+  a.levels = (int)segments.size() / 3;
+  long end = 0;
+  for (int l = 0; l < a.levels; ++l) {
+    a.off[l] = (int)segments[3 * l];
+    a.H[l] = (int)segments[3 * l + 1];
+    a.W[l] = (int)((segments[3 * l + 2] + 15) / 16 * 16);
+    TORCH_CHECK(a.off[l] == end, "raft_amd::corr_lookup_grad_rows: levels must tile the row");
+    end += (long)a.H[l] * a.W[l];
+  }
+  TORCH_CHECK(end == a.ld, "raft_amd::corr_lookup_grad_rows: levels must tile the row");
+  const long win = (2 * radius + 1) * (2 * radius + 1);
+  const auto gt = grads[0].scalar_type();
+  a.T = (int)coords.size();
+  for (int t = 0; t < a.T; ++t) {
+    check_coords(coords[t]);
+    const auto& g = grads[t];
+    check_gpu(g, "grad");
+    TORCH_CHECK(coords[t].sizes() == coords[0].sizes() && g.scalar_type() == gt && g.dim() == 4 && g.size(0) == B &&
+                    g.size(1) == H && g.size(2) == W && g.size(3) >= a.levels * win && g.stride(3) == 1 &&
+                    g.stride(2) == g.size(3) && g.stride(1) == W * g.size(3) && g.stride(0) == H * W * g.size(3) &&
+                    g.size(3) == grads[0].size(3),
+                "raft_amd::corr_lookup_grad_rows: grads must be contiguous (B, H, W, >= L*(2r+1)^2), one shape");
+    a.g[t] = g.data_ptr();
+    a.c[t] = coords[t].data_ptr<float>();
+  }
+  a.gstride = (int)grads[0].size(3);
+  a.out = out.data_ptr();
+  a.out_f32 = out.scalar_type() == at::kFloat;
+  a.accumulate = accumulate ? 1 : 0;
+  a.B = (int)B;
+  a.Hq = (int)H;
+  a.Wq = (int)W;
+  a.r = (int)radius;
+  const c10::DeviceGuard guard(out.device());
+  HIP_OK(launch_lookup_grad_rows(a, dtype_code(gt), cur_stream()));
 }
 
 // ---------------------------------------------------------------- convex upsampling
@@ -1174,6 +1233,8 @@ TORCH_LIBRARY(raft_amd, m) {
       "Tensor(c!)? motion=None) -> ()");
   m.def("convex_upsample_backward_into(Tensor flow, Tensor mask, Tensor grad, Tensor(a!) dmask, Tensor(b!) rows) -> ()");
   m.def("corr_lookup_backward_(Tensor(a!)[] dpyramid, Tensor coords, Tensor grad, int radius) -> ()");
+  m.def("corr_lookup_grad_rows(Tensor(a!) out, Tensor[] coords, Tensor[] grads, int[] segments, int radius, "
+        "bool accumulate=False) -> ()");
   m.def(
       "corr_gemm(Tensor A, Tensor B, Tensor(a!) C, int M, int N, int K, int batch, int lda, int sA, int ldb, int sB, "
       "int ldc, int sC, float alpha, bool a_trans, bool split, int epi, int cfg=0) -> ()");
@@ -1200,6 +1261,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("avgpool2x2", &raft_amd::avgpool2x2);
   m.impl("corr_lookup", &raft_amd::corr_lookup);
   m.impl("corr_lookup_backward_", &raft_amd::corr_lookup_backward_);
+  m.impl("corr_lookup_grad_rows", &raft_amd::corr_lookup_grad_rows);
   m.impl("corr_gemm", &raft_amd::corr_gemm);
   m.impl("pyramid_unpool", &raft_amd::pyramid_unpool);
   m.impl("convex_upsample", &raft_amd::convex_upsample);

@@ -119,7 +119,8 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
   check_w(w, "w");
   const int B = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), Cx = (int)x.size(3);
   const int N = (int)w.size(0), Cin = (int)w.size(1), KH = (int)w.size(2), KW = (int)w.size(3);
-  TORCH_CHECK(Cin <= Cx, "weight has more input channels than x");
+  TORCH_CHECK(Cin <= (split ? Cx / 3 : Cx), "weight has more input channels than x");
+  TORCH_CHECK(!split || Cx % 3 == 0, "split x must hold three planes");
   TORCH_CHECK(N % 8 == 0 && N <= 1024, "out channels");
   const int Ho = (H + 2 * (int)pad - KH) / (int)stride + 1, Wo = (W + 2 * (int)pad - KW) / (int)stride + 1;
   EncConvArgs a;
@@ -156,6 +157,7 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
   a.out = mbf(y);
   a.out_stride = split ? 3 * N : N;
   a.split = split ? 1 : 0;
+  a.split_w = split ? Cx / 3 : 0;  // the fp32 weight is split while packing
   at::Tensor b;
   if (bias.has_value() && bias->defined()) {
     b = bias->to(at::kFloat).contiguous();

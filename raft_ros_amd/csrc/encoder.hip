@@ -405,10 +405,18 @@ __global__ __launch_bounds__(256) void enc_pack_kernel(const EncConvArgs a, __bf
       const long s0 = w ? a.ws[1][0] : a.ws[0][0], s1 = w ? a.ws[1][1] : a.ws[0][1];
       const long s2 = w ? a.ws[1][2] : a.ws[0][2], s3 = w ? a.ws[1][3] : a.ws[0][3];
       const int cin = w ? a.wcin[1] : a.wcin[0];
-      if (a.pack_dgrad)
+      if (a.pack_dgrad) {
         v = wp[loc * s0 + row * s1 + ky * s2 + kx * s3];
-      else if (loc < cin)
+      } else if (a.split_w) {  // [W_hi | W_hi | W_lo] against the [hi | lo | hi] input planes
+        const int plane = loc / a.split_w, cl = loc - plane * a.split_w;
+        if (cl < cin) {
+          const float x = wp[row * s0 + cl * s1 + ky * s2 + kx * s3];
+          const float hi = static_cast<float>(static_cast<__bf16>(x));
+          v = plane < 2 ? hi : x - hi;
+        }
+      } else if (loc < cin) {
         v = wp[row * s0 + loc * s1 + ky * s2 + kx * s3];
+      }
     }
     out[cl.wofs + (long)row * cl.Kpad + k] = static_cast<__bf16>(v);
   }

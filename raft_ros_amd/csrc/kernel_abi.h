@@ -195,6 +195,9 @@ struct EncConvArgs {
   long ws[2][4];
   int wcin[2];
   int pack_dgrad;
+  // split-bf16 input planes (forward packing): > 0 = the plane width cx of x = [hi | lo | hi];
+  // the fp32 weight is packed as [W_hi | W_hi | W_lo], each plane zero-padded from Cin to cx
+  int split_w;
   // tables of more than kEncTab entries: device copies [kEncTabMax] (null: the arrays above)
   const int* tab_ptr;
   const int* ptab_ptr;
@@ -280,6 +283,23 @@ struct PyrDesc {
   int levels;
   int vbf16;   // levels hold bf16 (the AMP volume; forward lookups only -- gradients stay fp32)
   int blk;     // levels stored in 16-column blocks [W/16][H][16] (W = blocks * 16)
+};
+
+// Deferred lookup backward (csrc/corr_volume.hip lookup_grad_rows_kernel): the window
+// gradients of all T lookups of a step -> the dense level-gradient rows, each row
+// accumulated in LDS and written once (bf16 or fp32), replacing T read-modify-write passes
+// over an fp32 buffer and its memset.
+constexpr int kGradRowsMaxT = 32;
+constexpr int kGradRowsMaxLd = 15616;  // row floats in LDS (+ window staging) within 64 KB
+struct GradRowsArgs {
+  const void* g[kGradRowsMaxT];   // window gradients of lookup t: row pix at g[t] + pix * gstride
+  const float* c[kGradRowsMaxT];  // coordinates of lookup t, (B, 2, H, W) fp32
+  int T, gstride;
+  void* out;  // (B*H*W, ld) rows, 16-column-blocked levels at off[l]
+  long ld;
+  int out_f32, accumulate;  // accumulate: add to the rows already in out
+  int levels, off[4], H[4], W[4];  // W: padded to whole 16-column blocks
+  int B, Hq, Wq, r;
 };
 
 // One GEMM of the correlation path: C[b][m][n] (op)= alpha * sum_k A[b][m][k] * B[b][n][k]

@@ -160,7 +160,7 @@ class RAFT(nn.Module):
             from ..parallel.query_shard import ShardedCorrPyramid
 
             corr_fn = ShardedCorrPyramid(fmap1, fmap2, num_levels=self.args.corr_levels,
-                                         radius=self.args.corr_radius)
+                                         radius=self.args.corr_radius, split=split)
         else:
             corr_fn = CorrPyramid(fmap1, fmap2, radius=self.args.corr_radius, split=split)
 
@@ -240,7 +240,7 @@ class RAFT(nn.Module):
             corr = None
             if not dense:
                 c = corr_fn(coords1, out_dtype=torch.float32)
-                corr = c.permute(0, 2, 3, 1).reshape(-1, c.shape[1])
+                corr = c.permute(0, 2, 3, 1).reshape(-1, c.shape[1]).float().contiguous()
             _, flow_up, coords1 = upd.step(t, net if t == 0 else None, coords1, coords0, corr=corr, upsample=up)
             if up:
                 flow_predictions.append(flow_up)

@@ -14,8 +14,11 @@ Dense path on the GPU (kernels: csrc/corr_volume.hip):
   (core/raft.py:102-103); under AMP the operands are rounded to bf16.
   Its only differentiable output is a scalar *token*.
 * every refinement iteration calls ``_Lookup(token, coords)`` (or the fused
-  update step does the same lookup); the backward adds the window gradients, in
-  place and without atomics, into one fp32 gradient buffer per level.
+  update step does the same lookup); its backward only records the window
+  gradient.  The pyramid backward then writes every query's level-gradient row
+  once (``corr_lookup_grad_rows``: the row accumulated in LDS over all the
+  step's lookups, bf16 under AMP) -- instead of zeroing an fp32 buffer and
+  read-modify-writing it once per lookup.
 * autograd runs ``_BuildPyramid.backward`` only after every lookup's backward
   (they all feed the token): ``dF1 = sum_l dL_l . pool_l(f2)`` and
   ``dF2 = sum_l unpool_l(dL_l^T . f1)`` as GEMMs straight from the level
@@ -29,6 +32,7 @@ of 2r+2 rows, which is what the memory-bound lookup kernels pay for.
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -36,6 +40,11 @@ import torch.nn.functional as F
 
 from . import reference as ref
 from ._ext import ops, use_native
+
+# Lookup backward mode (see _PyramidState.add_grad): deferred row accumulation (default) or
+# one read-modify-write pass per lookup (RAFT_DEFER_LOOKUP_GRADS=0, for A/B measurements)
+DEFER_LOOKUP_GRADS = os.environ.get("RAFT_DEFER_LOOKUP_GRADS", "1") != "0"
+_GRAD_ROWS_MAX_LD = 15616  # csrc/kernel_abi.h kGradRowsMaxLd
 
 
 def _pad_to(n: int, m: int) -> int:
@@ -60,6 +69,35 @@ class _PyramidState:
         self.tail = None                       # stream of fused-step lookup backwards (to join)
         self.ld = 0
         self.shape = None
+        self.pending: List[tuple] = []         # deferred (coords, window gradient) of each lookup
+
+    def deferrable(self) -> bool:
+        """Whether lookup gradients can be deferred to one row-accumulating pass at the pyramid
+        backward (a level-gradient row fits the kernel's LDS) instead of read-modify-writing a
+        zeroed fp32 buffer once per lookup."""
+        return DEFER_LOOKUP_GRADS and 0 < self.ld <= _GRAD_ROWS_MAX_LD and self.radius <= 6 and self.num_levels <= 4
+
+    def add_grad(self, coords: torch.Tensor, grad: torch.Tensor) -> None:
+        """The window gradient ``grad`` (B, H, W, >= L*(2r+1)^2) of the lookup at ``coords``."""
+        if self.deferrable():
+            self.pending.append((coords, grad))
+        else:
+            ops().corr_lookup_backward_(self.grad_buffers(), coords, grad, self.radius)
+
+    def level_grads(self, dtype: torch.dtype) -> Optional[torch.Tensor]:
+        """(B*HW, ld) level-gradient rows of every lookup so far: the deferred ones written in
+        one pass (``dtype``: bf16 for the AMP volume, fp32 for split mode), or the buffer the
+        per-lookup backward accumulated into; None when no lookup has a gradient."""
+        if self.pending:
+            assert self.dbuf is None, "deferred and immediate lookup gradients cannot mix"
+            rows = torch.empty(self.buf.shape, device=self.buf.device, dtype=dtype)
+            for i in range(0, len(self.pending), 32):
+                chunk = self.pending[i:i + 32]
+                ops().corr_lookup_grad_rows(rows, [c for c, _ in chunk], [g for _, g in chunk], self.segments(),
+                                            self.radius, i > 0)
+            self.pending = []
+            return rows
+        return self.dbuf
 
     def views(self, buf: torch.Tensor) -> List[torch.Tensor]:
         # 16-column blocks: level pixel (y, x) at ((x // 16) * Hl + y) * 16 + x % 16, so a lookup
@@ -85,6 +123,7 @@ class _PyramidState:
         self.levels = []
         self.dbuf = None
         self.dlevels = None
+        self.pending = []
 
 
 def _pooled(f: torch.Tensor, levels: int) -> List[torch.Tensor]:
@@ -156,19 +195,21 @@ class _BuildPyramid(torch.autograd.Function):
             state.tail = None
             if state.dbuf is not None:
                 state.dbuf.record_stream(tail)
-        if state.dbuf is None:
+        split = ctx.split
+        # bf16 level gradients for the AMP volume: the two GEMMs below read them at half the
+        # bytes (they round their A operand to bf16 anyway unless split)
+        dbuf = state.level_grads(torch.float32 if split else torch.bfloat16)
+        if dbuf is None:
             state.release()
             return None, None, None, None
         B, C, H, W = state.shape
         HW, ld = H * W, state.ld
         k = ops()
         alpha = 1.0 / math.sqrt(C)
-        split = ctx.split
         f2t = k.pyramid_operand(fmap2.detach(), state.segments(), ld, True, True)  # (B, C, ld)
         f1t = k.pyramid_operand(fmap1.detach(), [0, H, W], _pad_to(HW, 8), False, True)  # (B, C, HW + pad)
         d1 = torch.empty(B, HW, C, device=fmap1.device)
         G = torch.empty(B, ld, C, device=fmap1.device)
-        dbuf = state.dbuf
         # dF1 = alpha * dL . f2cat            (M = HW, N = C, K = all levels)
         k.corr_gemm(dbuf, f2t, d1, HW, C, ld, B, ld, HW * ld, ld, C * ld, C, HW * C, alpha, False, split, 0)
         # G = alpha * dL^T . f1  per level row (M = all levels, N = C, K = HW; A read transposed),
@@ -196,7 +237,7 @@ class _Lookup(torch.autograd.Function):
         (coords,) = ctx.saved_tensors
         state: _PyramidState = ctx.state
         if state.levels:
-            ops().corr_lookup_backward_(state.grad_buffers(), coords, gout.contiguous(), state.radius)
+            state.add_grad(coords, gout.contiguous())
         return torch.zeros((), device=gout.device), None, None, None, None
 
 

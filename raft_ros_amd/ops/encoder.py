@@ -165,31 +165,16 @@ def _forward(L, x0, P):
 # ------------------------------------------------------------------ fp32-faithful inference
 # Without AMP (demo.py / evaluate.py / the ROS node default) the encoders run on the same
 # kernels in split-bf16 mode: activations are stored as [hi | lo | hi] bf16 planes and each
-# conv packs [W_hi | W_hi | W_lo], so a bf16 MFMA GEMM computes x_hi W_hi + x_lo W_hi + x_hi W_lo
+# conv packs [W_hi | W_hi | W_lo] (split while packing, csrc/encoder.hip enc_pack_kernel), so a bf16 MFMA GEMM computes x_hi W_hi + x_lo W_hi + x_hi W_lo
 # with fp32 accumulation; norm statistics come from the fp32 accumulators and the norm /
 # residual / ReLU apply pass reads and writes the planes in fp32 (csrc/encoder.hip).
 
-def _split_weight(L, w: torch.Tensor, cx: int) -> torch.Tensor:
-    """(N, Cin, kh, kw) fp32 -> (N, 3 cx, kh, kw) [W_hi | W_hi | W_lo], each plane zero-padded
-    from Cin to the input planes' cx channels (cached per parameter version)."""
-    key = (id(w), w._version, cx)
-    cache = L.__dict__.setdefault("split_w", {})
-    hit = cache.get(key)
-    if hit is not None:
-        return hit
-    wf = w.detach().float()
-    hi = wf.to(torch.bfloat16).float()
-    pad = cx - wf.shape[1]
-    pd = (lambda t: torch.nn.functional.pad(t, (0, 0, 0, 0, 0, pad))) if pad else (lambda t: t)  # noqa: E731
-    out = torch.cat([pd(hi), pd(hi), pd(wf - hi)], 1).contiguous()
-    cache.clear() if len(cache) > 64 else None
-    cache[key] = out
-    return out
-
-
 def _conv_split(L, x, cd, P, stats):
     b = P[cd["b"]] if cd["b"] >= 0 else None
-    return ops().enc_conv_fwd(x, _split_weight(L, P[cd["w"]], x.shape[3] // 3), b, cd["stride"], cd["pad"], stats, True)
+    # the fp32 weight is split into [W_hi | W_hi | W_lo] by the per-call packing kernel (no
+    # cached copy: an optimizer step -- fused AdamW does not bump the parameter versions --
+    # must never leave a stale split weight behind)
+    return ops().enc_conv_fwd(x, P[cd["w"]], b, cd["stride"], cd["pad"], stats, True)
 
 
 def _forward_split(L, x0, P):

@@ -507,7 +507,8 @@ class _Step(torch.autograd.Function):
         df1 = ar.take("df1", t, 128)
         dcorr = torch.empty(P, CORR_PAD, device=dev, dtype=bf)
         dense = not ctx.has_corr_in and run.pyr is not None and bool(run.pyr.levels)
-        pgrad = run.pyr.grad_buffers() if dense else None  # allocated (zeroed) on the main stream
+        if dense and not run.pyr.deferrable():
+            run.pyr.grad_buffers()  # allocated (zeroed) on the main stream
         tail = _tail_stream(dev) if dense and TAIL_STREAM and dev.type == "cuda" else None
         if tail is not None:
             tail.wait_stream(torch.cuda.current_stream(dev))
@@ -519,7 +520,7 @@ class _Step(torch.autograd.Function):
             dgrad("convc2", dcf[:, :192], 3, 3, dc1, 256, mask=c1)
             dgrad("convc1", dc1, 1, 1, dcorr, CORR_PAD)
             if dense:
-                k.corr_lookup_backward_(pgrad, run.coords[t], dcorr.reshape(B, H, W, CORR_PAD), run.pyr.radius)
+                run.pyr.add_grad(run.coords[t], dcorr.reshape(B, H, W, CORR_PAD))
         run.done.add(t)
         run.early_weight_grads(t)
 

@@ -279,8 +279,7 @@ class _Step(torch.autograd.Function):
         if ctx.has_corr_in:
             d_corr_in = dcorr.reshape(B, H, W, CORR_PAD)
         elif run.pyr is not None and run.pyr.levels:
-            k.corr_lookup_backward_(run.pyr.grad_buffers(), run.coords[t], dcorr.reshape(B, H, W, CORR_PAD),
-                                    run.pyr.radius)
+            run.pyr.add_grad(run.coords[t], dcorr.reshape(B, H, W, CORR_PAD))
         d_net = _nchw(d_net if ctx.net_dtype == torch.bfloat16 else d_net.to(ctx.net_dtype), B, H, W)
         d_inp = None
         if t == 0:  # the last step backward to run (every other step's d net feeds it)

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--eval_pairs", type=int, default=16)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--max_disp", type=float, default=20.0)
+    ap.add_argument("--precision", choices=["bf16", "fp32"], default="bf16",
+                    help="fp32: no autocast (the reference's train_standard.sh recipe); bf16: AMP")
     args = ap.parse_args()
 
     from raft_ros_amd.data.synthetic import synthetic_batch
@@ -51,7 +53,7 @@ def main():
     dev = torch.device("cuda", 0)
     _ext.set_backend(args.impl)
     torch.manual_seed(args.seed)
-    model = RAFT(Namespace(small=False, mixed_precision=True, amp_dtype="bf16", dropout=0.0,
+    model = RAFT(Namespace(small=False, mixed_precision=args.precision == "bf16", amp_dtype="bf16", dropout=0.0,
                            channels_last=args.impl == "native")).to(dev)
     if args.impl == "native":
         model = model.to(memory_format=torch.channels_last)
@@ -76,7 +78,7 @@ def main():
     model.train()
     for step in range(args.steps + 1):
         if step % args.eval_every == 0:
-            rec = {"impl": args.impl, "step": step, "val_epe": round(evaluate(), 5),
+            rec = {"impl": args.impl, "precision": args.precision, "step": step, "val_epe": round(evaluate(), 5),
                    "elapsed_s": round(time.perf_counter() - t0, 1)}
             print(json.dumps(rec), flush=True)
         if step == args.steps:
@@ -90,7 +92,7 @@ def main():
         opt.step()
         sched.step()
         if step % 50 == 0:
-            print(json.dumps({"impl": args.impl, "step": step, "loss": round(loss.item(), 4),
+            print(json.dumps({"impl": args.impl, "precision": args.precision, "step": step, "loss": round(loss.item(), 4),
                               "train_epe": round(metrics["epe"].item(), 4)}), flush=True)
 
 

@@ -24,6 +24,8 @@ for step in ${STEPS_LIST:-infer1080 infer_sintel alt_kitti dense_kitti conv_nati
     dense_kitti) run dense_kitti 300 python bench.py --image_size 376 1248 --batch 3 --steps 10 --warmup 3 ;;
     conv_native) run conv_native 600 python scripts/convergence.py --impl native --steps ${CONV_STEPS:-2000} ;;
     conv_reference) run conv_reference 900 python scripts/convergence.py --impl reference --steps ${CONV_STEPS:-2000} ;;
+    conv_fp32) run conv_fp32 1100 python scripts/convergence.py --impl native --precision fp32 --steps ${CONV_STEPS:-3000} --eval_every 250 ;;
+    conv_bf16) run conv_bf16 600 python scripts/convergence.py --impl native --precision bf16 --steps ${CONV_STEPS:-3000} --eval_every 250 ;;
     ref_bench) run ref_bench 600 python bench.py --impl reference --steps 10 --warmup 3 ;;
     train) run train 300 python bench.py --steps 30 --warmup 5 ;;
     train_fp32) run train_fp32 400 python bench.py --fp32 --steps 10 --warmup 3 ;;

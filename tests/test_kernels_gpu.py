@@ -142,6 +142,44 @@ def test_corr_lookup_fwd(cuda, radius, shape):
     torch.testing.assert_close(got16.permute(0, 3, 1, 2).float(), want, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("radius,T", [(4, 12), (3, 35)])
+def test_lookup_grad_rows_match_per_lookup_backward(cuda, radius, T):
+    """Deferred lookup backward (one LDS-accumulated row pass over all T lookups, T > 32 in
+    two launches) == T per-lookup read-modify-write passes into a zeroed fp32 buffer; the
+    bf16 rows are those fp32 rows rounded once."""
+    from raft_ros_amd.ops.corr import _PyramidState
+
+    torch.manual_seed(12)
+    B, H, W, L = 2, 19, 45, 4
+    st = _PyramidState(L, radius)
+    sizes, off = [], 0
+    for l in range(L):
+        Hl, Wl = H >> l, W >> l
+        sizes.append((Hl, Wl, off))
+        off += -(-Wl // 16) * 16 * Hl
+    st.sizes, st.ld = sizes, off
+    win = (2 * radius + 1) ** 2
+    coords = [(ref.coords_grid(B, H, W, cuda) + 6 * torch.randn(B, 2, H, W, device=cuda)).contiguous()
+              for _ in range(T)]
+    coords[1][0, :, 2, 2] = float("nan")
+    grads = [torch.randn(B, H, W, L * win + 4, device=cuda).bfloat16() for _ in range(T)]
+    want = torch.zeros(B * H * W, off, device=cuda)
+    lv = st.views(want)
+    for c, g in zip(coords, grads):
+        _ops().corr_lookup_backward_(lv, c, g, radius)
+    segs = st.segments()
+    for dt in (torch.float32, torch.bfloat16):
+        got = torch.full((B * H * W, off), float("nan"), device=cuda, dtype=dt)
+        for i in range(0, T, 32):
+            _ops().corr_lookup_grad_rows(got, coords[i:i + 32], grads[i:i + 32], segs, radius, i > 0)
+        if dt == torch.float32:
+            torch.testing.assert_close(got, want, rtol=1e-6, atol=1e-6)
+        elif T <= 32:
+            assert torch.equal(got, want.bfloat16())
+        else:  # the second launch re-reads the bf16 partial rows: rounded twice
+            assert ((got.float() - want).norm() / want.norm()).item() < 4e-3
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("blocked", [True, False])
 def test_pyramid_operand_matches_torch_ops(cuda, dtype, blocked):

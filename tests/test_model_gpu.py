@@ -35,6 +35,34 @@ def test_native_matches_reference_path_fp32(cuda, small):
     assert epe <= 1e-2, epe
 
 
+def test_fp32_native_inference_tracks_trained_weights_and_bn_stats(cuda):
+    """fp32 inference on the native split-bf16 encoders / update block after the weights move
+    under a fused AdamW step (which does not bump parameter versions) and with non-trivial
+    BatchNorm running statistics == the module path (regression: a version-keyed split-weight
+    cache served the pre-step weights, val EPE 88 px in an fp32 convergence run)."""
+    torch.manual_seed(0)
+    args = Namespace(small=False, mixed_precision=False, channels_last=True)
+    model = RAFT(args).to(cuda).to(memory_format=torch.channels_last).eval()
+    i1, i2, _, _ = _pair(cuda)
+    with torch.no_grad():
+        model(i1, i2, iters=2, test_mode=True)  # warm every cache of the native path
+    opt = torch.optim.AdamW(model.parameters(), lr=5e-2, fused=True)
+    for p in model.parameters():
+        p.grad = torch.randn_like(p)
+    opt.step()
+    for m in model.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-2, 2)
+            m.running_var.uniform_(0.05, 8)
+    with torch.no_grad():
+        lo, up = model(i1, i2, iters=4, test_mode=True)
+        args.native_encoder = args.fused_update = False
+        lo_m, up_m = model(i1, i2, iters=4, test_mode=True)
+    epe = (up - up_m).norm(dim=1).mean().item()
+    print(f"\nEPE native split vs module path after an optimizer step: {epe:.2e} px")
+    assert epe <= 1e-2 * max(1.0, up_m.norm(dim=1).mean().item()), epe
+
+
 def test_training_step_runs_and_decreases_loss(cuda):
     from raft_ros_amd.train.loss import sequence_loss
 
