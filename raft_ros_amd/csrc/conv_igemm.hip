@@ -792,7 +792,13 @@ typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8;
 // 16-byte LDS read at a 32-bit LDS byte address
 __device__ __forceinline__ bf16x8 lds_read16(unsigned addr) { return *(const lds_bf16x8*)(uintptr_t)addr; }
 
-template <int BM, int BN, int NW = 4>
+// PROBE (measurement builds only, cfg 30..32 of the 128x128 tile): 1 = no MFMAs, 2 = no
+// DMA, 3 = neither -- what bounds a step (scripts/probe_conv5.py, profiles/r3_probe_conv5.log:
+// 0.59 us per step, 0.40 us of it without MFMAs and DMA; ~7.5 us per launch outside the loop).
+// A v6 schedule that spread the next step's fragment reads behind the MFMA sub-steps and
+// moved the barrier behind the first sub-step (4-stage ring, no LDS drain) measured 5-10%
+// slower on every shape (profiles/r3_probe_conv6.log) and was dropped.
+template <int BM, int BN, int NW = 4, int PROBE = 0>
 __global__ __launch_bounds__(NW * 64) void conv_fwd5_kernel(const ConvFwdArgs a, int strip_rows) {
   extern __shared__ __attribute__((aligned(1024))) __bf16 dsm[];
   // NW waves in an (NW/2) x 2 layout; NW = 8 puts two waves on every SIMD of the CU (one
@@ -875,6 +881,15 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd5_kernel(const ConvFwdArgs a,
   // ---- DMA issue state (step `is_t`): chunk, tap, weight k offset, stage
   int is_t = 0, is_cc = 0, is_tap = 0, is_stage = 0;
   auto issue_next = [&]() __attribute__((always_inline)) {
+    if constexpr ((PROBE & 2) != 0) {
+      ++is_t;
+      is_stage = is_stage == 2 ? 0 : is_stage + 1;
+      if (++is_tap == ntaps) {
+        is_tap = 0;
+        ++is_cc;
+      }
+      return;
+    }
     if (is_tap == 0) {
       const int c0 = is_cc * 64;
       __amdgpu_buffer_rsrc_t rs = r0;
@@ -949,7 +964,10 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd5_kernel(const ConvFwdArgs a,
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+        if constexpr ((PROBE & 1) != 0)
+          acc[i][j][0] += static_cast<float>(fa[i][s][0]) * static_cast<float>(fb[j][s][0]);
+        else
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
   };
 
   bf16x8 fa0[TM][4], fb0[TN][4], fa1[TM][4], fb1[TN][4];
@@ -1595,6 +1613,24 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   bool ok5 = a.KH * a.KW > 1 && a.Cin % 64 == 0 && a.N >= 64 && a.P < (1L << 30);
   for (int i = 0; i < a.nsrc; ++i) ok5 = ok5 && a.src[i].C % 64 == 0;
   int v5 = cfg >= 20 ? cfg : 0;
+  if (ok5 && cfg >= 30 && cfg <= 32) {  // measurement probes of the 128x128 / 8-wave tile
+    const int rows = (128 + (a.KH - 1) * a.W + a.KW - 1 + 7) / 8 * 8;
+    const long lds = fwd5_lds_bytes(128, 128, rows);
+    if (lds == 0) return hipErrorInvalidValue;
+    const dim3 grid(tiles(128, 128));
+#define RAFT_PROBE(PR)                                                     \
+  set_lds_limit((const void*)conv_fwd5_kernel<128, 128, 8, PR>, (int)lds); \
+  hipLaunchKernelGGL((conv_fwd5_kernel<128, 128, 8, PR>), grid, dim3(512), lds, s, a, rows)
+    if (cfg == 30) {
+      RAFT_PROBE(1);
+    } else if (cfg == 31) {
+      RAFT_PROBE(2);
+    } else {
+      RAFT_PROBE(3);
+    }
+#undef RAFT_PROBE
+    return hipGetLastError();
+  }
   if (ok5 && v5 == 0 && cfg == 0) {
     // 8-wave tiles (two waves per SIMD, no register spills) for every shape they win on
     // (scripts/bench_convs.py, profiles/r2_bench_convs_nw.log): 3x3 with N >= 192 -> 256x128,
