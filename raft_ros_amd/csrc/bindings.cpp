@@ -580,8 +580,10 @@ std::tuple<at::Tensor, at::Tensor> local_corr_backward(const at::Tensor& f1, con
 // ---------------------------------------------------------------- local correlation on MFMA
 // f1 (P, C) bf16 query rows; f2 (B, R, C) bf16 concatenated pooled fmap2 levels with
 // segs = [off, h, w] per level; coords (B, 2, H, W).
+// max_c: 256 for the backward (dF1 tile in registers); the forward also takes the 3C-channel
+// split-bf16 operands ([hi | lo | hi] . [hi | hi | lo], fp32-faithful inference)
 LocalCorrArgs local_mfma_args(const at::Tensor& f1, const at::Tensor& f2, const at::Tensor& coords,
-                              at::IntArrayRef segs, int64_t radius, double scale) {
+                              at::IntArrayRef segs, int64_t radius, double scale, long max_c = 256) {
   check_gpu(f1, "fmap1");
   check_gpu(f2, "fmap2");
   check_coords(coords);
@@ -589,8 +591,8 @@ LocalCorrArgs local_mfma_args(const at::Tensor& f1, const at::Tensor& f2, const 
                   f2.dim() == 3 && f1.is_contiguous() && f2.is_contiguous(),
               "raft_amd::local_corr_mfma: fmap1 (P, C) and fmap2 (B, R, C) must be contiguous bf16");
   const long B = coords.size(0), H = coords.size(2), W = coords.size(3), C = f1.size(1);
-  TORCH_CHECK(f1.size(0) == B * H * W && f2.size(0) == B && f2.size(2) == C && C % 64 == 0 && C <= 256,
-              "raft_amd::local_corr_mfma: shape mismatch (C must be a multiple of 64, <= 256)");
+  TORCH_CHECK(f1.size(0) == B * H * W && f2.size(0) == B && f2.size(2) == C && C % 64 == 0 && C <= max_c,
+              "raft_amd::local_corr_mfma: shape mismatch (C must be a multiple of 64, <= ", max_c, ")");
   TORCH_CHECK(radius >= 1 && radius <= 4, "raft_amd::local_corr_mfma: radius 1..4");
   TORCH_CHECK(segs.size() % 3 == 0 && segs.size() >= 3 && segs.size() <= 12, "raft_amd::local_corr_mfma: 1..4 levels");
   LocalCorrArgs a{};
@@ -609,7 +611,7 @@ LocalCorrArgs local_mfma_args(const at::Tensor& f1, const at::Tensor& f2, const 
 
 void local_corr_mfma(const at::Tensor& f1, const at::Tensor& f2, const at::Tensor& coords, at::IntArrayRef segs,
                      int64_t radius, double scale, const at::Tensor& out) {
-  LocalCorrArgs a = local_mfma_args(f1, f2, coords, segs, radius, scale);
+  LocalCorrArgs a = local_mfma_args(f1, f2, coords, segs, radius, scale, 768);
   const long win = (2 * radius + 1) * (2 * radius + 1);
   check_gpu(out, "out");
   TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.size(0) == f1.size(0) && out.size(1) >= a.levels * win &&

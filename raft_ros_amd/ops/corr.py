@@ -327,14 +327,24 @@ class _LocalCorrMFMA(torch.autograd.Function):
         return d1.to(ctx.dtypes[0]), d2.to(ctx.dtypes[1]), None, None, None, None
 
 
+def _split_cat(x: torch.Tensor, planes) -> torch.Tensor:
+    """fp32 rows (..., C) -> bf16 (..., 3C): the hi (0) / lo (1) bf16 parts in ``planes`` order."""
+    xf = x.float()
+    hi = xf.to(torch.bfloat16)
+    lo = (xf - hi.float()).to(torch.bfloat16)
+    return torch.cat([(hi, lo)[p] for p in planes], dim=-1).contiguous()
+
+
 class LocalCorrPyramid:
     """Memory-efficient correlation: no HW x HW volume is ever stored.
 
     Pools fmap2 (not the volume; equivalent by linearity) into ``num_levels`` levels once,
     and per lookup computes the (2r+1)^2 window correlations on the fly.  Under AMP (bf16)
     every level is done by one MFMA kernel over 8x4 query tiles (``local_corr_mfma``);
-    without AMP (``split=True``) the exact fp32 kernel runs.  Both train (the reference's
-    alt_cuda_corr path is forward-only, core/corr.py:86).
+    without AMP (``split=True``) inference runs the same kernel on split-bf16 operands
+    (f1 as [hi | lo | hi], the pooled f2 as [hi | hi | lo] along K: one GEMM computes
+    hi.hi + lo.hi + hi.lo, fp32-faithful) and fp32 training the exact scalar fp32 kernel.
+    Both train (the reference's alt_cuda_corr path is forward-only, core/corr.py:86).
     """
 
     def __init__(self, fmap1: torch.Tensor, fmap2: torch.Tensor, num_levels: int = 4, radius: int = 4,
@@ -346,10 +356,13 @@ class LocalCorrPyramid:
         self.C = C
         self.shape = (B, C, H, W)
         self.scale = 1.0 / math.sqrt(C)
-        self.mfma = self.native and not split and C % 64 == 0 and C <= 256 and radius <= 4
+        mfma_ok = self.native and C % 64 == 0 and C <= 256 and radius <= 4
+        # split-bf16 MFMA: fp32-faithful, forward only (the backward keeps the exact kernel)
+        self.split_mfma = mfma_ok and split and not torch.is_grad_enabled()
+        self.mfma = mfma_ok and (not split or self.split_mfma)
         self.fmap1, self.fmap2 = fmap1, fmap2
         if self.mfma:
-            self.f1 = fmap1.detach().permute(0, 2, 3, 1).reshape(B * H * W, C).to(torch.bfloat16).contiguous()
+            f1 = fmap1.detach().permute(0, 2, 3, 1).reshape(B * H * W, C)
             segs, off = [], 0
             for l in range(num_levels):
                 Hl, Wl = H >> l, W >> l  # repeated 2x2 floor pooling
@@ -357,7 +370,13 @@ class LocalCorrPyramid:
                 off += _pad_to(Hl * Wl, 8)
             self.segs = segs
             # pooled fmap2 levels, (B, rows, C): one HIP launch (== _concat_levels(_pooled))
-            self.f2cat = ops().pyramid_operand(fmap2.detach(), segs, off, False, False).to(torch.bfloat16)
+            f2cat = ops().pyramid_operand(fmap2.detach(), segs, off, False, False)
+            if self.split_mfma:
+                self.f1 = _split_cat(f1, (0, 1, 0))
+                self.f2cat = _split_cat(f2cat, (0, 0, 1))
+            else:
+                self.f1 = f1.to(torch.bfloat16).contiguous()
+                self.f2cat = f2cat.to(torch.bfloat16)
         elif self.native:
             dt = feature_dtype or torch.float32
             self.f1 = fmap1.permute(0, 2, 3, 1).to(dt).contiguous()

@@ -31,6 +31,9 @@ for step in ${STEPS_LIST:-infer1080 infer_sintel alt_kitti dense_kitti conv_nati
     train_fp32) run train_fp32 400 python bench.py --fp32 --steps 10 --warmup 3 ;;
     infer_ros_fp32) run infer_ros_fp32 300 python bench.py --mode infer --fp32 --image_size 440 1024 --iters 20 --batch 1 --steps 20 --warmup 3 ;;
     infer_ros_bf16) run infer_ros_bf16 300 python bench.py --mode infer --image_size 440 1024 --iters 20 --batch 1 --steps 20 --warmup 3 ;;
+    alt_ros_fp32) run alt_ros_fp32 300 python bench.py --mode infer --fp32 --alternate_corr --image_size 440 1024 --iters 20 --batch 1 --steps 20 --warmup 3 ;;
+    train_sintel) run train_sintel 300 python bench.py --image_size 368 768 --batch 6 --steps 20 --warmup 5 ;;
+    train_full) run train_full 300 python bench.py --image_size 440 1024 --batch 6 --steps 10 --warmup 3 ;;
     prof_fp32) run prof_fp32 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_fp32 -o run -- python3 bench.py --mode infer --fp32 --image_size 440 1024 --iters 20 --batch 1 --steps 5 --warmup 2 ;;
     prof_train) run prof_train 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_train -o run -- python3 bench.py --steps 8 --warmup 4 ;;
   esac

@@ -382,6 +382,29 @@ def test_local_corr_mfma_matches_dense_reference(cuda, jitter):
     assert padded.shape == (B, H, W, 328) and (padded[..., 324:] == 0).all()
 
 
+@pytest.mark.parametrize("jitter", [3.0, 40.0])
+def test_local_corr_split_mfma_inference_is_fp32_faithful(cuda, jitter):
+    """fp32 inference of the alternate correlation on the MFMA kernel with split-bf16 operands
+    ([hi | lo | hi] . [hi | hi | lo] along K) == the fp32 dense reference lookup to ~1e-5."""
+    torch.manual_seed(9)
+    from raft_ros_amd.ops.corr import LocalCorrPyramid
+
+    B, C, H, W, r = 2, 256, 23, 37, 4
+    f1 = torch.randn(B, C, H, W, device=cuda)
+    f2 = torch.randn(B, C, H, W, device=cuda)
+    coords = ref.coords_grid(B, H, W, cuda) + jitter * torch.randn(B, 2, H, W, device=cuda)
+    with torch.no_grad():
+        lc = LocalCorrPyramid(f1, f2, 4, r, split=True)
+        assert lc.mfma and lc.split_mfma
+        out = lc(coords)
+        want = ref.pyramid_lookup(ref.build_pyramid(ref.corr_volume(f1, f2), 4), coords, r)
+    err = ((out - want).norm() / want.norm()).item()
+    print(f"\nsplit-MFMA local corr rel err {err:.2e}")
+    assert err < 3e-5
+    # with autograd the exact scalar kernel keeps training fp32
+    assert not LocalCorrPyramid(f1.requires_grad_(True), f2, 4, r, split=True).mfma
+
+
 @pytest.mark.parametrize("hw", [(1, 1), (5, 7), (46, 62)])
 def test_upflow8_matches_reference_fwd_bwd(hw):
     from raft_ros_amd.ops import reference as ref
