@@ -34,6 +34,7 @@
 #include "kernel_abi.h"
 
 #include <algorithm>
+#include <utility>
 
 namespace raft_amd {
 
@@ -415,21 +416,21 @@ __device__ __forceinline__ void load8(const __bf16* row, int S, float (&x)[8]) {
 // Shared epilogue of the forward kernels: the fp32 accumulators go through an LDS tile
 // (et, BM x (BN+4) floats) so each thread finishes 8 consecutive output channels of one
 // pixel with 16-byte accesses; applies alpha/bias and the fused epilogue selected by a.epi.
-template <int BM, int BN, int TM, int TN, int NW = 4>
+template <int BM, int BN, int TM, int TN, int NW = 4, int WGN = 2>
 __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f32x16 (&acc)[TM][TN], int m0,
                                              int n0, int P, int Nn) {
   constexpr int EPI_LD = BN + 4;  // fp32 epilogue tile row pitch
-  constexpr int NT = NW * 64;     // threads; waves are laid out (NW/2) x 2 over the tile
+  constexpr int NT = NW * 64;     // threads; waves are laid out (NW/WGN) x WGN over the tile
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WGN, wn = wave % WGN;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = wm * (BM / (NW / 2)) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int col = wn * (BN / 2) + j * 32 + (lane & 31);
+        const int row = wm * (BM / (NW / WGN)) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = wn * (BN / WGN) + j * 32 + (lane & 31);
         et[row * EPI_LD + col] = acc[i][j][r];
       }
   __syncthreads();
@@ -1030,6 +1031,288 @@ inline long fwd5_lds_bytes(int BM, int BN, int strip_rows) {
   return need <= 160 * 1024 ? need : 0;
 }
 
+// ============================================================================ forward v6 (lean halo strip)
+// Same operand reuse as v5 (one LDS strip per 64-channel chunk serves every tap, 3-stage
+// weight ring, LDS-DMA), re-built for instruction issue: a v5 K step issued ~185 instructions
+// per wave (~100 of them scalar bookkeeping of the runtime tap/chunk state machine) and
+// 2.5 LDS-DMA pieces around 8 MFMAs, so the waves were issue-bound (the MFMA-, DMA- and
+// read-free probes of profiles/r3_probe_conv5.log each removed only part of the step).  v6:
+//   * taps are template parameters: the tap loop is fully unrolled, the strip parity and the
+//     weight-ring stage of every step are compile-time, so LDS addresses are per-lane
+//     registers computed once (A: one base per tap and 32-row fragment with out-of-image
+//     taps redirected to a zero row; B: one per sub-step) plus immediate offsets;
+//   * 64x64 wave tiles (16 MFMAs per 64-deep step, 1 KB of LDS fragment reads per MFMA);
+//   * fragments of step t+1 are read right after step t's barrier, behind all 16 MFMAs of
+//     step t (one full step of latency cover);
+//   * tile shapes with fewer DMA pieces per MAC: 256x64 (4 waves, 4x1) moves 32% fewer bytes
+//     into the CU per MAC than 128x128 on a 3x3 conv (weights 8 KB + strip ~5 KB per 1 MMAC
+//     step vs 16 + 3.6 KB).
+// LDS (bytes): [0, RING) weight ring (NS stages of BN rows x 128 B), then two strip buffers of
+// SB bytes; the last 128-B row of each strip buffer is a zero row.
+constexpr int kLdsMax = 160 * 1024;
+
+template <int BN, int WGN, int NT>
+struct Fwd6Cfg {
+  static constexpr int NS = 3;                        // weight ring stages
+  static constexpr int U = (NT % 3 == 0) ? 2 : 6;     // chunks per unrolled block: U * NT % 6 == 0,
+                                                      // so stage (step % 3), register set (step & 1)
+                                                      // and strip parity (chunk & 1) are compile-time
+  static constexpr int RING = NS * BN * 128;
+  static constexpr int SB0 = ((kLdsMax - RING) / 2) & ~127;
+  static constexpr int SB = SB0 < 65408 ? SB0 : 65408;  // odd-chunk strip = +SB immediate offset
+  static constexpr int MAX_ROWS = SB / 128 - 1;         // strip rows (the last row is the zero row)
+  static constexpr int LDS = RING + 2 * SB;
+};
+
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_le(int n) {
+  // s_waitcnt needs an immediate: dispatch a runtime count (uniform) to the nearest
+  // immediate <= n (waiting for more than needed is safe)
+  if constexpr (N <= 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (n >= N) wait_vmcnt<N>();
+    else wait_vmcnt_le<N - 1>(n);
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, int KH, int KW, int SCHED = 1>
+__global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwdArgs a, int strip_rows) {
+  constexpr int NW = WGM * WGN;
+  constexpr int WM = BM / WGM, WN = BN / WGN;  // wave tile
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int NT = KH * KW;
+  using CF = Fwd6Cfg<BN, WGN, NT>;
+  constexpr int NS = CF::NS, SB = CF::SB, RING = CF::RING;
+  constexpr int BI = BN / (8 * NW);  // weight pieces (8 rows x 128 B) per wave per step
+  constexpr int BSTAGE = BN * 128;
+  static_assert(BI >= 1 && TM >= 1 && TN >= 1 && WM % 32 == 0 && WN % 32 == 0, "tile");
+  static_assert((NS - 1) * BSTAGE + (TN - 1) * 4096 < 65536, "ring offsets must fit the ds_read immediate");
+  extern __shared__ __attribute__((aligned(1024))) __bf16 dsm[];
+  char* const lds = reinterpret_cast<char*>(dsm);
+  const unsigned lds0 = (unsigned)(reinterpret_cast<uintptr_t>(dsm) & 0xffffffffu);
+
+  const int Cin = a.Cin, Kpad = a.Kpad, H = a.H, W = a.W, PH = a.PH, PW = a.PW;
+  const int P = (int)a.P;
+  const int Nn = a.N;
+  const int sc0 = a.src[0].C, sc1 = a.src[1].C;
+  const int nsrc = a.nsrc;
+  const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.src[0].ptr, (unsigned)(a.P * a.src[0].stride * 2));
+  const __amdgpu_buffer_rsrc_t r1 =
+      make_rsrc(nsrc > 1 ? a.src[1].ptr : a.src[0].ptr, nsrc > 1 ? (unsigned)(a.P * a.src[1].stride * 2) : 0u);
+  const __amdgpu_buffer_rsrc_t r2 =
+      make_rsrc(nsrc > 2 ? a.src[2].ptr : a.src[0].ptr, nsrc > 2 ? (unsigned)(a.P * a.src[2].stride * 2) : 0u);
+  const unsigned st0 = (unsigned)a.src[0].stride * 2, st1 = (unsigned)a.src[1].stride * 2,
+                 st2 = (unsigned)a.src[2].stride * 2;
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.wt, (unsigned)((long)Nn * Kpad * 2));
+
+  const int tilesN = (Nn + BN - 1) / BN;
+  const int tilesM = (P + BM - 1) / BM;
+  const int wg = xcd_remap(blockIdx.x, tilesM * tilesN);
+  const int tm = wg / tilesN, tn = wg - (wg / tilesN) * tilesN;
+  const int m0 = tm * BM;
+  const int n0 = tn * BN;
+  const int halo_lo = PH * W + PW;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int lrow = lane >> 3, lpc = lane & 7;
+  const int fr = lane & 31, fh = lane >> 5;
+  // zero rows (the last row of each strip buffer)
+  if (tid < 16) {
+    const int b = tid >> 3, c = tid & 7;
+    *reinterpret_cast<u32x4*>(lds + RING + b * SB + (SB - 128) + c * 16) = u32x4{0, 0, 0, 0};
+  }
+
+  // A: per (tap, 32-row fragment) LDS byte address of this lane's row in an even-chunk strip,
+  // XOR-ready (sub-step s reads addr ^ (s << 5)); out-of-image taps point at the zero row
+  unsigned abase[NT][TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int frow = wm * WM + i * 32 + fr;
+    const int p = m0 + frow;
+    int py = -(1 << 20), px = -(1 << 20);
+    if (p < P) {
+      const int rem = p % (H * W);
+      py = rem / W;
+      px = rem - py * W;
+    }
+#pragma unroll
+    for (int tap = 0; tap < NT; ++tap) {
+      const int ky = tap / KW, kx = tap % KW;
+      const int row = frow + ky * W + kx;
+      const bool ok = (unsigned)(py + ky - PH) < (unsigned)H && (unsigned)(px + kx - PW) < (unsigned)W;
+      abase[tap][i] = ok ? lds0 + RING + (unsigned)row * 128u + ((((row >> 1) & 7) ^ fh) << 4)
+                         : lds0 + RING + (SB - 128);
+    }
+  }
+  // B: per sub-step LDS byte offset of this lane's weight row within a stage
+  unsigned bb[4];
+  {
+    const int row = wn * WN + fr;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) bb[s] = lds0 + (unsigned)(row * 128) + (((((row >> 1) & 7) ^ fh) << 4) ^ (s << 5));
+  }
+  // weight DMA pieces of this wave: rows (wave * BI + i) * 8 + lrow of the stage
+  unsigned bvoff[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int row = (wave * BI + i) * 8 + lrow;
+    bvoff[i] = (n0 + row < Nn) ? (unsigned)((n0 + row) * Kpad * 2 + swz(row, lpc) * 16) : kOOB;
+  }
+  const int nchunks = Cin / 64;
+  const int spw = strip_rows / (8 * NW);  // strip pieces per wave (strip_rows % (8 NW) == 0)
+  const unsigned sswz = (unsigned)((lpc ^ (((wave & 1) << 2) | (lrow >> 1))) * 16);
+  const int pstrip = m0 - halo_lo + wave * 8 + lrow;  // pixel of this lane's row in piece 0
+
+  // ---- DMA issue of a step: chunk cu (runtime), tap TU, ring stage SU, strip parity HU
+  auto issue = [&](int cu, auto tuc, auto suc, auto huc) __attribute__((always_inline)) {
+    constexpr int TU = decltype(tuc)::value, SU = decltype(suc)::value, HU = decltype(huc)::value;
+    const unsigned k0b = (unsigned)((TU * Cin + cu * 64) * 2);
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      bload16(rw, reinterpret_cast<__bf16*>(lds + SU * BSTAGE + (wave * BI + i) * 1024), bvoff[i], k0b);
+    if constexpr (TU == 0) {
+      const int c0 = cu * 64;
+      __amdgpu_buffer_rsrc_t rs = r0;
+      unsigned st = st0, soff = (unsigned)c0 * 2;
+      if (c0 >= sc0 + sc1) {
+        rs = r2; st = st2; soff = (unsigned)(c0 - sc0 - sc1) * 2;
+      } else if (c0 >= sc0) {
+        rs = r1; st = st1; soff = (unsigned)(c0 - sc0) * 2;
+      }
+      char* const sbuf = lds + RING + HU * SB + wave * 1024;
+      for (int q = 0; q < spw; ++q) {
+        const int p = pstrip + q * NW * 8;
+        const unsigned voff = (unsigned)p < (unsigned)P ? (unsigned)p * st + sswz : kOOB;
+        bload16(rs, reinterpret_cast<__bf16*>(sbuf + q * NW * 1024), voff, soff);
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  bf16x8 fa[2][TM][4], fb[2][TN][4];
+  // fragments of the step with in-block index G (tap G % NT, stage G % 3, strip parity
+  // (G / NT) & 1) into register set G & 1
+  // sub-step s (16 k) of the fragments of the step with in-block index G
+  auto read_s = [&](auto gc, auto sc) __attribute__((always_inline)) {
+    constexpr int G = decltype(gc)::value, s = decltype(sc)::value;
+    constexpr int T = G % NT, R = G & 1;
+    constexpr unsigned AOFF = ((G / NT) & 1) ? (unsigned)SB : 0u;
+    constexpr unsigned BOFF = (unsigned)((G % NS) * BSTAGE);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa[R][i][s] = lds_read16((abase[T][i] ^ (unsigned)(s << 5)) + AOFF);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[R][j][s] = lds_read16(bb[s] + BOFF + (unsigned)(j * 4096));
+  };
+  auto read = [&](auto gc) __attribute__((always_inline)) {
+    static_for<4>([&](auto sc) __attribute__((always_inline)) { read_s(gc, sc); });
+  };
+  auto mfma_s = [&](auto rc, auto sc) __attribute__((always_inline)) {
+    constexpr int R = decltype(rc)::value, s = decltype(sc)::value;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[R][i][s], fb[R][j][s], acc[i][j], 0, 0, 0);
+  };
+  // issue the step with in-block index GU of the block starting at chunk cb (GU may run past
+  // the block: stage and parity stay compile-time because U * NT % 6 == 0)
+  auto issue_g = [&](int cb, auto guc) __attribute__((always_inline)) {
+    constexpr int GU = decltype(guc)::value;
+    const int cu = cb + GU / NT;
+    if (cu < nchunks)
+      issue(cu, std::integral_constant<int, GU % NT>{}, std::integral_constant<int, GU % NS>{},
+            std::integral_constant<int, (GU / NT) & 1>{});
+  };
+
+  // prologue: steps 0, 1, 2 in flight (NT >= 5: all in chunk 0), fragments of step 0
+  issue_g(0, std::integral_constant<int, 0>{});
+  issue_g(0, std::integral_constant<int, 1>{});
+  issue_g(0, std::integral_constant<int, 2>{});
+  wait_vmcnt<2 * BI>();
+  __syncthreads();  // also publishes the zero rows
+  read(std::integral_constant<int, 0>{});
+
+  // one K step: in-block index G of the block starting at chunk cb
+  auto step = [&](int cb, auto gc) __attribute__((always_inline)) {
+    constexpr int G = decltype(gc)::value;
+    const bool has1 = cb + (G + 1) / NT < nchunks;  // step t+1 exists
+    const bool has2 = cb + (G + 2) / NT < nchunks;  // step t+2 exists (issued one step ago)
+    // sched_barrier(0) fences keep the compiler from sinking each MFMA next to its fragment
+    // read (it would otherwise trade the one-step read-ahead for registers)
+    __builtin_amdgcn_sched_barrier(0);
+    if (has1) {
+      // step t+1 landed; step t+2 may stay in flight (BI pieces, + the strip when it opens a chunk)
+      if (!has2) wait_vmcnt<0>();
+      else if constexpr ((G + 2) % NT == 0) wait_vmcnt_le<40>(BI + spw);
+      else wait_vmcnt<BI>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // step t+3 into the stage of step t (its fragments were read before this barrier)
+      issue_g(cb, std::integral_constant<int, G + 3>{});
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (SCHED == 1) {
+        // MFMA sub-step s of step t, then the sub-step-s reads of step t+1: every MFMA group
+        // precedes the reads issued after it, so the compiler's lgkmcnt (at most 15 in flight)
+        // never holds an MFMA behind this step's new reads
+        static_for<4>([&](auto sc) __attribute__((always_inline)) {
+          mfma_s(std::integral_constant<int, G & 1>{}, sc);
+          __builtin_amdgcn_sched_barrier(0);
+          read_s(std::integral_constant<int, G + 1>{}, sc);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      } else {
+        // all reads of step t+1 first, then the 16 MFMAs of step t
+        read(std::integral_constant<int, G + 1>{});
+        __builtin_amdgcn_sched_barrier(0);
+        static_for<4>([&](auto sc) __attribute__((always_inline)) {
+          mfma_s(std::integral_constant<int, G & 1>{}, sc);
+        });
+      }
+    } else {
+      static_for<4>([&](auto sc) __attribute__((always_inline)) {
+        mfma_s(std::integral_constant<int, G & 1>{}, sc);
+      });
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int cb = 0; cb < nchunks; cb += CF::U) {
+    static_for<CF::U * NT>([&](auto gc) __attribute__((always_inline)) {
+      constexpr int G = decltype(gc)::value;
+      if (cb + G / NT < nchunks) step(cb, gc);
+    });
+  }
+  wait_vmcnt<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  fwd_epilogue<BM, BN, TM, TN, NW, WGN>(a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn);
+}
+
+// strip rows of conv_fwd6 for a shape (0 if it does not fit)
+inline int fwd6_strip_rows(int BM, int NW, int KH, int KW, int W, int max_rows) {
+  const int need = BM + (KH - 1) * W + KW - 1;
+  const int rows = (need + 8 * NW - 1) / (8 * NW) * (8 * NW);
+  return rows <= max_rows ? rows : 0;
+}
+
 // ============================================================================ wgrad helpers
 constexpr int WBK = kWgradBK;
 
@@ -1577,6 +1860,39 @@ __global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
 
 }  // namespace
 
+namespace {
+template <int BM, int BN, int WGM, int WGN, int KH, int KW, int SCHED>
+bool launch_fwd6_t(const ConvFwdArgs& a, hipStream_t s) {
+  using CF = Fwd6Cfg<BN, WGN, KH * KW>;
+  constexpr int NW = WGM * WGN;
+  const int rows = fwd6_strip_rows(BM, NW, KH, KW, a.W, CF::MAX_ROWS);
+  if (rows == 0) return false;
+  const dim3 grid((unsigned)(((a.P + BM - 1) / BM) * ((a.N + BN - 1) / BN)));
+  set_lds_limit((const void*)conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, SCHED>, CF::LDS);
+  hipLaunchKernelGGL((conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, SCHED>), grid, dim3(NW * 64), CF::LDS, s, a,
+                     rows);
+  return true;
+}
+template <int BM, int BN, int WGM, int WGN, int SCHED = 1>
+bool launch_fwd6_taps(const ConvFwdArgs& a, hipStream_t s) {
+  if (a.KH == 3 && a.KW == 3) return launch_fwd6_t<BM, BN, WGM, WGN, 3, 3, SCHED>(a, s);
+  if (a.KH == 1 && a.KW == 5) return launch_fwd6_t<BM, BN, WGM, WGN, 1, 5, SCHED>(a, s);
+  if (a.KH == 5 && a.KW == 1) return launch_fwd6_t<BM, BN, WGM, WGN, 5, 1, SCHED>(a, s);
+  return false;
+}
+bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
+  switch (cfg) {
+    case 40: return launch_fwd6_taps<128, 128, 2, 2>(a, s);
+    case 41: return launch_fwd6_taps<256, 64, 4, 1>(a, s);
+    case 43: return launch_fwd6_taps<128, 128, 2, 2, 0>(a, s);
+    case 44: return launch_fwd6_taps<256, 64, 4, 1, 0>(a, s);
+    case 45: return launch_fwd6_taps<256, 128, 2, 2>(a, s);
+    case 46: return launch_fwd6_taps<256, 128, 2, 2, 0>(a, s);
+    default: return false;
+  }
+}
+}  // namespace
+
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   if (a.P == 0 || a.N == 0) return hipSuccess;
   if (a.Kpad % FBK != 0) return hipErrorInvalidValue;
@@ -1630,6 +1946,16 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
     }
 #undef RAFT_PROBE
     return hipGetLastError();
+  }
+  if (cfg >= 40 && cfg <= 46) {
+    // v6 (measurement / forced): 40 = 128x128 (2x2 waves of 64x64), 41 = 256x64 (4x1 waves of
+    // 64x64), 45 = 256x128 (2x2 waves of 128x64); 43 / 44 / 46: the same tiles with all
+    // next-step reads issued before the step's MFMAs
+    const int taps = a.KH * a.KW;
+    const bool shape6 = (a.KH == 3 && a.KW == 3) || (taps == 5 && (a.KH == 1 || a.KW == 1));
+    if (!ok5 || !shape6 || a.PH != a.KH / 2 || a.PW != a.KW / 2) return hipErrorInvalidValue;
+    if (launch_conv_fwd6(a, cfg, s)) return hipGetLastError();
+    return hipErrorInvalidValue;
   }
   if (ok5 && v5 == 0 && cfg == 0) {
     // 8-wave tiles (two waves per SIMD, no register spills) for every shape they win on

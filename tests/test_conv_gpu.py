@@ -169,7 +169,7 @@ def test_gru_epilogues(cuda):
     assert _rel(_from_pm(hn, B, H, W), hn_ref) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 1, 8, 9])
+@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 1, 8, 9, 40, 41, 43, 44])
 @pytest.mark.parametrize("segs,cout,kh,kw,hw", [
     ([(256, 256)], 192, 3, 3, (46, 62)),
     ([(128, 128), (128, 128), (128, 128)], 256, 1, 5, (46, 62)),
@@ -178,8 +178,8 @@ def test_gru_epilogues(cuda):
     ([(64, 64)], 128, 3, 3, (17, 21)),
 ])
 def test_fwd_every_variant_full_size(cuda, cfg, segs, cout, kh, kw, hw):
-    """Every forward kernel variant (v5 halo-strip tiles, v4 tiles, generic) at RAFT sizes
-    vs an fp32 conv2d."""
+    """Every forward kernel variant (v6 / v5 halo-strip tiles, v4 tiles, generic) at RAFT
+    sizes vs an fp32 conv2d."""
     torch.manual_seed(4)
     B, (H, W) = 8, hw
     P = B * H * W
@@ -241,7 +241,7 @@ def test_wgrad_params_periodic_source_and_param_layout(cuda):
     assert torch.equal(gz, gz2)
 
 
-@pytest.mark.parametrize("cfg", [0, 8, 25, 26])
+@pytest.mark.parametrize("cfg", [0, 8, 25, 26, 40, 41])
 def test_gru_backward_epilogues_match_unfused(cuda, cfg):
     """EPI_GRU_BWD_A / _B / _LAST (gate backward fused into the data-gradient epilogue) vs
     the plain EPI_GRAD store followed by the separate gru_bwd_a / gru_bwd_b / masked_cast
