@@ -1214,6 +1214,9 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   auto read_s = [&](auto gc, auto sc) __attribute__((always_inline)) {
     constexpr int G = decltype(gc)::value, s = decltype(sc)::value;
     constexpr int T = G % NT, R = G & 1;
+    if constexpr ((SCHED & 8) != 0) {  // probe: no fragment reads after the prologue
+      if (G > 0) return;
+    }
     constexpr unsigned AOFF = ((G / NT) & 1) ? (unsigned)SB : 0u;
     constexpr unsigned BOFF = (unsigned)((G % NS) * BSTAGE);
 #pragma unroll
@@ -1230,12 +1233,18 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[R][i][s], fb[R][j][s], acc[i][j], 0, 0, 0);
+        if constexpr ((SCHED & 2) != 0)  // probe: no MFMAs
+          acc[i][j][0] += static_cast<float>(fa[R][i][s][0]) * static_cast<float>(fb[R][j][s][0]);
+        else
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[R][i][s], fb[R][j][s], acc[i][j], 0, 0, 0);
   };
   // issue the step with in-block index GU of the block starting at chunk cb (GU may run past
   // the block: stage and parity stay compile-time because U * NT % 6 == 0)
   auto issue_g = [&](int cb, auto guc) __attribute__((always_inline)) {
     constexpr int GU = decltype(guc)::value;
+    if constexpr ((SCHED & 4) != 0) {  // probe: no DMA after the prologue
+      if (GU > 2 || cb > 0) return;
+    }
     const int cu = cb + GU / NT;
     if (cu < nchunks)
       issue(cu, std::integral_constant<int, GU % NT>{}, std::integral_constant<int, GU % NS>{},
@@ -1264,12 +1273,12 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
       else if constexpr ((G + 2) % NT == 0) wait_vmcnt_le<40>(BI + spw);
       else wait_vmcnt<BI>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      if constexpr ((SCHED & 16) == 0) __builtin_amdgcn_s_barrier();  // (probe 16: none)
       __builtin_amdgcn_sched_barrier(0);
       // step t+3 into the stage of step t (its fragments were read before this barrier)
       issue_g(cb, std::integral_constant<int, G + 3>{});
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (SCHED == 1) {
+      if constexpr ((SCHED & 1) == 1) {
         // MFMA sub-step s of step t, then the sub-step-s reads of step t+1: every MFMA group
         // precedes the reads issued after it, so the compiler's lgkmcnt (at most 15 in flight)
         // never holds an MFMA behind this step's new reads
@@ -1303,7 +1312,18 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   wait_vmcnt<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  fwd_epilogue<BM, BN, TM, TN, NW, WGN>(a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn);
+  if constexpr ((SCHED & 32) != 0) {  // probe: no epilogue (one conditional store keeps acc live)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += acc[i][j][r];
+    if (t == 1234.5f) static_cast<float*>(a.out)[0] = t;
+  } else {
+    fwd_epilogue<BM, BN, TM, TN, NW, WGN>(a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn);
+  }
 }
 
 // strip rows of conv_fwd6 for a shape (0 if it does not fit)
@@ -1880,6 +1900,12 @@ bool launch_fwd6_taps(const ConvFwdArgs& a, hipStream_t s) {
   if (a.KH == 5 && a.KW == 1) return launch_fwd6_t<BM, BN, WGM, WGN, 5, 1, SCHED>(a, s);
   return false;
 }
+template <int SCHED>
+bool launch_fwd6_probe(const ConvFwdArgs& a, hipStream_t s) {
+  if (a.KH == 3 && a.KW == 3) return launch_fwd6_t<256, 64, 4, 1, 3, 3, SCHED>(a, s);
+  if (a.KH == 1 && a.KW == 5) return launch_fwd6_t<256, 64, 4, 1, 1, 5, SCHED>(a, s);
+  return false;
+}
 bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
   switch (cfg) {
     case 40: return launch_fwd6_taps<128, 128, 2, 2>(a, s);
@@ -1888,6 +1914,14 @@ bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
     case 44: return launch_fwd6_taps<256, 64, 4, 1, 0>(a, s);
     case 45: return launch_fwd6_taps<256, 128, 2, 2>(a, s);
     case 46: return launch_fwd6_taps<256, 128, 2, 2, 0>(a, s);
+    // measurement probes of the 256x64 tile (scripts/bench_conv6.py --probe): no MFMA / no
+    // in-loop DMA / no fragment reads / no barrier / no epilogue / bare loop
+    case 47: return launch_fwd6_probe<1 | 2>(a, s);
+    case 48: return launch_fwd6_probe<1 | 4>(a, s);
+    case 49: return launch_fwd6_probe<1 | 8>(a, s);
+    case 50: return launch_fwd6_probe<1 | 16>(a, s);
+    case 51: return launch_fwd6_probe<1 | 32>(a, s);
+    case 52: return launch_fwd6_probe<1 | 2 | 4 | 8 | 16>(a, s);
     default: return false;
   }
 }
@@ -1947,7 +1981,7 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
 #undef RAFT_PROBE
     return hipGetLastError();
   }
-  if (cfg >= 40 && cfg <= 46) {
+  if (cfg >= 40 && cfg <= 52) {
     // v6 (measurement / forced): 40 = 128x128 (2x2 waves of 64x64), 41 = 256x64 (4x1 waves of
     // 64x64), 45 = 256x128 (2x2 waves of 128x64); 43 / 44 / 46: the same tiles with all
     // next-step reads issued before the step's MFMAs

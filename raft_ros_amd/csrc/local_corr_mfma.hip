@@ -401,7 +401,10 @@ hipError_t launch_fixed_to_float(const long long* in, float* out, long n, const 
 }
 
 hipError_t launch_local_corr_mfma(const LocalCorrArgs& a, bool backward, hipStream_t s) {
-  if (a.r > 4 || a.C % KC != 0 || a.C > 256 || a.levels < 1 || a.levels > 4) return hipErrorInvalidValue;
+  // the forward loops over any number of 64-channel slices (split-bf16 inference: C = 3 x 256,
+  // [hi | lo | hi] . [hi | hi | lo]); the backward keeps dF1 of <= 4 slices in registers
+  if (a.r > 4 || a.C % KC != 0 || a.C > (backward ? 256 : 768) || a.levels < 1 || a.levels > 4)
+    return hipErrorInvalidValue;
   const long tiles = (long)a.B * ((a.H + TY - 1) / TY) * ((a.W + TX - 1) / TX);
   if (tiles == 0) return hipSuccess;
   if (backward)

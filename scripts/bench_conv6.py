@@ -44,11 +44,16 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--hw", type=int, nargs=2, default=[46, 62])
     ap.add_argument("--only", default="")
+    ap.add_argument("--probe", action="store_true",
+                    help="256x64 probes: 41 full, 47 no MFMA, 48 no DMA, 49 no reads, 50 no barrier, "
+                         "51 no epilogue, 52 bare loop")
     args = ap.parse_args()
     dev = torch.device("cuda")
     B, (H, W) = args.batch, args.hw
     P = B * H * W
     cfgs = [int(c) for c in args.cfgs.split(",")]
+    if args.probe:
+        cfgs = [41, 47, 48, 49, 50, 51, 52]
     names = args.only.split(",") if args.only else list(SHAPES)
     torch.manual_seed(0)
     for name in names:
@@ -80,7 +85,8 @@ def main():
             same = torch.equal(out[:, :cout], ref_out[:, :cout])
             err = (out[:, :cout].float() - yt).abs().max().item()
             us = timeit(lambda: C.conv_fwd([x], wt, g, cout, out[:, :cout], bias=b, act=1, cfg=cfg))
-            line.append(f"c{cfg} {us:6.1f}us ({2 * macs / us / 1e6:4.0f}TF) {'==' if same else f'err={err:.3f}'}")
+            tag = "" if args.probe and cfg != 41 else (" ==" if same else f" err={err:.3f}")
+            line.append(f"c{cfg} {us:6.1f}us ({2 * macs / us / 1e6:4.0f}TF){tag}")
         print("  ".join(line), flush=True)
 
 
