@@ -116,10 +116,14 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
     relink = cmds or not TARGET.exists() or any(o.stat().st_mtime > TARGET.stat().st_mtime for o in objs)
     if relink:
         _, tlib, _ = _torch_paths()
-        link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(TARGET),
+        # link to a temporary name and rename: a process (or a repo snapshot) that reads the
+        # library meanwhile sees the old or the new file, never a partial one
+        tmp = TARGET.with_name(TARGET.name + ".tmp")
+        link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp),
                 f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch",
                 f"-Wl,-rpath,{tlib}"]
         _compile(link)
+        os.replace(tmp, TARGET)
         if verbose:
             print("linked", TARGET)
     return TARGET

@@ -416,13 +416,42 @@ __device__ __forceinline__ void load8(const __bf16* row, int S, float (&x)[8]) {
 // Shared epilogue of the forward kernels: the fp32 accumulators go through an LDS tile
 // (et, BM x (BN+4) floats) so each thread finishes 8 consecutive output channels of one
 // pixel with 16-byte accesses; applies alpha/bias and the fused epilogue selected by a.epi.
-template <int BM, int BN, int TM, int TN, int NW = 4, int WGN = 2>
+// EPR (measurement probes of the epilogue cost, bias/act store path only): 1 = no global
+// stores, 2 = non-temporal stores, 3 = stores of zeros without the LDS staging
+template <int BM, int BN, int TM, int TN, int NW = 4, int WGN = 2, int EPR = 0, int EFAST = 0>
 __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f32x16 (&acc)[TM][TN], int m0,
                                              int n0, int P, int Nn) {
   constexpr int EPI_LD = BN + 4;  // fp32 epilogue tile row pitch
   constexpr int NT = NW * 64;     // threads; waves are laid out (NW/WGN) x WGN over the tile
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
+  constexpr int CPR = BN / 8;  // 8-channel chunks per tile row
+  static_assert(NT % CPR == 0, "a thread keeps one channel chunk across rows");
+  // Fast path (uniform branch) for the plain bias/act store (epi 0) and the gradient store
+  // (epi 1) without split planes: straight-line rows, the bias fetched as two 16-byte loads
+  // before the LDS staging so its latency hides behind it.  The generic path below (GRU gates,
+  // fused GRU backward, split-bf16 planes) tests its mode per row; for epi 0 / 1 its per-lane
+  // mode, masked scalar bias loads and branches cost ~5 us per launch (scripts/bench_conv6.py
+  // --probe, profiles/r3_conv6_probe.log).
+  // EFAST = 1 (probe): only the fast path is compiled in (the caller guarantees its modes)
+  const bool fast = EFAST == 1 || (a.epi <= 3 && a.split_g == 0 && EPR == 0);
+  f32x4 fb0{0.f, 0.f, 0.f, 0.f}, fb1{0.f, 0.f, 0.f, 0.f};
+  {
+    const int n = n0 + (tid % CPR) * 8;
+    if (fast && a.bias && n < Nn) {
+      if (n + 8 <= Nn && (reinterpret_cast<uintptr_t>(a.bias) & 15) == 0) {
+        fb0 = *reinterpret_cast<const f32x4*>(a.bias + n);
+        fb1 = *reinterpret_cast<const f32x4*>(a.bias + n + 4);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (n + q < Nn) fb0[q] = a.bias[n + q];
+          if (n + 4 + q < Nn) fb1[q] = a.bias[n + 4 + q];
+        }
+      }
+    }
+  }
+  if constexpr (EPR != 3) {
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -434,10 +463,133 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
         et[row * EPI_LD + col] = acc[i][j][r];
       }
   __syncthreads();
-  constexpr int CPR = BN / 8;  // 8-channel chunks per tile row
-  static_assert(NT % CPR == 0, "a thread keeps one channel chunk across rows");
-  // every thread owns the same 8-channel chunk in all of its rows (NT % CPR == 0): the
-  // bias is loaded once, before the row loop, instead of as a dependent load per row
+  }
+  if (fast) {
+    const int ch = tid % CPR;
+    const int n = n0 + ch * 8;
+    if (n >= Nn) return;
+    const bool full = n + 8 <= Nn;
+    const float alpha = a.alpha;
+    const bool relu = a.epi == 0 && a.act == 1;
+    const bool grad = a.epi == 1;
+    const bool accum = grad && n >= a.acc_c0;  // acc_c0 is a multiple of 8
+    const bool f32o = a.out_f32 != 0;
+    const bool vec = full && (!f32o || (a.out_stride & 3) == 0);
+    if (a.epi >= 2) {
+      // GRU gates (bf16, channel counts multiples of 8): epi 2 z||r: out = sigmoid, and for the r
+      // half out2 = r * h; epi 3: q = tanh, out = (1 - z) h + z q, out2 = q
+      const bool zr = a.epi == 2;
+      const int hc = zr ? n - (Nn >> 1) : n;  // h channel of this chunk (epi 2: r half only)
+      const bool has_h = !zr || hc >= 0;
+#pragma unroll 4
+      for (int row = tid / CPR; row < BM; row += NT / CPR) {
+        const long p = m0 + row;
+        if (p >= P) break;
+        f32x4 lo = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8);
+        f32x4 hi = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8 + 4);
+        lo = lo * alpha + fb0;
+        hi = hi * alpha + fb1;
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bf16x8 hv{};
+        if (has_h) hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + hc);
+        bf16x8 w0, w1;
+        if (zr) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float sg = sigmoidf_(v[q]);
+            w0[q] = static_cast<__bf16>(sg);
+            w1[q] = static_cast<__bf16>(static_cast<float>(w0[q]) * static_cast<float>(hv[q]));
+          }
+          *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = w0;
+          if (has_h) *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + hc) = w1;
+        } else {
+          const bf16x8 zv = *reinterpret_cast<const bf16x8*>(a.z + p * a.z_stride + n);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float qq = tanhf_(v[q]);
+            const float z = static_cast<float>(zv[q]);
+            w0[q] = static_cast<__bf16>((1.f - z) * static_cast<float>(hv[q]) + z * qq);
+            w1[q] = static_cast<__bf16>(qq);
+          }
+          *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = w0;
+          *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + n) = w1;
+        }
+      }
+      return;
+    }
+#pragma unroll 4
+    for (int row = tid / CPR; row < BM; row += NT / CPR) {
+      const long p = m0 + row;
+      if (p >= P) break;
+      f32x4 lo = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8);
+      f32x4 hi = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8 + 4);
+      lo = lo * alpha + fb0;
+      hi = hi * alpha + fb1;
+      if (relu) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          lo[q] = fmaxf(lo[q], 0.f);
+          hi[q] = fmaxf(hi[q], 0.f);
+        }
+      }
+      if (grad && a.mask) {
+        const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.mask + p * a.mask_stride + n);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (!(static_cast<float>(m[q]) > 0.f)) lo[q] = 0.f;
+          if (!(static_cast<float>(m[q + 4]) > 0.f)) hi[q] = 0.f;
+        }
+      }
+      if (f32o) {
+        float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
+        if (vec) {
+          if (accum) {
+            lo += *reinterpret_cast<const f32x4*>(o);
+            hi += *reinterpret_cast<const f32x4*>(o + 4);
+          }
+          *reinterpret_cast<f32x4*>(o) = lo;
+          *reinterpret_cast<f32x4*>(o + 4) = hi;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (n + q < Nn) {
+              const float x = q < 4 ? lo[q] : hi[q - 4];
+              o[q] = accum ? o[q] + x : x;
+            }
+        }
+      } else {
+        __bf16* o = static_cast<__bf16*>(a.out) + p * a.out_stride + n;
+        if (full) {
+          if (accum) {
+            const bf16x8 old = *reinterpret_cast<const bf16x8*>(o);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              lo[q] += static_cast<float>(old[q]);
+              hi[q] += static_cast<float>(old[q + 4]);
+            }
+          }
+          bf16x8 w;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            w[q] = static_cast<__bf16>(lo[q]);
+            w[q + 4] = static_cast<__bf16>(hi[q]);
+          }
+          *reinterpret_cast<bf16x8*>(o) = w;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (n + q < Nn) {
+              const float x = q < 4 ? lo[q] : hi[q - 4];
+              o[q] = static_cast<__bf16>(accum ? static_cast<float>(o[q]) + x : x);
+            }
+        }
+      }
+    }
+    return;
+  }
+  if constexpr (EFAST == 1) return;
+  // generic path: every thread owns the same 8-channel chunk in all of its rows (NT % CPR
+  // == 0): the bias is loaded once, before the row loop, instead of as a dependent load per row
   const int ch = tid % CPR;
   const int n = n0 + ch * 8;
   if (n >= Nn) return;
@@ -450,206 +602,229 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
   int epi = a.epi;
   if (epi == 4 || epi == 5) epi = n < a.gru_cols ? epi : 1;
   else if (epi == 6) epi = (n < a.gru_cols || n >= a.cm_c0) ? 6 : 1;
+  // one row loop per mode (the mode of a lane is fixed; in practice uniform per tile), so the
+  // mode tests are resolved at compile time instead of per row
+  auto rows = [&](auto mc) __attribute__((always_inline)) {
+    constexpr int M = decltype(mc)::value;
 #pragma unroll 2
-  for (int row = tid / CPR; row < BM; row += NT / CPR) {
-    const long p = m0 + row;
-    if (p >= P) break;
-    const f32x4 lo = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8);
-    const f32x4 hi = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8 + 4);
-    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = v[q] * alpha + bia[q];
-    if (epi == 4 || epi == 5) {
-      // fused GRU backward gate math (fp32 gradient rows; gru_cols is a multiple of 8)
-      float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
-      if (n >= a.acc_c0) {
+    for (int row = tid / CPR; row < BM; row += NT / CPR) {
+      const long p = m0 + row;
+      if (p >= P) break;
+      f32x4 lo{}, hi{};
+      if constexpr (EPR != 3) {
+        lo = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8);
+        hi = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8 + 4);
+      }
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  #pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = v[q] * alpha + bia[q];
+      if (M == 4 || M == 5) {
+        // fused GRU backward gate math (fp32 gradient rows; gru_cols is a multiple of 8)
+        float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
+        if (n >= a.acc_c0) {
+          const f32x4 o0 = *reinterpret_cast<const f32x4*>(o), o1 = *reinterpret_cast<const f32x4*>(o + 4);
+  #pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[q] += o0[q];
+            v[q + 4] += o1[q];
+          }
+        }
+        if (a.addsrc) {
+          const bf16x8 av = *reinterpret_cast<const bf16x8*>(a.addsrc + p * a.addsrc_stride + n);
+  #pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] += static_cast<float>(av[q]);
+        }
+        const bf16x8 gv = *reinterpret_cast<const bf16x8*>(a.g0 + p * a.g0_stride + n);
+        const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + n);
+        float* cp = a.carry + p * a.carry_stride + n;
+        bf16x8 d3;
+        if (M == 4) {
+          const bf16x8 zv = *reinterpret_cast<const bf16x8*>(a.z + p * a.z_stride + n);
+          bf16x8 dq;
+          float cr[8];
+  #pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float zz = static_cast<float>(zv[q]), qq = static_cast<float>(gv[q]), hh = static_cast<float>(hv[q]);
+            dq[q] = static_cast<__bf16>(v[q] * zz * (1.f - qq * qq));
+            d3[q] = static_cast<__bf16>(v[q] * (qq - hh) * zz * (1.f - zz));
+            cr[q] = v[q] * (1.f - zz);
+          }
+          *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + n) = dq;
+          *reinterpret_cast<f32x4*>(cp) = f32x4{cr[0], cr[1], cr[2], cr[3]};
+          *reinterpret_cast<f32x4*>(cp + 4) = f32x4{cr[4], cr[5], cr[6], cr[7]};
+        } else {
+          const f32x4 c0 = *reinterpret_cast<const f32x4*>(cp), c1 = *reinterpret_cast<const f32x4*>(cp + 4);
+          const float cv[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+          float ov[8];
+  #pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float rr = static_cast<float>(gv[q]), hh = static_cast<float>(hv[q]);
+            d3[q] = static_cast<__bf16>(v[q] * hh * rr * (1.f - rr));
+            ov[q] = cv[q] + v[q] * rr;
+          }
+          *reinterpret_cast<f32x4*>(o) = f32x4{ov[0], ov[1], ov[2], ov[3]};
+          *reinterpret_cast<f32x4*>(o + 4) = f32x4{ov[4], ov[5], ov[6], ov[7]};
+        }
+        *reinterpret_cast<bf16x8*>(a.out3 + p * a.out3_stride + n) = d3;
+      } else if (M == 6) {
+        // last GRU data gradient: bf16 d net / fp32 d inp / masked bf16 d motion
+        const float* o = static_cast<const float*>(a.out) + p * a.out_stride + n;
         const f32x4 o0 = *reinterpret_cast<const f32x4*>(o), o1 = *reinterpret_cast<const f32x4*>(o + 4);
-#pragma unroll
+  #pragma unroll
         for (int q = 0; q < 4; ++q) {
           v[q] += o0[q];
           v[q + 4] += o1[q];
         }
-      }
-      if (a.addsrc) {
-        const bf16x8 av = *reinterpret_cast<const bf16x8*>(a.addsrc + p * a.addsrc_stride + n);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] += static_cast<float>(av[q]);
-      }
-      const bf16x8 gv = *reinterpret_cast<const bf16x8*>(a.g0 + p * a.g0_stride + n);
-      const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + n);
-      float* cp = a.carry + p * a.carry_stride + n;
-      bf16x8 d3;
-      if (epi == 4) {
-        const bf16x8 zv = *reinterpret_cast<const bf16x8*>(a.z + p * a.z_stride + n);
-        bf16x8 dq;
-        float cr[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const float zz = static_cast<float>(zv[q]), qq = static_cast<float>(gv[q]), hh = static_cast<float>(hv[q]);
-          dq[q] = static_cast<__bf16>(v[q] * zz * (1.f - qq * qq));
-          d3[q] = static_cast<__bf16>(v[q] * (qq - hh) * zz * (1.f - zz));
-          cr[q] = v[q] * (1.f - zz);
-        }
-        *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + n) = dq;
-        *reinterpret_cast<f32x4*>(cp) = f32x4{cr[0], cr[1], cr[2], cr[3]};
-        *reinterpret_cast<f32x4*>(cp + 4) = f32x4{cr[4], cr[5], cr[6], cr[7]};
-      } else {
-        const f32x4 c0 = *reinterpret_cast<const f32x4*>(cp), c1 = *reinterpret_cast<const f32x4*>(cp + 4);
-        const float cv[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-        float ov[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const float rr = static_cast<float>(gv[q]), hh = static_cast<float>(hv[q]);
-          d3[q] = static_cast<__bf16>(v[q] * hh * rr * (1.f - rr));
-          ov[q] = cv[q] + v[q] * rr;
-        }
-        *reinterpret_cast<f32x4*>(o) = f32x4{ov[0], ov[1], ov[2], ov[3]};
-        *reinterpret_cast<f32x4*>(o + 4) = f32x4{ov[4], ov[5], ov[6], ov[7]};
-      }
-      *reinterpret_cast<bf16x8*>(a.out3 + p * a.out3_stride + n) = d3;
-    } else if (epi == 6) {
-      // last GRU data gradient: bf16 d net / fp32 d inp / masked bf16 d motion
-      const float* o = static_cast<const float*>(a.out) + p * a.out_stride + n;
-      const f32x4 o0 = *reinterpret_cast<const f32x4*>(o), o1 = *reinterpret_cast<const f32x4*>(o + 4);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[q] += o0[q];
-        v[q + 4] += o1[q];
-      }
-      bf16x8 w;
-      if (n < a.gru_cols) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(v[q]);
-        *reinterpret_cast<bf16x8*>(a.out3 + p * a.out3_stride + n) = w;
-      } else {
-        const int c = n - a.cm_c0;
-        if (c < a.cm_valid) {  // chunks wholly past cm_valid are not stored (cout may be narrower)
-          const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.cmask + p * a.cmask_stride + c);
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            w[q] = static_cast<__bf16>((c + q < a.cm_valid && static_cast<float>(m[q]) > 0.f) ? v[q] : 0.f);
-          *reinterpret_cast<bf16x8*>(a.cout + p * a.cout_stride + c) = w;
-        }
-      }
-    } else if (epi == 0) {
-      if (a.act == 1)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
-      if (a.split_g > 0 && !a.out_f32) {
-        split_store8(static_cast<__bf16*>(a.out) + p * a.out_stride, a.split_g, n, nv, v);
-      } else if (a.out_f32) {
-        float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
-        if (nv == 8 && (a.out_stride & 3) == 0) {
-          *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
-          *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
-        } else {
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (q < nv) o[q] = v[q];
-        }
-      } else {
-        __bf16* o = static_cast<__bf16*>(a.out) + p * a.out_stride + n;
-        if (nv == 8) {
-          bf16x8 w;
-#pragma unroll
+        bf16x8 w;
+        if (n < a.gru_cols) {
+  #pragma unroll
           for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(v[q]);
-          *reinterpret_cast<bf16x8*>(o) = w;
+          *reinterpret_cast<bf16x8*>(a.out3 + p * a.out3_stride + n) = w;
         } else {
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (q < nv) o[q] = static_cast<__bf16>(v[q]);
-        }
-      }
-    } else if (epi == 1) {
-      if (a.mask) {
-        const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.mask + p * a.mask_stride + n);
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (!(static_cast<float>(m[q]) > 0.f)) v[q] = 0.f;
-      }
-      const bool accum = n >= a.acc_c0;  // acc_c0 is a multiple of 8
-      if (a.out_f32) {
-        float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
-        if (nv == 8) {
-          f32x4 x0 = {v[0], v[1], v[2], v[3]}, x1 = {v[4], v[5], v[6], v[7]};
-          if (accum) {
-            x0 += *reinterpret_cast<const f32x4*>(o);
-            x1 += *reinterpret_cast<const f32x4*>(o + 4);
+          const int c = n - a.cm_c0;
+          if (c < a.cm_valid) {  // chunks wholly past cm_valid are not stored (cout may be narrower)
+            const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.cmask + p * a.cmask_stride + c);
+  #pragma unroll
+            for (int q = 0; q < 8; ++q)
+              w[q] = static_cast<__bf16>((c + q < a.cm_valid && static_cast<float>(m[q]) > 0.f) ? v[q] : 0.f);
+            *reinterpret_cast<bf16x8*>(a.cout + p * a.cout_stride + c) = w;
           }
-          *reinterpret_cast<f32x4*>(o) = x0;
-          *reinterpret_cast<f32x4*>(o + 4) = x1;
+        }
+      } else if (M == 0) {
+        if (a.act == 1)
+  #pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+        if (a.split_g > 0 && !a.out_f32) {
+          split_store8(static_cast<__bf16*>(a.out) + p * a.out_stride, a.split_g, n, nv, v);
+        } else if (a.out_f32) {
+          float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
+          if (nv == 8 && (a.out_stride & 3) == 0) {
+            *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+            *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+          } else {
+  #pragma unroll
+            for (int q = 0; q < 8; ++q)
+              if (q < nv) o[q] = v[q];
+          }
         } else {
-#pragma unroll
+          __bf16* o = static_cast<__bf16*>(a.out) + p * a.out_stride + n;
+          if (nv == 8) {
+            bf16x8 w;
+  #pragma unroll
+            for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(v[q]);
+            if constexpr (EPR == 1) {
+              if (v[0] == 1234.5f) *reinterpret_cast<bf16x8*>(o) = w;
+            } else if constexpr (EPR == 2) {
+              __builtin_nontemporal_store(w, reinterpret_cast<bf16x8*>(o));
+            } else {
+              *reinterpret_cast<bf16x8*>(o) = w;
+            }
+          } else {
+  #pragma unroll
+            for (int q = 0; q < 8; ++q)
+              if (q < nv) o[q] = static_cast<__bf16>(v[q]);
+          }
+        }
+      } else if (M == 1) {
+        if (a.mask) {
+          const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.mask + p * a.mask_stride + n);
+  #pragma unroll
           for (int q = 0; q < 8; ++q)
-            if (q < nv) o[q] = accum ? o[q] + v[q] : v[q];
+            if (!(static_cast<float>(m[q]) > 0.f)) v[q] = 0.f;
+        }
+        const bool accum = n >= a.acc_c0;  // acc_c0 is a multiple of 8
+        if (a.out_f32) {
+          float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
+          if (nv == 8) {
+            f32x4 x0 = {v[0], v[1], v[2], v[3]}, x1 = {v[4], v[5], v[6], v[7]};
+            if (accum) {
+              x0 += *reinterpret_cast<const f32x4*>(o);
+              x1 += *reinterpret_cast<const f32x4*>(o + 4);
+            }
+            *reinterpret_cast<f32x4*>(o) = x0;
+            *reinterpret_cast<f32x4*>(o + 4) = x1;
+          } else {
+  #pragma unroll
+            for (int q = 0; q < 8; ++q)
+              if (q < nv) o[q] = accum ? o[q] + v[q] : v[q];
+          }
+        } else {
+          __bf16* o = static_cast<__bf16*>(a.out) + p * a.out_stride + n;
+          if (nv == 8) {
+            bf16x8 w;
+            const bf16x8 old = accum ? *reinterpret_cast<const bf16x8*>(o) : bf16x8{};
+  #pragma unroll
+            for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(accum ? static_cast<float>(old[q]) + v[q] : v[q]);
+            *reinterpret_cast<bf16x8*>(o) = w;
+          } else {
+  #pragma unroll
+            for (int q = 0; q < 8; ++q)
+              if (q < nv) o[q] = static_cast<__bf16>(accum ? static_cast<float>(o[q]) + v[q] : v[q]);
+          }
+        }
+      } else if (M == 2 && a.split_g > 0) {
+        // split mode: sigmoid in fp32, r * h from the fp32-faithful h (hi + lo planes)
+        const int C = Nn >> 1;
+        float sg[8];
+  #pragma unroll
+        for (int q = 0; q < 8; ++q) sg[q] = sigmoidf_(v[q]);
+        split_store8(static_cast<__bf16*>(a.out) + p * a.out_stride, a.split_g, n, 8, sg);
+        if (n >= C) {
+          float hv[8];
+          load8(a.h + p * a.h_stride + (n - C), a.split_h, hv);
+  #pragma unroll
+          for (int q = 0; q < 8; ++q) hv[q] *= sg[q];
+          split_store8(a.out2 + p * a.out2_stride, a.split_g2, n - C, 8, hv);
+        }
+      } else if (M == 3 && a.split_g > 0) {
+        float zv[8], hv[8], hn[8];
+        load8(a.z + p * a.z_stride + n, a.split_z, zv);
+        load8(a.h + p * a.h_stride + n, a.split_h, hv);
+  #pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float qq = tanhf_(v[q]);
+          hn[q] = (1.f - zv[q]) * hv[q] + zv[q] * qq;
+          v[q] = qq;
+        }
+        split_store8(static_cast<__bf16*>(a.out) + p * a.out_stride, a.split_g, n, 8, hn);
+        if (a.out2) split_store8(a.out2 + p * a.out2_stride, a.split_g2 > 0 ? a.split_g2 : a.split_g, n, 8, v);
+      } else if (M == 2) {
+        const int C = Nn >> 1;
+        bf16x8 sg;
+  #pragma unroll
+        for (int q = 0; q < 8; ++q) sg[q] = static_cast<__bf16>(sigmoidf_(v[q]));
+        *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = sg;
+        if (n >= C) {
+          const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + (n - C));
+          bf16x8 rh;
+  #pragma unroll
+          for (int q = 0; q < 8; ++q) rh[q] = static_cast<__bf16>(static_cast<float>(sg[q]) * static_cast<float>(hv[q]));
+          *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + (n - C)) = rh;
         }
       } else {
-        __bf16* o = static_cast<__bf16*>(a.out) + p * a.out_stride + n;
-        if (nv == 8) {
-          bf16x8 w;
-          const bf16x8 old = accum ? *reinterpret_cast<const bf16x8*>(o) : bf16x8{};
-#pragma unroll
-          for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(accum ? static_cast<float>(old[q]) + v[q] : v[q]);
-          *reinterpret_cast<bf16x8*>(o) = w;
-        } else {
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (q < nv) o[q] = static_cast<__bf16>(accum ? static_cast<float>(o[q]) + v[q] : v[q]);
+        const bf16x8 zv = *reinterpret_cast<const bf16x8*>(a.z + p * a.z_stride + n);
+        const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + n);
+        bf16x8 hn, qo;
+  #pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float qq = tanhf_(v[q]);
+          const float z = static_cast<float>(zv[q]);
+          hn[q] = static_cast<__bf16>((1.f - z) * static_cast<float>(hv[q]) + z * qq);
+          qo[q] = static_cast<__bf16>(qq);
         }
+        *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = hn;
+        *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + n) = qo;
       }
-    } else if (epi == 2 && a.split_g > 0) {
-      // split mode: sigmoid in fp32, r * h from the fp32-faithful h (hi + lo planes)
-      const int C = Nn >> 1;
-      float sg[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) sg[q] = sigmoidf_(v[q]);
-      split_store8(static_cast<__bf16*>(a.out) + p * a.out_stride, a.split_g, n, 8, sg);
-      if (n >= C) {
-        float hv[8];
-        load8(a.h + p * a.h_stride + (n - C), a.split_h, hv);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) hv[q] *= sg[q];
-        split_store8(a.out2 + p * a.out2_stride, a.split_g2, n - C, 8, hv);
-      }
-    } else if (epi == 3 && a.split_g > 0) {
-      float zv[8], hv[8], hn[8];
-      load8(a.z + p * a.z_stride + n, a.split_z, zv);
-      load8(a.h + p * a.h_stride + n, a.split_h, hv);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float qq = tanhf_(v[q]);
-        hn[q] = (1.f - zv[q]) * hv[q] + zv[q] * qq;
-        v[q] = qq;
-      }
-      split_store8(static_cast<__bf16*>(a.out) + p * a.out_stride, a.split_g, n, 8, hn);
-      if (a.out2) split_store8(a.out2 + p * a.out2_stride, a.split_g2 > 0 ? a.split_g2 : a.split_g, n, 8, v);
-    } else if (epi == 2) {
-      const int C = Nn >> 1;
-      bf16x8 sg;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) sg[q] = static_cast<__bf16>(sigmoidf_(v[q]));
-      *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = sg;
-      if (n >= C) {
-        const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + (n - C));
-        bf16x8 rh;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) rh[q] = static_cast<__bf16>(static_cast<float>(sg[q]) * static_cast<float>(hv[q]));
-        *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + (n - C)) = rh;
-      }
-    } else {
-      const bf16x8 zv = *reinterpret_cast<const bf16x8*>(a.z + p * a.z_stride + n);
-      const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + n);
-      bf16x8 hn, qo;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float qq = tanhf_(v[q]);
-        const float z = static_cast<float>(zv[q]);
-        hn[q] = static_cast<__bf16>((1.f - z) * static_cast<float>(hv[q]) + z * qq);
-        qo[q] = static_cast<__bf16>(qq);
-      }
-      *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = hn;
-      *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + n) = qo;
     }
+  };
+  switch (epi) {
+    case 0: rows(std::integral_constant<int, 0>{}); break;
+    case 1: rows(std::integral_constant<int, 1>{}); break;
+    case 2: rows(std::integral_constant<int, 2>{}); break;
+    case 3: rows(std::integral_constant<int, 3>{}); break;
+    case 4: rows(std::integral_constant<int, 4>{}); break;
+    case 5: rows(std::integral_constant<int, 5>{}); break;
+    default: rows(std::integral_constant<int, 6>{}); break;
   }
 }
 
@@ -1322,7 +1497,8 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
         for (int r = 0; r < 16; ++r) t += acc[i][j][r];
     if (t == 1234.5f) static_cast<float*>(a.out)[0] = t;
   } else {
-    fwd_epilogue<BM, BN, TM, TN, NW, WGN>(a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn);
+    fwd_epilogue<BM, BN, TM, TN, NW, WGN, (SCHED >> 6) & 3, (SCHED >> 8) & 1>(a, reinterpret_cast<float*>(dsm), acc,
+                                                                            m0, n0, P, Nn);
   }
 }
 
@@ -1910,10 +2086,7 @@ bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
   switch (cfg) {
     case 40: return launch_fwd6_taps<128, 128, 2, 2>(a, s);
     case 41: return launch_fwd6_taps<256, 64, 4, 1>(a, s);
-    case 43: return launch_fwd6_taps<128, 128, 2, 2, 0>(a, s);
-    case 44: return launch_fwd6_taps<256, 64, 4, 1, 0>(a, s);
     case 45: return launch_fwd6_taps<256, 128, 2, 2>(a, s);
-    case 46: return launch_fwd6_taps<256, 128, 2, 2, 0>(a, s);
     // measurement probes of the 256x64 tile (scripts/bench_conv6.py --probe): no MFMA / no
     // in-loop DMA / no fragment reads / no barrier / no epilogue / bare loop
     case 47: return launch_fwd6_probe<1 | 2>(a, s);
@@ -1922,6 +2095,12 @@ bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
     case 50: return launch_fwd6_probe<1 | 16>(a, s);
     case 51: return launch_fwd6_probe<1 | 32>(a, s);
     case 52: return launch_fwd6_probe<1 | 2 | 4 | 8 | 16>(a, s);
+    // epilogue probes: no global stores / non-temporal stores / zero stores without LDS staging
+    case 53: return launch_fwd6_probe<1 | 64>(a, s);
+    case 54: return launch_fwd6_probe<1 | 128>(a, s);
+    case 55: return launch_fwd6_probe<1 | 192>(a, s);
+    // only the fast bias/act/gradient epilogue compiled in (code-size probe; epi <= 3, no split)
+    case 56: return launch_fwd6_probe<1 | 256>(a, s);
     default: return false;
   }
 }
@@ -1981,15 +2160,29 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
 #undef RAFT_PROBE
     return hipGetLastError();
   }
-  if (cfg >= 40 && cfg <= 52) {
+  if (cfg >= 40 && cfg <= 56) {
     // v6 (measurement / forced): 40 = 128x128 (2x2 waves of 64x64), 41 = 256x64 (4x1 waves of
-    // 64x64), 45 = 256x128 (2x2 waves of 128x64); 43 / 44 / 46: the same tiles with all
-    // next-step reads issued before the step's MFMAs
+    // 64x64), 45 = 256x128 (2x2 waves of 128x64).  (Issuing all next-step reads before the
+    // step's MFMAs measured 2-5% slower than interleaving them, 2.5-3.5x with the 256x128 tile's
+    // register spills: profiles/r3_bench_conv6_tiles.log, cfg 43 / 44 / 46.)
     const int taps = a.KH * a.KW;
     const bool shape6 = (a.KH == 3 && a.KW == 3) || (taps == 5 && (a.KH == 1 || a.KW == 1));
     if (!ok5 || !shape6 || a.PH != a.KH / 2 || a.PW != a.KW / 2) return hipErrorInvalidValue;
     if (launch_conv_fwd6(a, cfg, s)) return hipGetLastError();
     return hipErrorInvalidValue;
+  }
+  if (ok5 && cfg == 0 && a.PH == a.KH / 2 && a.PW == a.KW / 2) {
+    // v6 where it measured faster than v5 at config #2 (scripts/bench_conv6.py,
+    // profiles/r3_bench_conv6_tiles.log; bitwise-equal results): 3x3 with N <= 128 or N > 256
+    // (conv 32.0 -> 27.2 us, head data gradients 29.8 -> 25.1, heads 51.7 -> 45.6) and 1x5 with
+    // N <= 128 (q 26.4 -> 23.8) on 256x64 tiles; the 192-wide 3x3 on 256x128 (43.1 -> 41.8);
+    // every 5x1 (z||r 52.4 -> 46.9, q 27.9 -> 25.5, data gradient 58.5 -> 53.9) on 128x128.
+    // Shapes whose strip does not fit (wide images) fall through to v5 / v4.
+    int v6 = 0;
+    if (a.KH == 3 && a.KW == 3) v6 = (a.N <= 128 || a.N > 256) ? 41 : (a.N <= 192 ? 45 : 0);
+    else if (a.KH == 1 && a.KW == 5) v6 = a.N <= 128 ? 41 : 0;
+    else if (a.KH == 5 && a.KW == 1) v6 = 40;
+    if (v6 && launch_conv_fwd6(a, v6, s)) return hipGetLastError();
   }
   if (ok5 && v5 == 0 && cfg == 0) {
     // 8-wave tiles (two waves per SIMD, no register spills) for every shape they win on

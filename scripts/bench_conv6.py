@@ -40,20 +40,20 @@ SHAPES = {
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cfgs", default="40,41,45,43,44,46")
+    ap.add_argument("--cfgs", default="40,41,45")
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--hw", type=int, nargs=2, default=[46, 62])
     ap.add_argument("--only", default="")
     ap.add_argument("--probe", action="store_true",
                     help="256x64 probes: 41 full, 47 no MFMA, 48 no DMA, 49 no reads, 50 no barrier, "
-                         "51 no epilogue, 52 bare loop")
+                         "51 no epilogue, 52 bare loop, 53 no global stores, 54 nt stores, 55 zero stores without LDS staging, 56 only the fast epilogue compiled in")
     args = ap.parse_args()
     dev = torch.device("cuda")
     B, (H, W) = args.batch, args.hw
     P = B * H * W
     cfgs = [int(c) for c in args.cfgs.split(",")]
     if args.probe:
-        cfgs = [41, 47, 48, 49, 50, 51, 52]
+        cfgs = [41, 51, 52, 53, 56]
     names = args.only.split(",") if args.only else list(SHAPES)
     torch.manual_seed(0)
     for name in names:

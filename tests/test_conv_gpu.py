@@ -169,7 +169,7 @@ def test_gru_epilogues(cuda):
     assert _rel(_from_pm(hn, B, H, W), hn_ref) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 1, 8, 9, 40, 41, 43, 44])
+@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 1, 8, 9, 40, 41, 45])
 @pytest.mark.parametrize("segs,cout,kh,kw,hw", [
     ([(256, 256)], 192, 3, 3, (46, 62)),
     ([(128, 128), (128, 128), (128, 128)], 256, 1, 5, (46, 62)),
@@ -188,6 +188,8 @@ def test_fwd_every_variant_full_size(cuda, cfg, segs, cout, kh, kw, hw):
     w = torch.randn(cout, cin, kh, kw, device=cuda) / (cin * kh * kw) ** 0.5
     bias = torch.randn(cout, device=cuda)
     out = torch.full((P, cout), float("nan"), device=cuda, dtype=torch.bfloat16)
+    if cfg in (41, 45) and kh == 5 and 256 + 4 * W > 479:
+        pytest.skip("256-row v6 tiles: the 5x1 halo strip does not fit in LDS at this width")
     C.conv_fwd(srcs, C.pack_fwd(w, segs), C.geom(B, H, W, kh, kw, kh // 2, kw // 2), cout, out, bias=bias, act=1,
                cfg=cfg)
     x = torch.cat([_from_pm(s, B, H, W) for s in srcs], dim=1)
