@@ -35,6 +35,11 @@ SHAPES = {
     "d_zr15": (256, 384, 1, 5),
     "d_q15": (128, 384, 1, 5),
     "d_zr51": (256, 384, 5, 1),
+    "d_q51": (128, 384, 5, 1),
+    "convc1": (384, 256, 1, 1),
+    "mask2": (256, 576, 1, 1),
+    "d_convc1": (256, 384, 1, 1),
+    "d_mask2": (576, 256, 1, 1),
 }
 
 

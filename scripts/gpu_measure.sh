@@ -36,6 +36,7 @@ for step in ${STEPS_LIST:-infer1080 infer_sintel alt_kitti dense_kitti conv_nati
     train_full) run train_full 300 python bench.py --image_size 440 1024 --batch 6 --steps 10 --warmup 3 ;;
     prof_fp32) run prof_fp32 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_fp32 -o run -- python3 bench.py --mode infer --fp32 --image_size 440 1024 --iters 20 --batch 1 --steps 5 --warmup 2 ;;
     prof_train) run prof_train 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_train -o run -- python3 bench.py --steps 8 --warmup 4 ;;
+    prof_infer1080) run prof_infer1080 400 rocprofv3 --kernel-trace --stats -d $OUT/prof_infer1080 -o run -- python3 bench.py --mode infer --image_size 1080 1920 --iters 32 --batch 1 --steps 5 --warmup 2 ;;
   esac
 done
 echo done
