@@ -416,11 +416,30 @@ __device__ __forceinline__ void load8(const __bf16* row, int S, float (&x)[8]) {
 // Shared epilogue of the forward kernels: the fp32 accumulators go through an LDS tile
 // (et, BM x (BN+4) floats) so each thread finishes 8 consecutive output channels of one
 // pixel with 16-byte accesses; applies alpha/bias and the fused epilogue selected by a.epi.
+// Output-row -> pixel mapping of a tile: flat (TW2D == 0: rows m0 .. m0 + BM - 1 of the pixel
+// order) or a 2-D tile of TW2D columns (conv_fwd6 on wide images: row r -> image pixel
+// (y0 + r / TW2D, x0 + r % TW2D) of image pbase / (H W), rows outside the image are skipped)
+struct Tile2D {
+  long pbase;
+  int y0, x0, H, W;
+};
+template <int TW2D>
+__device__ __forceinline__ bool row_pixel(int row, int m0, int P, const Tile2D& t, long& p) {
+  if constexpr (TW2D == 0) {
+    p = m0 + row;
+    return p < P;
+  } else {
+    const int y = t.y0 + row / TW2D, x = t.x0 + row % TW2D;
+    p = t.pbase + (long)y * t.W + x;
+    return y < t.H && x < t.W;
+  }
+}
+
 // EPR (measurement probes of the epilogue cost, bias/act store path only): 1 = no global
 // stores, 2 = non-temporal stores, 3 = stores of zeros without the LDS staging
-template <int BM, int BN, int TM, int TN, int NW = 4, int WGN = 2, int EPR = 0, int EFAST = 0>
+template <int BM, int BN, int TM, int TN, int NW = 4, int WGN = 2, int EPR = 0, int EFAST = 0, int TW2D = 0>
 __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f32x16 (&acc)[TM][TN], int m0,
-                                             int n0, int P, int Nn) {
+                                             int n0, int P, int Nn, const Tile2D& t2 = Tile2D{}) {
   constexpr int EPI_LD = BN + 4;  // fp32 epilogue tile row pitch
   constexpr int NT = NW * 64;     // threads; waves are laid out (NW/WGN) x WGN over the tile
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -483,8 +502,11 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
       const bool has_h = !zr || hc >= 0;
 #pragma unroll 4
       for (int row = tid / CPR; row < BM; row += NT / CPR) {
-        const long p = m0 + row;
-        if (p >= P) break;
+        long p;
+        if (!row_pixel<TW2D>(row, m0, P, t2, p)) {
+          if constexpr (TW2D == 0) break;
+          else continue;
+        }
         f32x4 lo = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8);
         f32x4 hi = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8 + 4);
         lo = lo * alpha + fb0;
@@ -519,8 +541,11 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
     }
 #pragma unroll 4
     for (int row = tid / CPR; row < BM; row += NT / CPR) {
-      const long p = m0 + row;
-      if (p >= P) break;
+      long p;
+      if (!row_pixel<TW2D>(row, m0, P, t2, p)) {
+        if constexpr (TW2D == 0) break;
+        else continue;
+      }
       f32x4 lo = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8);
       f32x4 hi = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8 + 4);
       lo = lo * alpha + fb0;
@@ -608,8 +633,11 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
     constexpr int M = decltype(mc)::value;
 #pragma unroll 2
     for (int row = tid / CPR; row < BM; row += NT / CPR) {
-      const long p = m0 + row;
-      if (p >= P) break;
+      long p;
+      if (!row_pixel<TW2D>(row, m0, P, t2, p)) {
+        if constexpr (TW2D == 0) break;
+        else continue;
+      }
       f32x4 lo{}, hi{};
       if constexpr (EPR != 3) {
         lo = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8);
@@ -1260,7 +1288,11 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int KH, int KW, int SCHED = 1>
+// TW > 0: 2-D output tiles of (BM / TW) image rows x TW columns (wide images, where the flat
+// strip of BM + (KH-1) W + KW-1 rows no longer fits in LDS): the strip is the tile's halo
+// block of (BM/TW + KH-1) x (TW + KW-1) pixels with pitch TW + KW-1, so a tap is still one
+// constant row shift, and pixels outside the image are DMA'd as zeros (no per-tap masking).
+template <int BM, int BN, int WGM, int WGN, int KH, int KW, int SCHED = 1, int TW = 0>
 __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwdArgs a, int strip_rows) {
   constexpr int NW = WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;  // wave tile
@@ -1290,13 +1322,26 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
                  st2 = (unsigned)a.src[2].stride * 2;
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.wt, (unsigned)((long)Nn * Kpad * 2));
 
+  constexpr int TH = TW > 0 ? BM / TW : 1;          // 2-D tile rows
+  constexpr int HWD = TW + KW - 1;                  // 2-D halo block pitch (pixels)
+  constexpr int HROWS = (TH + KH - 1) * HWD;        // 2-D halo block pixels
+  constexpr int SPW2 = (HROWS + 8 * NW - 1) / (8 * NW);  // its DMA pieces per wave
+  static_assert(TW == 0 || (BM % TW == 0 && TW % 32 == 0 && SPW2 * 8 * NW <= CF::MAX_ROWS), "2-D tile");
   const int tilesN = (Nn + BN - 1) / BN;
-  const int tilesM = (P + BM - 1) / BM;
+  int tilesM;
+  if constexpr (TW == 0) tilesM = (P + BM - 1) / BM;
+  else tilesM = a.B * ((H + TH - 1) / TH) * ((W + TW - 1) / TW);
   const int wg = xcd_remap(blockIdx.x, tilesM * tilesN);
   const int tm = wg / tilesN, tn = wg - (wg / tilesN) * tilesN;
-  const int m0 = tm * BM;
+  const int m0 = TW == 0 ? tm * BM : 0;
   const int n0 = tn * BN;
   const int halo_lo = PH * W + PW;
+  Tile2D t2{};
+  if constexpr (TW > 0) {
+    const int tx = (W + TW - 1) / TW, per_img = tx * ((H + TH - 1) / TH);
+    const int b = tm / per_img, rem = tm - b * per_img;
+    t2 = Tile2D{(long)b * H * W, (rem / tx) * TH, (rem - (rem / tx) * tx) * TW, H, W};
+  }
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WGN, wn = wave % WGN;
@@ -1314,6 +1359,14 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int frow = wm * WM + i * 32 + fr;
+    if constexpr (TW > 0) {
+#pragma unroll
+      for (int tap = 0; tap < NT; ++tap) {
+        const int row = (frow / TW + tap / KW) * HWD + frow % TW + tap % KW;
+        abase[tap][i] = lds0 + RING + (unsigned)row * 128u + ((((row >> 1) & 7) ^ fh) << 4);
+      }
+      continue;
+    }
     const int p = m0 + frow;
     int py = -(1 << 20), px = -(1 << 20);
     if (p < P) {
@@ -1345,9 +1398,21 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
     bvoff[i] = (n0 + row < Nn) ? (unsigned)((n0 + row) * Kpad * 2 + swz(row, lpc) * 16) : kOOB;
   }
   const int nchunks = Cin / 64;
-  const int spw = strip_rows / (8 * NW);  // strip pieces per wave (strip_rows % (8 NW) == 0)
+  // strip pieces per wave (strip_rows % (8 NW) == 0)
+  const int spw = TW > 0 ? SPW2 : strip_rows / (8 * NW);
   const unsigned sswz = (unsigned)((lpc ^ (((wave & 1) << 2) | (lrow >> 1))) * 16);
   const int pstrip = m0 - halo_lo + wave * 8 + lrow;  // pixel of this lane's row in piece 0
+  // 2-D: image pixel of this lane's halo row in each of its pieces (-1: outside the image)
+  int spix[TW > 0 ? SPW2 : 1];
+  if constexpr (TW > 0) {
+#pragma unroll
+    for (int q = 0; q < SPW2; ++q) {
+      const int r = (wave + q * NW) * 8 + lrow;
+      const int y = t2.y0 - PH + r / HWD, x = t2.x0 - PW + r % HWD;
+      spix[q] = (r < HROWS && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) ? (int)t2.pbase + y * W + x
+                                                                                     : -1;
+    }
+  }
 
   // ---- DMA issue of a step: chunk cu (runtime), tap TU, ring stage SU, strip parity HU
   auto issue = [&](int cu, auto tuc, auto suc, auto huc) __attribute__((always_inline)) {
@@ -1366,10 +1431,18 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
         rs = r1; st = st1; soff = (unsigned)(c0 - sc0) * 2;
       }
       char* const sbuf = lds + RING + HU * SB + wave * 1024;
-      for (int q = 0; q < spw; ++q) {
-        const int p = pstrip + q * NW * 8;
-        const unsigned voff = (unsigned)p < (unsigned)P ? (unsigned)p * st + sswz : kOOB;
-        bload16(rs, reinterpret_cast<__bf16*>(sbuf + q * NW * 1024), voff, soff);
+      if constexpr (TW > 0) {
+#pragma unroll
+        for (int q = 0; q < SPW2; ++q) {
+          const unsigned voff = spix[q] >= 0 ? (unsigned)spix[q] * st + sswz : kOOB;
+          bload16(rs, reinterpret_cast<__bf16*>(sbuf + q * NW * 1024), voff, soff);
+        }
+      } else {
+        for (int q = 0; q < spw; ++q) {
+          const int p = pstrip + q * NW * 8;
+          const unsigned voff = (unsigned)p < (unsigned)P ? (unsigned)p * st + sswz : kOOB;
+          bload16(rs, reinterpret_cast<__bf16*>(sbuf + q * NW * 1024), voff, soff);
+        }
       }
     }
   };
@@ -1497,8 +1570,8 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
         for (int r = 0; r < 16; ++r) t += acc[i][j][r];
     if (t == 1234.5f) static_cast<float*>(a.out)[0] = t;
   } else {
-    fwd_epilogue<BM, BN, TM, TN, NW, WGN, (SCHED >> 6) & 3, (SCHED >> 8) & 1>(a, reinterpret_cast<float*>(dsm), acc,
-                                                                            m0, n0, P, Nn);
+    fwd_epilogue<BM, BN, TM, TN, NW, WGN, (SCHED >> 6) & 3, (SCHED >> 8) & 1, TW>(
+        a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn, t2);
   }
 }
 
@@ -2057,15 +2130,23 @@ __global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
 }  // namespace
 
 namespace {
-template <int BM, int BN, int WGM, int WGN, int KH, int KW, int SCHED>
+template <int BM, int BN, int WGM, int WGN, int KH, int KW, int SCHED, int TW = 0>
 bool launch_fwd6_t(const ConvFwdArgs& a, hipStream_t s) {
   using CF = Fwd6Cfg<BN, WGN, KH * KW>;
   constexpr int NW = WGM * WGN;
-  const int rows = fwd6_strip_rows(BM, NW, KH, KW, a.W, CF::MAX_ROWS);
-  if (rows == 0) return false;
-  const dim3 grid((unsigned)(((a.P + BM - 1) / BM) * ((a.N + BN - 1) / BN)));
-  set_lds_limit((const void*)conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, SCHED>, CF::LDS);
-  hipLaunchKernelGGL((conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, SCHED>), grid, dim3(NW * 64), CF::LDS, s, a,
+  int rows = 0;
+  long tiles;
+  if constexpr (TW == 0) {
+    rows = fwd6_strip_rows(BM, NW, KH, KW, a.W, CF::MAX_ROWS);
+    if (rows == 0) return false;
+    tiles = (a.P + BM - 1) / BM;
+  } else {
+    constexpr int TH = BM / TW;
+    tiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
+  }
+  const dim3 grid((unsigned)(tiles * ((a.N + BN - 1) / BN)));
+  set_lds_limit((const void*)conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, SCHED, TW>, CF::LDS);
+  hipLaunchKernelGGL((conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, SCHED, TW>), grid, dim3(NW * 64), CF::LDS, s, a,
                      rows);
   return true;
 }
@@ -2087,6 +2168,17 @@ bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
     case 40: return launch_fwd6_taps<128, 128, 2, 2>(a, s);
     case 41: return launch_fwd6_taps<256, 64, 4, 1>(a, s);
     case 45: return launch_fwd6_taps<256, 128, 2, 2>(a, s);
+    // 2-D tiles (wide images): 57 = 128x128 as 2 x 64 (3x3), 58 = 128x128 as 4 x 32 (5x1),
+    // 59 = 256x64 as 4 x 64 (3x3, 1x5), 60 = 256x64 as 8 x 32 (5x1)
+    case 57:
+      return a.KH == 3 && a.KW == 3 && launch_fwd6_t<128, 128, 2, 2, 3, 3, 1, 64>(a, s);
+    case 58:
+      return a.KH == 5 && a.KW == 1 && launch_fwd6_t<128, 128, 2, 2, 5, 1, 1, 32>(a, s);
+    case 59:
+      if (a.KH == 3 && a.KW == 3) return launch_fwd6_t<256, 64, 4, 1, 3, 3, 1, 64>(a, s);
+      return a.KH == 1 && a.KW == 5 && launch_fwd6_t<256, 64, 4, 1, 1, 5, 1, 64>(a, s);
+    case 60:
+      return a.KH == 5 && a.KW == 1 && launch_fwd6_t<256, 64, 4, 1, 5, 1, 1, 32>(a, s);
     // measurement probes of the 256x64 tile (scripts/bench_conv6.py --probe): no MFMA / no
     // in-loop DMA / no fragment reads / no barrier / no epilogue / bare loop
     case 47: return launch_fwd6_probe<1 | 2>(a, s);
@@ -2160,7 +2252,7 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
 #undef RAFT_PROBE
     return hipGetLastError();
   }
-  if (cfg >= 40 && cfg <= 56) {
+  if (cfg >= 40 && cfg <= 60) {
     // v6 (measurement / forced): 40 = 128x128 (2x2 waves of 64x64), 41 = 256x64 (4x1 waves of
     // 64x64), 45 = 256x128 (2x2 waves of 128x64).  (Issuing all next-step reads before the
     // step's MFMAs measured 2-5% slower than interleaving them, 2.5-3.5x with the 256x128 tile's
@@ -2178,10 +2270,24 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
     // N <= 128 (q 26.4 -> 23.8) on 256x64 tiles; the 192-wide 3x3 on 256x128 (43.1 -> 41.8);
     // every 5x1 (z||r 52.4 -> 46.9, q 27.9 -> 25.5, data gradient 58.5 -> 53.9) on 128x128.
     // Shapes whose strip does not fit (wide images) fall through to v5 / v4.
+    // Wide images (the flat strip does not fit: Sintel / KITTI / 1080p widths) take the 2-D
+    // tiles (profiles/r3_bench_conv6_2d.log): 4 x 64 for a 3x3 when its grid is one round of
+    // the 256 CUs or v4 would pad N (N = 64, 192, > 256: 1080p convc2 63.0 -> 41.8 us, Sintel
+    // conv 28.5 -> 23.0), otherwise v5 / v4 (1080p conv 37.1 v4 vs 45.6 with 272 workgroups);
+    // 8 x 32 for every 5x1 up to ~24k pixels (config #2 z||r 43.9 -> 38.9, Sintel q 22.8 -> 20.0;
+    // v4 keeps 1080p's 32k pixels: 29.5 vs 39.1 us).
+    const long wg59 = (long)a.B * ((a.H + 3) / 4) * ((a.W + 63) / 64) * ((a.N + 63) / 64);
+    const int np = (a.N + 63) / 64 * 64;
+    const bool flat3 = fwd6_strip_rows(256, 4, 3, 3, a.W, Fwd6Cfg<64, 1, 9>::MAX_ROWS) > 0;
     int v6 = 0;
-    if (a.KH == 3 && a.KW == 3) v6 = (a.N <= 128 || a.N > 256) ? 41 : (a.N <= 192 ? 45 : 0);
-    else if (a.KH == 1 && a.KW == 5) v6 = a.N <= 128 ? 41 : 0;
-    else if (a.KH == 5 && a.KW == 1) v6 = 40;
+    if (a.KH == 3 && a.KW == 3) {
+      if (flat3) v6 = (a.N <= 128 || a.N > 256) ? 41 : (a.N <= 192 ? 45 : 0);
+      else if (wg59 <= 256 || (np != 128 && np != 256)) v6 = 59;
+    } else if (a.KH == 1 && a.KW == 5) {
+      v6 = a.N <= 128 ? (a.P <= 24576 ? 59 : 41) : 0;  // config #2 q: 21.8 -> 20.6 us
+    } else if (a.KH == 5 && a.KW == 1) {
+      v6 = a.P <= 24576 ? 60 : 0;
+    }
     if (v6 && launch_conv_fwd6(a, v6, s)) return hipGetLastError();
   }
   if (ok5 && v5 == 0 && cfg == 0) {

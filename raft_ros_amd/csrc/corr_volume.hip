@@ -488,6 +488,14 @@ __device__ __forceinline__ float safe_floor(float v) {
 }
 
 // ---------------------------------------------------------------------------- lookup
+// this wave's LDS writes are visible to its other lanes: the LDS operations of one wave
+// execute in order, so only the compiler must not move LDS accesses across this point
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // One wave per query pixel, looping over the levels; 4 waves per block.  LDS per wave:
 // the (2r+2)^2 neighbourhood (<= 14 x 14 for r <= 6) as fp32.
 constexpr int NBMAX = 14 * 14;
@@ -509,7 +517,7 @@ __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const floa
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
   const long pix0 = (long)blockIdx.x * 4 + wave;
-  const bool live = pix0 < (long)B * HW;  // no early exit: the block synchronises per level
+  const bool live = pix0 < (long)B * HW;
   const long pix = live ? pix0 : 0;
   const int b = pix / HW, p = pix - (long)b * HW;
   const int rd = 2 * r + 1, nd = rd + 1, win = rd * rd, nn = nd * nd;
@@ -548,12 +556,15 @@ __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const floa
       v[k] = in ? (pyr.vbf16 ? static_cast<float>(rowb[off]) : row[off]) : 0.f;
     }
   };
+  // the neighbourhood buffer is private to the wave: its LDS accesses execute in issue order,
+  // so a wave-level fence (no workgroup barrier) orders the stores before the blend's reads
+  // and those reads before the next level's stores; the 4 waves of a block run decoupled
   issue(0, fx, fy);
   for (int l = 0; l < pyr.levels; ++l) {
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (lane + 64 * k < nn) nb[wave][lane + 64 * k] = v[k];
-    __syncthreads();
+    wave_lds_sync();
     if (l + 1 < pyr.levels) issue(l + 1, nfx, nfy);
     if (live)
       for (int ch = lane; ch < win; ch += 64) {
@@ -563,7 +574,7 @@ __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const floa
             (1.f - fy) * ((1.f - fx) * n0[0] + fx * n0[1]) + fy * ((1.f - fx) * n0[nd] + fx * n0[nd + 1]);
         o[l * win + ch] = from_f32<OutT>(val);
       }
-    __syncthreads();
+    wave_lds_sync();
     fx = nfx;
     fy = nfy;
   }
@@ -621,14 +632,6 @@ __global__ __launch_bounds__(256) void lookup_bwd_kernel(PyrDesc dpyr, const flo
     }
     __syncthreads();
   }
-}
-
-// this wave's LDS writes are visible to its other lanes: the LDS operations of one wave
-// execute in order, so only the compiler must not move LDS accesses across this point
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // One block per query row, wave l <-> level l: the wave replays the T lookups of the step

@@ -45,7 +45,7 @@ SHAPES = {
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cfgs", default="40,41,45")
+    ap.add_argument("--cfgs", default="40,41,45,57,58,59,60")
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--hw", type=int, nargs=2, default=[46, 62])
     ap.add_argument("--only", default="")

@@ -169,13 +169,15 @@ def test_gru_epilogues(cuda):
     assert _rel(_from_pm(hn, B, H, W), hn_ref) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 1, 8, 9, 40, 41, 45])
+@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 1, 8, 9, 40, 41, 45, 57, 58, 59, 60])
 @pytest.mark.parametrize("segs,cout,kh,kw,hw", [
     ([(256, 256)], 192, 3, 3, (46, 62)),
     ([(128, 128), (128, 128), (128, 128)], 256, 1, 5, (46, 62)),
     ([(128, 128), (128, 128), (128, 128)], 128, 5, 1, (46, 62)),
     ([(128, 128)], 512, 3, 3, (23, 31)),
     ([(64, 64)], 128, 3, 3, (17, 21)),
+    ([(128, 128), (128, 128), (128, 128)], 128, 5, 1, (27, 120)),
+    ([(128, 128)], 256, 3, 3, (27, 120)),
 ])
 def test_fwd_every_variant_full_size(cuda, cfg, segs, cout, kh, kw, hw):
     """Every forward kernel variant (v6 / v5 halo-strip tiles, v4 tiles, generic) at RAFT
@@ -188,8 +190,14 @@ def test_fwd_every_variant_full_size(cuda, cfg, segs, cout, kh, kw, hw):
     w = torch.randn(cout, cin, kh, kw, device=cuda) / (cin * kh * kw) ** 0.5
     bias = torch.randn(cout, device=cuda)
     out = torch.full((P, cout), float("nan"), device=cuda, dtype=torch.bfloat16)
-    if cfg in (41, 45) and kh == 5 and 256 + 4 * W > 479:
-        pytest.skip("256-row v6 tiles: the 5x1 halo strip does not fit in LDS at this width")
+    # v6 flat strips: BM + (kh - 1) W + kw - 1 rows must fit the LDS strip buffer
+    v6_flat = {40: (128, 447), 41: (256, 479), 45: (256, 447)}
+    if cfg in v6_flat and v6_flat[cfg][0] + (kh - 1) * W + kw - 1 > v6_flat[cfg][1]:
+        pytest.skip("v6 flat strip does not fit in LDS at this width (2-D tiles cover it)")
+    # v6 2-D tiles: 57 = 3x3, 58 / 60 = 5x1, 59 = 3x3 and 1x5
+    if (cfg == 57 and (kh, kw) != (3, 3)) or (cfg in (58, 60) and (kh, kw) != (5, 1)) or \
+            (cfg == 59 and (kh, kw) not in ((3, 3), (1, 5))):
+        pytest.skip("2-D tile variant built for other tap shapes")
     C.conv_fwd(srcs, C.pack_fwd(w, segs), C.geom(B, H, W, kh, kw, kh // 2, kw // 2), cout, out, bias=bias, act=1,
                cfg=cfg)
     x = torch.cat([_from_pm(s, B, H, W) for s in srcs], dim=1)
