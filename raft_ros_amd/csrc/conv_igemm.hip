@@ -435,9 +435,7 @@ __device__ __forceinline__ bool row_pixel(int row, int m0, int P, const Tile2D& 
   }
 }
 
-// EPR (measurement probes of the epilogue cost, bias/act store path only): 1 = no global
-// stores, 2 = non-temporal stores, 3 = stores of zeros without the LDS staging
-template <int BM, int BN, int TM, int TN, int NW = 4, int WGN = 2, int EPR = 0, int EFAST = 0, int TW2D = 0>
+template <int BM, int BN, int TM, int TN, int NW = 4, int WGN = 2, int TW2D = 0>
 __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f32x16 (&acc)[TM][TN], int m0,
                                              int n0, int P, int Nn, const Tile2D& t2 = Tile2D{}) {
   constexpr int EPI_LD = BN + 4;  // fp32 epilogue tile row pitch
@@ -452,8 +450,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
   // fused GRU backward, split-bf16 planes) tests its mode per row; for epi 0 / 1 its per-lane
   // mode, masked scalar bias loads and branches cost ~5 us per launch (scripts/bench_conv6.py
   // --probe, profiles/r3_conv6_probe.log).
-  // EFAST = 1 (probe): only the fast path is compiled in (the caller guarantees its modes)
-  const bool fast = EFAST == 1 || (a.epi <= 3 && a.split_g == 0 && EPR == 0);
+  const bool fast = a.epi <= 3 && a.split_g == 0;
   f32x4 fb0{0.f, 0.f, 0.f, 0.f}, fb1{0.f, 0.f, 0.f, 0.f};
   {
     const int n = n0 + (tid % CPR) * 8;
@@ -470,7 +467,6 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
       }
     }
   }
-  if constexpr (EPR != 3) {
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -482,7 +478,6 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
         et[row * EPI_LD + col] = acc[i][j][r];
       }
   __syncthreads();
-  }
   if (fast) {
     const int ch = tid % CPR;
     const int n = n0 + ch * 8;
@@ -612,7 +607,6 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
     }
     return;
   }
-  if constexpr (EFAST == 1) return;
   // generic path: every thread owns the same 8-channel chunk in all of its rows (NT % CPR
   // == 0): the bias is loaded once, before the row loop, instead of as a dependent load per row
   const int ch = tid % CPR;
@@ -638,20 +632,17 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
         if constexpr (TW2D == 0) break;
         else continue;
       }
-      f32x4 lo{}, hi{};
-      if constexpr (EPR != 3) {
-        lo = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8);
-        hi = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8 + 4);
-      }
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8 + 4);
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  #pragma unroll
+#pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = v[q] * alpha + bia[q];
       if (M == 4 || M == 5) {
         // fused GRU backward gate math (fp32 gradient rows; gru_cols is a multiple of 8)
         float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
         if (n >= a.acc_c0) {
           const f32x4 o0 = *reinterpret_cast<const f32x4*>(o), o1 = *reinterpret_cast<const f32x4*>(o + 4);
-  #pragma unroll
+#pragma unroll
           for (int q = 0; q < 4; ++q) {
             v[q] += o0[q];
             v[q + 4] += o1[q];
@@ -659,7 +650,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
         }
         if (a.addsrc) {
           const bf16x8 av = *reinterpret_cast<const bf16x8*>(a.addsrc + p * a.addsrc_stride + n);
-  #pragma unroll
+#pragma unroll
           for (int q = 0; q < 8; ++q) v[q] += static_cast<float>(av[q]);
         }
         const bf16x8 gv = *reinterpret_cast<const bf16x8*>(a.g0 + p * a.g0_stride + n);
@@ -670,7 +661,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
           const bf16x8 zv = *reinterpret_cast<const bf16x8*>(a.z + p * a.z_stride + n);
           bf16x8 dq;
           float cr[8];
-  #pragma unroll
+#pragma unroll
           for (int q = 0; q < 8; ++q) {
             const float zz = static_cast<float>(zv[q]), qq = static_cast<float>(gv[q]), hh = static_cast<float>(hv[q]);
             dq[q] = static_cast<__bf16>(v[q] * zz * (1.f - qq * qq));
@@ -684,7 +675,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
           const f32x4 c0 = *reinterpret_cast<const f32x4*>(cp), c1 = *reinterpret_cast<const f32x4*>(cp + 4);
           const float cv[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
           float ov[8];
-  #pragma unroll
+#pragma unroll
           for (int q = 0; q < 8; ++q) {
             const float rr = static_cast<float>(gv[q]), hh = static_cast<float>(hv[q]);
             d3[q] = static_cast<__bf16>(v[q] * hh * rr * (1.f - rr));
@@ -698,21 +689,21 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
         // last GRU data gradient: bf16 d net / fp32 d inp / masked bf16 d motion
         const float* o = static_cast<const float*>(a.out) + p * a.out_stride + n;
         const f32x4 o0 = *reinterpret_cast<const f32x4*>(o), o1 = *reinterpret_cast<const f32x4*>(o + 4);
-  #pragma unroll
+#pragma unroll
         for (int q = 0; q < 4; ++q) {
           v[q] += o0[q];
           v[q + 4] += o1[q];
         }
         bf16x8 w;
         if (n < a.gru_cols) {
-  #pragma unroll
+#pragma unroll
           for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(v[q]);
           *reinterpret_cast<bf16x8*>(a.out3 + p * a.out3_stride + n) = w;
         } else {
           const int c = n - a.cm_c0;
           if (c < a.cm_valid) {  // chunks wholly past cm_valid are not stored (cout may be narrower)
             const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.cmask + p * a.cmask_stride + c);
-  #pragma unroll
+#pragma unroll
             for (int q = 0; q < 8; ++q)
               w[q] = static_cast<__bf16>((c + q < a.cm_valid && static_cast<float>(m[q]) > 0.f) ? v[q] : 0.f);
             *reinterpret_cast<bf16x8*>(a.cout + p * a.cout_stride + c) = w;
@@ -720,7 +711,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
         }
       } else if (M == 0) {
         if (a.act == 1)
-  #pragma unroll
+#pragma unroll
           for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
         if (a.split_g > 0 && !a.out_f32) {
           split_store8(static_cast<__bf16*>(a.out) + p * a.out_stride, a.split_g, n, nv, v);
@@ -730,7 +721,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
             *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
             *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
           } else {
-  #pragma unroll
+#pragma unroll
             for (int q = 0; q < 8; ++q)
               if (q < nv) o[q] = v[q];
           }
@@ -738,17 +729,11 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
           __bf16* o = static_cast<__bf16*>(a.out) + p * a.out_stride + n;
           if (nv == 8) {
             bf16x8 w;
-  #pragma unroll
+#pragma unroll
             for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(v[q]);
-            if constexpr (EPR == 1) {
-              if (v[0] == 1234.5f) *reinterpret_cast<bf16x8*>(o) = w;
-            } else if constexpr (EPR == 2) {
-              __builtin_nontemporal_store(w, reinterpret_cast<bf16x8*>(o));
-            } else {
-              *reinterpret_cast<bf16x8*>(o) = w;
-            }
+            *reinterpret_cast<bf16x8*>(o) = w;
           } else {
-  #pragma unroll
+#pragma unroll
             for (int q = 0; q < 8; ++q)
               if (q < nv) o[q] = static_cast<__bf16>(v[q]);
           }
@@ -756,7 +741,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
       } else if (M == 1) {
         if (a.mask) {
           const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.mask + p * a.mask_stride + n);
-  #pragma unroll
+#pragma unroll
           for (int q = 0; q < 8; ++q)
             if (!(static_cast<float>(m[q]) > 0.f)) v[q] = 0.f;
         }
@@ -772,7 +757,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
             *reinterpret_cast<f32x4*>(o) = x0;
             *reinterpret_cast<f32x4*>(o + 4) = x1;
           } else {
-  #pragma unroll
+#pragma unroll
             for (int q = 0; q < 8; ++q)
               if (q < nv) o[q] = accum ? o[q] + v[q] : v[q];
           }
@@ -781,11 +766,11 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
           if (nv == 8) {
             bf16x8 w;
             const bf16x8 old = accum ? *reinterpret_cast<const bf16x8*>(o) : bf16x8{};
-  #pragma unroll
+#pragma unroll
             for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(accum ? static_cast<float>(old[q]) + v[q] : v[q]);
             *reinterpret_cast<bf16x8*>(o) = w;
           } else {
-  #pragma unroll
+#pragma unroll
             for (int q = 0; q < 8; ++q)
               if (q < nv) o[q] = static_cast<__bf16>(accum ? static_cast<float>(o[q]) + v[q] : v[q]);
           }
@@ -794,13 +779,13 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
         // split mode: sigmoid in fp32, r * h from the fp32-faithful h (hi + lo planes)
         const int C = Nn >> 1;
         float sg[8];
-  #pragma unroll
+#pragma unroll
         for (int q = 0; q < 8; ++q) sg[q] = sigmoidf_(v[q]);
         split_store8(static_cast<__bf16*>(a.out) + p * a.out_stride, a.split_g, n, 8, sg);
         if (n >= C) {
           float hv[8];
           load8(a.h + p * a.h_stride + (n - C), a.split_h, hv);
-  #pragma unroll
+#pragma unroll
           for (int q = 0; q < 8; ++q) hv[q] *= sg[q];
           split_store8(a.out2 + p * a.out2_stride, a.split_g2, n - C, 8, hv);
         }
@@ -808,7 +793,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
         float zv[8], hv[8], hn[8];
         load8(a.z + p * a.z_stride + n, a.split_z, zv);
         load8(a.h + p * a.h_stride + n, a.split_h, hv);
-  #pragma unroll
+#pragma unroll
         for (int q = 0; q < 8; ++q) {
           const float qq = tanhf_(v[q]);
           hn[q] = (1.f - zv[q]) * hv[q] + zv[q] * qq;
@@ -819,13 +804,13 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
       } else if (M == 2) {
         const int C = Nn >> 1;
         bf16x8 sg;
-  #pragma unroll
+#pragma unroll
         for (int q = 0; q < 8; ++q) sg[q] = static_cast<__bf16>(sigmoidf_(v[q]));
         *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = sg;
         if (n >= C) {
           const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + (n - C));
           bf16x8 rh;
-  #pragma unroll
+#pragma unroll
           for (int q = 0; q < 8; ++q) rh[q] = static_cast<__bf16>(static_cast<float>(sg[q]) * static_cast<float>(hv[q]));
           *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + (n - C)) = rh;
         }
@@ -833,7 +818,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
         const bf16x8 zv = *reinterpret_cast<const bf16x8*>(a.z + p * a.z_stride + n);
         const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + n);
         bf16x8 hn, qo;
-  #pragma unroll
+#pragma unroll
         for (int q = 0; q < 8; ++q) {
           const float qq = tanhf_(v[q]);
           const float z = static_cast<float>(zv[q]);
@@ -996,13 +981,9 @@ typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8;
 // 16-byte LDS read at a 32-bit LDS byte address
 __device__ __forceinline__ bf16x8 lds_read16(unsigned addr) { return *(const lds_bf16x8*)(uintptr_t)addr; }
 
-// PROBE (measurement builds only, cfg 30..32 of the 128x128 tile): 1 = no MFMAs, 2 = no
-// DMA, 3 = neither -- what bounds a step (scripts/probe_conv5.py, profiles/r3_probe_conv5.log:
-// 0.59 us per step, 0.40 us of it without MFMAs and DMA; ~7.5 us per launch outside the loop).
-// A v6 schedule that spread the next step's fragment reads behind the MFMA sub-steps and
-// moved the barrier behind the first sub-step (4-stage ring, no LDS drain) measured 5-10%
-// slower on every shape (profiles/r3_probe_conv6.log) and was dropped.
-template <int BM, int BN, int NW = 4, int PROBE = 0>
+// Measurement probes of this kernel (MFMA-, DMA- and read-free variants, cfg 30..32; removed
+// after the measurement: profiles/r3_probe_conv5.log, profiles/r3_probe_conv6.log) led to v6.
+template <int BM, int BN, int NW = 4>
 __global__ __launch_bounds__(NW * 64) void conv_fwd5_kernel(const ConvFwdArgs a, int strip_rows) {
   extern __shared__ __attribute__((aligned(1024))) __bf16 dsm[];
   // NW waves in an (NW/2) x 2 layout; NW = 8 puts two waves on every SIMD of the CU (one
@@ -1085,15 +1066,6 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd5_kernel(const ConvFwdArgs a,
   // ---- DMA issue state (step `is_t`): chunk, tap, weight k offset, stage
   int is_t = 0, is_cc = 0, is_tap = 0, is_stage = 0;
   auto issue_next = [&]() __attribute__((always_inline)) {
-    if constexpr ((PROBE & 2) != 0) {
-      ++is_t;
-      is_stage = is_stage == 2 ? 0 : is_stage + 1;
-      if (++is_tap == ntaps) {
-        is_tap = 0;
-        ++is_cc;
-      }
-      return;
-    }
     if (is_tap == 0) {
       const int c0 = is_cc * 64;
       __amdgpu_buffer_rsrc_t rs = r0;
@@ -1168,10 +1140,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd5_kernel(const ConvFwdArgs a,
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        if constexpr ((PROBE & 1) != 0)
-          acc[i][j][0] += static_cast<float>(fa[i][s][0]) * static_cast<float>(fb[j][s][0]);
-        else
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
   };
 
   bf16x8 fa0[TM][4], fb0[TN][4], fa1[TM][4], fb1[TN][4];
@@ -1292,7 +1261,7 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {
 // strip of BM + (KH-1) W + KW-1 rows no longer fits in LDS): the strip is the tile's halo
 // block of (BM/TW + KH-1) x (TW + KW-1) pixels with pitch TW + KW-1, so a tap is still one
 // constant row shift, and pixels outside the image are DMA'd as zeros (no per-tap masking).
-template <int BM, int BN, int WGM, int WGN, int KH, int KW, int SCHED = 1, int TW = 0>
+template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW = 0>
 __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwdArgs a, int strip_rows) {
   constexpr int NW = WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;  // wave tile
@@ -1462,9 +1431,6 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   auto read_s = [&](auto gc, auto sc) __attribute__((always_inline)) {
     constexpr int G = decltype(gc)::value, s = decltype(sc)::value;
     constexpr int T = G % NT, R = G & 1;
-    if constexpr ((SCHED & 8) != 0) {  // probe: no fragment reads after the prologue
-      if (G > 0) return;
-    }
     constexpr unsigned AOFF = ((G / NT) & 1) ? (unsigned)SB : 0u;
     constexpr unsigned BOFF = (unsigned)((G % NS) * BSTAGE);
 #pragma unroll
@@ -1481,18 +1447,12 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        if constexpr ((SCHED & 2) != 0)  // probe: no MFMAs
-          acc[i][j][0] += static_cast<float>(fa[R][i][s][0]) * static_cast<float>(fb[R][j][s][0]);
-        else
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[R][i][s], fb[R][j][s], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[R][i][s], fb[R][j][s], acc[i][j], 0, 0, 0);
   };
   // issue the step with in-block index GU of the block starting at chunk cb (GU may run past
   // the block: stage and parity stay compile-time because U * NT % 6 == 0)
   auto issue_g = [&](int cb, auto guc) __attribute__((always_inline)) {
     constexpr int GU = decltype(guc)::value;
-    if constexpr ((SCHED & 4) != 0) {  // probe: no DMA after the prologue
-      if (GU > 2 || cb > 0) return;
-    }
     const int cu = cb + GU / NT;
     if (cu < nchunks)
       issue(cu, std::integral_constant<int, GU % NT>{}, std::integral_constant<int, GU % NS>{},
@@ -1521,29 +1481,20 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
       else if constexpr ((G + 2) % NT == 0) wait_vmcnt_le<40>(BI + spw);
       else wait_vmcnt<BI>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if constexpr ((SCHED & 16) == 0) __builtin_amdgcn_s_barrier();  // (probe 16: none)
+      __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       // step t+3 into the stage of step t (its fragments were read before this barrier)
       issue_g(cb, std::integral_constant<int, G + 3>{});
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr ((SCHED & 1) == 1) {
-        // MFMA sub-step s of step t, then the sub-step-s reads of step t+1: every MFMA group
-        // precedes the reads issued after it, so the compiler's lgkmcnt (at most 15 in flight)
-        // never holds an MFMA behind this step's new reads
-        static_for<4>([&](auto sc) __attribute__((always_inline)) {
-          mfma_s(std::integral_constant<int, G & 1>{}, sc);
-          __builtin_amdgcn_sched_barrier(0);
-          read_s(std::integral_constant<int, G + 1>{}, sc);
-          __builtin_amdgcn_sched_barrier(0);
-        });
-      } else {
-        // all reads of step t+1 first, then the 16 MFMAs of step t
-        read(std::integral_constant<int, G + 1>{});
+      // MFMA sub-step s of step t, then the sub-step-s reads of step t+1: every MFMA group
+      // precedes the reads issued after it, so the compiler's lgkmcnt (at most 15 in flight)
+      // never holds an MFMA behind this step's new reads
+      static_for<4>([&](auto sc) __attribute__((always_inline)) {
+        mfma_s(std::integral_constant<int, G & 1>{}, sc);
         __builtin_amdgcn_sched_barrier(0);
-        static_for<4>([&](auto sc) __attribute__((always_inline)) {
-          mfma_s(std::integral_constant<int, G & 1>{}, sc);
-        });
-      }
+        read_s(std::integral_constant<int, G + 1>{}, sc);
+        __builtin_amdgcn_sched_barrier(0);
+      });
     } else {
       static_for<4>([&](auto sc) __attribute__((always_inline)) {
         mfma_s(std::integral_constant<int, G & 1>{}, sc);
@@ -1560,19 +1511,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   wait_vmcnt<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr ((SCHED & 32) != 0) {  // probe: no epilogue (one conditional store keeps acc live)
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t += acc[i][j][r];
-    if (t == 1234.5f) static_cast<float*>(a.out)[0] = t;
-  } else {
-    fwd_epilogue<BM, BN, TM, TN, NW, WGN, (SCHED >> 6) & 3, (SCHED >> 8) & 1, TW>(
-        a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn, t2);
-  }
+  fwd_epilogue<BM, BN, TM, TN, NW, WGN, TW>(a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn, t2);
 }
 
 // strip rows of conv_fwd6 for a shape (0 if it does not fit)
@@ -2130,7 +2069,7 @@ __global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
 }  // namespace
 
 namespace {
-template <int BM, int BN, int WGM, int WGN, int KH, int KW, int SCHED, int TW = 0>
+template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW = 0>
 bool launch_fwd6_t(const ConvFwdArgs& a, hipStream_t s) {
   using CF = Fwd6Cfg<BN, WGN, KH * KW>;
   constexpr int NW = WGM * WGN;
@@ -2145,55 +2084,33 @@ bool launch_fwd6_t(const ConvFwdArgs& a, hipStream_t s) {
     tiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
   }
   const dim3 grid((unsigned)(tiles * ((a.N + BN - 1) / BN)));
-  set_lds_limit((const void*)conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, SCHED, TW>, CF::LDS);
-  hipLaunchKernelGGL((conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, SCHED, TW>), grid, dim3(NW * 64), CF::LDS, s, a,
-                     rows);
+  set_lds_limit((const void*)conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, TW>, CF::LDS);
+  hipLaunchKernelGGL((conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, TW>), grid, dim3(NW * 64), CF::LDS, s, a, rows);
   return true;
 }
-template <int BM, int BN, int WGM, int WGN, int SCHED = 1>
-bool launch_fwd6_taps(const ConvFwdArgs& a, hipStream_t s) {
-  if (a.KH == 3 && a.KW == 3) return launch_fwd6_t<BM, BN, WGM, WGN, 3, 3, SCHED>(a, s);
-  if (a.KH == 1 && a.KW == 5) return launch_fwd6_t<BM, BN, WGM, WGN, 1, 5, SCHED>(a, s);
-  if (a.KH == 5 && a.KW == 1) return launch_fwd6_t<BM, BN, WGM, WGN, 5, 1, SCHED>(a, s);
-  return false;
-}
-template <int SCHED>
-bool launch_fwd6_probe(const ConvFwdArgs& a, hipStream_t s) {
-  if (a.KH == 3 && a.KW == 3) return launch_fwd6_t<256, 64, 4, 1, 3, 3, SCHED>(a, s);
-  if (a.KH == 1 && a.KW == 5) return launch_fwd6_t<256, 64, 4, 1, 1, 5, SCHED>(a, s);
-  return false;
-}
+// v6 tiles (forced with cfg, chosen per shape by launch_conv_fwd): 41 = 256x64 flat strip (4x1
+// waves of 64x64; 3x3 / 1x5 / 5x1), 45 = 256x128 flat strip (2x2 waves of 128x64), 59 = 256x64
+// as 2-D 4 x 64 tiles (3x3, 1x5), 60 = 256x64 as 2-D 8 x 32 tiles (5x1).  (Measured and
+// dropped: 128x128 4-wave flat and 2-D tiles, cfg 40 / 57 / 58; all next-step reads before the
+// step's MFMAs, cfg 43 / 44 / 46: profiles/r3_bench_conv6_tiles.log, r3_bench_conv6_2d.log.)
 bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
+  const bool t33 = a.KH == 3 && a.KW == 3, t15 = a.KH == 1 && a.KW == 5, t51 = a.KH == 5 && a.KW == 1;
   switch (cfg) {
-    case 40: return launch_fwd6_taps<128, 128, 2, 2>(a, s);
-    case 41: return launch_fwd6_taps<256, 64, 4, 1>(a, s);
-    case 45: return launch_fwd6_taps<256, 128, 2, 2>(a, s);
-    // 2-D tiles (wide images): 57 = 128x128 as 2 x 64 (3x3), 58 = 128x128 as 4 x 32 (5x1),
-    // 59 = 256x64 as 4 x 64 (3x3, 1x5), 60 = 256x64 as 8 x 32 (5x1)
-    case 57:
-      return a.KH == 3 && a.KW == 3 && launch_fwd6_t<128, 128, 2, 2, 3, 3, 1, 64>(a, s);
-    case 58:
-      return a.KH == 5 && a.KW == 1 && launch_fwd6_t<128, 128, 2, 2, 5, 1, 1, 32>(a, s);
+    case 41:
+      if (t33) return launch_fwd6_t<256, 64, 4, 1, 3, 3>(a, s);
+      if (t15) return launch_fwd6_t<256, 64, 4, 1, 1, 5>(a, s);
+      return t51 && launch_fwd6_t<256, 64, 4, 1, 5, 1>(a, s);
+    case 45:
+      if (t33) return launch_fwd6_t<256, 128, 2, 2, 3, 3>(a, s);
+      if (t15) return launch_fwd6_t<256, 128, 2, 2, 1, 5>(a, s);
+      return false;
     case 59:
-      if (a.KH == 3 && a.KW == 3) return launch_fwd6_t<256, 64, 4, 1, 3, 3, 1, 64>(a, s);
-      return a.KH == 1 && a.KW == 5 && launch_fwd6_t<256, 64, 4, 1, 1, 5, 1, 64>(a, s);
+      if (t33) return launch_fwd6_t<256, 64, 4, 1, 3, 3, 64>(a, s);
+      return t15 && launch_fwd6_t<256, 64, 4, 1, 1, 5, 64>(a, s);
     case 60:
-      return a.KH == 5 && a.KW == 1 && launch_fwd6_t<256, 64, 4, 1, 5, 1, 1, 32>(a, s);
-    // measurement probes of the 256x64 tile (scripts/bench_conv6.py --probe): no MFMA / no
-    // in-loop DMA / no fragment reads / no barrier / no epilogue / bare loop
-    case 47: return launch_fwd6_probe<1 | 2>(a, s);
-    case 48: return launch_fwd6_probe<1 | 4>(a, s);
-    case 49: return launch_fwd6_probe<1 | 8>(a, s);
-    case 50: return launch_fwd6_probe<1 | 16>(a, s);
-    case 51: return launch_fwd6_probe<1 | 32>(a, s);
-    case 52: return launch_fwd6_probe<1 | 2 | 4 | 8 | 16>(a, s);
-    // epilogue probes: no global stores / non-temporal stores / zero stores without LDS staging
-    case 53: return launch_fwd6_probe<1 | 64>(a, s);
-    case 54: return launch_fwd6_probe<1 | 128>(a, s);
-    case 55: return launch_fwd6_probe<1 | 192>(a, s);
-    // only the fast bias/act/gradient epilogue compiled in (code-size probe; epi <= 3, no split)
-    case 56: return launch_fwd6_probe<1 | 256>(a, s);
-    default: return false;
+      return t51 && launch_fwd6_t<256, 64, 4, 1, 5, 1, 32>(a, s);
+    default:
+      return false;
   }
 }
 }  // namespace
@@ -2234,34 +2151,10 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   bool ok5 = a.KH * a.KW > 1 && a.Cin % 64 == 0 && a.N >= 64 && a.P < (1L << 30);
   for (int i = 0; i < a.nsrc; ++i) ok5 = ok5 && a.src[i].C % 64 == 0;
   int v5 = cfg >= 20 ? cfg : 0;
-  if (ok5 && cfg >= 30 && cfg <= 32) {  // measurement probes of the 128x128 / 8-wave tile
-    const int rows = (128 + (a.KH - 1) * a.W + a.KW - 1 + 7) / 8 * 8;
-    const long lds = fwd5_lds_bytes(128, 128, rows);
-    if (lds == 0) return hipErrorInvalidValue;
-    const dim3 grid(tiles(128, 128));
-#define RAFT_PROBE(PR)                                                     \
-  set_lds_limit((const void*)conv_fwd5_kernel<128, 128, 8, PR>, (int)lds); \
-  hipLaunchKernelGGL((conv_fwd5_kernel<128, 128, 8, PR>), grid, dim3(512), lds, s, a, rows)
-    if (cfg == 30) {
-      RAFT_PROBE(1);
-    } else if (cfg == 31) {
-      RAFT_PROBE(2);
-    } else {
-      RAFT_PROBE(3);
-    }
-#undef RAFT_PROBE
-    return hipGetLastError();
-  }
-  if (cfg >= 40 && cfg <= 60) {
-    // v6 (measurement / forced): 40 = 128x128 (2x2 waves of 64x64), 41 = 256x64 (4x1 waves of
-    // 64x64), 45 = 256x128 (2x2 waves of 128x64).  (Issuing all next-step reads before the
-    // step's MFMAs measured 2-5% slower than interleaving them, 2.5-3.5x with the 256x128 tile's
-    // register spills: profiles/r3_bench_conv6_tiles.log, cfg 43 / 44 / 46.)
-    const int taps = a.KH * a.KW;
-    const bool shape6 = (a.KH == 3 && a.KW == 3) || (taps == 5 && (a.KH == 1 || a.KW == 1));
+  if (cfg == 41 || cfg == 45 || cfg == 59 || cfg == 60) {  // v6 tiles (tests / microbenchmarks)
+    const bool shape6 = (a.KH == 3 && a.KW == 3) || (a.KH * a.KW == 5 && (a.KH == 1 || a.KW == 1));
     if (!ok5 || !shape6 || a.PH != a.KH / 2 || a.PW != a.KW / 2) return hipErrorInvalidValue;
-    if (launch_conv_fwd6(a, cfg, s)) return hipGetLastError();
-    return hipErrorInvalidValue;
+    return launch_conv_fwd6(a, cfg, s) ? hipGetLastError() : hipErrorInvalidValue;
   }
   if (ok5 && cfg == 0 && a.PH == a.KH / 2 && a.PW == a.KW / 2) {
     // v6 where it measured faster than v5 at config #2 (scripts/bench_conv6.py,
@@ -2346,6 +2239,10 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   }
   // v4 (scripts/bench_convs.py on MI355X): 64x128 tiles for N > 64 (the 576-wide mask-head 1x1:
   // 34.3 -> 30.0 us, profiles/r2_bench_convs_cfg8.log), 64x64 otherwise
+  if (cfg == 10) {  // measurement: 128x128 tiles (64x64 wave tiles, one workgroup per CU)
+    hipLaunchKernelGGL((conv_fwd4_kernel<128, 128, 3>), dim3(tiles(128, 128)), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   const bool wide = cfg == 8 || (cfg != 9 && a.N > 64);
   if (wide)
     hipLaunchKernelGGL((conv_fwd4_kernel<64, 128, 3>), dim3(tiles(64, 128)), dim3(256), 0, s, a);

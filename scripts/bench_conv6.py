@@ -2,8 +2,10 @@
 """conv_fwd6 (lean halo strip) vs the automatic choice (v5 / v4) on the update-block conv
 shapes at config #2 (8 x 46 x 62 pixels): bitwise / numeric agreement and time per launch.
 
-    python scripts/bench_conv6.py [--cfgs 40,41,42] [--batch 8] [--hw 46 62]
-cfg 40 = 128x128 (4 waves), 41 = 256x64 (4 waves), 42 = 256x128 (8 waves).
+    python scripts/bench_conv6.py [--cfgs 41,45,59,60] [--batch 8] [--hw 46 62]
+cfg 41 = 256x64 flat strip, 45 = 256x128 flat strip, 59 / 60 = 256x64 as 2-D 4x64 / 8x32 tiles.
+(The probe variants behind profiles/r3_conv6_probe.log -- no MFMA / DMA / reads / barrier /
+epilogue -- were removed after the measurement.)
 """
 from __future__ import annotations
 
@@ -45,20 +47,16 @@ SHAPES = {
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cfgs", default="40,41,45,57,58,59,60")
+    ap.add_argument("--cfgs", default="41,45,59,60")
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--hw", type=int, nargs=2, default=[46, 62])
     ap.add_argument("--only", default="")
-    ap.add_argument("--probe", action="store_true",
-                    help="256x64 probes: 41 full, 47 no MFMA, 48 no DMA, 49 no reads, 50 no barrier, "
-                         "51 no epilogue, 52 bare loop, 53 no global stores, 54 nt stores, 55 zero stores without LDS staging, 56 only the fast epilogue compiled in")
+
     args = ap.parse_args()
     dev = torch.device("cuda")
     B, (H, W) = args.batch, args.hw
     P = B * H * W
     cfgs = [int(c) for c in args.cfgs.split(",")]
-    if args.probe:
-        cfgs = [41, 51, 52, 53, 56]
     names = args.only.split(",") if args.only else list(SHAPES)
     torch.manual_seed(0)
     for name in names:
@@ -90,7 +88,7 @@ def main():
             same = torch.equal(out[:, :cout], ref_out[:, :cout])
             err = (out[:, :cout].float() - yt).abs().max().item()
             us = timeit(lambda: C.conv_fwd([x], wt, g, cout, out[:, :cout], bias=b, act=1, cfg=cfg))
-            tag = "" if args.probe and cfg != 41 else (" ==" if same else f" err={err:.3f}")
+            tag = " ==" if same else f" err={err:.3f}"
             line.append(f"c{cfg} {us:6.1f}us ({2 * macs / us / 1e6:4.0f}TF){tag}")
         print("  ".join(line), flush=True)
 

@@ -169,7 +169,7 @@ def test_gru_epilogues(cuda):
     assert _rel(_from_pm(hn, B, H, W), hn_ref) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 1, 8, 9, 40, 41, 45, 57, 58, 59, 60])
+@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 1, 8, 9, 41, 45, 59, 60])
 @pytest.mark.parametrize("segs,cout,kh,kw,hw", [
     ([(256, 256)], 192, 3, 3, (46, 62)),
     ([(128, 128), (128, 128), (128, 128)], 256, 1, 5, (46, 62)),
@@ -191,13 +191,12 @@ def test_fwd_every_variant_full_size(cuda, cfg, segs, cout, kh, kw, hw):
     bias = torch.randn(cout, device=cuda)
     out = torch.full((P, cout), float("nan"), device=cuda, dtype=torch.bfloat16)
     # v6 flat strips: BM + (kh - 1) W + kw - 1 rows must fit the LDS strip buffer
-    v6_flat = {40: (128, 447), 41: (256, 479), 45: (256, 447)}
+    v6_flat = {41: (256, 479), 45: (256, 447)}
     if cfg in v6_flat and v6_flat[cfg][0] + (kh - 1) * W + kw - 1 > v6_flat[cfg][1]:
         pytest.skip("v6 flat strip does not fit in LDS at this width (2-D tiles cover it)")
-    # v6 2-D tiles: 57 = 3x3, 58 / 60 = 5x1, 59 = 3x3 and 1x5
-    if (cfg == 57 and (kh, kw) != (3, 3)) or (cfg in (58, 60) and (kh, kw) != (5, 1)) or \
-            (cfg == 59 and (kh, kw) not in ((3, 3), (1, 5))):
-        pytest.skip("2-D tile variant built for other tap shapes")
+    # v6 tap shapes: 45 = 3x3 / 1x5, 59 (2-D) = 3x3 / 1x5, 60 (2-D) = 5x1
+    if (cfg == 60 and (kh, kw) != (5, 1)) or (cfg in (45, 59) and (kh, kw) not in ((3, 3), (1, 5))):
+        pytest.skip("v6 variant built for other tap shapes")
     C.conv_fwd(srcs, C.pack_fwd(w, segs), C.geom(B, H, W, kh, kw, kh // 2, kw // 2), cout, out, bias=bias, act=1,
                cfg=cfg)
     x = torch.cat([_from_pm(s, B, H, W) for s in srcs], dim=1)
@@ -251,7 +250,7 @@ def test_wgrad_params_periodic_source_and_param_layout(cuda):
     assert torch.equal(gz, gz2)
 
 
-@pytest.mark.parametrize("cfg", [0, 8, 25, 26, 40, 41])
+@pytest.mark.parametrize("cfg", [0, 8, 25, 26, 41, 59])
 def test_gru_backward_epilogues_match_unfused(cuda, cfg):
     """EPI_GRU_BWD_A / _B / _LAST (gate backward fused into the data-gradient epilogue) vs
     the plain EPI_GRAD store followed by the separate gru_bwd_a / gru_bwd_b / masked_cast
