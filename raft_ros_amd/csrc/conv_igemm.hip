@@ -2238,11 +2238,8 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
     }
   }
   // v4 (scripts/bench_convs.py on MI355X): 64x128 tiles for N > 64 (the 576-wide mask-head 1x1:
-  // 34.3 -> 30.0 us, profiles/r2_bench_convs_cfg8.log), 64x64 otherwise
-  if (cfg == 10) {  // measurement: 128x128 tiles (64x64 wave tiles, one workgroup per CU)
-    hipLaunchKernelGGL((conv_fwd4_kernel<128, 128, 3>), dim3(tiles(128, 128)), dim3(256), 0, s, a);
-    return hipGetLastError();
-  }
+  // 34.3 -> 30.0 us, profiles/r2_bench_convs_cfg8.log), 64x64 otherwise; 128x128 tiles (one
+  // workgroup per CU) measured 21-30% slower on every 1x1 shape (profiles/r3_conv_1x1_tiles.log)
   const bool wide = cfg == 8 || (cfg != 9 && a.N > 64);
   if (wide)
     hipLaunchKernelGGL((conv_fwd4_kernel<64, 128, 3>), dim3(tiles(64, 128)), dim3(256), 0, s, a);
