@@ -1230,10 +1230,10 @@ struct Fwd6Cfg {
                                                       // so stage (step % 3), register set (step & 1)
                                                       // and strip parity (chunk & 1) are compile-time
   static constexpr int RING = NS * BN * 128;
-  static constexpr int SB0 = ((kLdsMax - RING) / 2) & ~127;
-  static constexpr int SB = SB0 < 65408 ? SB0 : 65408;  // odd-chunk strip = +SB immediate offset
-  static constexpr int MAX_ROWS = SB / 128 - 1;         // strip rows (the last row is the zero row)
+  static constexpr int SB = fwd6_sb(BN);              // odd-chunk strip = +SB immediate offset
+  static constexpr int MAX_ROWS = fwd6_max_rows(BN);  // strip rows (the last row is the zero row)
   static constexpr int LDS = RING + 2 * SB;
+  static_assert(LDS <= kLdsMax, "LDS budget");
 };
 
 template <class F, int... I>
@@ -1514,12 +1514,6 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   fwd_epilogue<BM, BN, TM, TN, NW, WGN, TW>(a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn, t2);
 }
 
-// strip rows of conv_fwd6 for a shape (0 if it does not fit)
-inline int fwd6_strip_rows(int BM, int NW, int KH, int KW, int W, int max_rows) {
-  const int need = BM + (KH - 1) * W + KW - 1;
-  const int rows = (need + 8 * NW - 1) / (8 * NW) * (8 * NW);
-  return rows <= max_rows ? rows : 0;
-}
 
 // ============================================================================ wgrad helpers
 constexpr int WBK = kWgradBK;
@@ -2168,19 +2162,9 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
     // the 256 CUs or v4 would pad N (N = 64, 192, > 256: 1080p convc2 63.0 -> 41.8 us, Sintel
     // conv 28.5 -> 23.0), otherwise v5 / v4 (1080p conv 37.1 v4 vs 45.6 with 272 workgroups);
     // 8 x 32 for every 5x1 up to ~24k pixels (config #2 z||r 43.9 -> 38.9, Sintel q 22.8 -> 20.0;
-    // v4 keeps 1080p's 32k pixels: 29.5 vs 39.1 us).
-    const long wg59 = (long)a.B * ((a.H + 3) / 4) * ((a.W + 63) / 64) * ((a.N + 63) / 64);
-    const int np = (a.N + 63) / 64 * 64;
-    const bool flat3 = fwd6_strip_rows(256, 4, 3, 3, a.W, Fwd6Cfg<64, 1, 9>::MAX_ROWS) > 0;
-    int v6 = 0;
-    if (a.KH == 3 && a.KW == 3) {
-      if (flat3) v6 = (a.N <= 128 || a.N > 256) ? 41 : (a.N <= 192 ? 45 : 0);
-      else if (wg59 <= 256 || (np != 128 && np != 256)) v6 = 59;
-    } else if (a.KH == 1 && a.KW == 5) {
-      v6 = a.N <= 128 ? (a.P <= 24576 ? 59 : 41) : 0;  // config #2 q: 21.8 -> 20.6 us
-    } else if (a.KH == 5 && a.KW == 1) {
-      v6 = a.P <= 24576 ? 60 : 0;
-    }
+    // v4 keeps 1080p's 32k pixels: 29.5 vs 39.1 us).  The rule: choose_fwd6 (kernel_abi.h,
+    // unit-tested on the host).
+    const int v6 = choose_fwd6(a.KH, a.KW, a.N, a.B, a.H, a.W);
     if (v6 && launch_conv_fwd6(a, v6, s)) return hipGetLastError();
   }
   if (ok5 && v5 == 0 && cfg == 0) {

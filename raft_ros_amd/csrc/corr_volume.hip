@@ -509,10 +509,13 @@ struct FlowPack {
   long smo;
 };
 
-template <typename OutT>
+// RC > 0: the radius as a compile-time constant (RAFT's r = 4): the window index math divides by
+// constants (a runtime 32-bit division is ~30 VALU per use)
+template <typename OutT, int RC = 0>
 __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const float* __restrict__ coords,
-                                                         OutT* __restrict__ out, int B, int H, int W, int r,
+                                                         OutT* __restrict__ out, int B, int H, int W, int r_arg,
                                                          int out_ch, const FlowPack fp) {
+  const int r = RC > 0 ? RC : r_arg;
   __shared__ float nb[4][NBMAX];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
@@ -639,7 +642,7 @@ __global__ __launch_bounds__(256) void lookup_bwd_kernel(PyrDesc dpyr, const flo
 // lane) into the row's level-l region in LDS; the block then writes the whole row once
 // (padding columns as zeros: no memset of the buffer).  Same per-element fp32 summation
 // order as T sequential lookup_bwd launches into a zeroed buffer.
-template <typename GT>
+template <typename GT, int RC = 0>
 __global__ __launch_bounds__(256) void lookup_grad_rows_kernel(const GradRowsArgs a) {
   extern __shared__ float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -661,7 +664,7 @@ __global__ __launch_bounds__(256) void lookup_grad_rows_kernel(const GradRowsArg
     for (long i = tid * 4; i < ld; i += 1024) *reinterpret_cast<f32x4*>(row + i) = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   __syncthreads();
-  const int r = a.r, rd = 2 * r + 1, nd = rd + 1, win = rd * rd;
+  const int r = RC > 0 ? RC : a.r, rd = 2 * r + 1, nd = rd + 1, win = rd * rd;
   if (wave < a.levels) {
     const int l = wave, Hl = a.H[l], Wl = a.W[l];
     float* lrow = row + a.off[l];
@@ -822,7 +825,13 @@ hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void*
   if (npix == 0) return hipSuccess;
   if (r > 6) return hipErrorInvalidValue;
   const dim3 g((unsigned)((npix + 3) / 4)), blk(256);
-  if (out_dtype == kBF16)
+  if (out_dtype == kBF16 && r == 4)
+    hipLaunchKernelGGL((lookup_fwd_kernel<__bf16, 4>), g, blk, 0, s, pyr, coords, static_cast<__bf16*>(out), B, H, W,
+                       r, out_ch, fp);
+  else if (out_dtype == kF32 && r == 4)
+    hipLaunchKernelGGL((lookup_fwd_kernel<float, 4>), g, blk, 0, s, pyr, coords, static_cast<float*>(out), B, H, W, r,
+                       out_ch, fp);
+  else if (out_dtype == kBF16)
     hipLaunchKernelGGL(lookup_fwd_kernel<__bf16>, g, blk, 0, s, pyr, coords, static_cast<__bf16*>(out), B, H, W, r,
                        out_ch, fp);
   else if (out_dtype == kF16)
@@ -841,7 +850,11 @@ hipError_t launch_lookup_grad_rows(const GradRowsArgs& a, int g_dtype, hipStream
     return hipErrorInvalidValue;
   const size_t shm = (size_t)(a.ld + 4 * 176) * sizeof(float);
   const dim3 g((unsigned)npix), blk(256);
-  if (g_dtype == kBF16)
+  if (g_dtype == kBF16 && a.r == 4)
+    hipLaunchKernelGGL((lookup_grad_rows_kernel<__bf16, 4>), g, blk, shm, s, a);
+  else if (g_dtype == kF32 && a.r == 4)
+    hipLaunchKernelGGL((lookup_grad_rows_kernel<float, 4>), g, blk, shm, s, a);
+  else if (g_dtype == kBF16)
     hipLaunchKernelGGL(lookup_grad_rows_kernel<__bf16>, g, blk, shm, s, a);
   else if (g_dtype == kF16)
     hipLaunchKernelGGL(lookup_grad_rows_kernel<_Float16>, g, blk, shm, s, a);

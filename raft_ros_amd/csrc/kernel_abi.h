@@ -462,6 +462,56 @@ inline WgradPlan plan_conv_wgrad(const ConvWgradArgs& a) {
 }
 
 
+// ---------------------------------------------------------------------------- conv_fwd6 plan
+// LDS of a conv_fwd6 workgroup (csrc/conv_igemm.hip): a 3-stage weight ring of BN rows x 128 B,
+// then two strip buffers of fwd6_sb(BN) bytes whose last 128-B row is a zero row.  The odd
+// strip is reached with the ds_read immediate offset, hence SB <= 65408.
+constexpr int kFwd6Lds = 160 * 1024;
+RAFT_HD constexpr int fwd6_sb(int BN) {
+  return (((kFwd6Lds - 3 * BN * 128) / 2) & ~127) < 65408 ? (((kFwd6Lds - 3 * BN * 128) / 2) & ~127) : 65408;
+}
+RAFT_HD constexpr int fwd6_max_rows(int BN) { return fwd6_sb(BN) / 128 - 1; }
+
+// flat strip (rows m0 - (PH W + PW) ... of the pixel order) of a BM-pixel tile, padded to
+// whole DMA pieces of the NW waves; 0 when it does not fit
+RAFT_HD inline int fwd6_strip_rows(int BM, int NW, int KH, int KW, int W, int max_rows) {
+  const int need = BM + (KH - 1) * W + KW - 1;
+  const int rows = (need + 8 * NW - 1) / (8 * NW) * (8 * NW);
+  return rows <= max_rows ? rows : 0;
+}
+
+// 2-D tile of TH x TW output pixels: its halo block of (TH + KH - 1) x (TW + KW - 1) pixels,
+// padded to whole DMA pieces
+RAFT_HD inline int fwd6_halo_rows(int TH, int TW, int KH, int KW, int NW) {
+  const int rows = (TH + KH - 1) * (TW + KW - 1);
+  return (rows + 8 * NW - 1) / (8 * NW) * (8 * NW);
+}
+
+// v6 variant the forward dispatcher picks for a multi-tap stride-1 conv of N outputs over
+// B x H x W pixels (0: v5 / v4), from the measurements in profiles/r3_bench_conv6_*.log:
+//   41 = 256x64 flat strip, 45 = 256x128 flat strip, 59 = 256x64 as 4 x 64 2-D tiles (3x3,
+//   1x5), 60 = 256x64 as 8 x 32 2-D tiles (5x1).
+RAFT_HD inline int choose_fwd6(int KH, int KW, int N, int B, int H, int W) {
+  const long P = (long)B * H * W;
+  if (KH == 3 && KW == 3) {
+    if (fwd6_strip_rows(256, 4, 3, 3, W, fwd6_max_rows(64)) > 0) {
+      if (N <= 128 || N > 256) return 41;
+      if (N <= 192) return fwd6_strip_rows(256, 4, 3, 3, W, fwd6_max_rows(128)) > 0 ? 45 : 0;
+      return 0;
+    }
+    // wide images: 2-D tiles when the grid is one round of the 256 CUs or v4 would pad N
+    const long wg = (long)B * ((H + 3) / 4) * ((W + 63) / 64) * ((N + 63) / 64);
+    const int np = (N + 63) / 64 * 64;
+    return (wg <= 256 || (np != 128 && np != 256)) ? 59 : 0;
+  }
+  if (KH == 1 && KW == 5) {
+    if (N > 128) return 0;
+    return P <= 24576 ? 59 : 41;
+  }
+  if (KH == 5 && KW == 1) return P <= 24576 ? 60 : 0;
+  return 0;
+}
+
 }  // namespace raft_amd
 
 #ifndef RAFT_ABI_NO_HIP
