@@ -149,7 +149,9 @@ __device__ __forceinline__ void tile_setup(const LocalCorrArgs& a, TileGeo& g, f
   }
 }
 
-template <typename OutT>
+// RC > 0: the radius as a compile-time constant (RAFT's r = 4), so the per-element window
+// index math divides by constants instead of running 32-bit divisions
+template <typename OutT, int RC = 0>
 __global__ __launch_bounds__(256) void local_corr_mfma_fwd_kernel(const LocalCorrArgs a) {
   __shared__ TileGeo g;
   __shared__ float cx[NQ], cy[NQ];
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(256) void local_corr_mfma_fwd_kernel(const LocalCor
   int b;
   tile_setup(a, g, cx, cy, b, tid);
   __syncthreads();
-  const int rd = 2 * a.r + 1, win = rd * rd;
+  const int rd = 2 * (RC > 0 ? RC : a.r) + 1, win = rd * rd;
   for (int l = 0; l < a.levels; ++l) {
     tile_level_geometry(a, g, l, cx, cy, tid);
     for (int i = tid; i < NQ * win; i += 256) taps[i] = 0.f;
@@ -232,6 +234,7 @@ __global__ __launch_bounds__(256) void local_corr_mfma_fwd_kernel(const LocalCor
   }
 }
 
+template <int RC = 0>
 __global__ __launch_bounds__(256) void local_corr_mfma_bwd_kernel(const LocalCorrArgs a) {
   __shared__ TileGeo g;
   __shared__ float cx[NQ], cy[NQ];
@@ -242,7 +245,7 @@ __global__ __launch_bounds__(256) void local_corr_mfma_bwd_kernel(const LocalCor
   int b;
   tile_setup(a, g, cx, cy, b, tid);
   __syncthreads();
-  const int rd = 2 * a.r + 1, nd = rd + 1, win = rd * rd;
+  const int rd = 2 * (RC > 0 ? RC : a.r) + 1, nd = rd + 1, win = rd * rd;
   const int nkc = a.C / KC;  // <= 4 (C <= 256)
   const float fs = a.g2fix != nullptr ? *a.fix_scale : 0.f;  // fixed-point scale (deterministic mode)
   // dF1 accumulators: MFMA 16x16x32, wave w owns channels [16w, 16w + 16) of every 64-slice,
@@ -407,12 +410,19 @@ hipError_t launch_local_corr_mfma(const LocalCorrArgs& a, bool backward, hipStre
     return hipErrorInvalidValue;
   const long tiles = (long)a.B * ((a.H + TY - 1) / TY) * ((a.W + TX - 1) / TX);
   if (tiles == 0) return hipSuccess;
-  if (backward)
-    hipLaunchKernelGGL(local_corr_mfma_bwd_kernel, dim3((unsigned)tiles), dim3(256), 0, s, a);
+  const bool r4 = a.r == 4;
+  if (backward && r4)
+    hipLaunchKernelGGL(local_corr_mfma_bwd_kernel<4>, dim3((unsigned)tiles), dim3(256), 0, s, a);
+  else if (backward)
+    hipLaunchKernelGGL(local_corr_mfma_bwd_kernel<0>, dim3((unsigned)tiles), dim3(256), 0, s, a);
+  else if (a.out_f32 && r4)
+    hipLaunchKernelGGL((local_corr_mfma_fwd_kernel<float, 4>), dim3((unsigned)tiles), dim3(256), 0, s, a);
   else if (a.out_f32)
-    hipLaunchKernelGGL(local_corr_mfma_fwd_kernel<float>, dim3((unsigned)tiles), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((local_corr_mfma_fwd_kernel<float, 0>), dim3((unsigned)tiles), dim3(256), 0, s, a);
+  else if (r4)
+    hipLaunchKernelGGL((local_corr_mfma_fwd_kernel<__bf16, 4>), dim3((unsigned)tiles), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL(local_corr_mfma_fwd_kernel<__bf16>, dim3((unsigned)tiles), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((local_corr_mfma_fwd_kernel<__bf16, 0>), dim3((unsigned)tiles), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
