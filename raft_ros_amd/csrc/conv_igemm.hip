@@ -2011,11 +2011,14 @@ __global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
   const int HW = a.H * a.W;
   const long stride = a.src[0].stride;
   const long step = (long)gridDim.x * 4 * PPW;
-  for (long p = ((long)blockIdx.x * 4 + wave) * PPW + sub; p < a.P + sub; p += step) {
+  // 32-bit pixel arithmetic (the host guarantees P < 2^31): a 64-bit modulo per pixel was a
+  // large share of this short loop body
+  const int P = (int)a.P;
+  for (int p = (blockIdx.x * 4 + wave) * PPW + sub; p < P + sub; p += (int)step) {
     float s0 = 0.f, s1 = 0.f;
-    if (p < a.P) {
-      const int rem = (int)(p % HW);
-      const int py = rem / a.W, px = rem - (rem / a.W) * a.W;
+    if (p < P) {
+      const int rem = p % HW;
+      const int py = rem / a.W, px = rem - py * a.W;
       // no break/continue: the tap loop must fully unroll so that w[][t][] stays in
       // registers (a data-dependent exit demotes w to scratch -- 6x slower); out-of-range
       // taps load zeros under the exec mask instead
@@ -2114,6 +2117,7 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   if (a.Kpad % FBK != 0) return hipErrorInvalidValue;
   const int cfg = a.cfg;
   if (cfg == 0 && a.N <= 2 && a.epi == 0 && a.nsrc == 1 && a.KH * a.KW <= 9 && a.src[0].C == a.Cin &&
+      a.P < (1L << 30) &&
       (a.Cin == 64 || a.Cin == 128 || a.Cin == 256 || a.Cin == 512)) {
     // narrow output (flow-head conv2): register dot products, not a GEMM
     const int lpp = a.Cin / 8;

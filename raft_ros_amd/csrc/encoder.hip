@@ -770,24 +770,50 @@ __global__ __launch_bounds__(256) void enc_norm_finalize_kernel(const NormFinArg
 }
 
 // y = relu_out( f(a) + g(r) ),  f(a) = [relu](a * scale + shift),  g(r) = r * scale_r + shift_r | r | 0
+// Per-pixel elementwise passes (norm apply, norm backward apply): every thread keeps ONE
+// 8-channel chunk (n = tid % G) and walks pixels with a fixed stride, so the per-image
+// coefficient vectors stay in registers (reloaded only when the image changes) instead of
+// ~10-20 cached 16-byte coefficient loads and a 64-bit division per chunk.
+struct PixWalk {
+  int n, p, stride;  // channel offset, first pixel, pixel stride (-1 p: idle thread)
+};
+__device__ __forceinline__ PixWalk pix_walk(int G) {
+  const int ppb = 256 / G;  // pixel lanes per block (threads >= ppb * G idle)
+  const int t = threadIdx.x;
+  PixWalk w;
+  w.n = (t % G) * 8;
+  w.p = t < ppb * G ? blockIdx.x * ppb + t / G : -1;
+  w.stride = gridDim.x * ppb;
+  return w;
+}
+
 __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict__ a, const float* __restrict__ ca,
                                                         int relu_a, const __bf16* __restrict__ r,
                                                         const float* __restrict__ cr, int relu_out,
                                                         __bf16* __restrict__ out, int B, int HW, int N, int split) {
   const int G = N / 8;
   const int rs = split ? 3 * N : N;  // row stride: split rows hold hi / lo / hi planes
-  const long total = (long)B * HW * G;
-  for (long ch = (long)blockIdx.x * 256 + threadIdx.x; ch < total; ch += (long)gridDim.x * 256) {
-    const long p = ch / G;
-    const int n = (int)(ch - p * G) * 8;
-    const int b = (int)(p / HW);
-    float v[8], s[8], t[8];
+  const PixWalk w = pix_walk(G);
+  if (w.p < 0) return;
+  const int n = w.n, P = B * HW;
+  int b = -1, bend = 0;
+  float s[8], t[8], s2[8], t2[8];
+  for (int p = w.p; p < P; p += w.stride) {
+    if (p >= bend) {  // next image: its coefficients
+      b = p / HW;
+      bend = (b + 1) * HW;
+      loadf8(ca + (long)b * 4 * N + n, s);
+      loadf8(ca + (long)b * 4 * N + N + n, t);
+      if (r && cr) {
+        loadf8(cr + (long)b * 4 * N + n, s2);
+        loadf8(cr + (long)b * 4 * N + N + n, t2);
+      }
+    }
+    float v[8];
     if (split)
-      load8_split(a + p * rs + n, N, v);
+      load8_split(a + (long)p * rs + n, N, v);
     else
-      load8(a + p * N + n, v);
-    loadf8(ca + (long)b * 4 * N + n, s);
-    loadf8(ca + (long)b * 4 * N + N + n, t);
+      load8(a + (long)p * N + n, v);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       v[e] = v[e] * s[e] + t[e];
@@ -796,15 +822,12 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
     if (r) {
       float rv[8];
       if (split)
-        load8_split(r + p * rs + n, N, rv);
+        load8_split(r + (long)p * rs + n, N, rv);
       else
-        load8(r + p * N + n, rv);
-      if (cr) {
-        loadf8(cr + (long)b * 4 * N + n, s);
-        loadf8(cr + (long)b * 4 * N + N + n, t);
+        load8(r + (long)p * N + n, rv);
+      if (cr)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) rv[e] = rv[e] * s[e] + t[e];
-      }
+        for (int e = 0; e < 8; ++e) rv[e] = rv[e] * s2[e] + t2[e];
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += rv[e];
     }
@@ -812,9 +835,9 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     if (split)
-      store8_split(out + p * rs + n, N, v);
+      store8_split(out + (long)p * rs + n, N, v);
     else
-      store8(out + p * N + n, v);
+      store8(out + (long)p * N + n, v);
   }
 }
 
@@ -955,25 +978,40 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_finalize_kernel(const NormBw
 // pass 3: da_j = k1 * dy_j + k2 * xhat_j + k3
 __global__ __launch_bounds__(256) void enc_norm_bwd_apply_kernel(const NormBwdArgs a) {
   const int N = a.N, G = N / 8;
-  const long total = (long)a.B * a.HW * G;
-  for (long ch = (long)blockIdx.x * 256 + threadIdx.x; ch < total; ch += (long)gridDim.x * 256) {
-    const long p = ch / G;
-    const int n = (int)(ch - p * G) * 8;
-    const int b = (int)(p / a.HW);
-    float gv[8], av[8], k1[8], k2[8], k3[8], rs[8], mu[8], o[8];
-    load8(a.g + p * N + n, gv);
-    load8(a.a0 + p * N + n, av);
-    const float* c0 = a.c0 + (long)b * 4 * N;
-    const float* bc = a.bcoef + (long)b * 2 * 3 * N;
-    loadf8(bc + n, k1);
-    loadf8(bc + N + n, k2);
-    loadf8(bc + 2 * N + n, k3);
-    loadf8(c0 + 2 * N + n, rs);
-    loadf8(c0 + 3 * N + n, mu);
+  const PixWalk w = pix_walk(G);
+  if (w.p < 0) return;
+  const int n = w.n, P = a.B * a.HW;
+  int bend = 0;
+  float k1[8], k2[8], k3[8], rs[8], mu[8], sc[8], sh[8];
+  float q1[8], q2[8], q3[8], rs1[8], mu1[8];
+  for (int p = w.p; p < P; p += w.stride) {
+    if (p >= bend) {  // next image: its coefficients
+      const int b = p / a.HW;
+      bend = (b + 1) * a.HW;
+      const float* c0 = a.c0 + (long)b * 4 * N;
+      const float* bc = a.bcoef + (long)b * 2 * 3 * N;
+      loadf8(bc + n, k1);
+      loadf8(bc + N + n, k2);
+      loadf8(bc + 2 * N + n, k3);
+      loadf8(c0 + 2 * N + n, rs);
+      loadf8(c0 + 3 * N + n, mu);
+      if (a.relu0) {
+        loadf8(c0 + n, sc);
+        loadf8(c0 + N + n, sh);
+      }
+      if (a.a1) {
+        const float* c1 = a.c1 + (long)b * 4 * N;
+        loadf8(bc + 3 * N + n, q1);
+        loadf8(bc + 4 * N + n, q2);
+        loadf8(bc + 5 * N + n, q3);
+        loadf8(c1 + 2 * N + n, rs1);
+        loadf8(c1 + 3 * N + n, mu1);
+      }
+    }
+    float gv[8], av[8], o[8];
+    load8(a.g + (long)p * N + n, gv);
+    load8(a.a0 + (long)p * N + n, av);
     if (a.relu0) {
-      float sc[8], sh[8];
-      loadf8(c0 + n, sc);
-      loadf8(c0 + N + n, sh);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float dy = (av[e] * sc[e] + sh[e] > 0.f) ? gv[e] : 0.f;
@@ -983,20 +1021,21 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_apply_kernel(const NormBwdAr
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = k1[e] * gv[e] + k2[e] * (av[e] - mu[e]) * rs[e] + k3[e];
     }
-    store8(a.out0 + p * N + n, o);
+    store8(a.out0 + (long)p * N + n, o);
     if (a.a1) {
-      load8(a.a1 + p * N + n, av);
-      const float* c1 = a.c1 + (long)b * 4 * N;
-      loadf8(bc + 3 * N + n, k1);
-      loadf8(bc + 4 * N + n, k2);
-      loadf8(bc + 5 * N + n, k3);
-      loadf8(c1 + 2 * N + n, rs);
-      loadf8(c1 + 3 * N + n, mu);
+      load8(a.a1 + (long)p * N + n, av);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = k1[e] * gv[e] + k2[e] * (av[e] - mu[e]) * rs[e] + k3[e];
-      store8(a.out1 + p * N + n, o);
+      for (int e = 0; e < 8; ++e) o[e] = q1[e] * gv[e] + q2[e] * (av[e] - mu1[e]) * rs1[e] + q3[e];
+      store8(a.out1 + (long)p * N + n, o);
     }
   }
+}
+
+// blocks of a PixWalk launch: 256 / (N / 8) pixel lanes per block, at most 4096 blocks
+int grid_pix(int B, int HW, int N) {
+  const long ppb = 256 / (N / 8);
+  const long g = ((long)B * HW + ppb - 1) / ppb;
+  return (int)std::min<long>(std::max<long>(g, 1), 4096);
 }
 
 int grid_for(long chunks) {
@@ -1303,8 +1342,8 @@ hipError_t launch_enc_norm_finalize(const NormFinArgs& a, hipStream_t s) {
 
 hipError_t launch_enc_apply(const void* a, const float* ca, bool relu_a, const void* r, const float* cr,
                             bool relu_out, void* out, int B, int HW, int N, int split, hipStream_t s) {
-  const long chunks = (long)B * HW * (N / 8);
-  hipLaunchKernelGGL(enc_apply_kernel, dim3(grid_for(chunks)), dim3(256), 0, s, static_cast<const __bf16*>(a), ca,
+  if (N % 8 != 0 || N / 8 > 256 || (long)B * HW >= (1L << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(enc_apply_kernel, dim3(grid_pix(B, HW, N)), dim3(256), 0, s, static_cast<const __bf16*>(a), ca,
                      relu_a ? 1 : 0, static_cast<const __bf16*>(r), cr, relu_out ? 1 : 0, static_cast<__bf16*>(out), B,
                      HW, N, split);
   return hipGetLastError();
@@ -1325,8 +1364,8 @@ hipError_t launch_enc_norm_bwd_stages(const NormBwdArgs& a, int stages, int b_fi
     RAFT_HIP_CHECK(hipGetLastError());
   }
   if (stages & 4) {
-    const long chunks = (long)a.B * a.HW * (a.N / 8);
-    hipLaunchKernelGGL(enc_norm_bwd_apply_kernel, dim3(grid_for(chunks)), dim3(256), 0, s, a);
+    if (a.N % 8 != 0 || a.N / 8 > 256 || (long)a.B * a.HW >= (1L << 31)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(enc_norm_bwd_apply_kernel, dim3(grid_pix(a.B, a.HW, a.N)), dim3(256), 0, s, a);
     RAFT_HIP_CHECK(hipGetLastError());
   }
   return hipSuccess;
