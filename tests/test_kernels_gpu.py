@@ -264,13 +264,17 @@ def test_corr_pyramid_autograd_matches_reference(cuda):
         assert err < 1e-2, err
 
 
-def test_convex_upsample_fwd_bwd(cuda):
+@pytest.mark.parametrize("shape,layout", [((2, 13, 17), "cl"), ((1, 9, 40), "cl"), ((2, 13, 17), "nchw")])
+def test_convex_upsample_fwd_bwd(cuda, shape, layout):
+    """channels-last masks take the row-segment kernels (16 pixels per workgroup, partial last
+    segment at W = 17 / 40), NCHW masks the per-pixel ones."""
     torch.manual_seed(3)
     from raft_ros_amd.ops.upsample import convex_upsample
 
-    B, H, W = 2, 13, 17
+    B, H, W = shape
+    fmt = torch.channels_last if layout == "cl" else torch.contiguous_format
     flow = torch.randn(B, 2, H, W, device=cuda, requires_grad=True)
-    mask = torch.randn(B, 576, H, W, device=cuda).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    mask = torch.randn(B, 576, H, W, device=cuda).contiguous(memory_format=fmt).requires_grad_(True)
     out = convex_upsample(flow, mask)
     want = ref.convex_upsample(flow, mask)
     torch.testing.assert_close(out, want, rtol=1e-4, atol=1e-4)
@@ -283,6 +287,13 @@ def test_convex_upsample_fwd_bwd(cuda):
     mb = mask.detach().bfloat16()
     torch.testing.assert_close(convex_upsample(flow.detach(), mb), ref.convex_upsample(flow.detach(), mb.float()),
                                rtol=1e-4, atol=1e-4)
+    # bf16 backward: dmask in the mask's dtype and layout, the flow gradient in fp32
+    dfb, dmb = _ops().convex_upsample_backward(flow.detach(), mb, g)
+    assert dmb.dtype == torch.bfloat16 and dmb.stride() == mb.stride()
+    mf = mb.float().requires_grad_(True)
+    rfb, rmb = torch.autograd.grad(ref.convex_upsample(flow, mf), (flow, mf), g)
+    torch.testing.assert_close(dfb, rfb, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(dmb.float(), rmb, rtol=2e-2, atol=2e-3)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
