@@ -67,7 +67,7 @@ def parse():
                     help="replay the step as captured HIP graph(s) (train: fwd+loss+bwd+clip+AdamW, grads "
                          "all-reduced between two graphs when N>1; infer: the forward). Default: on for infer; "
                          "off for train, where the step is GPU-bound and eager keeps more of the multi-stream overlap "
-                         "(graph 372 vs eager 386 pairs/s on MI355X, profiles/r2_graph_vs_eager_final.log)")
+                         "(graph 394.6 vs eager 402.0 pairs/s on MI355X; 1080p inference 60.9 graph vs 60.7 eager, profiles/r3_graph_vs_eager.log)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: gloo-backend plumbing check of the launch path only (tests), never a measurement")
     return ap.parse_args()

@@ -28,6 +28,8 @@ for step in ${STEPS_LIST:-infer1080 infer_sintel alt_kitti dense_kitti conv_nati
     conv_bf16) run conv_bf16 600 python scripts/convergence.py --impl native --precision bf16 --steps ${CONV_STEPS:-3000} --eval_every 250 ;;
     ref_bench) run ref_bench 600 python bench.py --impl reference --steps 10 --warmup 3 ;;
     train) run train 300 python bench.py --steps 30 --warmup 5 ;;
+    train_graph) run train_graph 300 python bench.py --graph --steps 30 --warmup 5 ;;
+    infer1080_eager) run infer1080_eager 300 python bench.py --mode infer --no-graph --image_size 1080 1920 --iters 32 --batch 1 --steps 10 --warmup 3 ;;
     train_fp32) run train_fp32 400 python bench.py --fp32 --steps 10 --warmup 3 ;;
     infer_ros_fp32) run infer_ros_fp32 300 python bench.py --mode infer --fp32 --image_size 440 1024 --iters 20 --batch 1 --steps 20 --warmup 3 ;;
     infer_ros_bf16) run infer_ros_bf16 300 python bench.py --mode infer --image_size 440 1024 --iters 20 --batch 1 --steps 20 --warmup 3 ;;
