@@ -384,101 +384,139 @@ __global__ __launch_bounds__(256) void pyramid_unpool_kernel(const UnpoolArgs u)
 }
 
 // ---------------------------------------------------------------------------- pyramid operand
-__device__ __forceinline__ float pyr_src(const PyrOperandArgs& a, int b, int c, int y, int x) {
-  const long i = b * a.sB + c * a.sC + y * a.sH + x * a.sW;
-  return a.src_bf16 ? static_cast<float>(static_cast<const __bf16*>(a.src)[i]) : static_cast<const float*>(a.src)[i];
+// Level-l pixel (y, x) of 4 consecutive channels c..c+3 (C % 4 == 0): the 2^l x 2^l source block
+// averaged in F.avg_pool2d's order (each level sums its 4 children from 0 then divides by 4),
+// so the result is bitwise equal to the pooled tensors.  VEC: channel-contiguous source, one
+// 16-byte (fp32) / 8-byte (bf16) load per source pixel.  The level-2/3 loops stay rolled, so a
+// level-3 column does not keep 64 source vectors live.
+__device__ __forceinline__ bool pyr_vec(const PyrOperandArgs& a) {
+  return a.sC == 1 && ((a.sB | a.sH | a.sW) & 3) == 0 && (reinterpret_cast<uintptr_t>(a.src) & 15) == 0;
 }
 
-// level-L pixel (y, x): 2x2 average of level L-1, summed in F.avg_pool2d's order
-template <int L>
-__device__ float pyr_pool(const PyrOperandArgs& a, int b, int c, int y, int x) {
-  if constexpr (L == 0) {
-    return pyr_src(a, b, c, y, x);
-  } else {
-    float s = 0.f;
-    s += pyr_pool<L - 1>(a, b, c, 2 * y, 2 * x);
-    s += pyr_pool<L - 1>(a, b, c, 2 * y, 2 * x + 1);
-    s += pyr_pool<L - 1>(a, b, c, 2 * y + 1, 2 * x);
-    s += pyr_pool<L - 1>(a, b, c, 2 * y + 1, 2 * x + 1);
+template <bool VEC>
+__device__ __forceinline__ f32x4 pyr_src4(const PyrOperandArgs& a, int b, int c, int y, int x) {
+  const long i = b * a.sB + c * a.sC + y * a.sH + x * a.sW;
+  if (VEC) {
+    if (a.src_bf16) {
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      const bf16x4 v = *reinterpret_cast<const bf16x4*>(static_cast<const __bf16*>(a.src) + i);
+      return f32x4{static_cast<float>(v[0]), static_cast<float>(v[1]), static_cast<float>(v[2]),
+                   static_cast<float>(v[3])};
+    }
+    return *reinterpret_cast<const f32x4*>(static_cast<const float*>(a.src) + i);
+  }
+  f32x4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    v[e] = a.src_bf16 ? static_cast<float>(static_cast<const __bf16*>(a.src)[i + e * a.sC])
+                      : static_cast<const float*>(a.src)[i + e * a.sC];
+  return v;
+}
+
+template <bool VEC>
+__device__ __forceinline__ f32x4 pyr_pool1(const PyrOperandArgs& a, int b, int c, int y, int x) {
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  s += pyr_src4<VEC>(a, b, c, 2 * y, 2 * x);
+  s += pyr_src4<VEC>(a, b, c, 2 * y, 2 * x + 1);
+  s += pyr_src4<VEC>(a, b, c, 2 * y + 1, 2 * x);
+  s += pyr_src4<VEC>(a, b, c, 2 * y + 1, 2 * x + 1);
+  return s / 4.f;
+}
+
+template <bool VEC>
+__device__ f32x4 pyr_value4(const PyrOperandArgs& a, int l, int b, int c, int y, int x) {
+  if (l == 0) return pyr_src4<VEC>(a, b, c, y, x);
+  if (l == 1) return pyr_pool1<VEC>(a, b, c, y, x);
+  if (l == 2) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int k = 0; k < 4; ++k) s += pyr_pool1<VEC>(a, b, c, 2 * y + (k >> 1), 2 * x + (k & 1));
     return s / 4.f;
   }
-}
-
-__device__ __forceinline__ float pyr_value(const PyrOperandArgs& a, int l, int b, int c, int y, int x) {
-  switch (l) {
-    case 0: return pyr_pool<0>(a, b, c, y, x);
-    case 1: return pyr_pool<1>(a, b, c, y, x);
-    case 2: return pyr_pool<2>(a, b, c, y, x);
-    default: return pyr_pool<3>(a, b, c, y, x);
+  f32x4 s3 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int k3 = 0; k3 < 4; ++k3) {
+    f32x4 s2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int k2 = 0; k2 < 4; ++k2)
+      s2 += pyr_pool1<VEC>(a, b, c, 4 * y + 2 * (k3 >> 1) + (k2 >> 1), 4 * x + 2 * (k3 & 1) + (k2 & 1));
+    s3 += s2 / 4.f;
   }
+  return s3 / 4.f;
 }
 
-// column q of the operand -> (level, y, x); false for padding columns
-__device__ __forceinline__ bool pyr_column(const PyrOperandArgs& a, long q, int& l, int& y, int& x) {
+// column q of the operand -> (level, y, x); false for padding columns (32-bit: the launcher
+// checks ld)
+__device__ __forceinline__ bool pyr_column(const PyrOperandArgs& a, int q, int& l, int& y, int& x) {
   for (l = a.nseg - 1; l > 0 && q < a.off[l]; --l) {
   }
   if (q < a.off[l]) return false;
-  const long j = q - a.off[l];
+  const int j = q - a.off[l];
   const int Hl = a.h[l], Wl = a.w[l];
   if (a.blk) {
-    const long blk = j / (16L * Hl), rem = j - blk * 16L * Hl;
-    y = (int)(rem / 16);
-    x = (int)(blk * 16 + rem % 16);
+    const int blk = j / (16 * Hl), rem = j - blk * 16 * Hl;
+    y = rem >> 4;
+    x = blk * 16 + (rem & 15);
     return y < Hl && x < Wl;
   }
-  if (j >= (long)Hl * Wl) return false;
-  y = (int)(j / Wl);
-  x = (int)(j - (long)y * Wl);
+  if (j >= Hl * Wl) return false;
+  y = j / Wl;
+  x = j - y * Wl;
   return true;
 }
 
 // (B, C, ld) layout: a block computes a 64-column x 64-channel tile with channel-contiguous
-// reads (4 channels per thread, as the row layout) and writes it transposed through LDS, so
-// both the NHWC source reads and the column-contiguous stores are coalesced.
+// reads (4 channels per thread, one vector load per source pixel) and writes it transposed
+// through LDS as 16-byte column-contiguous stores (4 channel rows x 256 B per wave store).
 __global__ __launch_bounds__(256) void pyramid_operand_t_kernel(const PyrOperandArgs a) {
   __shared__ float tile[64][65];
   const int tid = threadIdx.x;
-  const long q0 = (long)blockIdx.x * 64;
+  const int ld = (int)a.ld;
+  const int q0 = blockIdx.x * 64;
   const int c0 = blockIdx.y * 64, b = blockIdx.z;
   const int c4 = (tid & 15) * 4;
+  const bool vec = pyr_vec(a);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int qq = (tid >> 4) + 16 * k;
-    const long q = q0 + qq;
+    const int q = q0 + qq;
     int l, y, x;
-    const bool live = q < a.ld && pyr_column(a, q, l, y, x);
+    const bool live = q < ld && c0 + c4 < a.C && pyr_column(a, q, l, y, x);
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (live) v = vec ? pyr_value4<true>(a, l, b, c0 + c4, y, x) : pyr_value4<false>(a, l, b, c0 + c4, y, x);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = c0 + c4 + e;
-      tile[c4 + e][qq] = (live && c < a.C) ? pyr_value(a, l, b, c, y, x) : 0.f;
-    }
+    for (int e = 0; e < 4; ++e) tile[c4 + e][qq] = v[e];
   }
   __syncthreads();
-  const int cl = tid >> 2, qs = (tid & 3) * 16;
-  const int c = c0 + cl;
-  if (c >= a.C) return;
-  float* o = a.out + ((long)b * a.C + c) * a.ld + q0;
+  const int qs = (tid & 15) * 4;
+  const bool vst = (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
 #pragma unroll
-  for (int j = 0; j < 16; ++j)
-    if (q0 + qs + j < a.ld) o[qs + j] = tile[cl][qs + j];
+  for (int pass = 0; pass < 4; ++pass) {
+    const int cl = (tid >> 4) + 16 * pass, c = c0 + cl;
+    if (c >= a.C) break;
+    float* o = a.out + ((long)b * a.C + c) * ld + q0 + qs;
+    if (vst && q0 + qs + 4 <= ld) {
+      *reinterpret_cast<f32x4*>(o) = f32x4{tile[cl][qs], tile[cl][qs + 1], tile[cl][qs + 2], tile[cl][qs + 3]};
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (q0 + qs + j < ld) o[j] = tile[cl][qs + j];
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void pyramid_operand_kernel(const PyrOperandArgs a) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  {  // (B, ld, C): 4 channels per thread
-    const int C4 = a.C / 4;
-    const long total = (long)a.B * a.ld * C4;
-    if (i >= total) return;
-    const int c = (int)(i % C4) * 4;
-    const long bq = i / C4, q = bq % a.ld;
-    const int b = (int)(bq / a.ld);
-    int l, y, x;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (pyr_column(a, q, l, y, x))
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = pyr_value(a, l, b, c + e, y, x);
-    *reinterpret_cast<f32x4*>(a.out + (bq * a.C + c)) = v;
-  }
+  // (B, ld, C): 4 channels per thread (32-bit indices: the launcher checks B * ld * C)
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int C4 = a.C / 4, ld = (int)a.ld;
+  if (i >= a.B * ld * C4) return;
+  const int bq = i / C4, c = (i - bq * C4) * 4;
+  const int b = bq / ld, q = bq - b * ld;
+  int l, y, x;
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (pyr_column(a, q, l, y, x))
+    v = pyr_vec(a) ? pyr_value4<true>(a, l, b, c, y, x) : pyr_value4<false>(a, l, b, c, y, x);
+  *reinterpret_cast<f32x4*>(a.out + (long)i * 4) = v;
 }
 
 __device__ __forceinline__ float safe_floor(float v) {
@@ -800,6 +838,7 @@ hipError_t launch_pyramid_unpool(const UnpoolArgs& u, hipStream_t s) {
 
 hipError_t launch_pyramid_operand(const PyrOperandArgs& a, hipStream_t s) {
   if ((long)a.B * a.C * a.ld == 0) return hipSuccess;
+  if ((long)a.B * a.C * a.ld >= (1L << 31) || a.C % 4 != 0) return hipErrorInvalidValue;
   if (a.nchw) {
     const dim3 grid((unsigned)((a.ld + 63) / 64), (unsigned)((a.C + 63) / 64), (unsigned)a.B);
     hipLaunchKernelGGL(pyramid_operand_t_kernel, grid, dim3(256), 0, s, a);

@@ -182,13 +182,17 @@ def test_lookup_grad_rows_match_per_lookup_backward(cuda, radius, T):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("blocked", [True, False])
-def test_pyramid_operand_matches_torch_ops(cuda, dtype, blocked):
-    """The one-launch pyramid GEMM operand == F.avg_pool2d levels + pad/permute copies, bit for bit."""
+@pytest.mark.parametrize("fmt", ["cl", "nchw"])
+def test_pyramid_operand_matches_torch_ops(cuda, dtype, blocked, fmt):
+    """The one-launch pyramid GEMM operand == F.avg_pool2d levels + pad/permute copies, bit for bit
+    (channels-last sources take the 4-channel vector loads, NCHW ones the per-channel path)."""
     from raft_ros_amd.ops.corr import _concat_levels, _pad_to, _pooled
 
     torch.manual_seed(8)
     B, C, H, W = 2, 64, 27, 45  # odd sizes: floor pooling, partial 16-column blocks
-    fmap = torch.randn(B, C, H, W, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    fmap = torch.randn(B, C, H, W, device=cuda).to(dtype)
+    if fmt == "cl":
+        fmap = fmap.contiguous(memory_format=torch.channels_last)
     fs = _pooled(fmap.float(), 4)
     segs, off = [], 0
     for f in fs:
