@@ -253,7 +253,17 @@ __global__ __launch_bounds__(256, 2) void corr_volume_bf16_kernel(const CorrGemm
   const int per_b = tilesM * tilesN;
   const int wg = xcd_remap(blockIdx.x, per_b * g.batch);
   const int b = wg / per_b, t = wg - b * per_b;
-  const int m0 = (t / tilesN) * VBM, n0 = (t - (t / tilesN) * tilesN) * VBN;
+  // grouped tile order: runs of GM row tiles sweep the column tiles together, so the ~64
+  // workgroups an XCD runs at once share a few A and B tiles in its L2 instead of re-streaming
+  // all of B once per row tile.  Measured (profiles/r3_bench_corr_grouped.log, vs row-major):
+  // GM = 8 while one image's B fits 8 MB (train 83.9 -> 80.0 us, Sintel 61.9 -> 56.8 us); at
+  // 1080p (B = 22 MB, 2.8 GB of stores) GM = 4 (1272 -> 1194 us; GM = 8 / 16 lose there, the
+  // store stream spreads over too many rows).  cfg 2 / 3 / 4 / 5 force GM = 1 / 2 / 4 / 16.
+  const int GM = g.cfg >= 2 ? (g.cfg == 2 ? 1 : g.cfg == 3 ? 2 : g.cfg == 4 ? 4 : 16)
+                            : ((long)g.N * g.K * 2 <= (8L << 20) ? 8 : 4);
+  const int grp = t / (GM * tilesN), first = grp * GM, gsz = min(tilesM - first, GM);
+  const int r = t - grp * GM * tilesN;
+  const int m0 = (first + r % gsz) * VBM, n0 = (r / gsz) * VBN;
   const __bf16* A = static_cast<const __bf16*>(g.A) + (long)b * g.sA;
   const __bf16* B = static_cast<const __bf16*>(g.B) + (long)b * g.sB;
   const __amdgpu_buffer_rsrc_t ra = vrsrc(A, (unsigned)((long)g.M * g.lda * 2));

@@ -314,7 +314,7 @@ struct CorrGemmArgs {
   float alpha;
   int a_f32, b_f32, a_trans, split, c_bf16;
   int epi;  // 0 store, 1 accumulate
-  int cfg;  // 1: force the generic kernel (tests)
+  int cfg;  // 1: force the generic kernel (tests); 2-5: v2 volume kernel with a forced tile grouping
 };
 
 // Adjoint of the pyramid pools: out[b][y][x][c] = sum_l G[b][off_l + (y>>l)*w_l + (x>>l)][c] / 4^l
