@@ -344,15 +344,6 @@ __global__ __launch_bounds__(256) void convex_up_gather_rows_kernel(const float*
   }
 }
 
-// The row-segment kernels need the mask (and dmask) as dense 16-byte-aligned (P, 576) rows and
-// every offset they form to fit in 32 bits.
-bool up_seg_ok(const void* m, int esz, long sN, long sC, long sH, long sW, int B, int H, int W) {
-  const long align = 16 / esz;
-  return sC == 1 && sW == 576 && sH % align == 0 && sN % align == 0 &&
-         (reinterpret_cast<uintptr_t>(m) & 15) == 0 && (long)B * sN < (1L << 31) &&
-         (long)B * H * W * 128 < (1L << 31) && (long)sH * H <= sN;
-}
-
 }  // namespace
 
 hipError_t launch_convex_up_fwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
@@ -360,7 +351,7 @@ hipError_t launch_convex_up_fwd(const float* flow, const void* mask, int m_dtype
   const long npix = (long)B * H * W;
   if (npix == 0) return hipSuccess;
   const int esz = m_dtype == kF32 ? 4 : 2;
-  if (up_seg_ok(mask, esz, msN, msC, msH, msW, B, H, W)) {
+  if (up_seg_ok(reinterpret_cast<uintptr_t>(mask), esz, msN, msC, msH, msW, B, H, W)) {
     const int nseg = (W + kUpSeg - 1) / kUpSeg;
     const dim3 g(B * H * nseg), blk(256);
     if (m_dtype == kBF16)
@@ -395,7 +386,8 @@ hipError_t launch_convex_up_bwd(const float* flow, const void* mask, int m_dtype
   if (npix == 0) return hipSuccess;
   const dim3 blk(256);
   const int esz = m_dtype == kF32 ? 4 : 2;
-  if (up_seg_ok(mask, esz, msN, msC, msH, msW, B, H, W) && up_seg_ok(dmask, esz, dsN, dsC, dsH, dsW, B, H, W)) {
+  if (up_seg_ok(reinterpret_cast<uintptr_t>(mask), esz, msN, msC, msH, msW, B, H, W) &&
+      up_seg_ok(reinterpret_cast<uintptr_t>(dmask), esz, dsN, dsC, dsH, dsW, B, H, W)) {
     const int nseg = (W + kUpSeg - 1) / kUpSeg;
     const dim3 g(B * H * nseg);
     if (m_dtype == kBF16)

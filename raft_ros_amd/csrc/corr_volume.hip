@@ -258,9 +258,8 @@ __global__ __launch_bounds__(256, 2) void corr_volume_bf16_kernel(const CorrGemm
   // all of B once per row tile.  Measured (profiles/r3_bench_corr_grouped.log, vs row-major):
   // GM = 8 while one image's B fits 8 MB (train 83.9 -> 80.0 us, Sintel 61.9 -> 56.8 us); at
   // 1080p (B = 22 MB, 2.8 GB of stores) GM = 4 (1272 -> 1194 us; GM = 8 / 16 lose there, the
-  // store stream spreads over too many rows).  cfg 2 / 3 / 4 / 5 force GM = 1 / 2 / 4 / 16.
-  const int GM = g.cfg >= 2 ? (g.cfg == 2 ? 1 : g.cfg == 3 ? 2 : g.cfg == 4 ? 4 : 16)
-                            : ((long)g.N * g.K * 2 <= (8L << 20) ? 8 : 4);
+  // store stream spreads over too many rows).  kernel_abi.h corr_group_rows.
+  const int GM = corr_group_rows(g.N, g.K, g.cfg);
   const int grp = t / (GM * tilesN), first = grp * GM, gsz = min(tilesM - first, GM);
   const int r = t - grp * GM * tilesN;
   const int m0 = (first + r % gsz) * VBM, n0 = (r / gsz) * VBN;

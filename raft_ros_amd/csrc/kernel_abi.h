@@ -512,6 +512,24 @@ RAFT_HD inline int choose_fwd6(int KH, int KW, int N, int B, int H, int W) {
   return 0;
 }
 
+// ============================================================================ convex upsampling
+// The row-segment kernels (csrc/convex_upsample.hip) take a dense channels-last mask: (P, 576)
+// rows (channel stride 1, pixel stride 576), 16-byte aligned rows of a 2- or 4-byte type, and
+// every offset they form (B * H * W * 128 output floats, B * sN mask elements) within 32 bits.
+inline bool up_seg_ok(unsigned long addr, int esz, long sN, long sC, long sH, long sW, int B, int H, int W) {
+  const long align = 16 / esz;
+  return sC == 1 && sW == 576 && sH % align == 0 && sN % align == 0 && (addr & 15) == 0 &&
+         (long)B * sN < (1L << 31) && (long)B * H * W * 128 < (1L << 31) && (long)sH * H <= sN;
+}
+
+// ============================================================================ correlation build
+// Row tiles per group of the v2 volume build's tile order (cfg 2-5 force 1 / 2 / 4 / 16):
+// 8 while one image's B operand (N x K bf16) fits 8 MB, 4 beyond (the 1080p store stream).
+RAFT_HD inline int corr_group_rows(long N, long K, int cfg) {
+  if (cfg >= 2) return cfg == 2 ? 1 : cfg == 3 ? 2 : cfg == 4 ? 4 : 16;
+  return N * K * 2 <= (8L << 20) ? 8 : 4;
+}
+
 }  // namespace raft_amd
 
 #ifndef RAFT_ABI_NO_HIP

@@ -6,7 +6,8 @@
 //     has no empty split, pads N to whole row tiles and keeps the pixel ranges in bounds;
 //   * the slab sizes the bindings allocate from a plan stay addressable;
 //   * the conv_fwd6 variant choice (measured winners at the benchmark shapes; every chosen
-//     strip / halo block fits the kernel's LDS at any width).
+//     strip / halo block fits the kernel's LDS at any width);
+//   * the convex-upsampling kernel choice and the correlation build's tile grouping.
 #define RAFT_ABI_NO_HIP
 #include "kernel_abi.h"
 
@@ -167,8 +168,26 @@ static void test_fwd6_plan() {
   EXPECT(2 * fwd6_sb(128) + 3 * 128 * 128 <= kFwd6Lds && fwd6_sb(64) <= 65408, "LDS layout");
 }
 
+// convex upsampling: channels-last masks (the mask head's rows) take the row-segment kernels,
+// NCHW / misaligned / oversized ones the per-pixel kernels
+static void test_upsample_and_corr_selection() {
+  const int B = 8, H = 46, W = 62;
+  const long HW = (long)H * W;
+  EXPECT(up_seg_ok(0x1000, 2, HW * 576, 1, W * 576L, 576, B, H, W), "channels-last bf16");
+  EXPECT(up_seg_ok(0x1000, 4, HW * 576, 1, W * 576L, 576, B, H, W), "channels-last fp32");
+  EXPECT(!up_seg_ok(0x1000, 2, 576 * HW, HW, W, 1, B, H, W), "NCHW");
+  EXPECT(!up_seg_ok(0x1008, 2, HW * 576, 1, W * 576L, 576, B, H, W), "misaligned");
+  EXPECT(!up_seg_ok(0x1000, 2, HW * 576 + 4, 1, W * 576L, 576, B, H, W), "unaligned image stride");
+  EXPECT(!up_seg_ok(0x1000, 2, 4000L * 4000 * 576, 1, 4000L * 576, 576, 2, 4000, 4000), "32-bit offsets");
+  // correlation build tile groups: 8 at config #2 / Sintel, 4 at 1080p, forced by cfg 2-5
+  EXPECT(corr_group_rows(3936, 256, 0) == 8 && corr_group_rows(9280, 256, 0) == 8, "small B");
+  EXPECT(corr_group_rows(43600, 256, 0) == 4, "1080p");
+  EXPECT(corr_group_rows(43600, 256, 2) == 1 && corr_group_rows(10, 256, 5) == 16, "forced");
+}
+
 int main() {
   test_xcd_remap();
+  test_upsample_and_corr_selection();
   test_wgrad_plans();
   test_fwd6_plan();
   if (failures) {
