@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--fp32", action="store_true",
                     help="no autocast (mixed_precision=False): the reference's default for demo.py / evaluate.py / "
                          "the ROS node and train_standard.sh")
+    ap.add_argument("--corr_fp32", action="store_true",
+                    help="bf16 AMP with the reference's fp32-faithful correlation volume (core/raft.py:102-103)")
     ap.add_argument("--lr", type=float, default=4e-4)
     # ~10 MB buckets: the update-block gradients (12.5 MB, ready first -- batched wgrads run
     # before the encoders' backward) all-reduce over xGMI while the encoders backpropagate
@@ -123,6 +125,25 @@ def _allreduce_ms(model, device, world, reps: int = 10) -> float:
     return 1000.0 * float(t.item())
 
 
+def _paths(model, image, args):
+    """(encoder path, update-block path) the model's dispatch takes for this run's mode."""
+    if args.impl == "reference":
+        return "reference", "reference"
+    amp = not args.fp32
+    grad = args.mode == "train"
+    with torch.set_grad_enabled(grad):
+        enc = "native-hip" if model._use_native_encoders(image, amp) else "module"
+        if amp:
+            upd = ("fused-hip-" + args.amp_dtype) if model._use_fused(image, amp) else "module"
+        elif grad:
+            upd = "split-fp32-hip" if model._use_split_train(image, amp) else "module"
+        else:
+            upd = "split-fp32-hip" if model._use_split(image, amp) else "module"
+    if enc == "native-hip" and not amp:
+        enc = "native-hip-split-fp32"
+    return enc, upd
+
+
 def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -157,7 +178,7 @@ def run(args):
     margs = Namespace(small=args.small, mixed_precision=not args.fp32, amp_dtype=args.amp_dtype,
                       alternate_corr=args.alternate_corr,
                       dropout=0.0, channels_last=args.impl == "native",
-                      fused_update=not args.no_fused)
+                      fused_update=not args.no_fused, corr_fp32=args.corr_fp32)
     model = RAFT(margs).to(device)
     if args.impl == "native":
         model = model.to(memory_format=torch.channels_last)
@@ -236,6 +257,7 @@ def run(args):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ar_ms = _allreduce_ms(model, device, world)
+    enc_path, upd_path = _paths(model, pool[0][0], args)
     pairs = args.batch * world * args.steps
     value = pairs / elapsed
     if rank == 0:
@@ -263,7 +285,11 @@ def run(args):
                 "iters": args.iters,
                 "parallelism": f"dp{world}",
                 "impl": args.impl,
-                "fused_update": (args.impl == "native" and not args.no_fused),
+                # the code paths that actually ran (decided by the model's own dispatch rules)
+                "fused_update": upd_path not in ("module", "reference"),
+                "update_path": upd_path,
+                "encoder_path": enc_path,
+                "corr_volume": "fp32" if (args.fp32 or args.corr_fp32 or args.amp_dtype == "fp16") else "bf16",
                 "mode": args.mode,
                 "alternate_corr": args.alternate_corr,
                 "hip_graph": bool(train_graph or (args.graph is not False and args.mode == "infer")),

@@ -116,6 +116,8 @@ def main(argv=None):
     p.add_argument("--mixed_precision", action="store_true", help="use mixed precision")
     p.add_argument("--alternate_corr", action="store_true", help="use efficent correlation implementation")
     p.add_argument("--amp_dtype", default="bf16", choices=["bf16", "fp16"])
+    p.add_argument("--corr_fp32", action="store_true",
+                   help="with --mixed_precision bf16: fp32-faithful correlation volume (the reference's precision)")
     p.add_argument("--device", default=DEVICE)
     p.add_argument("--iters", type=int, default=20)
     p.add_argument("--output", default="demo-output")

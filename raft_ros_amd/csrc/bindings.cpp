@@ -564,10 +564,12 @@ std::tuple<at::Tensor, at::Tensor> local_corr_backward(const at::Tensor& f1, con
   auto g2 = at::zeros({B, H2, W2, C}, f1.options().dtype(at::kFloat));
   at::Tensor fix = deterministic ? at::zeros({B, H2, W2, C}, f1.options().dtype(at::kLong)) : at::Tensor();
   long long* fp = deterministic ? reinterpret_cast<long long*>(fix.data_ptr<int64_t>()) : nullptr;
-  // one level per call: a level-0 pixel of f2 takes at most (2r+2)^2 window corners of each of
-  // the queries that map onto it (H1*W1 / (H2*W2) of them, rounded up)
-  const double per_px = std::ceil((double)(H1 * W1) / (double)(H2 * W2));
-  at::Tensor fs = deterministic ? fixed_point_scale(g, f1, scale, per_px * 4.0 * (rd + 1) * (rd + 1)) : at::Tensor();
+  // the accumulator bound must hold for ANY coordinates: lookups follow the predicted flow, so a
+  // converging / zooming-out flow can send every query of an image onto one f2 pixel, each
+  // through up to 4 (2r+2)^2 window corners.  With the 2^62 target that still leaves >= 2^40
+  // fixed-point steps below the magnitude of a typical pixel's sum.
+  const double nq = (double)(H1 * W1);
+  at::Tensor fs = deterministic ? fixed_point_scale(g, f1, scale, nq * 4.0 * (rd + 1) * (rd + 1)) : at::Tensor();
   HIP_OK(launch_local_corr_bwd(f1.data_ptr(), f2.data_ptr(), dtype_code(f1.scalar_type()),
                                coords.data_ptr<float>(), g.data_ptr<float>(), g1.data_ptr<float>(),
                                g2.data_ptr<float>(), fp, deterministic ? fs.data_ptr<float>() : nullptr, B, H1, W1,
@@ -644,9 +646,10 @@ void local_corr_mfma_backward(const at::Tensor& f1, const at::Tensor& f2, const 
   a.g2fix = deterministic ? reinterpret_cast<long long*>(fix.data_ptr<int64_t>()) : nullptr;
   at::Tensor fs;
   if (deterministic) {
-    // the coarsest level gathers the most queries per pixel: 4^(L-1) of them, each touching it
-    // through up to (2r+2)^2 window corners
-    fs = fixed_point_scale(gout, f1, scale, std::pow(4.0, a.levels - 1) * 4.0 * (2 * radius + 2) * (2 * radius + 2));
+    // worst case over any coordinates (see local_corr_backward): every query of an image on one
+    // pooled-f2 pixel, through up to 4 (2r+2)^2 window corners of each of the L levels
+    fs = fixed_point_scale(gout, f1, scale,
+                           (double)a.H * a.W * a.levels * 4.0 * (2 * radius + 2) * (2 * radius + 2));
     a.fix_scale = fs.data_ptr<float>();
   }
   HIP_OK(launch_local_corr_mfma(a, true, cur_stream()));
@@ -767,14 +770,25 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
   TORCH_CHECK(geom.size() == 7, "raft_amd conv_fwd: geom = (B, H, W, KH, KW, PH, PW)");
   ConvFwdArgs a{};
   if (!split.empty()) {
-    // split-bf16 epilogues (kernel_abi.h ConvFwdArgs::split_g): [G_out, G_out2, S_h, S_z]
-    TORCH_CHECK(split.size() == 4 && (epi == 0 || epi == 2 || epi == 3) && split[0] > 0 && split[0] % 8 == 0,
-                "raft_amd conv_fwd: split = [G_out, G_out2, S_h, S_z] with epilogue 0, 2 or 3");
-    for (int i = 1; i < 4; ++i) TORCH_CHECK(split[i] >= 0 && split[i] % 8 == 0, "raft_amd conv_fwd: split");
+    // split-bf16 epilogues (kernel_abi.h ConvFwdArgs::split_g): [G_out, G_out2, S_h, S_z] and, for
+    // the fp32-training backward, [.., S_g0, G_out3, S_add, G_cout]
+    TORCH_CHECK((split.size() == 4 || split.size() == 8) && epi >= 0 && epi <= 6,
+                "raft_amd conv_fwd: split = [G_out, G_out2, S_h, S_z(, S_g0, G_out3, S_add, G_cout)]");
+    for (size_t i = 0; i < split.size(); ++i)
+      TORCH_CHECK(split[i] >= 0 && split[i] % 8 == 0, "raft_amd conv_fwd: split entries are multiples of 8");
     a.split_g = (int)split[0];
     a.split_g2 = (int)split[1];
     a.split_h = (int)split[2];
     a.split_z = (int)split[3];
+    if (split.size() == 8) {
+      a.split_g0 = (int)split[4];
+      a.split_g3 = (int)split[5];
+      a.split_add = (int)split[6];
+      a.split_cout = (int)split[7];
+    }
+    TORCH_CHECK((epi != 0 && epi != 2 && epi != 3) || a.split_g > 0, "raft_amd conv_fwd: split store needs G_out");
+    TORCH_CHECK(epi != 1 || acc_c0 >= N, "raft_amd conv_fwd: a split gradient store does not accumulate");
+    TORCH_CHECK(epi < 4 || a.split_g == 0, "raft_amd conv_fwd: GRU backward epilogues write fp32 out");
     TORCH_CHECK(epi != 2 || (a.split_g2 > 0 && a.split_h > 0), "raft_amd conv_fwd: split z||r needs G_out2 and S_h");
     TORCH_CHECK(epi != 3 || (a.split_h > 0 && a.split_z > 0), "raft_amd conv_fwd: split blend needs S_h and S_z");
   }

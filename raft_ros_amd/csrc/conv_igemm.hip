@@ -649,26 +649,36 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
           }
         }
         if (a.addsrc) {
-          const bf16x8 av = *reinterpret_cast<const bf16x8*>(a.addsrc + p * a.addsrc_stride + n);
+          float av[8];
+          load8(a.addsrc + p * a.addsrc_stride + n, a.split_add, av);
 #pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] += static_cast<float>(av[q]);
+          for (int q = 0; q < 8; ++q) v[q] += av[q];
         }
-        const bf16x8 gv = *reinterpret_cast<const bf16x8*>(a.g0 + p * a.g0_stride + n);
-        const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + n);
+        // gate operands: bf16, or split planes (hi + lo) in fp32 training
+        float gv[8], hv[8];
+        load8(a.g0 + p * a.g0_stride + n, a.split_g0, gv);
+        load8(a.h + p * a.h_stride + n, a.split_h, hv);
         float* cp = a.carry + p * a.carry_stride + n;
-        bf16x8 d3;
+        float d3[8];
         if (M == 4) {
-          const bf16x8 zv = *reinterpret_cast<const bf16x8*>(a.z + p * a.z_stride + n);
-          bf16x8 dq;
-          float cr[8];
+          float zv[8];
+          load8(a.z + p * a.z_stride + n, a.split_z, zv);
+          float dq[8], cr[8];
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            const float zz = static_cast<float>(zv[q]), qq = static_cast<float>(gv[q]), hh = static_cast<float>(hv[q]);
-            dq[q] = static_cast<__bf16>(v[q] * zz * (1.f - qq * qq));
-            d3[q] = static_cast<__bf16>(v[q] * (qq - hh) * zz * (1.f - zz));
+            const float zz = zv[q], qq = gv[q], hh = hv[q];
+            dq[q] = v[q] * zz * (1.f - qq * qq);
+            d3[q] = v[q] * (qq - hh) * zz * (1.f - zz);
             cr[q] = v[q] * (1.f - zz);
           }
-          *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + n) = dq;
+          if (a.split_g2 > 0) {
+            split_store8(a.out2 + p * a.out2_stride, a.split_g2, n, 8, dq);
+          } else {
+            bf16x8 w;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(dq[q]);
+            *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + n) = w;
+          }
           *reinterpret_cast<f32x4*>(cp) = f32x4{cr[0], cr[1], cr[2], cr[3]};
           *reinterpret_cast<f32x4*>(cp + 4) = f32x4{cr[4], cr[5], cr[6], cr[7]};
         } else {
@@ -677,14 +687,21 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
           float ov[8];
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            const float rr = static_cast<float>(gv[q]), hh = static_cast<float>(hv[q]);
-            d3[q] = static_cast<__bf16>(v[q] * hh * rr * (1.f - rr));
+            const float rr = gv[q], hh = hv[q];
+            d3[q] = v[q] * hh * rr * (1.f - rr);
             ov[q] = cv[q] + v[q] * rr;
           }
           *reinterpret_cast<f32x4*>(o) = f32x4{ov[0], ov[1], ov[2], ov[3]};
           *reinterpret_cast<f32x4*>(o + 4) = f32x4{ov[4], ov[5], ov[6], ov[7]};
         }
-        *reinterpret_cast<bf16x8*>(a.out3 + p * a.out3_stride + n) = d3;
+        if (a.split_g3 > 0) {
+          split_store8(a.out3 + p * a.out3_stride, a.split_g3, n, 8, d3);
+        } else {
+          bf16x8 w;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(d3[q]);
+          *reinterpret_cast<bf16x8*>(a.out3 + p * a.out3_stride + n) = w;
+        }
       } else if (M == 6) {
         // last GRU data gradient: bf16 d net / fp32 d inp / masked bf16 d motion
         const float* o = static_cast<const float*>(a.out) + p * a.out_stride + n;
@@ -696,17 +713,27 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
         }
         bf16x8 w;
         if (n < a.gru_cols) {
+          if (a.split_g3 > 0) {
+            split_store8(a.out3 + p * a.out3_stride, a.split_g3, n, 8, v);
+          } else {
 #pragma unroll
-          for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(v[q]);
-          *reinterpret_cast<bf16x8*>(a.out3 + p * a.out3_stride + n) = w;
+            for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(v[q]);
+            *reinterpret_cast<bf16x8*>(a.out3 + p * a.out3_stride + n) = w;
+          }
         } else {
           const int c = n - a.cm_c0;
           if (c < a.cm_valid) {  // chunks wholly past cm_valid are not stored (cout may be narrower)
             const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.cmask + p * a.cmask_stride + c);
+            float mv[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
-              w[q] = static_cast<__bf16>((c + q < a.cm_valid && static_cast<float>(m[q]) > 0.f) ? v[q] : 0.f);
-            *reinterpret_cast<bf16x8*>(a.cout + p * a.cout_stride + c) = w;
+            for (int q = 0; q < 8; ++q) mv[q] = (c + q < a.cm_valid && static_cast<float>(m[q]) > 0.f) ? v[q] : 0.f;
+            if (a.split_cout > 0) {
+              split_store8(a.cout + p * a.cout_stride, a.split_cout, c, 8, mv);
+            } else {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(mv[q]);
+              *reinterpret_cast<bf16x8*>(a.cout + p * a.cout_stride + c) = w;
+            }
           }
         }
       } else if (M == 0) {
@@ -746,7 +773,9 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
             if (!(static_cast<float>(m[q]) > 0.f)) v[q] = 0.f;
         }
         const bool accum = n >= a.acc_c0;  // acc_c0 is a multiple of 8
-        if (a.out_f32) {
+        if (a.split_g > 0) {  // split planes (fp32 training data gradients; never accumulated)
+          split_store8(static_cast<__bf16*>(a.out) + p * a.out_stride, a.split_g, n, nv, v);
+        } else if (a.out_f32) {
           float* o = static_cast<float*>(a.out) + p * a.out_stride + n;
           if (nv == 8) {
             f32x4 x0 = {v[0], v[1], v[2], v[3]}, x1 = {v[4], v[5], v[6], v[7]};

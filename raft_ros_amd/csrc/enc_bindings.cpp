@@ -87,21 +87,39 @@ void run_conv(EncConvArgs& a, int rows, const at::TensorOptions& o) {
 }
 
 // Decode / packing tables too deep for the kernel arguments (the split-bf16 layout's 3x
-// channels): one device copy per conv geometry, built on first use (so a HIP-graph capture
-// must follow a warm-up forward, as GraphedRAFT's does).
-const int* device_tables(const std::vector<int>& tab, const std::vector<int>& ptab, std::array<int, 5> key,
+// channels): one device copy per distinct table, built on first use (so a HIP-graph capture
+// must follow a warm-up forward, as GraphedRAFT's does).  The cache is a leaked heap object:
+// its device tensors must not be freed by static destructors after the HIP runtime is gone.
+const int* device_tables(const std::vector<int>& tab, const std::vector<int>& ptab, int device,
                          const at::TensorOptions& o) {
-  static std::map<std::array<int, 5>, at::Tensor> cache;
-  static std::mutex mu;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = cache.find(key);
-  if (it == cache.end()) {
-    std::vector<int> both(tab);
-    both.insert(both.end(), ptab.begin(), ptab.end());
+  using Key = std::pair<int, std::vector<int>>;
+  static auto* cache = new std::map<Key, at::Tensor>();
+  static auto* mu = new std::mutex();
+  std::lock_guard<std::mutex> lock(*mu);
+  std::vector<int> both(tab);
+  both.insert(both.end(), ptab.begin(), ptab.end());
+  Key key{device, both};
+  auto it = cache->find(key);
+  if (it == cache->end()) {
     at::Tensor host = at::from_blob(both.data(), {(long)both.size()}, at::TensorOptions().dtype(at::kInt)).clone();
-    it = cache.emplace(key, host.to(o.dtype(at::kInt))).first;
+    it = cache->emplace(std::move(key), host.to(o.dtype(at::kInt))).first;
   }
   return it->second.data_ptr<int>();
+}
+
+// Fill the decode / packing tables of a launch: inline when they fit the arguments, else the
+// device copies (tables of kEncTabMax entries, -1 = zero columns)
+void set_tables(EncConvArgs& a, const std::vector<int>& tab, const std::vector<int>& ptab, int used, int device,
+                const at::TensorOptions& o) {
+  TORCH_CHECK(used <= kEncTabMax, "conv too deep for the decode table");
+  if (used <= kEncTab) {
+    std::copy(tab.begin(), tab.begin() + kEncTab, a.tab);
+    std::copy(ptab.begin(), ptab.begin() + kEncTab, a.ptab);
+  } else {
+    const int* dt = device_tables(tab, ptab, device, o);
+    a.tab_ptr = dt;
+    a.ptab_ptr = dt + kEncTabMax;
+  }
 }
 
 void init_args(EncConvArgs& a) {
@@ -139,15 +157,7 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
         ++e;
       }
   const int K = e * 8, Kpad = round_up(K, 64);
-  TORCH_CHECK(Kpad / 8 <= kEncTabMax, "conv too deep for the decode table");
-  if (Kpad / 8 <= kEncTab) {
-    std::copy(tab.begin(), tab.begin() + kEncTab, a.tab);
-    std::copy(ptab.begin(), ptab.begin() + kEncTab, a.ptab);
-  } else {
-    const int* dt = device_tables(tab, ptab, {x.get_device(), KH, KW, (int)pad, Cx}, x.options());
-    a.tab_ptr = dt;
-    a.ptab_ptr = dt + kEncTabMax;
-  }
+  set_tables(a, tab, ptab, Kpad / 8, x.get_device(), x.options());
   a.cls[0] = EncClass{0, Ho, Wo, 0, 0, K, Kpad, 0, 0, 0};
   a.ncls = 1;
   at::Tensor y = at::empty({B, Ho, Wo, split ? 3 * N : N}, x.options());
@@ -182,9 +192,13 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
 
 // dx[B,H,W,Cin] = sum_j conv_transpose(dys[j], ws[j]) (+ res) (* [mask > 0]);
 // stride[j] / pad[j] per conv, every conv maps x[B,H,W,Cin] -> dys[j].
+//
+// split (fp32 training): dys are split rows [hi | lo | hi] of 3 Cout channels, the weights are
+// packed [W_hi | W_hi | W_lo] along Cout, dx (and res) are split rows of 3 Cin, the ReLU' mask
+// is read from the hi plane of split rows.
 at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef strides, at::IntArrayRef pads,
                           int64_t H, int64_t W, const c10::optional<at::Tensor>& res,
-                          const c10::optional<at::Tensor>& mask) {
+                          const c10::optional<at::Tensor>& mask, bool split) {
   const int nconv = (int)dys.size();
   TORCH_CHECK(nconv >= 1 && nconv <= 2 && (int)ws.size() == nconv && (int)strides.size() == nconv &&
                   (int)pads.size() == nconv,
@@ -201,7 +215,9 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
   for (int j = 0; j < nconv; ++j) {
     check_nhwc(dys[j], "dy");
     check_w(ws[j], "w");
-    TORCH_CHECK(dys[j].size(0) == B && ws[j].size(1) == Cin && dys[j].size(3) == ws[j].size(0), "dgrad shapes");
+    TORCH_CHECK(dys[j].size(0) == B && ws[j].size(1) == Cin && dys[j].size(3) == (split ? 3 : 1) * ws[j].size(0),
+                "dgrad shapes");
+    TORCH_CHECK(!split || ws[j].size(0) == ws[0].size(0), "split dgrad: convs share Cout");
     TORCH_CHECK(S % strides[j] == 0, "strides must divide the largest stride");
     const int KH = (int)ws[j].size(2), KW = (int)ws[j].size(3);
     const int Ho = ((int)H + 2 * (int)pads[j] - KH) / (int)strides[j] + 1;
@@ -211,6 +227,7 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
     a.src[j] = {cbf(dys[j]), C, C, Ho, Wo, S / (int)strides[j]};
     set_weight(a, j, ws[j]);
   }
+  std::vector<int> tab(kEncTabMax, -1), ptab(kEncTabMax, -1);
   int e = 0, ncls = 0;
   for (int py = 0; py < S; ++py)
     for (int px = 0; px < S; ++px) {
@@ -227,37 +244,41 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
             const int vx = px + p - kx;
             if (((vx % s) + s) % s) continue;
             for (int c = 0; c < C; c += 8) {
-              TORCH_CHECK(e < kEncTab, "dgrad too deep for the decode table");
-              a.tab[e] = enc_tab_entry(vy / s, vx / s, j, c);
-              a.ptab[e] = enc_ptab_entry(j, ky, kx, c);
+              TORCH_CHECK(e < kEncTabMax, "dgrad too deep for the decode table");
+              tab[e] = enc_tab_entry(vy / s, vx / s, j, c);
+              ptab[e] = enc_ptab_entry(j, ky, kx, c);
               ++e;
             }
           }
         }
       }
       const int K = (e - t0) * 8, Kpad = std::max(64, round_up(K, 64));
-      TORCH_CHECK(t0 + Kpad / 8 <= kEncTab, "dgrad too deep for the decode table");
+      TORCH_CHECK(t0 + Kpad / 8 <= kEncTabMax, "dgrad too deep for the decode table");
       e = t0 + Kpad / 8;  // padded entries stay -1
       a.cls[ncls++] = EncClass{t0, Gh, Gw, py, px, K, Kpad, 0, 0, 0};
     }
   a.ncls = ncls;
-  at::Tensor dx = at::empty({B, H, W, Cin}, dys[0].options());
+  set_tables(a, tab, ptab, e, dys[0].get_device(), dys[0].options());
+  const int rs = split ? 3 * Cin : Cin;  // dx / res / mask row pitch
+  at::Tensor dx = at::empty({B, H, W, rs}, dys[0].options());
   a.Ho = (int)H;
   a.Wo = (int)W;
   a.os = S;
   a.out = mbf(dx);
-  a.out_stride = Cin;
+  a.out_stride = rs;
+  a.split = split ? 1 : 0;
+  a.split_w = split ? (int)ws[0].size(0) : 0;
   if (res.has_value() && res->defined()) {
     check_nhwc(*res, "res");
     TORCH_CHECK(res->sizes() == dx.sizes(), "res shape");
     a.res = cbf(*res);
-    a.res_stride = Cin;
+    a.res_stride = rs;
   }
   if (mask.has_value() && mask->defined()) {
     check_nhwc(*mask, "mask");
     TORCH_CHECK(mask->sizes() == dx.sizes(), "mask shape");
     a.mask = cbf(*mask);
-    a.mask_stride = Cin;
+    a.mask_stride = rs;
   }
   a.pack_dgrad = 1;
   run_conv(a, Cin, dys[0].options());
@@ -265,10 +286,23 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
 }
 
 // dw (fp32, any strides, [Cout, Cin, KH, KW]) (+)= wgrad; db (+)= sum_p dy
+// x and dy may be channel slices of NHWC rows (a split tensor's [hi | lo] or hi planes):
+// unit channel stride, pixel pitch stride(2), rows of one image contiguous in pitch.
+void check_rows(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4 && t.stride(3) == 1, name,
+              ": expected [B, H, W, C] bf16 rows with unit channel stride");
+  TORCH_CHECK(t.size(3) % 8 == 0 && t.stride(2) % 8 == 0 && t.stride(2) >= t.size(3) &&
+                  t.stride(1) == t.size(2) * t.stride(2) && t.stride(0) == t.size(1) * t.stride(1) &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              name, ": channel slice of contiguous NHWC rows (channels and pitch multiples of 8, 16-byte aligned)");
+  TORCH_CHECK(t.size(0) * t.stride(0) < (1L << 31), name, ": too large");
+}
+
 void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, const c10::optional<at::Tensor>& db,
                     int64_t stride, int64_t pad, bool accumulate, bool db_zero) {
-  check_nhwc(x, "x");
-  check_nhwc(dy, "dy");
+  check_rows(x, "x");
+  check_rows(dy, "dy");
+  const int xpitch = (int)x.stride(2), dypitch = (int)dy.stride(2);
   TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == at::kFloat && dw.dim() == 4, "dw: fp32 4-D");
   const int B = (int)x.size(0), Hx = (int)x.size(1), Wx = (int)x.size(2), Cx = (int)x.size(3);
   const int N = (int)dw.size(0), Cin = (int)dw.size(1), KH = (int)dw.size(2), KW = (int)dw.size(3);
@@ -287,7 +321,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
   // 158 -> 122 us at 16 x 184 x 248; the 128-channel stage-3 conv is faster below (47 vs 55 us)
   if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && Cin == Cx && Cin == 64 && N % 8 == 0) {
     ConvWgradArgs w{};
-    w.src[0] = ConvSrc{cbf(x), (long)Cx, Cin, 0};
+    w.src[0] = ConvSrc{cbf(x), (long)xpitch, Cin, 0};
     w.nsrc = 1;
     w.Cin = Cin;
     w.B = B;
@@ -300,7 +334,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
     w.K = 9 * Cin;
     w.Kpad = round_up(w.K, 64);
     w.dy = cbf(dy);
-    w.dy_stride = N;
+    w.dy_stride = dypitch;
     w.N = N;
     w.P = (long)B * Hx * Wx;
     if (wgrad_supported(w)) {
@@ -331,7 +365,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
   }
   EncWgradArgs a{};
   a.x = cbf(x);
-  a.xstride = Cx;
+  a.xstride = xpitch;
   a.Cx = Cx;
   a.B = B;
   a.Hx = Hx;
@@ -343,7 +377,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
   a.stride = (int)stride;
   a.pad = (int)pad;
   a.dy = cbf(dy);
-  a.dy_stride = N;
+  a.dy_stride = dypitch;
   a.N = N;
   const int BM = (N % 128 == 0) ? 128 : 64;
   a.tilesM = (N + BM - 1) / BM;
@@ -486,11 +520,12 @@ at::Tensor enc_apply(const at::Tensor& x, const at::Tensor& coef, bool relu_a, c
 std::vector<at::Tensor> enc_norm_bwd_impl(const at::Tensor& g, const at::Tensor& a0, const at::Tensor& c0, bool relu0,
                                           const c10::optional<at::Tensor>& a1, const c10::optional<at::Tensor>& c1,
                                           int64_t kind, int stage, const c10::optional<at::Tensor>& part_in,
-                                          int64_t b_fin) {
+                                          int64_t b_fin, bool split) {
   check_nhwc(g, "g");
   check_nhwc(a0, "a0");
   TORCH_CHECK(a0.sizes() == g.sizes(), "a0 shape");
-  const int B = (int)g.size(0), HW = (int)(g.size(1) * g.size(2)), N = (int)g.size(3);
+  TORCH_CHECK(!split || g.size(3) % 24 == 0, "norm backward: split rows hold 3 planes of a multiple of 8 channels");
+  const int B = (int)g.size(0), HW = (int)(g.size(1) * g.size(2)), N = (int)g.size(3) / (split ? 3 : 1);
   TORCH_CHECK(N <= 256, "norm backward: at most 256 channels");
   NormBwdArgs a{};
   a.g = cbf(g);
@@ -509,6 +544,7 @@ std::vector<at::Tensor> enc_norm_bwd_impl(const at::Tensor& g, const at::Tensor&
   a.N = N;
   a.R = std::min(kNormChunks, std::max(1, HW / 256));
   a.kind = (int)kind;
+  a.split = split ? 1 : 0;
   auto fo = g.options().dtype(at::kFloat);
   const long bf = stage == 2 ? (long)b_fin : (long)B;
   TORCH_CHECK(stage != 2 || (kind == 2 && bf >= B && part_in.has_value() && part_in->defined() &&
@@ -544,20 +580,21 @@ std::vector<at::Tensor> enc_norm_bwd_impl(const at::Tensor& g, const at::Tensor&
 
 std::vector<at::Tensor> enc_norm_bwd(const at::Tensor& g, const at::Tensor& a0, const at::Tensor& c0, bool relu0,
                                      const c10::optional<at::Tensor>& a1, const c10::optional<at::Tensor>& c1,
-                                     int64_t kind) {
-  return enc_norm_bwd_impl(g, a0, c0, relu0, a1, c1, kind, 0, c10::nullopt, 0);
+                                     int64_t kind, bool split) {
+  return enc_norm_bwd_impl(g, a0, c0, relu0, a1, c1, kind, 0, c10::nullopt, 0, split);
 }
 
 at::Tensor enc_norm_bwd_part(const at::Tensor& g, const at::Tensor& a0, const at::Tensor& c0, bool relu0,
-                             const c10::optional<at::Tensor>& a1, const c10::optional<at::Tensor>& c1, int64_t kind) {
-  return enc_norm_bwd_impl(g, a0, c0, relu0, a1, c1, kind, 1, c10::nullopt, 0)[0];
+                             const c10::optional<at::Tensor>& a1, const c10::optional<at::Tensor>& c1, int64_t kind,
+                             bool split) {
+  return enc_norm_bwd_impl(g, a0, c0, relu0, a1, c1, kind, 1, c10::nullopt, 0, split)[0];
 }
 
 std::vector<at::Tensor> enc_norm_bwd_finish(const at::Tensor& g, const at::Tensor& a0, const at::Tensor& c0,
                                             bool relu0, const c10::optional<at::Tensor>& a1,
                                             const c10::optional<at::Tensor>& c1, int64_t kind, const at::Tensor& part,
-                                            int64_t b_fin) {
-  return enc_norm_bwd_impl(g, a0, c0, relu0, a1, c1, kind, 2, part, b_fin);
+                                            int64_t b_fin, bool split) {
+  return enc_norm_bwd_impl(g, a0, c0, relu0, a1, c1, kind, 2, part, b_fin, split);
 }
 
 }  // namespace raft_amd
@@ -566,8 +603,8 @@ TORCH_LIBRARY_FRAGMENT(raft_amd, m) {
   m.def("enc_conv_fwd(Tensor x, Tensor w, Tensor? bias, int stride, int pad, bool stats, bool split=False) -> "
         "(Tensor, Tensor)");
   m.def(
-      "enc_conv_dgrad(Tensor[] dys, Tensor[] ws, int[] strides, int[] pads, int H, int W, Tensor? res, Tensor? mask) "
-      "-> Tensor");
+      "enc_conv_dgrad(Tensor[] dys, Tensor[] ws, int[] strides, int[] pads, int H, int W, Tensor? res, Tensor? mask, "
+      "bool split=False) -> Tensor");
   m.def("enc_conv_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, Tensor(b!)? db, int stride, int pad, bool accumulate, "
         "bool db_zero=False) -> ()");
   m.def("enc_prep(Tensor img0, Tensor? img1, bool split=False) -> Tensor");
@@ -576,11 +613,13 @@ TORCH_LIBRARY_FRAGMENT(raft_amd, m) {
       "Tensor(b!)? rvar, Tensor(c!)? nbt, float momentum, float eps, int W=0) -> Tensor");
   m.def("enc_apply(Tensor a, Tensor coef, bool relu_a, Tensor? r, Tensor? coef_r, bool relu_out, bool split=False) "
         "-> Tensor");
-  m.def("enc_norm_bwd(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind) -> Tensor[]");
-  m.def("enc_norm_bwd_part(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind) -> Tensor");
+  m.def("enc_norm_bwd(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind, "
+        "bool split=False) -> Tensor[]");
+  m.def("enc_norm_bwd_part(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind, "
+        "bool split=False) -> Tensor");
   m.def(
       "enc_norm_bwd_finish(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind, Tensor part, "
-      "int b_fin) -> Tensor[]");
+      "int b_fin, bool split=False) -> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {

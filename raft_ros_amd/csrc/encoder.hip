@@ -367,7 +367,8 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
     }
     if (a.res) {
       float r[8];
-      load8(a.res + pix * a.res_stride + n, r);
+      if (a.split) load8_split(a.res + pix * a.res_stride + n, a.N, r);
+      else load8(a.res + pix * a.res_stride + n, r);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += r[e];
     }
@@ -405,7 +406,12 @@ __global__ __launch_bounds__(256) void enc_pack_kernel(const EncConvArgs a, __bf
       const long s0 = w ? a.ws[1][0] : a.ws[0][0], s1 = w ? a.ws[1][1] : a.ws[0][1];
       const long s2 = w ? a.ws[1][2] : a.ws[0][2], s3 = w ? a.ws[1][3] : a.ws[0][3];
       const int cin = w ? a.wcin[1] : a.wcin[0];
-      if (a.pack_dgrad) {
+      if (a.pack_dgrad && a.split_w) {  // split dY rows [hi | lo | hi] of Cout: [W_hi | W_hi | W_lo]
+        const int plane = loc / a.split_w, co = loc - plane * a.split_w;
+        const float x = wp[co * s0 + row * s1 + ky * s2 + kx * s3];
+        const float hi = static_cast<float>(static_cast<__bf16>(x));
+        v = plane < 2 ? hi : x - hi;
+      } else if (a.pack_dgrad) {
         v = wp[loc * s0 + row * s1 + ky * s2 + kx * s3];
       } else if (a.split_w) {  // [W_hi | W_hi | W_lo] against the [hi | lo | hi] input planes
         const int plane = loc / a.split_w, cl = loc - plane * a.split_w;
@@ -855,7 +861,12 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_reduce_kernel(const NormBwdA
   const bool active = pr < PPB;
   const int n = cg * 8;
   const int chunk = (a.HW + a.R - 1) / a.R;
+  const long rs = a.split ? 3L * N : N;  // row pitch (split rows: hi / lo / hi planes of N)
   const int pb = r * chunk, pe = min(a.HW, pb + chunk);
+  auto ld8 = [&](const __bf16* q, float* v) __attribute__((always_inline)) {
+    if (a.split) load8_split(q, N, v);
+    else load8(q, v);
+  };
   float S[4][8];
 #pragma unroll
   for (int qd = 0; qd < 4; ++qd)
@@ -878,13 +889,13 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_reduce_kernel(const NormBwdA
     for (int p = pb + pr; p < pe; p += 2 * PPB) {
       const bool two = p + PPB < pe;
       float gv[2][8], av[2][8], dv[2][8];
-      load8(a.g + (base + p) * N + n, gv[0]);
-      load8(a.a0 + (base + p) * N + n, av[0]);
-      if (a.a1) load8(a.a1 + (base + p) * N + n, dv[0]);
+      ld8(a.g + (base + p) * rs + n, gv[0]);
+      ld8(a.a0 + (base + p) * rs + n, av[0]);
+      if (a.a1) ld8(a.a1 + (base + p) * rs + n, dv[0]);
       if (two) {
-        load8(a.g + (base + p + PPB) * N + n, gv[1]);
-        load8(a.a0 + (base + p + PPB) * N + n, av[1]);
-        if (a.a1) load8(a.a1 + (base + p + PPB) * N + n, dv[1]);
+        ld8(a.g + (base + p + PPB) * rs + n, gv[1]);
+        ld8(a.a0 + (base + p + PPB) * rs + n, av[1]);
+        if (a.a1) ld8(a.a1 + (base + p + PPB) * rs + n, dv[1]);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -981,6 +992,15 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_apply_kernel(const NormBwdAr
   const PixWalk w = pix_walk(G);
   if (w.p < 0) return;
   const int n = w.n, P = a.B * a.HW;
+  const long rp = a.split ? 3L * N : N;  // row pitch (split rows: hi / lo / hi planes of N)
+  auto ld8 = [&](const __bf16* q, float* v) __attribute__((always_inline)) {
+    if (a.split) load8_split(q, N, v);
+    else load8(q, v);
+  };
+  auto st8 = [&](__bf16* q, const float* v) __attribute__((always_inline)) {
+    if (a.split) store8_split(q, N, v);
+    else store8(q, v);
+  };
   int bend = 0;
   float k1[8], k2[8], k3[8], rs[8], mu[8], sc[8], sh[8];
   float q1[8], q2[8], q3[8], rs1[8], mu1[8];
@@ -1009,8 +1029,8 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_apply_kernel(const NormBwdAr
       }
     }
     float gv[8], av[8], o[8];
-    load8(a.g + (long)p * N + n, gv);
-    load8(a.a0 + (long)p * N + n, av);
+    ld8(a.g + (long)p * rp + n, gv);
+    ld8(a.a0 + (long)p * rp + n, av);
     if (a.relu0) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -1021,12 +1041,12 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_apply_kernel(const NormBwdAr
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = k1[e] * gv[e] + k2[e] * (av[e] - mu[e]) * rs[e] + k3[e];
     }
-    store8(a.out0 + (long)p * N + n, o);
+    st8(a.out0 + (long)p * rp + n, o);
     if (a.a1) {
-      load8(a.a1 + (long)p * N + n, av);
+      ld8(a.a1 + (long)p * rp + n, av);
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = q1[e] * gv[e] + q2[e] * (av[e] - mu1[e]) * rs1[e] + q3[e];
-      store8(a.out1 + (long)p * N + n, o);
+      st8(a.out1 + (long)p * rp + n, o);
     }
   }
 }

@@ -109,6 +109,14 @@ struct ConvFwdArgs {
   int split_g2;  // > 0: out2 is split with group width split_g2
   int split_h;   // > 0: h is split; its lo plane is split_h channels after the hi plane
   int split_z;   // > 0: z is split (lo plane offset)
+  // fp32 training (split-bf16 backward, ops/update_split.py): epilogue 1 stores split planes
+  // (split_g, no accumulation); the GRU-backward epilogues 4 / 5 / 6 read g0 and addsrc as
+  // split planes (lo plane offsets) and store out3 / cout as split planes of group widths
+  // split_g3 / split_cout; mask / cmask are then hi-plane views (x > 0 <=> hi(x) > 0)
+  int split_g0;    // > 0: g0 is split (lo plane offset)
+  int split_g3;    // > 0: out3 is split with group width split_g3
+  int split_add;   // > 0: addsrc is split (lo plane offset)
+  int split_cout;  // > 0: cout is split with group width split_cout
 };
 
 struct ConvWgradArgs {
@@ -202,7 +210,10 @@ struct EncConvArgs {
   const int* tab_ptr;
   const int* ptab_ptr;
   // split-bf16 output (fp32-faithful inference, see ConvFwdArgs::split_g): out rows hold
-  // [hi | lo | hi] planes of N channels each (out_stride = 3N)
+  // [hi | lo | hi] planes of N channels each (out_stride = 3N).  A split data gradient (fp32
+  // training) also reads res as split rows (res_stride = 3N, lo plane at +N) and the ReLU'
+  // mask from the hi plane of split rows (mask_stride = 3N); its dY sources are split rows of
+  // 3 Cout channels, packed against [W_hi | W_hi | W_lo] along Cout (split_w = Cout)
   int split;
 };
 
@@ -247,6 +258,7 @@ struct NormBwdArgs {
   float* dbeta[2];
   __bf16* out0;
   __bf16* out1;
+  int split;  // g, a0, a1, out0, out1 are split-bf16 rows of 3N (hi / lo / hi planes; fp32 training)
 };
 
 // 3x3 / stride-1 encoder convs with 64 input and 64 output channels (both encoders' stage-1

@@ -19,6 +19,10 @@ Execution differences (GPU):
 * fp32 inference (no AMP, no autograd: the demo / evaluate / ROS default) runs the
   encoders and the refinement step on the same kernels in split-bf16 mode (hi / lo
   bf16 planes, 3 MFMA products per GEMM: fp32-faithful), so no MIOpen kernel runs;
+* fp32 training (no AMP, autograd: the reference's default recipe) runs the encoders and
+  the refinement step on the split-bf16 kernels too, forward and backward
+  (``ops/update_split.py``, ``ops/encoder.py``);
+* ``args.corr_fp32`` keeps the correlation volume fp32-faithful under bf16 AMP;
 * the lookup emits channels-last features already in the autocast dtype;
 * mixed precision uses ``args.amp_dtype`` (default bf16 on MI355X; 'fp16'
   reproduces the reference's fp16 autocast);
@@ -35,7 +39,7 @@ import torch.nn as nn
 
 from ..ops import CorrPyramid, LocalCorrPyramid, convex_upsample, upflow8
 from ..ops import encoder as encoder_native
-from ..ops import update_fused, update_fused_small
+from ..ops import update_fused, update_fused_small, update_split
 from ..ops._ext import use_native
 from ..ops.reference import coords_grid
 from .extractor import BasicEncoder, SmallEncoder
@@ -140,7 +144,7 @@ class RAFT(nn.Module):
             side = self._side_stream(raw1.device)
             main = torch.cuda.current_stream(raw1.device)
             side.wait_stream(main)
-            split = not amp  # fp32 inference: split-bf16 (fp32-faithful) encoder kernels
+            split = not amp  # fp32: split-bf16 (fp32-faithful) encoder kernels
             with torch.cuda.stream(side):
                 cnet_native = encoder_native.encode(self.cnet, raw1, join_stream=main, split=split)
             fmap1, fmap2 = encoder_native.encode(self.fnet, raw1, raw2, split=split).split(raw1.shape[0], dim=0)
@@ -150,8 +154,10 @@ class RAFT(nn.Module):
         fmap1, fmap2 = fmap1.float(), fmap2.float()
         # the correlation keeps fp32 numerics (split-bf16 MFMA) except under bf16 AMP: the
         # reference builds it in fp32 outside autocast in every mode (core/raft.py:102-103),
-        # so fp16 AMP and fp32 runs both get the fp32-faithful volume
-        split = not (amp and dev == "cuda" and self.amp_dtype == torch.bfloat16)
+        # so fp16 AMP and fp32 runs both get the fp32-faithful volume; ``args.corr_fp32`` keeps
+        # it under bf16 AMP too (bf16 features are then looked up from the fp32 volume)
+        split = (not (amp and dev == "cuda" and self.amp_dtype == torch.bfloat16)
+                 or bool(_arg(self.args, "corr_fp32", False)))
         if self.args.alternate_corr:
             corr_fn = LocalCorrPyramid(fmap1, fmap2, radius=self.args.corr_radius, split=split)
         elif _arg(self.args, "query_shard", False) and not torch.is_grad_enabled():
@@ -184,6 +190,8 @@ class RAFT(nn.Module):
             return self._forward_fused(corr_fn, net, inp, coords0, coords1, iters, test_mode)
         if self._use_split(image1, amp):
             return self._forward_split(corr_fn, net, inp, coords0, coords1, iters, test_mode)
+        if self._use_split_train(image1, amp):
+            return self._forward_split_train(corr_fn, net, inp, coords0, coords1, iters, test_mode)
         for it in range(iters):
             coords1 = coords1.detach()
             corr = corr_fn(coords1, out_dtype=corr_dtype)
@@ -212,8 +220,8 @@ class RAFT(nn.Module):
         return aux_stream(device, "side")
 
     def _use_native_encoders(self, image1, amp: bool) -> bool:
-        """bf16 AMP (training and inference), or fp32 inference on the split-bf16 kernels."""
-        mode_ok = (self.amp_dtype == torch.bfloat16) if amp else not torch.is_grad_enabled()
+        """bf16 AMP, or fp32 (training and inference) on the split-bf16 kernels."""
+        mode_ok = (self.amp_dtype == torch.bfloat16) if amp else True
         return (mode_ok and _arg(self.args, "native_encoder", True)
                 and encoder_native.supported(self.fnet, image1) and encoder_native.supported(self.cnet, image1))
 
@@ -227,6 +235,31 @@ class RAFT(nn.Module):
         """fp32 inference (no AMP, no autograd) on the fused HIP step in split-bf16 mode."""
         return (not amp and not torch.is_grad_enabled() and _arg(self.args, "fused_update", True)
                 and update_fused.supported(self.update_block) and use_native(image1))
+
+    def _use_split_train(self, image1, amp: bool) -> bool:
+        """fp32 training (no AMP, autograd on: the reference's default recipe) on the fused HIP
+        step in split-bf16 mode (ops/update_split.py)."""
+        return (not amp and torch.is_grad_enabled() and _arg(self.args, "fused_update", True)
+                and update_split.supported(self.update_block) and use_native(image1))
+
+    def _forward_split_train(self, corr_fn, net, inp, coords0, coords1, iters: int, test_mode: bool):
+        """fp32 refinement loop with autograd, every conv on the hand-written kernels (split-bf16:
+        fp32-faithful products, fp32 gates / coordinates / accumulation)."""
+        dense = isinstance(corr_fn, CorrPyramid)
+        upd = update_split.SplitTrainBasicUpdate(self.update_block, inp, coords0, iters,
+                                                 pyramid=corr_fn.state if dense else None)
+        flow_predictions = []
+        flow_up = None
+        for t in range(iters):
+            if dense:
+                net, flow_up, coords1 = upd.step(t, net, coords1, ptoken=corr_fn.token)
+            else:
+                c = corr_fn(coords1.detach(), out_dtype=torch.float32).permute(0, 2, 3, 1)
+                net, flow_up, coords1 = upd.step(t, net, coords1, corr=c)
+            flow_predictions.append(flow_up)
+        if test_mode:
+            return coords1 - coords0, flow_up
+        return flow_predictions
 
     def _forward_split(self, corr_fn, net, inp, coords0, coords1, iters: int, test_mode: bool):
         """fp32-faithful refinement loop (ops/update_fused.py SplitBasicUpdate): same math as

@@ -130,8 +130,8 @@ def register() -> None:
         return x.new_empty((B, Ho, Wo, N)), st
 
     @fake(lib + "enc_conv_dgrad")
-    def _(dys, ws, strides, pads, H, W, res, mask):
-        return dys[0].new_empty((dys[0].shape[0], H, W, ws[0].shape[1]))
+    def _(dys, ws, strides, pads, H, W, res, mask, split=False):
+        return dys[0].new_empty((dys[0].shape[0], H, W, (3 if split else 1) * ws[0].shape[1]))
 
     @fake(lib + "enc_prep")
     def _(img0, img1, split=False):
@@ -148,8 +148,8 @@ def register() -> None:
         return torch.empty_like(a)
 
     @fake(lib + "enc_norm_bwd")
-    def _(g, a0, c0, relu0, a1, c1, kind):
-        N = g.shape[3]
+    def _(g, a0, c0, relu0, a1, c1, kind, split=False):
+        N = g.shape[3] // (3 if split else 1)
         bn = kind in (2, 3)
         two = a1 is not None
         f = lambda: g.new_empty((N,), dtype=torch.float32)  # noqa: E731
@@ -158,14 +158,15 @@ def register() -> None:
                 f() if bn and two else g.new_empty((0,)), f() if bn and two else g.new_empty((0,))]
 
     @fake(lib + "enc_norm_bwd_part")
-    def _(g, a0, c0, relu0, a1, c1, kind):
+    def _(g, a0, c0, relu0, a1, c1, kind, split=False):
         B, H, W, N = g.shape
+        N //= 3 if split else 1
         R = min(64, max(1, H * W // 256))  # csrc kNormChunks
         return g.new_empty((B, R, 4, N), dtype=torch.float32)
 
     @fake(lib + "enc_norm_bwd_finish")
-    def _(g, a0, c0, relu0, a1, c1, kind, part, b_fin):
-        N = g.shape[3]
+    def _(g, a0, c0, relu0, a1, c1, kind, part, b_fin, split=False):
+        N = g.shape[3] // (3 if split else 1)
         two = a1 is not None
         f = lambda: g.new_empty((N,), dtype=torch.float32)  # noqa: E731
         return [torch.empty_like(g), torch.empty_like(g) if two else g.new_empty((0,)), f(), f(),

@@ -90,6 +90,10 @@ class _PyramidState:
         per-lookup backward accumulated into; None when no lookup has a gradient."""
         if self.pending:
             assert self.dbuf is None, "deferred and immediate lookup gradients cannot mix"
+            # more lookups than one row-accumulating pass takes (kGradRowsMaxT): chunks add into
+            # the rows, so keep them fp32 (no bf16 rounding of the partial sums between chunks)
+            if len(self.pending) > 32:
+                dtype = torch.float32
             rows = torch.empty(self.buf.shape, device=self.buf.device, dtype=dtype)
             for i in range(0, len(self.pending), 32):
                 chunk = self.pending[i:i + 32]

@@ -122,94 +122,95 @@ def _stats(a, st, nd, P, split: bool = False):
     return ops().enc_norm_stats(st, B, H * W, N, k, None, None, None, None, None, 0.0, eps, W)
 
 
-def _conv(x, cd, P, stats):
+def _conv(x, cd, P, stats, split: bool = False):
     b = P[cd["b"]] if cd["b"] >= 0 else None
-    return ops().enc_conv_fwd(x, P[cd["w"]], b, cd["stride"], cd["pad"], stats)
+    # split: the fp32 weight is split into [W_hi | W_hi | W_lo] by the per-call packing kernel (no
+    # cached copy: an optimizer step -- fused AdamW does not bump the parameter versions -- must
+    # never leave a stale split weight behind)
+    return ops().enc_conv_fwd(x, P[cd["w"]], b, cd["stride"], cd["pad"], stats, split)
 
 
-def _forward(L, x0, P):
-    """Run the encoder; returns (output NHWC, saved records)."""
+def _forward(L, x0, P, split: bool = False):
+    """Run the encoder; returns (output NHWC, saved records).  ``split``: every activation as
+    split-bf16 planes (fp32-faithful, see below)."""
     o = ops()
     sc, sn = L.stem
-    a0, st = _conv(x0, sc, P, True)
-    c0 = _stats(a0, st, sn, P)
-    h = o.enc_apply(a0, c0, True, None, None, False)
+    a0, st = _conv(x0, sc, P, True, split)
+    c0 = _stats(a0, st, sn, P, split)
+    h = o.enc_apply(a0, c0, True, None, None, False, split)
     stem_rec = (x0, a0, c0, h)
     recs = []
     for units, down in L.blocks:
         hin = h
-        ins, acts, coefs, outs = [], [], [], []
+        ins, acts, coefs = [], [], []
         cur = hin
         for ui, (cd, nd) in enumerate(units):
-            a, st = _conv(cur, cd, P, nd["kind"] != _BATCH_EVAL)
-            c = _stats(a, st, nd, P)
+            a, st = _conv(cur, cd, P, nd["kind"] != _BATCH_EVAL, split)
+            c = _stats(a, st, nd, P, split)
             ins.append(cur)
             acts.append(a)
             coefs.append(c)
             if ui + 1 < len(units):
-                cur = o.enc_apply(a, c, True, None, None, False)
+                cur = o.enc_apply(a, c, True, None, None, False, split)
         drec = None
         if down is not None:
             dcd, dnd = down
-            ad, st = _conv(hin, dcd, P, dnd["kind"] != _BATCH_EVAL)
-            cdn = _stats(ad, st, dnd, P)
-            h = o.enc_apply(acts[-1], coefs[-1], True, ad, cdn, True)
+            ad, st = _conv(hin, dcd, P, dnd["kind"] != _BATCH_EVAL, split)
+            cdn = _stats(ad, st, dnd, P, split)
+            h = o.enc_apply(acts[-1], coefs[-1], True, ad, cdn, True, split)
             drec = (ad, cdn)
         else:
-            h = o.enc_apply(acts[-1], coefs[-1], True, hin, None, True)
+            h = o.enc_apply(acts[-1], coefs[-1], True, hin, None, True, split)
         recs.append((ins, acts, coefs, drec, h))
-    y, _ = _conv(h, L.out, P, False)
+    y, _ = _conv(h, L.out, P, False, split)
     return y, stem_rec, recs
 
 
-# ------------------------------------------------------------------ fp32-faithful inference
-# Without AMP (demo.py / evaluate.py / the ROS node default) the encoders run on the same
-# kernels in split-bf16 mode: activations are stored as [hi | lo | hi] bf16 planes and each
-# conv packs [W_hi | W_hi | W_lo] (split while packing, csrc/encoder.hip enc_pack_kernel), so a bf16 MFMA GEMM computes x_hi W_hi + x_lo W_hi + x_hi W_lo
-# with fp32 accumulation; norm statistics come from the fp32 accumulators and the norm /
-# residual / ReLU apply pass reads and writes the planes in fp32 (csrc/encoder.hip).
-
-def _conv_split(L, x, cd, P, stats):
-    b = P[cd["b"]] if cd["b"] >= 0 else None
-    # the fp32 weight is split into [W_hi | W_hi | W_lo] by the per-call packing kernel (no
-    # cached copy: an optimizer step -- fused AdamW does not bump the parameter versions --
-    # must never leave a stale split weight behind)
-    return ops().enc_conv_fwd(x, P[cd["w"]], b, cd["stride"], cd["pad"], stats, True)
-
+# ------------------------------------------------------------------ fp32-faithful (split) mode
+# Without AMP (the reference's default for training, demo.py, evaluate.py and the ROS node) the
+# encoders run on the same kernels in split-bf16 mode: activations -- and in training every
+# data gradient -- are stored as [hi | lo | hi] bf16 planes and each conv packs [W_hi | W_hi |
+# W_lo] (split while packing, csrc/encoder.hip enc_pack_kernel; the data-gradient convs split
+# along Cout against split dY planes), so a bf16 MFMA GEMM computes x_hi W_hi + x_lo W_hi +
+# x_hi W_lo with fp32 accumulation; norm statistics come from the fp32 accumulators, the norm
+# apply / backward passes read and write the planes in fp32, and each weight gradient is two
+# GEMMs ([X_hi | X_lo]^T dY_hi + X_hi^T dY_lo) folded into the fp32 parameter layout.
 
 def _forward_split(L, x0, P):
-    """``_forward`` on split-bf16 planes (inference only); returns the split output rows."""
-    o = ops()
-    sc, sn = L.stem
-    a0, st = _conv_split(L, x0, sc, P, True)
-    h = o.enc_apply(a0, _stats(a0, st, sn, P, True), True, None, None, False, True)
-    for units, down in L.blocks:
-        hin = h
-        cur = hin
-        for ui, (cd, nd) in enumerate(units):
-            a, st = _conv_split(L, cur, cd, P, nd["kind"] != _BATCH_EVAL)
-            c = _stats(a, st, nd, P, True)
-            if ui + 1 < len(units):
-                cur = o.enc_apply(a, c, True, None, None, False, True)
-        if down is not None:
-            dcd, dnd = down
-            ad, st = _conv_split(L, hin, dcd, P, dnd["kind"] != _BATCH_EVAL)
-            h = o.enc_apply(a, c, True, ad, _stats(ad, st, dnd, P, True), True, True)
-        else:
-            h = o.enc_apply(a, c, True, hin, None, True, True)
-    y, _ = _conv_split(L, h, L.out, P, False)
-    return y
+    """``_forward`` on split-bf16 planes without records (inference); the split output rows."""
+    return _forward(L, x0, P, True)[0]
 
 
-def _wgrad(x, dy, cd, P, grads, nd=None):
+def _split_rows(g: torch.Tensor) -> torch.Tensor:
+    """fp32 [..., C] -> bf16 [..., 3C] split planes [hi | lo | hi]."""
+    g = g.float()
+    hi = g.to(torch.bfloat16)
+    lo = (g - hi.float()).to(torch.bfloat16)
+    return torch.cat([hi, lo, hi], dim=-1).contiguous()
+
+
+def _wgrad(x, dy, cd, P, grads, nd=None, split: bool = False):
     """Weight / bias gradient of conv ``cd``; ``nd``: the norm it feeds.  InstanceNorm and
     training-mode BatchNorm subtract the per-channel mean, so a conv bias in front of them
-    has an exactly zero gradient (written as 0, not as bf16 rounding noise)."""
+    has an exactly zero gradient (written as 0, not as bf16 rounding noise).  ``split``: x and
+    dy are split rows; two GEMMs [X_hi | X_lo]^T dY_hi and X_hi^T dY_lo, planes folded."""
     w = P[cd["w"]]
-    dw = torch.empty_like(w, dtype=torch.float32)
-    db = torch.empty(w.shape[0], device=w.device, dtype=torch.float32) if cd["b"] >= 0 else None
     zero = nd is not None and nd["kind"] in (_INSTANCE, _BATCH_TRAIN)
-    ops().enc_conv_wgrad(x, dy, dw, db, cd["stride"], cd["pad"], False, zero)
+    has_b = cd["b"] >= 0
+    if split:
+        N, Cin, KH, KW = w.shape
+        cx = x.shape[3] // 3
+        f32 = dict(device=w.device, dtype=torch.float32)
+        dwa, dwb = torch.empty(N, 2 * cx, KH, KW, **f32), torch.empty(N, cx, KH, KW, **f32)
+        dba, dbb = (torch.empty(N, **f32), torch.empty(N, **f32)) if has_b else (None, None)
+        ops().enc_conv_wgrad(x[..., :2 * cx], dy[..., :N], dwa, dba, cd["stride"], cd["pad"], False, zero)
+        ops().enc_conv_wgrad(x[..., :cx], dy[..., N:2 * N], dwb, dbb, cd["stride"], cd["pad"], False, zero)
+        dw = (dwa[:, :cx] + dwa[:, cx:] + dwb)[:, :Cin].contiguous()
+        db = dba + dbb if has_b else None
+    else:
+        dw = torch.empty_like(w, dtype=torch.float32)
+        db = torch.empty(w.shape[0], device=w.device, dtype=torch.float32) if has_b else None
+        ops().enc_conv_wgrad(x, dy, dw, db, cd["stride"], cd["pad"], False, zero)
     grads[cd["w"]] = dw.to(w.dtype) if w.dtype != torch.float32 else dw
     if db is not None:
         b = P[cd["b"]]
@@ -222,26 +223,27 @@ def _norm_grads(nd, dg, dbt, grads):
         grads[nd["bt"]] = dbt
 
 
-def _norm_bwd(o, nd, g, a0, c0, relu0, a1, c1):
+def _norm_bwd(o, nd, g, a0, c0, relu0, a1, c1, split: bool = False):
     """Norm backward of one conv tail (optionally both tail branches of a block)."""
     m = nd["module"]
     if nd["kind"] == _BATCH_TRAIN and sync_bn.is_synced(m):
-        return sync_bn.native_norm_bwd(o, g, a0, c0, relu0, a1, c1, nd["kind"], m.process_group)
-    return o.enc_norm_bwd(g, a0, c0, relu0, a1, c1, nd["kind"])
+        return sync_bn.native_norm_bwd(o, g, a0, c0, relu0, a1, c1, nd["kind"], m.process_group, split)
+    return o.enc_norm_bwd(g, a0, c0, relu0, a1, c1, nd["kind"], split)
 
 
-def _backward(L, P, gy, stem_rec, recs):
+def _backward(L, P, gy, stem_rec, recs, split: bool = False):
     o = ops()
+    sp = split
     grads = [None] * len(P)
     last_h = recs[-1][4] if recs else stem_rec[3]
-    _wgrad(last_h, gy, L.out, P, grads)
+    _wgrad(last_h, gy, L.out, P, grads, split=sp)
     oc = L.out
     g = o.enc_conv_dgrad([gy], [P[oc["w"]]], [oc["stride"]], [oc["pad"]], last_h.shape[1], last_h.shape[2],
-                         None, last_h)
+                         None, last_h, sp)
     for (units, down), (ins, acts, coefs, drec, _h) in zip(reversed(L.blocks), reversed(recs)):
         dnd = down[1] if down is not None else None
         r = _norm_bwd(o, units[-1][1], g, acts[-1], coefs[-1], True, drec[0] if drec else None,
-                      drec[1] if drec else None)
+                      drec[1] if drec else None, sp)
         # both tail norms of a block share a kind (one norm_fn per encoder)
         da, dad = r[0], r[1] if drec else None
         _norm_grads(units[-1][1], r[2], r[3], grads)
@@ -250,12 +252,12 @@ def _backward(L, P, gy, stem_rec, recs):
         for u in range(len(units) - 1, -1, -1):
             cd, nd = units[u]
             x = ins[u]
-            _wgrad(x, da, cd, P, grads, nd)
+            _wgrad(x, da, cd, P, grads, nd, split=sp)
             if u > 0:
                 dh = o.enc_conv_dgrad([da], [P[cd["w"]]], [cd["stride"]], [cd["pad"]], x.shape[1], x.shape[2],
-                                      None, x)
+                                      None, x, sp)
                 pnd = units[u - 1][1]
-                r = _norm_bwd(o, pnd, dh, acts[u - 1], coefs[u - 1], False, None, None)
+                r = _norm_bwd(o, pnd, dh, acts[u - 1], coefs[u - 1], False, None, None, sp)
                 da = r[0]
                 _norm_grads(pnd, r[2], r[3], grads)
             else:
@@ -266,31 +268,38 @@ def _backward(L, P, gy, stem_rec, recs):
                     ws.append(P[dcd["w"]])
                     ss.append(dcd["stride"])
                     ps.append(dcd["pad"])
-                    _wgrad(x, dad, dcd, P, grads, dnd)
-                g = o.enc_conv_dgrad(dys, ws, ss, ps, x.shape[1], x.shape[2], None if down is not None else g, x)
+                    _wgrad(x, dad, dcd, P, grads, dnd, split=sp)
+                g = o.enc_conv_dgrad(dys, ws, ss, ps, x.shape[1], x.shape[2], None if down is not None else g, x, sp)
     x0, a0, c0, _h0 = stem_rec
     sc, sn = L.stem
-    r = _norm_bwd(o, sn, g, a0, c0, False, None, None)
+    r = _norm_bwd(o, sn, g, a0, c0, False, None, None, sp)
     _norm_grads(sn, r[2], r[3], grads)
-    _wgrad(x0, r[0], sc, P, grads, sn)
+    _wgrad(x0, r[0], sc, P, grads, sn, split=sp)
     return grads
 
 
 class _EncoderFn(torch.autograd.Function):
+    """bf16 AMP (``split=False``: bf16 NHWC output) or fp32 training (``split=True``: the
+    split-bf16 network, fp32 NHWC output = hi + lo planes)."""
+
     @staticmethod
-    def forward(ctx, layout, x0, join, *params):
-        y, stem_rec, recs = _forward(layout, x0, params)
+    def forward(ctx, layout, x0, join, split, *params):
+        y, stem_rec, recs = _forward(layout, x0, params, split)
         ctx.layout = layout
         ctx.params = params
         ctx.join = join
+        ctx.split = split
         # records hold only tensors created here (activations, statistics coefficients)
         ctx.stem_rec, ctx.recs = stem_rec, recs
+        if split:
+            N = y.shape[3] // 3
+            return y[..., :N].float() + y[..., N:2 * N].float()
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        gy = gy.contiguous().to(torch.bfloat16)
-        grads = _backward(ctx.layout, ctx.params, gy, ctx.stem_rec, ctx.recs)
+        gy = _split_rows(gy) if ctx.split else gy.contiguous().to(torch.bfloat16)
+        grads = _backward(ctx.layout, ctx.params, gy, ctx.stem_rec, ctx.recs, ctx.split)
         ctx.stem_rec = ctx.recs = None
         if ctx.join is not None:
             # the forward ran on a side stream, so autograd ran this backward there too: make
@@ -304,13 +313,15 @@ class _EncoderFn(torch.autograd.Function):
                 for g in grads:
                     if g is not None:
                         g.record_stream(ctx.join)
-        return (None, None, None, *grads)
+        return (None, None, None, None, *grads)
 
 
 def _layout(enc):
     # the parameter objects and the BatchNorm train/eval state define the layout
+    # (and the norm modules themselves: convert_sync_bn swaps BatchNorm2d modules for synced ones
+    # that keep the same parameter objects)
     key = tuple(id(p) for p in enc.parameters()) + tuple(
-        m.training for m in enc.modules() if isinstance(m, nn.BatchNorm2d))
+        (id(m), type(m), m.training) for m in enc.modules() if isinstance(m, nn.BatchNorm2d))
     cached = getattr(enc, "_native_layout", None)
     if cached is None or cached[0] != key:
         cached = (key, _Layout(enc))
@@ -324,14 +335,12 @@ def encode(enc, image1: torch.Tensor, image2: torch.Tensor | None = None,
     paired batch).  Returns the (n, C, H/8, W/8) bf16 feature map in channels-last
     layout (``n`` = 2B when paired).  ``join_stream``: when this runs on a side stream,
     the stream that must see the parameter gradients complete (see ``_EncoderFn.backward``).
-    ``split``: fp32-faithful inference (no autograd): the fp32 feature map."""
+    ``split``: fp32-faithful mode (no AMP; training or inference): the fp32 feature map."""
     L = _layout(enc)
-    if split:
-        assert not torch.is_grad_enabled(), "the split-bf16 encoder is inference-only"
-        x0 = ops().enc_prep(image1.float(), image2.float() if image2 is not None else None, True)
+    x0 = ops().enc_prep(image1.float(), image2.float() if image2 is not None else None, split)
+    if split and not torch.is_grad_enabled():
         y = _forward_split(L, x0, L.params)
         N = y.shape[3] // 3
         return (y[..., :N].float() + y[..., N:2 * N].float()).permute(0, 3, 1, 2)
-    x0 = ops().enc_prep(image1.float(), image2.float() if image2 is not None else None)
-    y = _EncoderFn.apply(L, x0, join_stream, *L.params)
+    y = _EncoderFn.apply(L, x0, join_stream, bool(split), *L.params)
     return y.permute(0, 3, 1, 2)

@@ -150,13 +150,13 @@ def native_norm_stats(st: torch.Tensor, group) -> tuple:
     return allst, allst.shape[0]
 
 
-def native_norm_bwd(o, g, a0, c0, relu0, a1, c1, kind, group):
+def native_norm_bwd(o, g, a0, c0, relu0, a1, c1, kind, group, split: bool = False):
     """Synchronized-BN backward of the native encoder's norm tail: reduce pass per rank,
     all-gather of the partial sums, finalize over the global batch, apply per rank.  The
     returned dgamma / dbeta are this rank's own sums (DDP averages them)."""
-    part = o.enc_norm_bwd_part(g, a0, c0, relu0, a1, c1, kind)
+    part = o.enc_norm_bwd_part(g, a0, c0, relu0, a1, c1, kind, split)
     allp = all_gather_cat(part, group)
-    r = list(o.enc_norm_bwd_finish(g, a0, c0, relu0, a1, c1, kind, allp, allp.shape[0]))
+    r = list(o.enc_norm_bwd_finish(g, a0, c0, relu0, a1, c1, kind, allp, allp.shape[0], split))
     loc = part.sum((0, 1))  # [4, N]: dbeta0, dgamma0, dbeta1, dgamma1 of this rank
     r[2], r[3] = loc[1].contiguous(), loc[0].contiguous()
     if a1 is not None:

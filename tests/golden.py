@@ -54,3 +54,60 @@ def run(m, dev, fix, pair: int, **kw):
 
 def epe(a, b) -> float:
     return float((torch.as_tensor(a) - torch.as_tensor(b)).norm(dim=1).mean())
+
+
+# ------------------------------------------------------------------ training-gradient golden
+GRAD_FIXTURE = os.path.join(ROOT, "tests", "fixtures", "golden_grads.npz")
+
+
+def grad_fixture():
+    return np.load(GRAD_FIXTURE, allow_pickle=False)
+
+
+def grad_step(m, dev, **fwd):
+    """One training step's loss + per-parameter fp32 gradients on the fixture batch
+    (scripts/make_golden_grads.py: demo-frame crops, synthetic GT, reference sequence loss)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from make_golden_grads import ITERS, batch
+
+    from raft_ros_amd.train.loss import sequence_loss
+
+    i1, i2, flow, valid = (t.to(dev) for t in batch())
+    m.zero_grad(set_to_none=True)
+    preds = m(i1, i2, iters=ITERS, **fwd)
+    loss, _ = sequence_loss(preds, flow, valid, gamma=0.8)
+    loss.backward()
+    grads = {n: p.grad.detach().double().cpu().reshape(-1) for n, p in m.named_parameters() if p.grad is not None}
+    return float(loss), preds[-1].detach().float().cpu(), grads
+
+
+def grad_errors(grads, fix, name):
+    """-> {param: relative error vs the reference gradient} (full tensor or its 16 fixed
+    projections); parameters whose reference gradient is ~0 (conv biases in front of a norm)
+    report their absolute norm relative to the whole gradient instead."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from make_golden_grads import projections
+
+    total = float(np.sqrt(sum(float(fix[k]) ** 2 for k in fix.files if k.startswith(f"{name}/gnorm/"))))
+    errs = {}
+    for k in fix.files:
+        if not k.startswith(f"{name}/gnorm/"):
+            continue
+        pn = k[len(f"{name}/gnorm/"):]
+        g = grads.get(pn)
+        assert g is not None, f"no gradient for {pn}"
+        gn = float(fix[k])
+        if gn < 1e-6 * total:
+            errs[pn] = float(g.norm()) / total
+            continue
+        if f"{name}/gfull/{pn}" in fix.files:
+            ref = torch.from_numpy(fix[f"{name}/gfull/{pn}"])
+            errs[pn] = float((g - ref).norm() / ref.norm())
+        else:
+            ref = torch.from_numpy(fix[f"{name}/gproj/{pn}"])
+            errs[pn] = float((projections(pn, g.numel()) @ g - ref).norm() / ref.norm())
+    return errs

@@ -44,3 +44,41 @@ def test_native_bf16_within_3x_of_torch_autocast(cuda, small):
         print(f"\n{name} pair {p}: bf16 EPE vs reference  native {dn:.4f}  torch autocast {da:.4f} px "
               f"(mean |flow| {float(ref.norm(dim=1).mean()):.2f})")
         assert dn <= max(3 * da, 1e-3), (p, dn, da)
+
+
+# ------------------------------------------------------------------ training gradients
+def _grad_errs(cuda, small, **kw):
+    from golden import grad_errors, grad_fixture, grad_step
+
+    fix = grad_fixture()
+    m = model(small, fixture(), **kw).to(cuda).train()
+    loss, pred, grads = grad_step(m, cuda)
+    return fix, loss, grad_errors(grads, fix, "small" if small else "base")
+
+
+@pytest.mark.parametrize("small", [False, True])
+def test_native_fp32_training_gradients_match_reference(cuda, small):
+    """Native fp32 training (split-bf16 kernels: encoders + refinement step) vs the REAL
+    reference's CPU fp32 gradients (tests/fixtures/golden_grads.npz): <= 1e-3 relative per
+    parameter (16 fixed projections or the full tensor)."""
+    name = "small" if small else "base"
+    fix, loss, errs = _grad_errs(cuda, small, mixed_precision=False)
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:3]
+    print(f"\n{name}: native fp32 training vs reference: loss {loss:.6f} (ref {float(fix[name + '/loss']):.6f}), "
+          f"worst parameter-gradient rel err {worst}")
+    assert abs(loss - float(fix[f"{name}/loss"])) <= 1e-4 * abs(float(fix[f"{name}/loss"]))
+    assert worst[0][1] <= 1e-3, worst
+
+
+@pytest.mark.parametrize("small", [False, True])
+def test_native_bf16_training_gradients_within_3x_of_torch_autocast(cuda, small):
+    """Native bf16 training vs the reference's fp32 gradients: the per-parameter error (RMS
+    over parameters) within 3x of PyTorch's own bf16 autocast of the module path."""
+    name = "small" if small else "base"
+    _, _, en = _grad_errs(cuda, small, mixed_precision=True, amp_dtype="bf16")
+    _, _, ea = _grad_errs(cuda, small, mixed_precision=True, amp_dtype="bf16", fused_update=False,
+                          native_encoder=False)
+    rms = lambda e: (sum(v * v for v in e.values()) / len(e)) ** 0.5  # noqa: E731
+    print(f"\n{name}: bf16 training gradients vs reference: native RMS rel err {rms(en):.4f}, "
+          f"torch autocast {rms(ea):.4f}")
+    assert rms(en) <= 3 * rms(ea), (rms(en), rms(ea))

@@ -1,7 +1,7 @@
 """Fused HIP path (native encoders + fused update steps) vs the fp32 module path.
 
-Oracle: the same RAFT in fp32 (``mixed_precision=False``: PyTorch/MIOpen convs, fp32-
-faithful correlation).  Tolerance: the error of the module path's own bf16 autocast
+Oracle: the same RAFT in fp32 on the module path (``mixed_precision=False, fused_update=False,
+native_encoder=False``: PyTorch/MIOpen convs, fp32-faithful correlation).  Tolerance: the error of the module path's own bf16 autocast
 (MIOpen, ``fused_update=False, native_encoder=False``) against that oracle -- the fused
 bf16 kernels must be at least about as close to fp32 as PyTorch's bf16 AMP is.
 """
@@ -37,7 +37,7 @@ def test_fused_path_matches_fp32_module(cuda, small, shape):
     B, H, W = shape
     torch.manual_seed(0)
     mk = lambda **kw: RAFT(Namespace(small=small, **kw)).to(cuda)  # noqa: E731
-    f32 = mk(mixed_precision=False)
+    f32 = mk(mixed_precision=False, fused_update=False, native_encoder=False)
     amp = mk(mixed_precision=True, amp_dtype="bf16", fused_update=False, native_encoder=False)
     fused = mk(mixed_precision=True, amp_dtype="bf16")
     for m in (amp, fused):

@@ -43,6 +43,9 @@ def build_parser() -> argparse.ArgumentParser:
     g = p.add_argument_group("MI355X options")
     g.add_argument("--amp_dtype", default="bf16", choices=["bf16", "fp16"], help="autocast dtype for --mixed_precision")
     g.add_argument("--alternate_corr", action="store_true", help="memory-efficient local correlation (trainable)")
+    g.add_argument("--corr_fp32", action="store_true",
+                   help="with --mixed_precision bf16: keep the correlation volume fp32-faithful (split-bf16 GEMM, "
+                        "fp32 storage) like the reference (core/raft.py:102-103) instead of the bf16 volume")
     g.add_argument("--no_channels_last", dest="channels_last", action="store_false")
     g.add_argument("--no_fused_update", dest="fused_update", action="store_false",
                    help="run the update block on PyTorch convs instead of the fused HIP kernels")
