@@ -1030,6 +1030,31 @@ std::tuple<at::Tensor, c10::optional<at::Tensor>, at::Tensor> pack_conv_weights(
   return {wf, wd, bias};
 }
 
+// Split-bf16 (fp32-mode) operands: forward [N][Kf] over every segment's [hi | lo | hi] planes
+// against [W_hi | W_hi | W_lo]; optional data-gradient operand [Cin_pad][Kd] over dY planes of
+// width G_dy (ops/update_split.py); fp32 scaled bias [N].
+std::tuple<at::Tensor, c10::optional<at::Tensor>, at::Tensor> pack_conv_weights_split(
+    at::TensorList w, const c10::List<c10::optional<at::Tensor>>& b, at::IntArrayRef segs, double scale, int64_t Kf,
+    int64_t Kd, int64_t G_dy) {
+  ConvParamDesc d = param_desc(w, b, segs, scale, "pack_conv_weights_split");
+  const int N = d.rows[0] + d.rows[1];
+  const int taps = d.KH * d.KW;
+  TORCH_CHECK(Kf >= taps * 3 * d.Cin_pad && Kf % 64 == 0, "raft_amd pack_conv_weights_split: Kf too small / not % 64");
+  TORCH_CHECK(Kd == 0 || (G_dy >= N && G_dy % 8 == 0 && Kd >= taps * 3 * G_dy && Kd % 64 == 0),
+              "raft_amd pack_conv_weights_split: bad data-gradient layout");
+  d.split_fw = 1;
+  d.split_dy = (int)G_dy;
+  const c10::DeviceGuard guard(w[0].device());
+  auto bopt = w[0].options().dtype(at::kBFloat16);
+  auto wf = at::empty({N, Kf}, bopt);
+  c10::optional<at::Tensor> wd;
+  if (Kd > 0) wd = at::empty({d.Cin_pad, Kd}, bopt);
+  auto bias = at::empty({N}, w[0].options());
+  HIP_OK(launch_pack_conv_weights(d, N, wf.data_ptr(), (int)Kf, Kd > 0 ? wd->data_ptr() : nullptr, (int)Kd, 0,
+                                  bias.data_ptr<float>(), cur_stream()));
+  return {wf, wd, bias};
+}
+
 // ---------------------------------------------------------------- update-block elementwise
 void pm_any(const at::Tensor& t, const char* name, long P, at::ScalarType dt) {
   check_gpu(t, name);
@@ -1229,6 +1254,8 @@ TORCH_LIBRARY(raft_amd, m) {
         "bool accumulate=True) -> ()");
   m.def("conv_wgrad_params(Tensor[] srcs, Tensor dy, int[] geom, Tensor(a!)[] wgrad, Tensor?[] bgrad, int[] segs, "
         "float scale, bool accumulate) -> ()");
+  m.def("pack_conv_weights_split(Tensor[] w, Tensor?[] b, int[] segs, float scale, int Kf, int Kd, int G_dy) -> "
+        "(Tensor, Tensor?, Tensor)");
   m.def("pack_conv_weights(Tensor[] w, Tensor?[] b, int[] segs, float scale, int Kf, int Kd, int cout_pad) -> "
         "(Tensor, Tensor?, Tensor)");
   m.def("gru_gates(Tensor zr, Tensor h) -> (Tensor, Tensor)");
@@ -1303,6 +1330,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("conv_wgrad", &raft_amd::conv_wgrad);
   m.impl("conv_wgrad_params", &raft_amd::conv_wgrad_params);
   m.impl("pack_conv_weights", &raft_amd::pack_conv_weights);
+  m.impl("pack_conv_weights_split", &raft_amd::pack_conv_weights_split);
   m.impl("gru_gates", &raft_amd::gru_gates);
   m.impl("gru_gates_backward", &raft_amd::gru_gates_backward);
   m.impl("gru_blend", &raft_amd::gru_blend);

@@ -95,167 +95,9 @@ __device__ __forceinline__ PixCoord decode_pix(long p, long P, int H, int W) {
   return c;
 }
 
-// ============================================================================ forward / dgrad
-// BM x BN output tile, BK = 64, 256 threads as 2x2 waves, each wave (BM/2)x(BN/2)
-// = TM x TN MFMA 32x32x16 tiles; two LDS stages, one barrier per K step.
-constexpr int FBK = 64, FLDK = FBK + 8;  // padded row: 144 B -> conflict-free ds_read_b128 groups
-
-template <int BM, int BN>
-__global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvFwdArgs a) {
-  constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int ACH = BM * FBK / 8 / 256, BCH = BN * FBK / 8 / 256;
-  constexpr int STAGE = (BM + BN) * FLDK;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
-
-  const int tilesN = (a.N + BN - 1) / BN;
-  const int tilesM = (int)((a.P + BM - 1) / BM);
-  const int wg = xcd_remap(blockIdx.x, tilesM * tilesN);
-  const int tm = wg / tilesN, tn = wg - (wg / tilesN) * tilesN;
-  const long m0 = (long)tm * BM;
-  const int n0 = tn * BN;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int kc = tid & 7;  // fixed 16-byte column of every chunk this thread stages
-
-  PixCoord pc[ACH];
-#pragma unroll
-  for (int i = 0; i < ACH; ++i) pc[i] = decode_pix(m0 + (tid >> 3) + 32 * i, a.P, a.H, a.W);
-
-  // the K step never straddles a tap / source segment when every segment is a multiple
-  // of FBK channels (or the conv is 1x1): tap + segment are then wave-uniform (scalar)
-  bool uniform = (a.KH * a.KW == 1) || (a.Cin % FBK == 0);
-  for (int i = 0; i < 3; ++i) uniform = uniform && (a.src[i].C % FBK == 0 || a.KH * a.KW == 1);
-  const int nk = a.Kpad / FBK;
-
-  u32x4 ra[ACH], rb[BCH];
-  auto load = [&](int k0) __attribute__((always_inline)) {
-    if (uniform) {
-      int tap = k0 / a.Cin;
-      int c0 = k0 - tap * a.Cin;
-      if (a.KH * a.KW == 1) { tap = 0; c0 = k0; }
-      const int ky = tap / a.KW, kx = tap - (tap / a.KW) * a.KW;
-      const int dy = ky - a.PH, dx = kx - a.PW;
-      const SrcSel s = select_src(a.src, c0);
-      const long doff = (long)dy * a.W + dx;
-#pragma unroll
-      for (int i = 0; i < ACH; ++i) {
-        const int y = pc[i].py + dy, x = pc[i].px + dx;
-        const bool ok = pc[i].p >= 0 && k0 + kc * 8 < a.K && y >= 0 && y < a.H && x >= 0 && x < a.W;
-        ra[i] = ok ? *reinterpret_cast<const u32x4*>(s.ptr + (pc[i].p + doff) * s.stride + s.c + kc * 8)
-                   : u32x4{0, 0, 0, 0};
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < ACH; ++i) {
-        const long p = pc[i].p;
-        const int b = p >= 0 ? (int)(p / ((long)a.H * a.W)) : 0;
-        ra[i] = im2col_chunk(a.src, a.Cin, a.K, a.H, a.W, a.KW, a.PH, a.PW, p >= 0, b, pc[i].py, pc[i].px,
-                             k0 + kc * 8);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < BCH; ++i) {
-      const int n = n0 + (tid >> 3) + 32 * i;
-      rb[i] = n < a.N ? *reinterpret_cast<const u32x4*>(a.wt + (long)n * a.Kpad + k0 + kc * 8)
-                      : u32x4{0, 0, 0, 0};
-    }
-  };
-  auto store = [&](int buf) __attribute__((always_inline)) {
-    __bf16* sA = smem + buf * STAGE;
-    __bf16* sB = sA + BM * FLDK;
-#pragma unroll
-    for (int i = 0; i < ACH; ++i)
-      *reinterpret_cast<u32x4*>(sA + ((tid >> 3) + 32 * i) * FLDK + kc * 8) = ra[i];
-#pragma unroll
-    for (int i = 0; i < BCH; ++i)
-      *reinterpret_cast<u32x4*>(sB + ((tid >> 3) + 32 * i) * FLDK + kc * 8) = rb[i];
-  };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int fr = lane & 31, fk = (lane >> 5) * 8;
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int t = 0; t < nk; ++t) {
-    if (t + 1 < nk) load((t + 1) * FBK);
-    const __bf16* sA = smem + (t & 1) * STAGE;
-    const __bf16* sB = sA + BM * FLDK;
-#pragma unroll
-    for (int s = 0; s < FBK / 16; ++s) {
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(sA + (wm * (BM / 2) + i * 32 + fr) * FLDK + s * 16 + fk);
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(sB + (wn * (BN / 2) + j * 32 + fr) * FLDK + s * 16 + fk);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    if (t + 1 < nk) store((t + 1) & 1);
-    __syncthreads();
-  }
-
-  // ------------------------------------------------------------------ epilogue
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
-    if (n >= a.N) continue;
-    const float bias = a.bias ? a.bias[n] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row >= a.P) continue;
-        float v = acc[i][j][r] * a.alpha + bias;
-        if (a.epi == 0) {
-          if (a.act == 1) v = fmaxf(v, 0.f);
-          if (a.out_f32)
-            static_cast<float*>(a.out)[row * a.out_stride + n] = v;
-          else
-            static_cast<__bf16*>(a.out)[row * a.out_stride + n] = static_cast<__bf16>(v);
-        } else if (a.epi == 1) {
-          if (a.mask && !(static_cast<float>(a.mask[row * a.mask_stride + n]) > 0.f)) v = 0.f;
-          if (a.out_f32) {
-            float* o = static_cast<float*>(a.out) + row * a.out_stride + n;
-            *o = n >= a.acc_c0 ? *o + v : v;
-          } else {
-            __bf16* o = static_cast<__bf16*>(a.out) + row * a.out_stride + n;
-            *o = static_cast<__bf16>(n >= a.acc_c0 ? static_cast<float>(*o) + v : v);
-          }
-        } else if (a.epi == 2) {
-          // z||r gates: out = sigmoid(zr) (2C channels), out2 = r * h
-          const int C = a.N >> 1;
-          const float sg = sigmoidf_(v);
-          static_cast<__bf16*>(a.out)[row * a.out_stride + n] = static_cast<__bf16>(sg);
-          if (n >= C) {
-            const float hv = static_cast<float>(a.h[row * a.h_stride + (n - C)]);
-            a.out2[row * a.out2_stride + (n - C)] = static_cast<__bf16>(sg * hv);
-          }
-        } else {
-          // candidate + blend: out = (1-z) h + z tanh(q), out2 = tanh(q)
-          const float q = tanhf_(v);
-          const float zv = static_cast<float>(a.z[row * a.z_stride + n]);
-          const float hv = static_cast<float>(a.h[row * a.h_stride + n]);
-          static_cast<__bf16*>(a.out)[row * a.out_stride + n] =
-              static_cast<__bf16>((1.f - zv) * hv + zv * q);
-          a.out2[row * a.out2_stride + n] = static_cast<__bf16>(q);
-        }
-      }
-  }
-}
+// K step of the forward / dgrad kernels; padded LDS row of the generic kernel: 144 B ->
+// conflict-free ds_read_b128 groups
+constexpr int FBK = 64, FLDK = FBK + 8;
 
 // ============================================================================ DMA helpers
 // Direct-to-LDS pipeline: every 16-byte chunk of the A (im2col) and B (packed weight)
@@ -868,6 +710,124 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
     case 5: rows(std::integral_constant<int, 5>{}); break;
     default: rows(std::integral_constant<int, 6>{}); break;
   }
+}
+
+// ============================================================================ forward / dgrad (generic)
+// BM x BN output tile, BK = 64, 256 threads as 2x2 waves, each wave (BM/2)x(BN/2)
+// = TM x TN MFMA 32x32x16 tiles; two LDS stages, one barrier per K step; register-staged
+// im2col for any source layout (the DMA kernels below need 64-channel segments).
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvFwdArgs a) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int ACH = BM * FBK / 8 / 256, BCH = BN * FBK / 8 / 256;
+  constexpr int STAGE = (BM + BN) * FLDK;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+
+  const int tilesN = (a.N + BN - 1) / BN;
+  const int tilesM = (int)((a.P + BM - 1) / BM);
+  const int wg = xcd_remap(blockIdx.x, tilesM * tilesN);
+  const int tm = wg / tilesN, tn = wg - (wg / tilesN) * tilesN;
+  const long m0 = (long)tm * BM;
+  const int n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int kc = tid & 7;  // fixed 16-byte column of every chunk this thread stages
+
+  PixCoord pc[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) pc[i] = decode_pix(m0 + (tid >> 3) + 32 * i, a.P, a.H, a.W);
+
+  // the K step never straddles a tap / source segment when every segment is a multiple
+  // of FBK channels (or the conv is 1x1): tap + segment are then wave-uniform (scalar)
+  bool uniform = (a.KH * a.KW == 1) || (a.Cin % FBK == 0);
+  for (int i = 0; i < 3; ++i) uniform = uniform && (a.src[i].C % FBK == 0 || a.KH * a.KW == 1);
+  const int nk = a.Kpad / FBK;
+
+  u32x4 ra[ACH], rb[BCH];
+  auto load = [&](int k0) __attribute__((always_inline)) {
+    if (uniform) {
+      int tap = k0 / a.Cin;
+      int c0 = k0 - tap * a.Cin;
+      if (a.KH * a.KW == 1) { tap = 0; c0 = k0; }
+      const int ky = tap / a.KW, kx = tap - (tap / a.KW) * a.KW;
+      const int dy = ky - a.PH, dx = kx - a.PW;
+      const SrcSel s = select_src(a.src, c0);
+      const long doff = (long)dy * a.W + dx;
+#pragma unroll
+      for (int i = 0; i < ACH; ++i) {
+        const int y = pc[i].py + dy, x = pc[i].px + dx;
+        const bool ok = pc[i].p >= 0 && k0 + kc * 8 < a.K && y >= 0 && y < a.H && x >= 0 && x < a.W;
+        ra[i] = ok ? *reinterpret_cast<const u32x4*>(s.ptr + (pc[i].p + doff) * s.stride + s.c + kc * 8)
+                   : u32x4{0, 0, 0, 0};
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < ACH; ++i) {
+        const long p = pc[i].p;
+        const int b = p >= 0 ? (int)(p / ((long)a.H * a.W)) : 0;
+        ra[i] = im2col_chunk(a.src, a.Cin, a.K, a.H, a.W, a.KW, a.PH, a.PW, p >= 0, b, pc[i].py, pc[i].px,
+                             k0 + kc * 8);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int n = n0 + (tid >> 3) + 32 * i;
+      rb[i] = n < a.N ? *reinterpret_cast<const u32x4*>(a.wt + (long)n * a.Kpad + k0 + kc * 8)
+                      : u32x4{0, 0, 0, 0};
+    }
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+    __bf16* sA = smem + buf * STAGE;
+    __bf16* sB = sA + BM * FLDK;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i)
+      *reinterpret_cast<u32x4*>(sA + ((tid >> 3) + 32 * i) * FLDK + kc * 8) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BCH; ++i)
+      *reinterpret_cast<u32x4*>(sB + ((tid >> 3) + 32 * i) * FLDK + kc * 8) = rb[i];
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int fr = lane & 31, fk = (lane >> 5) * 8;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) load((t + 1) * FBK);
+    const __bf16* sA = smem + (t & 1) * STAGE;
+    const __bf16* sB = sA + BM * FLDK;
+#pragma unroll
+    for (int s = 0; s < FBK / 16; ++s) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(sA + (wm * (BM / 2) + i * 32 + fr) * FLDK + s * 16 + fk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(sB + (wn * (BN / 2) + j * 32 + fr) * FLDK + s * 16 + fk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nk) store((t + 1) & 1);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------------ epilogue
+  // the shared LDS-staged epilogue of the DMA kernels (every store mode, GRU gates and their
+  // backward, split-bf16 planes); the operand ring is free after the last K step's barrier
+  static_assert(BM * (BN + 4) * 4 <= 2 * STAGE * 2, "epilogue tile must fit the operand ring");
+  fwd_epilogue<BM, BN, TM, TN>(a, reinterpret_cast<float*>(smem), acc, (int)m0, n0, (int)a.P, a.N);
 }
 
 template <int BM, int BN, int S>
@@ -2166,8 +2126,7 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   for (int i = 0; i < a.nsrc; ++i) maxbytes = std::max(maxbytes, a.P * a.src[i].stride * 2);
   const bool dma_ok = (uniform || a.nsrc == 1) && maxbytes < (1L << 31) && (long)a.N * a.Kpad * 2 < (1L << 31);
   if (!dma_ok || cfg == 1) {
-    // the fused GRU epilogues and the split-bf16 stores live in the v4/v5 kernels
-    if (a.epi >= 4 || a.split_g > 0) return hipErrorInvalidValue;
+    if (a.P >= (1L << 31)) return hipErrorInvalidValue;  // 32-bit tile rows in the shared epilogue
     hipLaunchKernelGGL((conv_fwd_kernel<64, 64>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
     return hipGetLastError();
   }

@@ -154,6 +154,11 @@ struct ConvParamDesc {
   int seg_real[3], seg_pad[3];
   int Cin, Cin_pad, KH, KW;
   float scale;
+  // split-bf16 packing (fp32 mode, ops/update_split.py): split_fw = 1 -> the forward operand
+  // runs over every segment's [hi | lo | hi] planes (3 x seg_pad channels each) against
+  // [W_hi | W_hi | W_lo]; split_dy = G > 0 -> the data-gradient operand runs over dY planes
+  // [hi | lo | hi] of width G (k = tapflip * 3G + plane * G + n) against [W_hi | W_hi | W_lo]
+  int split_fw, split_dy;
 };
 
 // ============================================================================ encoder convs

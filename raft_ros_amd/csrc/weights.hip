@@ -55,6 +55,70 @@ __device__ __forceinline__ float param_at(const ConvParamDesc& d, int n, int c, 
   return w[nn * d.ws[which][0] + c * d.ws[which][1] + ky * d.ws[which][2] + kx * d.ws[which][3]];
 }
 
+// split-bf16 plane of a scaled fp32 weight: planes 0 / 1 -> hi = bf16(v), plane 2 -> lo = bf16(v - hi)
+__device__ __forceinline__ __bf16 plane_of(float v, int plane) {
+  const __bf16 hi = static_cast<__bf16>(v);
+  return plane < 2 ? hi : static_cast<__bf16>(v - static_cast<float>(hi));
+}
+
+// forward column c3 of a split operand (every segment tripled) -> (real channel or -1, plane)
+__device__ __forceinline__ int split_channel(const ConvParamDesc& d, int c3, int& plane) {
+  int r0 = 0, p0 = 0;
+  for (int i = 0; i < d.nseg; ++i) {
+    const int w = 3 * d.seg_pad[i];
+    if (c3 < p0 + w) {
+      const int loc = c3 - p0;
+      plane = loc / d.seg_pad[i];
+      const int o = loc - plane * d.seg_pad[i];
+      return o < d.seg_real[i] ? r0 + o : -1;
+    }
+    r0 += d.seg_real[i];
+    p0 += w;
+  }
+  plane = 0;
+  return -1;
+}
+
+__global__ __launch_bounds__(256) void pack_conv_weights_split_kernel(ConvParamDesc d, int N, __bf16* __restrict__ wf,
+                                                                      int Kf, __bf16* __restrict__ wd, int Kd,
+                                                                      float* __restrict__ bias) {
+  const int taps = d.KH * d.KW;
+  const int Cin3 = 3 * d.Cin_pad, G = d.split_dy;
+  const long nf = (long)N * Kf;
+  const long nd = wd ? (long)d.Cin_pad * Kd : 0;
+  const long total = nf + nd + N;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    if (i < nf) {
+      const int n = (int)(i / Kf), k = (int)(i - (long)n * Kf);
+      const int tap = k / Cin3;
+      __bf16 v = static_cast<__bf16>(0.f);
+      if (tap < taps) {
+        int plane;
+        const int c = split_channel(d, k - tap * Cin3, plane);
+        if (c >= 0) v = plane_of(d.scale * param_at(d, n, c, tap / d.KW, tap - (tap / d.KW) * d.KW), plane);
+      }
+      wf[i] = v;
+    } else if (i < nf + nd) {
+      const long j = i - nf;
+      const int cp = (int)(j / Kd), k = (int)(j - (long)cp * Kd);
+      const int tapf = k / (3 * G), n3 = k - tapf * 3 * G;
+      const int plane = n3 / G, n = n3 - plane * G;
+      __bf16 v = static_cast<__bf16>(0.f);
+      if (tapf < taps && n < N) {
+        const int c = real_channel(d, cp);
+        const int kyf = tapf / d.KW, kxf = tapf - kyf * d.KW;
+        if (c >= 0) v = plane_of(d.scale * param_at(d, n, c, d.KH - 1 - kyf, d.KW - 1 - kxf), plane);
+      }
+      wd[j] = v;
+    } else {
+      const int n = (int)(i - nf - nd);
+      const int which = n < d.rows[0] ? 0 : 1;
+      const float* b = d.b[which];
+      bias[n] = b ? d.scale * b[which == 0 ? n : n - d.rows[0]] : 0.f;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void pack_conv_weights_kernel(ConvParamDesc d, int N, __bf16* __restrict__ wf,
                                                                 int Kf, __bf16* __restrict__ wd, int Kd,
                                                                 int Cout_pad, float* __restrict__ bias) {
@@ -190,6 +254,12 @@ inline dim3 grid_of(long total) {
 hipError_t launch_pack_conv_weights(const ConvParamDesc& d, int N, void* wf, int Kf, void* wd, int Kd, int Cout_pad,
                                     float* bias, hipStream_t s) {
   const long total = (long)N * Kf + (wd ? (long)d.Cin_pad * Kd : 0) + N;
+  if (d.split_fw) {
+    if (wd && d.split_dy <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pack_conv_weights_split_kernel, grid_of(total), dim3(256), 0, s, d, N, static_cast<__bf16*>(wf),
+                       Kf, static_cast<__bf16*>(wd), Kd, bias);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(pack_conv_weights_kernel, grid_of(total), dim3(256), 0, s, d, N, static_cast<__bf16*>(wf), Kf,
                      static_cast<__bf16*>(wd), Kd, Cout_pad, bias);
   return hipGetLastError();

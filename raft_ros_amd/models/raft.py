@@ -39,7 +39,7 @@ import torch.nn as nn
 
 from ..ops import CorrPyramid, LocalCorrPyramid, convex_upsample, upflow8
 from ..ops import encoder as encoder_native
-from ..ops import update_fused, update_fused_small, update_split
+from ..ops import update_fused, update_fused_small, update_split, update_split_small
 from ..ops._ext import use_native
 from ..ops.reference import coords_grid
 from .extractor import BasicEncoder, SmallEncoder
@@ -129,6 +129,16 @@ class RAFT(nn.Module):
 
         hdim, cdim = self.hidden_dim, self.context_dim
         amp = bool(self.args.mixed_precision)
+        # the batched weight-gradient token of the fused step is created before the encoders, so
+        # its backward overlaps theirs (ops/update_fused.py WeightToken)
+        wtoken = None
+        if torch.is_grad_enabled() and update_fused.EARLY_WGRAD:
+            if self._use_fused(image1, amp) and update_fused.supported(self.update_block):
+                wtoken = update_fused.WeightToken(self.update_block)
+            elif self._use_split_train(image1, amp):
+                wtoken = (update_split_small.weight_token(self.update_block)
+                          if update_split_small.supported(self.update_block)
+                          else update_split.SplitWeightToken(self.update_block))
         native = self._use_native_encoders(image1, amp)
         raw1, raw2 = image1, image2
         if not native:
@@ -187,11 +197,11 @@ class RAFT(nn.Module):
         flow_predictions = []
         flow_up = None
         if self._use_fused(image1, amp):
-            return self._forward_fused(corr_fn, net, inp, coords0, coords1, iters, test_mode)
+            return self._forward_fused(corr_fn, net, inp, coords0, coords1, iters, test_mode, wtoken)
         if self._use_split(image1, amp):
             return self._forward_split(corr_fn, net, inp, coords0, coords1, iters, test_mode)
         if self._use_split_train(image1, amp):
-            return self._forward_split_train(corr_fn, net, inp, coords0, coords1, iters, test_mode)
+            return self._forward_split_train(corr_fn, net, inp, coords0, coords1, iters, test_mode, wtoken)
         for it in range(iters):
             coords1 = coords1.detach()
             corr = corr_fn(coords1, out_dtype=corr_dtype)
@@ -234,28 +244,33 @@ class RAFT(nn.Module):
     def _use_split(self, image1, amp: bool) -> bool:
         """fp32 inference (no AMP, no autograd) on the fused HIP step in split-bf16 mode."""
         return (not amp and not torch.is_grad_enabled() and _arg(self.args, "fused_update", True)
-                and update_fused.supported(self.update_block) and use_native(image1))
+                and (update_fused.supported(self.update_block) or update_split_small.supported(self.update_block))
+                and use_native(image1))
 
     def _use_split_train(self, image1, amp: bool) -> bool:
         """fp32 training (no AMP, autograd on: the reference's default recipe) on the fused HIP
         step in split-bf16 mode (ops/update_split.py)."""
         return (not amp and torch.is_grad_enabled() and _arg(self.args, "fused_update", True)
-                and update_split.supported(self.update_block) and use_native(image1))
+                and (update_split.supported(self.update_block) or update_split_small.supported(self.update_block))
+                and use_native(image1))
 
-    def _forward_split_train(self, corr_fn, net, inp, coords0, coords1, iters: int, test_mode: bool):
-        """fp32 refinement loop with autograd, every conv on the hand-written kernels (split-bf16:
-        fp32-faithful products, fp32 gates / coordinates / accumulation)."""
+    def _forward_split_train(self, corr_fn, net, inp, coords0, coords1, iters: int, test_mode: bool, wtoken=None):
+        """fp32 refinement loop (with autograd; RAFT-small also without), every conv on the
+        hand-written kernels (split-bf16: fp32-faithful products, fp32 gates / coordinates /
+        accumulation): ops/update_split.py (base), ops/update_split_small.py (small)."""
         dense = isinstance(corr_fn, CorrPyramid)
-        upd = update_split.SplitTrainBasicUpdate(self.update_block, inp, coords0, iters,
-                                                 pyramid=corr_fn.state if dense else None)
+        small = update_split_small.supported(self.update_block)
+        cls = update_split_small.SplitSmallUpdate if small else update_split.SplitTrainBasicUpdate
+        upd = cls(self.update_block, inp, coords0, iters, pyramid=corr_fn.state if dense else None, token=wtoken)
         flow_predictions = []
         flow_up = None
         for t in range(iters):
+            up = not test_mode or t == iters - 1
             if dense:
-                net, flow_up, coords1 = upd.step(t, net, coords1, ptoken=corr_fn.token)
+                net, flow_up, coords1 = upd.step(t, net, coords1, ptoken=corr_fn.token, upsample=up)
             else:
                 c = corr_fn(coords1.detach(), out_dtype=torch.float32).permute(0, 2, 3, 1)
-                net, flow_up, coords1 = upd.step(t, net, coords1, corr=c)
+                net, flow_up, coords1 = upd.step(t, net, coords1, corr=c, upsample=up)
             flow_predictions.append(flow_up)
         if test_mode:
             return coords1 - coords0, flow_up
@@ -264,6 +279,8 @@ class RAFT(nn.Module):
     def _forward_split(self, corr_fn, net, inp, coords0, coords1, iters: int, test_mode: bool):
         """fp32-faithful refinement loop (ops/update_fused.py SplitBasicUpdate): same math as
         the module loop above, every conv on the hand-written kernels."""
+        if update_split_small.supported(self.update_block):
+            return self._forward_split_train(corr_fn, net, inp, coords0, coords1, iters, test_mode)
         dense = isinstance(corr_fn, CorrPyramid)
         upd = update_fused.SplitBasicUpdate(self.update_block, inp, iters, pyramid=corr_fn.state if dense else None)
         flow_predictions = []
@@ -281,7 +298,7 @@ class RAFT(nn.Module):
             return coords1 - coords0, flow_up
         return flow_predictions
 
-    def _forward_fused(self, corr_fn, net, inp, coords0, coords1, iters: int, test_mode: bool):
+    def _forward_fused(self, corr_fn, net, inp, coords0, coords1, iters: int, test_mode: bool, wtoken=None):
         """Refinement loop on the fused HIP step (raft_ros_amd/ops/update_fused.py): lookup,
         update block, coords update and convex upsampling as one autograd node per
         iteration, weight gradients batched over all iterations; same math as the loop
@@ -290,7 +307,8 @@ class RAFT(nn.Module):
         small = update_fused_small.supported(self.update_block)
         fused = update_fused_small.FusedSmallUpdate if small else update_fused.FusedBasicUpdate
         pad = update_fused_small.CORR_PAD if small else update_fused.CORR_PAD
-        upd = fused(self.update_block, inp, iters, pyramid=corr_fn.state if dense else None)
+        kw = {} if small else {"token": wtoken}
+        upd = fused(self.update_block, inp, iters, pyramid=corr_fn.state if dense else None, **kw)
         flow_predictions = []
         flow_up = None
         for t in range(iters):

@@ -102,6 +102,14 @@ def register() -> None:
     def _(x, dy, stats, relu):
         return _cl(x, x.shape)
 
+    @fake(lib + "pack_conv_weights_split")
+    def _(w, b, segs, scale, Kf, Kd, G_dy):
+        n = sum(t.shape[0] for t in w)
+        cin_pad = sum(segs[1::2])
+        wf = w[0].new_empty((n, Kf), dtype=torch.bfloat16)
+        wd = w[0].new_empty((cin_pad, Kd), dtype=torch.bfloat16) if Kd > 0 else None
+        return wf, wd, w[0].new_empty((n,))
+
     @fake(lib + "pack_conv_weights")
     def _(w, b, segs, scale, Kf, Kd, cout_pad):
         n = sum(t.shape[0] for t in w)

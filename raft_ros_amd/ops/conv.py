@@ -149,7 +149,8 @@ def split_pack(src: torch.Tensor, dst: torch.Tensor, G: int, c0: int = 0, cpad: 
 
 
 def pack_weights_split(weights, biases, source_segments, scale: float = 1.0):
-    """Forward weights of a conv over split-bf16 operands (no data-gradient operand).
+    """Forward weights of a conv over split-bf16 operands (no data-gradient operand); the torch
+    reference of ``pack_weights_split_native`` (tests).
 
     ``source_segments``: one list of (real, padded) segments per SOURCE tensor (a source is one
     split operand [hi | lo | hi] of its padded width).  The packed K runs over each source's
@@ -164,9 +165,23 @@ def pack_weights_split(weights, biases, source_segments, scale: float = 1.0):
         c += r
     assert c == w.shape[1], (c, w.shape)
     b = [None if t is None else t.detach().float() * scale for t in biases]
-    wf, _, bias = pack_weights([torch.cat(parts, 1)], [torch.cat(b) if all(x is not None for x in b) else None],
-                               split_segments_by_source(source_segments), 1.0, dgrad=False)
-    return wf, bias
+    bias = torch.cat(b) if all(x is not None for x in b) else torch.zeros(w.shape[0], device=w.device)
+    return pack_fwd(torch.cat(parts, 1), split_segments_by_source(source_segments)), bias
+
+
+def pack_weights_split_native(weights, biases, segments, scale: float = 1.0, G_dy: int = 0):
+    """One HIP launch (csrc/weights.hip pack_conv_weights_split_kernel): the split-bf16 forward
+    operand -- every segment (one per source) as [W_hi | W_hi | W_lo] against its [hi | lo | hi]
+    planes -- and, for ``G_dy > 0``, the data-gradient operand over dY planes of width ``G_dy``
+    (the layouts of ``pack_weights_split`` / ``ops.update_split.pack_dgrad_split``) plus the
+    fp32 scaled bias -> (wf, wd or None, bias)."""
+    cout = sum(w.shape[0] for w in weights)
+    _, cin, kh, kw = weights[0].shape
+    cin_p = sum(p for _, p in segments)
+    kf = _round(kh * kw * 3 * cin_p, KBLK)
+    kd = _round(kh * kw * 3 * G_dy, KBLK) if G_dy else 0
+    return ops().pack_conv_weights_split([t.detach() for t in weights], [None if t is None else t.detach() for t in biases],
+                                         flat_segments(segments), scale, kf, kd, G_dy)
 
 
 def split_segments_by_source(source_segments) -> List[Tuple[int, int]]:

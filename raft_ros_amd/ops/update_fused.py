@@ -249,6 +249,8 @@ TAIL_STREAM = True  # motion-encoder backward on its own stream (see _Step.backw
 # wgrad stream as soon as their iterations' backward is done (_Run.early_weight_grads)
 WGRAD_SPLIT = int(os.environ.get("RAFT_WGRAD_SPLIT", "1"))  # 2: -1.5 % (gpurun_out r3 A/B), kept off
 HEAD_STREAM = True  # upsampler / head backward ahead of the d-net chain (see _Step.backward)
+# batched weight gradients on the tail stream beside the encoders' backward (see WeightToken)
+EARLY_WGRAD = os.environ.get("RAFT_EARLY_WGRAD", "1") != "0"
 
 
 def _head_stream(device) -> torch.cuda.Stream:
@@ -272,19 +274,52 @@ def _side_stream(device) -> torch.cuda.Stream:
     return aux_stream(device, "side")
 
 
+class WeightToken:
+    """The autograd token of the batched weight gradients, created BEFORE the encoders run.
+
+    Autograd executes ready nodes in decreasing creation order, so a token created before the
+    encoders has its backward run only after the encoders' backward (and the pyramid's) have
+    been issued.  It then computes the weight gradients on the tail stream, starting from the
+    event the last refinement step's backward recorded (``_Run.steps_done``): they overlap the
+    encoders' backward on the main and side streams instead of running before it (both are
+    far from filling the GPU alone).  The current stream waits for them before the gradients
+    are handed back, i.e. behind the already-issued encoder backward."""
+
+    def __init__(self, block):
+        self.run = None
+        self.tensor = _PackWeights.apply(self, *_params(block))
+
+
 class _PackWeights(torch.autograd.Function):
     """Token node: its backward (after every step's backward) runs the batched weight grads."""
 
     @staticmethod
-    def forward(ctx, run: _Run, *params):
-        ctx.run = run
+    def forward(ctx, holder, *params):
+        ctx.holder = holder  # a _Run, or a WeightToken whose run is filled in later
         ctx.set_materialize_grads(False)  # the steps send no token gradient (None): no zero fills
         return params[0].new_zeros(())
 
     @staticmethod
     def backward(ctx, gtoken):
-        run: _Run = ctx.run
+        h = ctx.holder
+        run: _Run = h.run if isinstance(h, WeightToken) else h
+        if run is None:  # the token's forward pass never reached the update loop
+            return (None,) * (len(ctx.needs_input_grad))
         cur = torch.cuda.current_stream() if run.inp_bf.is_cuda else None
+        ev = getattr(run, "steps_done", None)
+        if ev is not None and run.wgrads is None and cur is not None:
+            ws = _tail_stream(cur.device)
+            ws.wait_event(ev)  # the steps' backward on the main stream (the tail stream is ordered)
+            with torch.cuda.stream(ws):
+                grads = run.weight_grads()
+            cur.wait_stream(ws)
+            for g in grads:
+                g.record_stream(cur)
+            for b in run.arena.bufs.values():
+                b.record_stream(ws)
+            run.arena.bufs.clear()
+            run.tail = None
+            return (None, *grads)
         if run.tail is not None:  # the steps' motion-encoder backward wrote dY on the tail stream
             cur.wait_stream(run.tail)
         if run.wgrads is not None:
@@ -528,6 +563,9 @@ class _Step(torch.autograd.Function):
         d_net = _nchw(d_net if ctx.net_dtype == bf else d_net.to(ctx.net_dtype), B, H, W)
         d_inp = None
         if t == 0:  # the last step backward to run (every other step's d net feeds it)
+            if EARLY_WGRAD and dev.type == "cuda" and ar.keep:
+                run.steps_done = torch.cuda.Event()
+                run.steps_done.record(torch.cuda.current_stream(dev))
             done = sorted(run.done)
             gi = run.g_all[:, :, HID:2 * HID] if len(done) == run.iters else run.g_all[done][:, :, HID:2 * HID]
             d_inp = _nchw(gi.sum(0), B, H, W)
@@ -540,10 +578,14 @@ class _Step(torch.autograd.Function):
 class FusedBasicUpdate:
     """Per-forward driver: packs the weights once, then runs fused refinement steps."""
 
-    def __init__(self, block, inp: torch.Tensor, iters: int, pyramid=None):
+    def __init__(self, block, inp: torch.Tensor, iters: int, pyramid=None, token: Optional[WeightToken] = None):
         keep = torch.is_grad_enabled()
         self.run = _Run(block, inp, iters, pyramid=pyramid, keep=keep)
-        self.token = _PackWeights.apply(self.run, *_params(block))
+        if token is not None and keep:
+            token.run = self.run  # created before the encoders (see WeightToken)
+            self.token = token.tensor
+        else:
+            self.token = _PackWeights.apply(self.run, *_params(block))
         # the fp32 ``inp`` keeps autograd's cross-iteration gradient sum in fp32
         self.inp32 = inp.float().contiguous(memory_format=torch.channels_last)
 
@@ -608,8 +650,8 @@ class SplitBasicUpdate:
         self.wf, self.bias = {}, {}
         for name, mods, _, scale, _ in _LAYERS:
             ms = mods(block)
-            self.wf[name], self.bias[name] = C.pack_weights_split([m.weight for m in ms], [m.bias for m in ms],
-                                                                  _SPLIT_SOURCES[name], scale)
+            self.wf[name], _, self.bias[name] = C.pack_weights_split_native(
+                [m.weight for m in ms], [m.bias for m in ms], [s for src in _SPLIT_SOURCES[name] for s in src], scale)
         bf = torch.bfloat16
         e = lambda n: torch.empty(P, n, device=dev, dtype=bf)  # noqa: E731
         self.inp = C.split_pack(_pm(inp.float()), e(384), HID)

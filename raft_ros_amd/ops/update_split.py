@@ -31,6 +31,7 @@ import torch
 
 from . import conv as C
 from ._ext import ops
+from .streams import aux_stream
 from .update_fused import _Arena, _nchw, _pm, _side_stream
 
 HID = 128
@@ -123,13 +124,16 @@ def _fold_planes(dw: torch.Tensor, N: int, taps: int, widths: List[int], planes:
     return torch.cat(parts, 2)
 
 
-def wgrad_split(srcs, dy: torch.Tensor, G_dy: int, geom, shape, segments, scale: float = 1.0):
+def wgrad_split(srcs, dy: torch.Tensor, G_dy: int, geom, shape, segments, scale: float = 1.0,
+                concat: bool = False):
     """fp32-faithful weight / bias gradient of a conv over split operands.
 
     ``srcs``: (tensor, plane width) per split source (rows [hi | lo | hi]); ``dy``: split rows of
     plane width ``G_dy``.  Two GEMMs -- [X_hi | X_lo]^T dY_hi and X_hi^T dY_lo -- into packed fp32
     buffers, folded into ``shape`` (Cout, Cin, kh, kw) (``segments``: the real / padded input
-    channels of each source) -> (dW, db), both times ``scale``."""
+    channels of each source) -> (dW, db), both times ``scale``.  ``concat``: materialise the
+    sources as one operand per GEMM (multi-source layouts the kernels do not take: segments
+    that are not multiples of 128 channels); periodic sources are repeated."""
     N, _, kh, kw = shape
     taps = kh * kw
     widths = [w for _, w in srcs]
@@ -137,6 +141,9 @@ def wgrad_split(srcs, dy: torch.Tensor, G_dy: int, geom, shape, segments, scale:
     out = []
     for planes, dyv in ((2, dy[:, :G_dy]), (1, dy[:, G_dy:2 * G_dy])):
         views = [t[:, :planes * w] for t, w in srcs]
+        if concat and len(views) > 1:
+            n = dy.shape[0]
+            views = [torch.cat([v if v.shape[0] == n else v.repeat(n // v.shape[0], 1) for v in views], dim=1)]
         K = taps * planes * sum(widths)
         dw = torch.empty(N, -(-K // C.KBLK) * C.KBLK, device=dev, dtype=torch.float32)
         db = torch.empty(N, device=dev, dtype=torch.float32)
@@ -174,10 +181,13 @@ class _SRun:
         self.wd: Dict[str, torch.Tensor] = {}
         for name, mods, fsrc, dsegs, dyg, scale in _LAYERS:
             ms = mods(block)
-            self.wf[name], self.bias[name] = C.pack_weights_split([m.weight for m in ms], [m.bias for m in ms],
-                                                                  fsrc, scale)
-            if keep and dsegs is not None:
-                self.wd[name] = pack_dgrad_split([m.weight for m in ms], dsegs, dyg, scale)
+            # one HIP launch per conv: forward + (training) data-gradient operands, bias
+            gdy = dyg[0][2] if (keep and dsegs is not None) else 0
+            wf, wd, b = C.pack_weights_split_native([m.weight for m in ms], [m.bias for m in ms],
+                                                    [s for src in fsrc for s in src], scale, gdy)
+            self.wf[name], self.bias[name] = wf, b
+            if gdy:
+                self.wd[name] = wd
         self.inp_s = C.split_pack(_pm(inp.detach().float()).contiguous(),
                                   torch.empty(P, 3 * HID, device=inp.device, dtype=torch.bfloat16), HID)
 
@@ -240,19 +250,44 @@ class _SRun:
         return out
 
 
+class SplitWeightToken:
+    """Weight-gradient token created before the encoders (see ops/update_fused.py WeightToken):
+    the batched split weight gradients run on the tail stream beside the encoders' backward."""
+
+    def __init__(self, block, params_fn=None):
+        self.run = None
+        self.tensor = _SplitToken.apply(self, *(params_fn or _params)(block))
+
+
 class _SplitToken(torch.autograd.Function):
     """Token node: its backward (after every step's backward) runs the batched weight grads."""
 
     @staticmethod
-    def forward(ctx, run: _SRun, *params):
-        ctx.run = run
+    def forward(ctx, holder, *params):
+        ctx.holder = holder  # a run, or a SplitWeightToken whose run is filled in later
         ctx.set_materialize_grads(False)
         return params[0].new_zeros(())
 
     @staticmethod
     def backward(ctx, gtoken):
-        run: _SRun = ctx.run
-        grads = run.weight_grads()
+        h = ctx.holder
+        run = h.run if isinstance(h, SplitWeightToken) else h
+        if run is None:
+            return (None,) * len(ctx.needs_input_grad)
+        ev = getattr(run, "steps_done", None)
+        if ev is not None:
+            cur = torch.cuda.current_stream(run.inp_s.device)
+            ws = aux_stream(cur.device, "tail")
+            ws.wait_event(ev)
+            with torch.cuda.stream(ws):
+                grads = run.weight_grads()
+            cur.wait_stream(ws)
+            for g in grads:
+                g.record_stream(cur)
+            for b in run.arena.bufs.values():
+                b.record_stream(ws)
+        else:
+            grads = run.weight_grads()
         run.arena.bufs.clear()
         run.dnet.clear()
         return (None, *grads)
@@ -426,6 +461,8 @@ class _SplitStep(torch.autograd.Function):
 
         d_net_out = d_inp = None
         if t == 0:  # the last step backward to run
+            run.steps_done = torch.cuda.Event()
+            run.steps_done.record(torch.cuda.current_stream(dev))
             d_net_out = _nchw(d_net[:, :HID].float() + d_net[:, HID:2 * HID].float(), B, H, W)
             done = sorted(run.done)
             gi = run.g_all[:, :, HID:2 * HID] if len(done) == run.iters else run.g_all[done][:, :, HID:2 * HID]
@@ -438,9 +475,14 @@ class _SplitStep(torch.autograd.Function):
 class SplitTrainBasicUpdate:
     """Per-forward driver of the fp32 (split-bf16) fused refinement step, with autograd."""
 
-    def __init__(self, block, inp: torch.Tensor, coords0: torch.Tensor, iters: int, pyramid=None):
+    def __init__(self, block, inp: torch.Tensor, coords0: torch.Tensor, iters: int, pyramid=None,
+                 token: Optional[SplitWeightToken] = None):
         self.run = _SRun(block, inp, coords0, iters, pyramid=pyramid, keep=torch.is_grad_enabled())
-        self.token = _SplitToken.apply(self.run, *_params(block))
+        if token is not None and self.run.keep:
+            token.run = self.run
+            self.token = token.tensor
+        else:
+            self.token = _SplitToken.apply(self.run, *_params(block))
         self.inp32 = inp.float().contiguous(memory_format=torch.channels_last)
 
     def step(self, t: int, net, coords1, ptoken=None, corr=None,

@@ -33,13 +33,13 @@ def _run(m, batch, iters):
     return preds, {n: p.grad.float().clone() for n, p in m.named_parameters() if p.grad is not None}
 
 
-def _compare(cuda, shape, iters, tol, native_encoder, **kw):
+def _compare(cuda, shape, iters, tol, native_encoder, small=False, **kw):
     from raft_ros_amd.data.synthetic import synthetic_batch
 
     B, H, W = shape
     torch.manual_seed(0)
-    ref = RAFT(Namespace(small=False, mixed_precision=False, fused_update=False, native_encoder=False, **kw)).to(cuda)
-    nat = RAFT(Namespace(small=False, mixed_precision=False, native_encoder=native_encoder, **kw)).to(cuda)
+    ref = RAFT(Namespace(small=small, mixed_precision=False, fused_update=False, native_encoder=False, **kw)).to(cuda)
+    nat = RAFT(Namespace(small=small, mixed_precision=False, native_encoder=native_encoder, **kw)).to(cuda)
     nat.load_state_dict(ref.state_dict())
     for m in (ref, nat):
         m.train()
@@ -76,6 +76,28 @@ def test_split_training_native_encoders_matches_fp32_module(cuda):
     _compare(cuda, (2, 128, 192), 3, 1e-4, native_encoder=True)
 
 
+def test_split_small_training_matches_fp32_module(cuda):
+    _compare(cuda, (2, 128, 192), 3, 1e-4, native_encoder=True, small=True)
+
+
+def test_split_small_inference_matches_fp32_module(cuda):
+    """RAFT-small fp32 inference (demo.py --small / the ROS node's is_small) on the split step."""
+    from raft_ros_amd.data.synthetic import synthetic_batch
+
+    torch.manual_seed(0)
+    ref = RAFT(Namespace(small=True, mixed_precision=False, fused_update=False, native_encoder=False)).to(cuda).eval()
+    nat = RAFT(Namespace(small=True, mixed_precision=False)).to(cuda).eval()
+    nat.load_state_dict(ref.state_dict())
+    i1, i2, _, _ = synthetic_batch(1, 136, 200, max_disp=6, seed=2, device=cuda)
+    with torch.no_grad():
+        assert nat._use_split(i1, False)
+        lo_r, up_r = ref(i1, i2, iters=12, test_mode=True)
+        lo_n, up_n = nat(i1, i2, iters=12, test_mode=True)
+    err = (up_n - up_r).norm(dim=1).mean().item()
+    print(f"small fp32 inference split vs module: EPE {err:.2e} px")
+    assert err <= 1e-3, err
+
+
 def test_split_training_alternate_corr(cuda):
     _compare(cuda, (1, 128, 192), 3, 1e-4, native_encoder=False, alternate_corr=True)
 
@@ -101,3 +123,27 @@ def test_split_training_path_runs_no_miopen_conv(cuda):
     finally:
         torch.nn.functional.conv2d = orig
     assert not calls, calls
+
+
+@pytest.mark.parametrize("small", [False, True])
+def test_split_weight_packing_kernel_matches_python(cuda, small):
+    """csrc/weights.hip pack_conv_weights_split_kernel == the torch reference packing
+    (ops.conv.pack_weights_split + ops.update_split.pack_dgrad_split), bitwise."""
+    from raft_ros_amd.ops import conv as C
+    from raft_ros_amd.ops import update_split, update_split_small
+
+    torch.manual_seed(0)
+    m = RAFT(Namespace(small=small, mixed_precision=False)).to(cuda)
+    mod = update_split_small if small else update_split
+    for spec in mod._LAYERS:
+        name, mods, fsrc, dsegs, dyg = spec[:5]
+        scale = spec[5] if len(spec) > 5 else 1.0
+        ms = mods(m.update_block)
+        w, b = [x.weight for x in ms], [x.bias for x in ms]
+        gdy = dyg[0][2] if dsegs is not None else 0
+        wf, wd, bias = C.pack_weights_split_native(w, b, [s for src in fsrc for s in src], scale, gdy)
+        wf_ref, bias_ref = C.pack_weights_split(w, b, fsrc, scale)
+        assert torch.equal(wf, wf_ref), name
+        torch.testing.assert_close(bias, bias_ref, rtol=0, atol=0)
+        if gdy:
+            assert torch.equal(wd, update_split.pack_dgrad_split(w, dsegs, dyg, scale)), name
