@@ -439,7 +439,7 @@ void convex_upsample_backward_into(const at::Tensor& flow, const at::Tensor& mas
               "raft_amd::convex_upsample_backward_into: bad grad shape");
   TORCH_CHECK(dmask.sizes() == mask.sizes() && dmask.scalar_type() == mask.scalar_type(),
               "raft_amd::convex_upsample_backward_into: dmask must match mask");
-  pm_any(rows, "rows", B * H * W, at::kBFloat16);
+  pm_any(rows, "rows", B * H * W, mask.scalar_type() == at::kHalf ? at::kHalf : at::kBFloat16);
   TORCH_CHECK(rows.size(1) >= 2, "raft_amd::convex_upsample_backward_into: rows need >= 2 channels");
   auto g = grad.to(at::kFloat).contiguous();
   const c10::DeviceGuard guard(flow.device());
@@ -742,6 +742,13 @@ void check_pm(const at::Tensor& t, const char* name, long P) {
 
 // Sources of a conv: (rows, C) pixel-major views.  rows == P, or (weight gradient only) a
 // divisor of P: a periodic source whose row p % rows is read for pixel p.
+// 16-bit operand dtype of a conv launch: bf16, or fp16 (fp16 AMP) -> ConvFwdArgs::f16
+bool is_half16(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf, "raft_amd conv: ", what,
+              " must be bf16 or fp16");
+  return t.scalar_type() == at::kHalf;
+}
+
 int fill_srcs(at::TensorList srcs, long P, ConvSrc* out, bool allow_period) {
   TORCH_CHECK(srcs.size() >= 1 && srcs.size() <= 3, "raft_amd conv: 1..3 input sources");
   int Cin = 0;
@@ -750,7 +757,9 @@ int fill_srcs(at::TensorList srcs, long P, ConvSrc* out, bool allow_period) {
     const long rows = srcs[i].size(0);
     const bool periodic = allow_period && rows != P && rows > 0 && P % rows == 0;
     check_pm(srcs[i], "src", periodic ? rows : P);
-    TORCH_CHECK(srcs[i].scalar_type() == at::kBFloat16, "raft_amd conv: sources must be bf16");
+    TORCH_CHECK(srcs[i].scalar_type() == srcs[0].scalar_type() && (srcs[i].scalar_type() == at::kBFloat16 ||
+                                                                   srcs[i].scalar_type() == at::kHalf),
+                "raft_amd conv: sources must share one 16-bit dtype (bf16, or fp16 for fp16 AMP)");
     TORCH_CHECK(srcs[i].size(1) % 8 == 0, "raft_amd conv: source channels must be multiples of 8");
     out[i] = ConvSrc{static_cast<const __bf16*>(srcs[i].data_ptr()), srcs[i].stride(0), static_cast<int>(srcs[i].size(1)),
                      periodic ? static_cast<int>(rows) : 0};
@@ -798,8 +807,11 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
   a.Cin = fill_srcs(srcs, a.P, a.src, false);
   a.K = a.KH * a.KW * a.Cin;
   a.cfg = static_cast<int>(cfg);
+  a.f16 = is_half16(srcs[0], "sources") ? 1 : 0;
+  const at::ScalarType dt16 = srcs[0].scalar_type();
+  TORCH_CHECK(!a.f16 || split.empty(), "raft_amd conv_fwd: split-bf16 planes are bf16");
   check_gpu(wt, "wt");
-  TORCH_CHECK(wt.scalar_type() == at::kBFloat16 && wt.dim() == 2 && wt.is_contiguous() && wt.size(0) >= N &&
+  TORCH_CHECK(wt.scalar_type() == dt16 && wt.dim() == 2 && wt.is_contiguous() && wt.size(0) >= N &&
                   wt.size(1) >= a.K && wt.size(1) % 64 == 0,
               "raft_amd conv_fwd: wt must be contiguous bf16 [>=N][Kpad], Kpad % 64 == 0, Kpad >= K (", a.K, ")");
   a.Kpad = static_cast<int>(wt.size(1));
@@ -819,7 +831,12 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
   a.out = out.data_ptr();
   a.out_stride = out.stride(0);
   a.out_f32 = out.scalar_type() == at::kFloat;
-  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "raft_amd conv_fwd: out dtype");
+  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == dt16,
+              "raft_amd conv_fwd: out must be fp32 or the sources' 16-bit dtype");
+  // 16-bit epilogue operands share the sources' dtype
+  for (const auto* t : {&mask, &h, &z, &out2, &g0, &out3, &addsrc, &cout, &cmask})
+    if (t->has_value()) TORCH_CHECK((*t)->scalar_type() == dt16, "raft_amd conv_fwd: epilogue operands must be ",
+                                    dt16 == at::kHalf ? "fp16" : "bf16", " like the sources");
   if (epi == 2 || epi == 3) TORCH_CHECK(!a.out_f32, "raft_amd conv_fwd: GRU epilogues write bf16");
   if (mask) {
     check_pm(*mask, "mask", a.P);
@@ -855,8 +872,8 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
     auto bf_rows = [&](const c10::optional<at::Tensor>& t, const char* what, long& stride) -> __bf16* {
       TORCH_CHECK(t.has_value(), "raft_amd conv_fwd: GRU backward epilogue needs ", what);
       check_pm(*t, what, a.P);
-      TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->stride(0) % 8 == 0 && al16(t->data_ptr()),
-                  "raft_amd conv_fwd: ", what, " must be bf16 with 16-byte aligned rows");
+      TORCH_CHECK(t->scalar_type() == dt16 && t->stride(0) % 8 == 0 && al16(t->data_ptr()),
+                  "raft_amd conv_fwd: ", what, " must be 16-bit (the sources' dtype) with 16-byte aligned rows");
       stride = t->stride(0);
       return static_cast<__bf16*>(t->data_ptr());
     };
@@ -902,7 +919,8 @@ ConvWgradArgs wgrad_args(at::TensorList srcs, const at::Tensor& dy, at::IntArray
   a.K = a.KH * a.KW * a.Cin;
   a.Kpad = (a.K + 63) / 64 * 64;
   check_pm(dy, "dy", a.P);
-  TORCH_CHECK(dy.scalar_type() == at::kBFloat16, "raft_amd conv_wgrad: dy must be bf16");
+  TORCH_CHECK(dy.scalar_type() == srcs[0].scalar_type(), "raft_amd conv_wgrad: dy must share the sources' dtype");
+  a.f16 = is_half16(dy, "dy") ? 1 : 0;
   TORCH_CHECK(dy.size(1) >= (N + 7) / 8 * 8, "raft_amd conv_wgrad: dy must hold N channels (rounded to 8)");
   a.dy = static_cast<const __bf16*>(dy.data_ptr());
   a.dy_stride = dy.stride(0);
@@ -1012,15 +1030,16 @@ void conv_wgrad_params(at::TensorList srcs, const at::Tensor& dy, at::IntArrayRe
 // [Cin_pad][Kd] (flipped taps, Cout padded to cout_pad), fp32 scaled bias [N].
 std::tuple<at::Tensor, c10::optional<at::Tensor>, at::Tensor> pack_conv_weights(
     at::TensorList w, const c10::List<c10::optional<at::Tensor>>& b, at::IntArrayRef segs, double scale, int64_t Kf,
-    int64_t Kd, int64_t cout_pad) {
+    int64_t Kd, int64_t cout_pad, bool f16) {
   ConvParamDesc d = param_desc(w, b, segs, scale, "pack_conv_weights");
+  d.f16 = f16 ? 1 : 0;
   const int N = d.rows[0] + d.rows[1];
   const int taps = d.KH * d.KW;
   TORCH_CHECK(Kf >= taps * d.Cin_pad && Kf % 64 == 0, "raft_amd pack_conv_weights: Kf too small / not % 64");
   TORCH_CHECK(Kd == 0 || (cout_pad >= N && Kd >= taps * cout_pad && Kd % 64 == 0),
               "raft_amd pack_conv_weights: bad dgrad layout");
   const c10::DeviceGuard guard(w[0].device());
-  auto bopt = w[0].options().dtype(at::kBFloat16);
+  auto bopt = w[0].options().dtype(f16 ? at::kHalf : at::kBFloat16);
   auto wf = at::empty({N, Kf}, bopt);
   c10::optional<at::Tensor> wd;
   if (Kd > 0) wd = at::empty({d.Cin_pad, Kd}, bopt);
@@ -1118,19 +1137,20 @@ void pack_flow(const at::Tensor& flow, const at::Tensor& flow8, const c10::optio
   TORCH_CHECK(flow.scalar_type() == at::kFloat && flow.is_contiguous() && flow.dim() == 4 && flow.size(1) == 2,
               "raft_amd pack_flow: flow must be contiguous fp32 (B, 2, H, W)");
   const long B = flow.size(0), HW = flow.size(2) * flow.size(3);
-  TORCH_CHECK(flow8.is_contiguous() && flow8.scalar_type() == at::kBFloat16 && flow8.numel() == B * HW * 8,
-              "raft_amd pack_flow: flow8 must be contiguous bf16 (P, 8)");
+  TORCH_CHECK(flow8.is_contiguous() && (flow8.scalar_type() == at::kBFloat16 || flow8.scalar_type() == at::kHalf) &&
+                  flow8.numel() == B * HW * 8,
+              "raft_amd pack_flow: flow8 must be contiguous bf16 / fp16 (P, 8)");
   void* mo = nullptr;
   long smo = 0;
   if (motion) {
-    pm_any(*motion, "motion", B * HW, at::kBFloat16);
+    pm_any(*motion, "motion", B * HW, flow8.scalar_type());
     TORCH_CHECK(motion->size(1) >= 2, "raft_amd pack_flow: motion slice needs 2 channels");
     mo = motion->data_ptr();
     smo = motion->stride(0);
   }
   const c10::DeviceGuard guard(flow.device());
   HIP_OK(launch_pack_flow(flow.data_ptr<float>(), flow8.data_ptr(), mo, smo, B, HW, (int)flow.size(3),
-                          from_coords ? 1 : 0, cur_stream()));
+                          (from_coords ? 1 : 0) | (flow8.scalar_type() == at::kHalf ? 2 : 0), cur_stream()));
 }
 
 // fp32 (P, C) rows -> split-bf16 planes of group width G in dst (P, *) bf16 rows, channels
@@ -1187,11 +1207,13 @@ void corr_lookup_into(at::TensorList pyramid, const at::Tensor& coords, int64_t 
   void* mo = nullptr;
   long smo = 0;
   if (flow8) {
-    TORCH_CHECK(flow8->is_contiguous() && flow8->scalar_type() == at::kBFloat16 && flow8->numel() == B * H * W * 8,
-                "raft_amd::corr_lookup_into: flow8 must be contiguous bf16 (P, 8)");
+    TORCH_CHECK(flow8->is_contiguous() && flow8->scalar_type() == out.scalar_type() &&
+                    (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kHalf) &&
+                    flow8->numel() == B * H * W * 8,
+                "raft_amd::corr_lookup_into: flow8 must be contiguous (P, 8) in the 16-bit out dtype");
     f8 = flow8->data_ptr();
     if (motion) {
-      pm_any(*motion, "motion", B * H * W, at::kBFloat16);
+      pm_any(*motion, "motion", B * H * W, out.scalar_type());
       TORCH_CHECK(motion->size(1) >= 2, "raft_amd::corr_lookup_into: motion slice needs 2 channels");
       mo = motion->data_ptr();
       smo = motion->stride(0);
@@ -1256,7 +1278,8 @@ TORCH_LIBRARY(raft_amd, m) {
         "float scale, bool accumulate) -> ()");
   m.def("pack_conv_weights_split(Tensor[] w, Tensor?[] b, int[] segs, float scale, int Kf, int Kd, int G_dy) -> "
         "(Tensor, Tensor?, Tensor)");
-  m.def("pack_conv_weights(Tensor[] w, Tensor?[] b, int[] segs, float scale, int Kf, int Kd, int cout_pad) -> "
+  m.def("pack_conv_weights(Tensor[] w, Tensor?[] b, int[] segs, float scale, int Kf, int Kd, int cout_pad, "
+        "bool f16=False) -> "
         "(Tensor, Tensor?, Tensor)");
   m.def("gru_gates(Tensor zr, Tensor h) -> (Tensor, Tensor)");
   m.def("gru_gates_backward(Tensor zr, Tensor h, Tensor gz, Tensor grh) -> (Tensor, Tensor)");

@@ -16,6 +16,27 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// 16-bit operand storage: bf16, or IEEE fp16 under fp16 AMP (the kernels keep __bf16 as the
+// storage type of both; ``f16`` is uniform per launch)
+__device__ __forceinline__ __bf16 st16(float v, bool f16) {
+  return f16 ? __builtin_bit_cast(__bf16, static_cast<_Float16>(v)) : static_cast<__bf16>(v);
+}
+__device__ __forceinline__ float ld16(__bf16 x, bool f16) {
+  return f16 ? static_cast<float>(__builtin_bit_cast(_Float16, x)) : static_cast<float>(x);
+}
+
+// v_mfma_f32_32x32x16_{bf16,f16}: the same 8 x 16-bit operand registers per lane
+template <bool F16>
+__device__ __forceinline__ f32x16 mma16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                   0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
 // dtype codes shared with bindings.cpp
 enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 

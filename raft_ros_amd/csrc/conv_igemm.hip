@@ -244,10 +244,10 @@ __device__ __forceinline__ void split_store8(__bf16* row, int G, int n, int nv, 
   }
 }
 
-__device__ __forceinline__ void load8(const __bf16* row, int S, float (&x)[8]) {
+__device__ __forceinline__ void load8(const __bf16* row, int S, float (&x)[8], bool f16 = false) {
   const bf16x8 hv = *reinterpret_cast<const bf16x8*>(row);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) x[q] = static_cast<float>(hv[q]);
+  for (int q = 0; q < 8; ++q) x[q] = ld16(hv[q], f16 && S == 0);
   if (S > 0) {
     const bf16x8 lv = *reinterpret_cast<const bf16x8*>(row + S);
 #pragma unroll
@@ -277,12 +277,13 @@ __device__ __forceinline__ bool row_pixel(int row, int m0, int P, const Tile2D& 
   }
 }
 
-template <int BM, int BN, int TM, int TN, int NW = 4, int WGN = 2, int TW2D = 0>
+template <int BM, int BN, int TM, int TN, int NW = 4, int WGN = 2, int TW2D = 0, bool F16 = false>
 __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f32x16 (&acc)[TM][TN], int m0,
                                              int n0, int P, int Nn, const Tile2D& t2 = Tile2D{}) {
   constexpr int EPI_LD = BN + 4;  // fp32 epilogue tile row pitch
   constexpr int NT = NW * 64;     // threads; waves are laid out (NW/WGN) x WGN over the tile
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr bool f16 = F16;  // 16-bit operands / outputs are fp16 (fp16 AMP)
   const int wm = wave / WGN, wn = wave % WGN;
   constexpr int CPR = BN / 8;  // 8-channel chunks per tile row
   static_assert(NT % CPR == 0, "a thread keeps one channel chunk across rows");
@@ -356,8 +357,8 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const float sg = sigmoidf_(v[q]);
-            w0[q] = static_cast<__bf16>(sg);
-            w1[q] = static_cast<__bf16>(static_cast<float>(w0[q]) * static_cast<float>(hv[q]));
+            w0[q] = st16(sg, f16);
+            w1[q] = st16(ld16(w0[q], f16) * ld16(hv[q], f16), f16);
           }
           *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = w0;
           if (has_h) *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + hc) = w1;
@@ -366,9 +367,9 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const float qq = tanhf_(v[q]);
-            const float z = static_cast<float>(zv[q]);
-            w0[q] = static_cast<__bf16>((1.f - z) * static_cast<float>(hv[q]) + z * qq);
-            w1[q] = static_cast<__bf16>(qq);
+            const float z = ld16(zv[q], f16);
+            w0[q] = st16((1.f - z) * ld16(hv[q], f16) + z * qq, f16);
+            w1[q] = st16(qq, f16);
           }
           *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = w0;
           *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + n) = w1;
@@ -398,8 +399,8 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
         const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.mask + p * a.mask_stride + n);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          if (!(static_cast<float>(m[q]) > 0.f)) lo[q] = 0.f;
-          if (!(static_cast<float>(m[q + 4]) > 0.f)) hi[q] = 0.f;
+          if (!(ld16(m[q], f16) > 0.f)) lo[q] = 0.f;
+          if (!(ld16(m[q + 4], f16) > 0.f)) hi[q] = 0.f;
         }
       }
       if (f32o) {
@@ -426,15 +427,15 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
             const bf16x8 old = *reinterpret_cast<const bf16x8*>(o);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              lo[q] += static_cast<float>(old[q]);
-              hi[q] += static_cast<float>(old[q + 4]);
+              lo[q] += ld16(old[q], f16);
+              hi[q] += ld16(old[q + 4], f16);
             }
           }
           bf16x8 w;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            w[q] = static_cast<__bf16>(lo[q]);
-            w[q + 4] = static_cast<__bf16>(hi[q]);
+            w[q] = st16(lo[q], f16);
+            w[q + 4] = st16(hi[q], f16);
           }
           *reinterpret_cast<bf16x8*>(o) = w;
         } else {
@@ -442,7 +443,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
           for (int q = 0; q < 8; ++q)
             if (n + q < Nn) {
               const float x = q < 4 ? lo[q] : hi[q - 4];
-              o[q] = static_cast<__bf16>(accum ? static_cast<float>(o[q]) + x : x);
+              o[q] = st16(accum ? ld16(o[q], f16) + x : x, f16);
             }
         }
       }
@@ -492,19 +493,19 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
         }
         if (a.addsrc) {
           float av[8];
-          load8(a.addsrc + p * a.addsrc_stride + n, a.split_add, av);
+          load8(a.addsrc + p * a.addsrc_stride + n, a.split_add, av, f16);
 #pragma unroll
           for (int q = 0; q < 8; ++q) v[q] += av[q];
         }
         // gate operands: bf16, or split planes (hi + lo) in fp32 training
         float gv[8], hv[8];
-        load8(a.g0 + p * a.g0_stride + n, a.split_g0, gv);
-        load8(a.h + p * a.h_stride + n, a.split_h, hv);
+        load8(a.g0 + p * a.g0_stride + n, a.split_g0, gv, f16);
+        load8(a.h + p * a.h_stride + n, a.split_h, hv, f16);
         float* cp = a.carry + p * a.carry_stride + n;
         float d3[8];
         if (M == 4) {
           float zv[8];
-          load8(a.z + p * a.z_stride + n, a.split_z, zv);
+          load8(a.z + p * a.z_stride + n, a.split_z, zv, f16);
           float dq[8], cr[8];
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
@@ -518,7 +519,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
           } else {
             bf16x8 w;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(dq[q]);
+            for (int q = 0; q < 8; ++q) w[q] = st16(dq[q], f16);
             *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + n) = w;
           }
           *reinterpret_cast<f32x4*>(cp) = f32x4{cr[0], cr[1], cr[2], cr[3]};
@@ -541,7 +542,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
         } else {
           bf16x8 w;
 #pragma unroll
-          for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(d3[q]);
+          for (int q = 0; q < 8; ++q) w[q] = st16(d3[q], f16);
           *reinterpret_cast<bf16x8*>(a.out3 + p * a.out3_stride + n) = w;
         }
       } else if (M == 6) {
@@ -559,7 +560,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
             split_store8(a.out3 + p * a.out3_stride, a.split_g3, n, 8, v);
           } else {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(v[q]);
+            for (int q = 0; q < 8; ++q) w[q] = st16(v[q], f16);
             *reinterpret_cast<bf16x8*>(a.out3 + p * a.out3_stride + n) = w;
           }
         } else {
@@ -568,12 +569,12 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
             const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.cmask + p * a.cmask_stride + c);
             float mv[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) mv[q] = (c + q < a.cm_valid && static_cast<float>(m[q]) > 0.f) ? v[q] : 0.f;
+            for (int q = 0; q < 8; ++q) mv[q] = (c + q < a.cm_valid && ld16(m[q], f16) > 0.f) ? v[q] : 0.f;
             if (a.split_cout > 0) {
               split_store8(a.cout + p * a.cout_stride, a.split_cout, c, 8, mv);
             } else {
 #pragma unroll
-              for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(mv[q]);
+              for (int q = 0; q < 8; ++q) w[q] = st16(mv[q], f16);
               *reinterpret_cast<bf16x8*>(a.cout + p * a.cout_stride + c) = w;
             }
           }
@@ -599,12 +600,12 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
           if (nv == 8) {
             bf16x8 w;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(v[q]);
+            for (int q = 0; q < 8; ++q) w[q] = st16(v[q], f16);
             *reinterpret_cast<bf16x8*>(o) = w;
           } else {
 #pragma unroll
             for (int q = 0; q < 8; ++q)
-              if (q < nv) o[q] = static_cast<__bf16>(v[q]);
+              if (q < nv) o[q] = st16(v[q], f16);
           }
         }
       } else if (M == 1) {
@@ -612,7 +613,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
           const bf16x8 m = *reinterpret_cast<const bf16x8*>(a.mask + p * a.mask_stride + n);
 #pragma unroll
           for (int q = 0; q < 8; ++q)
-            if (!(static_cast<float>(m[q]) > 0.f)) v[q] = 0.f;
+            if (!(ld16(m[q], f16) > 0.f)) v[q] = 0.f;
         }
         const bool accum = n >= a.acc_c0;  // acc_c0 is a multiple of 8
         if (a.split_g > 0) {  // split planes (fp32 training data gradients; never accumulated)
@@ -638,12 +639,12 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
             bf16x8 w;
             const bf16x8 old = accum ? *reinterpret_cast<const bf16x8*>(o) : bf16x8{};
 #pragma unroll
-            for (int q = 0; q < 8; ++q) w[q] = static_cast<__bf16>(accum ? static_cast<float>(old[q]) + v[q] : v[q]);
+            for (int q = 0; q < 8; ++q) w[q] = st16(accum ? ld16(old[q], f16) + v[q] : v[q], f16);
             *reinterpret_cast<bf16x8*>(o) = w;
           } else {
 #pragma unroll
             for (int q = 0; q < 8; ++q)
-              if (q < nv) o[q] = static_cast<__bf16>(accum ? static_cast<float>(o[q]) + v[q] : v[q]);
+              if (q < nv) o[q] = st16(accum ? ld16(o[q], f16) + v[q] : v[q], f16);
           }
         }
       } else if (M == 2 && a.split_g > 0) {
@@ -676,13 +677,13 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
         const int C = Nn >> 1;
         bf16x8 sg;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) sg[q] = static_cast<__bf16>(sigmoidf_(v[q]));
+        for (int q = 0; q < 8; ++q) sg[q] = st16(sigmoidf_(v[q]), f16);
         *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = sg;
         if (n >= C) {
           const bf16x8 hv = *reinterpret_cast<const bf16x8*>(a.h + p * a.h_stride + (n - C));
           bf16x8 rh;
 #pragma unroll
-          for (int q = 0; q < 8; ++q) rh[q] = static_cast<__bf16>(static_cast<float>(sg[q]) * static_cast<float>(hv[q]));
+          for (int q = 0; q < 8; ++q) rh[q] = st16(ld16(sg[q], f16) * ld16(hv[q], f16), f16);
           *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + (n - C)) = rh;
         }
       } else {
@@ -692,9 +693,9 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const float qq = tanhf_(v[q]);
-          const float z = static_cast<float>(zv[q]);
-          hn[q] = static_cast<__bf16>((1.f - z) * static_cast<float>(hv[q]) + z * qq);
-          qo[q] = static_cast<__bf16>(qq);
+          const float z = ld16(zv[q], f16);
+          hn[q] = st16((1.f - z) * ld16(hv[q], f16) + z * qq, f16);
+          qo[q] = st16(qq, f16);
         }
         *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = hn;
         *reinterpret_cast<bf16x8*>(a.out2 + p * a.out2_stride + n) = qo;
@@ -716,7 +717,7 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
 // BM x BN output tile, BK = 64, 256 threads as 2x2 waves, each wave (BM/2)x(BN/2)
 // = TM x TN MFMA 32x32x16 tiles; two LDS stages, one barrier per K step; register-staged
 // im2col for any source layout (the DMA kernels below need 64-channel segments).
-template <int BM, int BN>
+template <int BM, int BN, bool F16 = false>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvFwdArgs a) {
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int ACH = BM * FBK / 8 / 256, BCH = BN * FBK / 8 / 256;
@@ -817,7 +818,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvFwdArgs a) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mma16<F16>(af[i], bfr[j], acc[i][j]);
     }
     if (t + 1 < nk) store((t + 1) & 1);
     __syncthreads();
@@ -827,10 +828,10 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const ConvFwdArgs a) {
   // the shared LDS-staged epilogue of the DMA kernels (every store mode, GRU gates and their
   // backward, split-bf16 planes); the operand ring is free after the last K step's barrier
   static_assert(BM * (BN + 4) * 4 <= 2 * STAGE * 2, "epilogue tile must fit the operand ring");
-  fwd_epilogue<BM, BN, TM, TN>(a, reinterpret_cast<float*>(smem), acc, (int)m0, n0, (int)a.P, a.N);
+  fwd_epilogue<BM, BN, TM, TN, 4, 2, 0, F16>(a, reinterpret_cast<float*>(smem), acc, (int)m0, n0, (int)a.P, a.N);
 }
 
-template <int BM, int BN, int S>
+template <int BM, int BN, int S, bool F16 = false>
 __global__ __launch_bounds__(256) void conv_fwd4_kernel(const ConvFwdArgs a) {
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int AI = BM / 32, BI = BN / 32;
@@ -940,7 +941,7 @@ __global__ __launch_bounds__(256) void conv_fwd4_kernel(const ConvFwdArgs a) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mma16<F16>(af[i], bfr[j], acc[i][j]);
     }
   }
 #undef RAFT_FWD4_ISSUE
@@ -948,7 +949,7 @@ __global__ __launch_bounds__(256) void conv_fwd4_kernel(const ConvFwdArgs a) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
-  fwd_epilogue<BM, BN, TM, TN>(a, reinterpret_cast<float*>(smem), acc, m0, n0, P, Nn);
+  fwd_epilogue<BM, BN, TM, TN, 4, 2, 0, F16>(a, reinterpret_cast<float*>(smem), acc, m0, n0, P, Nn);
 }
 
 // ============================================================================ forward v5 (halo strip)
@@ -972,7 +973,7 @@ __device__ __forceinline__ bf16x8 lds_read16(unsigned addr) { return *(const lds
 
 // Measurement probes of this kernel (MFMA-, DMA- and read-free variants, cfg 30..32; removed
 // after the measurement: profiles/r3_probe_conv5.log, profiles/r3_probe_conv6.log) led to v6.
-template <int BM, int BN, int NW = 4>
+template <int BM, int BN, int NW = 4, bool F16 = false>
 __global__ __launch_bounds__(NW * 64) void conv_fwd5_kernel(const ConvFwdArgs a, int strip_rows) {
   extern __shared__ __attribute__((aligned(1024))) __bf16 dsm[];
   // NW waves in an (NW/2) x 2 layout; NW = 8 puts two waves on every SIMD of the CU (one
@@ -1129,7 +1130,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd5_kernel(const ConvFwdArgs a,
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+        acc[i][j] = mma16<F16>(fa[i][s], fb[j][s], acc[i][j]);
   };
 
   bf16x8 fa0[TM][4], fb0[TN][4], fa1[TM][4], fb1[TN][4];
@@ -1166,7 +1167,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd5_kernel(const ConvFwdArgs a,
   wait_vmcnt<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  fwd_epilogue<BM, BN, TM, TN, NW>(a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn);
+  fwd_epilogue<BM, BN, TM, TN, NW, 2, 0, F16>(a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn);
 }
 
 // raise a kernel's dynamic-LDS limit once (it only ever grows)
@@ -1250,7 +1251,7 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {
 // strip of BM + (KH-1) W + KW-1 rows no longer fits in LDS): the strip is the tile's halo
 // block of (BM/TW + KH-1) x (TW + KW-1) pixels with pitch TW + KW-1, so a tap is still one
 // constant row shift, and pixels outside the image are DMA'd as zeros (no per-tap masking).
-template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW = 0>
+template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW = 0, bool F16 = false>
 __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwdArgs a, int strip_rows) {
   constexpr int NW = WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;  // wave tile
@@ -1436,7 +1437,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[R][i][s], fb[R][j][s], acc[i][j], 0, 0, 0);
+        acc[i][j] = mma16<F16>(fa[R][i][s], fb[R][j][s], acc[i][j]);
   };
   // issue the step with in-block index GU of the block starting at chunk cb (GU may run past
   // the block: stage and parity stay compile-time because U * NT % 6 == 0)
@@ -1500,7 +1501,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   wait_vmcnt<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  fwd_epilogue<BM, BN, TM, TN, NW, WGN, TW>(a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn, t2);
+  fwd_epilogue<BM, BN, TM, TN, NW, WGN, TW, F16>(a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn, t2);
 }
 
 
@@ -1531,7 +1532,7 @@ __device__ __forceinline__ int wswz(int row, int chunk) {
   return COLS == 128 ? (chunk ^ ((row & 3) << 2)) : (chunk ^ (((row >> 1) & 1) << 2));
 }
 
-template <int BM, int BN, int S>
+template <int BM, int BN, int S, bool F16 = false>
 __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a) {
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int ACPR = BM / 8, BCPR = BN / 8;      // chunks per row
@@ -1651,7 +1652,7 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
     for (int r = 0; r < 16; ++r) accb[i][r] = 0.f;
   bf16x8 ones;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = static_cast<__bf16>(1.0f);
+  for (int e = 0; e < 8; ++e) ones[e] = st16(1.0f, F16);
 
   // transposed-read lane geometry
   const int hh = lane >> 5, gi = (lane >> 4) & 1, q = (lane & 15) >> 2, pq = lane & 3;
@@ -1695,10 +1696,10 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mma16<F16>(af[i], bfr[j], acc[i][j]);
       if (db_step) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i) accb[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], ones, accb[i], 0, 0, 0);
+        for (int i = 0; i < TM; ++i) accb[i] = mma16<F16>(af[i], ones, accb[i]);
       }
     }
   }
@@ -1760,7 +1761,7 @@ struct WG3Geo {
   static constexpr int TAPS = KH * KW;
 };
 
-template <int KH, int KW, int TH, int TW, int MT, int S>
+template <int KH, int KW, int TH, int TW, int MT, int S, bool F16 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv_wgrad3_kernel(const ConvWgradArgs a) {
   using G3 = WG3Geo<KH, KW, TH, TW>;
   static_assert(TH * TW == 64, "64-pixel tiles");
@@ -1879,7 +1880,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     for (int r = 0; r < 16; ++r) accb[i][r] = 0.f;
   bf16x8 ones;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = static_cast<__bf16>(1.0f);
+  for (int e = 0; e < 8; ++e) ones[e] = st16(1.0f, F16);
 
   // transposed-read lane geometry: 16-lane group gi, row q within a 4-row block, column group pq
   const int hh = lane >> 5, gi = (lane >> 4) & 1, q = (lane & 15) >> 2, pq = lane & 3;
@@ -1934,11 +1935,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
         for (int i = 0; i < MT; ++i)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+          acc[i][j] = mma16<F16>(af[i], bfr, acc[i][j]);
       }
       if (db_step) {
 #pragma unroll
-        for (int i = 0; i < MT; ++i) accb[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], ones, accb[i], 0, 0, 0);
+        for (int i = 0; i < MT; ++i) accb[i] = mma16<F16>(af[i], ones, accb[i]);
       }
     }
   }
@@ -1985,6 +1986,7 @@ __global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int sub = lane / LPP, cl = lane - sub * LPP;
   const int ntaps = a.KH * a.KW;
+  const bool f16 = a.f16 != 0;
   const int Cin = a.Cin;
   float w[2][9][8];
 #pragma unroll
@@ -1994,7 +1996,7 @@ __global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
       bf16x8 v{};
       if (n < a.N && t < ntaps) v = *reinterpret_cast<const bf16x8*>(a.wt + (long)n * a.Kpad + t * Cin + cl * 8);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) w[n][t][q] = static_cast<float>(v[q]);
+      for (int q = 0; q < 8; ++q) w[n][t][q] = ld16(v[q], f16);
     }
   const float b0 = a.bias ? a.bias[0] : 0.f, b1 = (a.bias && a.N > 1) ? a.bias[1] : 0.f;
   const int HW = a.H * a.W;
@@ -2022,7 +2024,7 @@ __global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
                                                cl * 8);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          const float xv = static_cast<float>(v[q]);
+          const float xv = ld16(v[q], f16);
           s0 += xv * w[0][t][q];
           s1 += xv * w[1][t][q];
         }
@@ -2045,8 +2047,8 @@ __global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
         if (a.N > 1) o[1] = v1;
       } else {
         __bf16* o = static_cast<__bf16*>(a.out) + p * a.out_stride;
-        o[0] = static_cast<__bf16>(v0);
-        if (a.N > 1) o[1] = static_cast<__bf16>(v1);
+        o[0] = st16(v0, f16);
+        if (a.N > 1) o[1] = st16(v1, f16);
       }
     }
   }
@@ -2055,7 +2057,7 @@ __global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
 }  // namespace
 
 namespace {
-template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW = 0>
+template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW, bool F16>
 bool launch_fwd6_t(const ConvFwdArgs& a, hipStream_t s) {
   using CF = Fwd6Cfg<BN, WGN, KH * KW>;
   constexpr int NW = WGM * WGN;
@@ -2070,8 +2072,8 @@ bool launch_fwd6_t(const ConvFwdArgs& a, hipStream_t s) {
     tiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
   }
   const dim3 grid((unsigned)(tiles * ((a.N + BN - 1) / BN)));
-  set_lds_limit((const void*)conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, TW>, CF::LDS);
-  hipLaunchKernelGGL((conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, TW>), grid, dim3(NW * 64), CF::LDS, s, a, rows);
+  set_lds_limit((const void*)conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, TW, F16>, CF::LDS);
+  hipLaunchKernelGGL((conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, TW, F16>), grid, dim3(NW * 64), CF::LDS, s, a, rows);
   return true;
 }
 // v6 tiles (forced with cfg, chosen per shape by launch_conv_fwd): 41 = 256x64 flat strip (4x1
@@ -2079,29 +2081,31 @@ bool launch_fwd6_t(const ConvFwdArgs& a, hipStream_t s) {
 // as 2-D 4 x 64 tiles (3x3, 1x5), 60 = 256x64 as 2-D 8 x 32 tiles (5x1).  (Measured and
 // dropped: 128x128 4-wave flat and 2-D tiles, cfg 40 / 57 / 58; all next-step reads before the
 // step's MFMAs, cfg 43 / 44 / 46: profiles/r3_bench_conv6_tiles.log, r3_bench_conv6_2d.log.)
+template <bool F16>
 bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
   const bool t33 = a.KH == 3 && a.KW == 3, t15 = a.KH == 1 && a.KW == 5, t51 = a.KH == 5 && a.KW == 1;
   switch (cfg) {
     case 41:
-      if (t33) return launch_fwd6_t<256, 64, 4, 1, 3, 3>(a, s);
-      if (t15) return launch_fwd6_t<256, 64, 4, 1, 1, 5>(a, s);
-      return t51 && launch_fwd6_t<256, 64, 4, 1, 5, 1>(a, s);
+      if (t33) return launch_fwd6_t<256, 64, 4, 1, 3, 3, 0, F16>(a, s);
+      if (t15) return launch_fwd6_t<256, 64, 4, 1, 1, 5, 0, F16>(a, s);
+      return t51 && launch_fwd6_t<256, 64, 4, 1, 5, 1, 0, F16>(a, s);
     case 45:
-      if (t33) return launch_fwd6_t<256, 128, 2, 2, 3, 3>(a, s);
-      if (t15) return launch_fwd6_t<256, 128, 2, 2, 1, 5>(a, s);
+      if (t33) return launch_fwd6_t<256, 128, 2, 2, 3, 3, 0, F16>(a, s);
+      if (t15) return launch_fwd6_t<256, 128, 2, 2, 1, 5, 0, F16>(a, s);
       return false;
     case 59:
-      if (t33) return launch_fwd6_t<256, 64, 4, 1, 3, 3, 64>(a, s);
-      return t15 && launch_fwd6_t<256, 64, 4, 1, 1, 5, 64>(a, s);
+      if (t33) return launch_fwd6_t<256, 64, 4, 1, 3, 3, 64, F16>(a, s);
+      return t15 && launch_fwd6_t<256, 64, 4, 1, 1, 5, 64, F16>(a, s);
     case 60:
-      return t51 && launch_fwd6_t<256, 64, 4, 1, 5, 1, 32>(a, s);
+      return t51 && launch_fwd6_t<256, 64, 4, 1, 5, 1, 32, F16>(a, s);
     default:
       return false;
   }
 }
 }  // namespace
 
-hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
+template <bool F16>
+hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
   if (a.P == 0 || a.N == 0) return hipSuccess;
   if (a.Kpad % FBK != 0) return hipErrorInvalidValue;
   const int cfg = a.cfg;
@@ -2127,7 +2131,7 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   const bool dma_ok = (uniform || a.nsrc == 1) && maxbytes < (1L << 31) && (long)a.N * a.Kpad * 2 < (1L << 31);
   if (!dma_ok || cfg == 1) {
     if (a.P >= (1L << 31)) return hipErrorInvalidValue;  // 32-bit tile rows in the shared epilogue
-    hipLaunchKernelGGL((conv_fwd_kernel<64, 64>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<64, 64, F16>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
     return hipGetLastError();
   }
   // v5 (halo strip): multi-tap convs whose 64-channel chunks never straddle a source segment.
@@ -2140,7 +2144,7 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   if (cfg == 41 || cfg == 45 || cfg == 59 || cfg == 60) {  // v6 tiles (tests / microbenchmarks)
     const bool shape6 = (a.KH == 3 && a.KW == 3) || (a.KH * a.KW == 5 && (a.KH == 1 || a.KW == 1));
     if (!ok5 || !shape6 || a.PH != a.KH / 2 || a.PW != a.KW / 2) return hipErrorInvalidValue;
-    return launch_conv_fwd6(a, cfg, s) ? hipGetLastError() : hipErrorInvalidValue;
+    return launch_conv_fwd6<F16>(a, cfg, s) ? hipGetLastError() : hipErrorInvalidValue;
   }
   if (ok5 && cfg == 0 && a.PH == a.KH / 2 && a.PW == a.KW / 2) {
     // v6 where it measured faster than v5 at config #2 (scripts/bench_conv6.py,
@@ -2157,7 +2161,7 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
     // v4 keeps 1080p's 32k pixels: 29.5 vs 39.1 us).  The rule: choose_fwd6 (kernel_abi.h,
     // unit-tested on the host).
     const int v6 = choose_fwd6(a.KH, a.KW, a.N, a.B, a.H, a.W);
-    if (v6 && launch_conv_fwd6(a, v6, s)) return hipGetLastError();
+    if (v6 && launch_conv_fwd6<F16>(a, v6, s)) return hipGetLastError();
   }
   if (ok5 && v5 == 0 && cfg == 0) {
     // 8-wave tiles (two waves per SIMD, no register spills) for every shape they win on
@@ -2191,24 +2195,24 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
       const dim3 grid(tiles(bm_of(v5), bn_of(v5)));
       switch (v5) {
         case 20:
-          set_lds_limit((const void*)conv_fwd5_kernel<64, 128>, (int)lds);
-          hipLaunchKernelGGL((conv_fwd5_kernel<64, 128>), grid, dim3(256), lds, s, a, rows);
+          set_lds_limit((const void*)conv_fwd5_kernel<64, 128, 4, F16>, (int)lds);
+          hipLaunchKernelGGL((conv_fwd5_kernel<64, 128, 4, F16>), grid, dim3(256), lds, s, a, rows);
           break;
         case 24:
-          set_lds_limit((const void*)conv_fwd5_kernel<256, 128, 8>, (int)lds);
-          hipLaunchKernelGGL((conv_fwd5_kernel<256, 128, 8>), grid, dim3(512), lds, s, a, rows);
+          set_lds_limit((const void*)conv_fwd5_kernel<256, 128, 8, F16>, (int)lds);
+          hipLaunchKernelGGL((conv_fwd5_kernel<256, 128, 8, F16>), grid, dim3(512), lds, s, a, rows);
           break;
         case 25:
-          set_lds_limit((const void*)conv_fwd5_kernel<128, 128, 8>, (int)lds);
-          hipLaunchKernelGGL((conv_fwd5_kernel<128, 128, 8>), grid, dim3(512), lds, s, a, rows);
+          set_lds_limit((const void*)conv_fwd5_kernel<128, 128, 8, F16>, (int)lds);
+          hipLaunchKernelGGL((conv_fwd5_kernel<128, 128, 8, F16>), grid, dim3(512), lds, s, a, rows);
           break;
         case 26:
-          set_lds_limit((const void*)conv_fwd5_kernel<128, 256, 8>, (int)lds);
-          hipLaunchKernelGGL((conv_fwd5_kernel<128, 256, 8>), grid, dim3(512), lds, s, a, rows);
+          set_lds_limit((const void*)conv_fwd5_kernel<128, 256, 8, F16>, (int)lds);
+          hipLaunchKernelGGL((conv_fwd5_kernel<128, 256, 8, F16>), grid, dim3(512), lds, s, a, rows);
           break;
         default:
-          set_lds_limit((const void*)conv_fwd5_kernel<128, 128>, (int)lds);
-          hipLaunchKernelGGL((conv_fwd5_kernel<128, 128>), grid, dim3(256), lds, s, a, rows);
+          set_lds_limit((const void*)conv_fwd5_kernel<128, 128, 4, F16>, (int)lds);
+          hipLaunchKernelGGL((conv_fwd5_kernel<128, 128, 4, F16>), grid, dim3(256), lds, s, a, rows);
       }
       return hipGetLastError();
     }
@@ -2218,9 +2222,32 @@ hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
   // workgroup per CU) measured 21-30% slower on every 1x1 shape (profiles/r3_conv_1x1_tiles.log)
   const bool wide = cfg == 8 || (cfg != 9 && a.N > 64);
   if (wide)
-    hipLaunchKernelGGL((conv_fwd4_kernel<64, 128, 3>), dim3(tiles(64, 128)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_fwd4_kernel<64, 128, 3, F16>), dim3(tiles(64, 128)), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((conv_fwd4_kernel<64, 64, 4>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv_fwd4_kernel<64, 64, 4, F16>), dim3(tiles(64, 64)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
+  return a.f16 ? conv_fwd_dispatch<true>(a, s) : conv_fwd_dispatch<false>(a, s);
+}
+
+template <bool F16>
+hipError_t conv_wgrad_dispatch(const ConvWgradArgs& a, const WgradPlan& pl, hipStream_t s) {
+  const dim3 grid((unsigned)((long)pl.tilesM * pl.tilesN * pl.nsplit));
+  if (pl.kind == 3) {
+    if (a.KH == 3)
+      hipLaunchKernelGGL((conv_wgrad3_kernel<3, 3, 8, 8, 1, 3, F16>), grid, dim3(256), 0, s, a);
+    else if (a.KH == 5)
+      hipLaunchKernelGGL((conv_wgrad3_kernel<5, 1, 16, 4, 1, 3, F16>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_wgrad3_kernel<1, 5, 1, 64, 1, 3, F16>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
+  if (pl.BM == 128)
+    hipLaunchKernelGGL((conv_wgrad2_kernel<128, 128, 3, F16>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_wgrad2_kernel<64, 128, 3, F16>), grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -2230,21 +2257,7 @@ hipError_t launch_conv_wgrad(ConvWgradArgs a, const WgradPlan& pl, hipStream_t s
   a.pix_per_split = pl.pix_per_split;
   a.xcd_g = pl.xcd_g;
   a.Npad = pl.Npad;
-  const dim3 grid((unsigned)((long)pl.tilesM * pl.tilesN * pl.nsplit));
-  if (pl.kind == 3) {
-    if (a.KH == 3)
-      hipLaunchKernelGGL((conv_wgrad3_kernel<3, 3, 8, 8, 1, 3>), grid, dim3(256), 0, s, a);
-    else if (a.KH == 5)
-      hipLaunchKernelGGL((conv_wgrad3_kernel<5, 1, 16, 4, 1, 3>), grid, dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((conv_wgrad3_kernel<1, 5, 1, 64, 1, 3>), grid, dim3(256), 0, s, a);
-    return hipGetLastError();
-  }
-  if (pl.BM == 128)
-    hipLaunchKernelGGL((conv_wgrad2_kernel<128, 128, 3>), grid, dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((conv_wgrad2_kernel<64, 128, 3>), grid, dim3(256), 0, s, a);
-  return hipGetLastError();
+  return a.f16 ? conv_wgrad_dispatch<true>(a, pl, s) : conv_wgrad_dispatch<false>(a, pl, s);
 }
 
 }  // namespace raft_amd

@@ -317,7 +317,7 @@ __global__ __launch_bounds__(256) void convex_up_gather_kernel(const float* __re
 __global__ __launch_bounds__(256) void convex_up_gather_rows_kernel(const float* __restrict__ part,
                                                                     __bf16* __restrict__ rows, int ld,
                                                                     float* __restrict__ dflow, int B, int H,
-                                                                    int W) {
+                                                                    int W, int f16) {
   const long HW = (long)H * W;
   const long p = (long)blockIdx.x * 256 + threadIdx.x;
   if (p >= (long)B * HW) return;
@@ -335,9 +335,9 @@ __global__ __launch_bounds__(256) void convex_up_gather_rows_kernel(const float*
     }
   }
   __bf16* r = rows + p * ld;
-  r[0] = static_cast<__bf16>(s0);
-  r[1] = static_cast<__bf16>(s1);
-  for (int c = 2; c < ld; ++c) r[c] = static_cast<__bf16>(0.f);
+  r[0] = st16(s0, f16 != 0);
+  r[1] = st16(s1, f16 != 0);
+  for (int c = 2; c < ld; ++c) r[c] = st16(0.f, false);
   if (dflow) {
     dflow[(long)b * 2 * HW + y * W + x] = s0;
     dflow[(long)b * 2 * HW + HW + y * W + x] = s1;
@@ -420,7 +420,7 @@ hipError_t launch_convex_up_bwd(const float* flow, const void* mask, int m_dtype
   RAFT_HIP_CHECK(hipGetLastError());
   if (rows) {
     hipLaunchKernelGGL(convex_up_gather_rows_kernel, dim3((npix + 255) / 256), blk, 0, s, part,
-                       static_cast<__bf16*>(rows), rows_ld, dflow, B, H, W);
+                       static_cast<__bf16*>(rows), rows_ld, dflow, B, H, W, m_dtype == kF16 ? 1 : 0);
     return hipGetLastError();
   }
   const long tot = (long)B * 2 * H * W;

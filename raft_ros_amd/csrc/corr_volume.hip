@@ -554,6 +554,7 @@ struct FlowPack {
   __bf16* flow8;
   __bf16* motion;
   long smo;
+  int f16;  // 16-bit storage is fp16 (fp16 AMP)
 };
 
 // RC > 0: the radius as a compile-time constant (RAFT's r = 4): the window index math divides by
@@ -576,7 +577,7 @@ __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const floa
   if (fp.flow8 && live && lane < 8) {
     const int py = p / W;
     const float u = cx0 - (float)(p - py * W), v = cy0 - (float)py;
-    const __bf16 f = static_cast<__bf16>(lane == 0 ? u : (lane == 1 ? v : 0.f));
+    const __bf16 f = st16(lane == 0 ? u : (lane == 1 ? v : 0.f), fp.f16 != 0);
     fp.flow8[pix * 8 + lane] = f;
     if (fp.motion && lane < 2) fp.motion[pix * fp.smo + lane] = f;
   }
@@ -868,7 +869,7 @@ hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int 
 
 hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void* out, int out_dtype, int B, int H,
                                   int W, int r, int out_ch, hipStream_t s, void* flow8, void* motion, long smo) {
-  const FlowPack fp{static_cast<__bf16*>(flow8), static_cast<__bf16*>(motion), smo};
+  const FlowPack fp{static_cast<__bf16*>(flow8), static_cast<__bf16*>(motion), smo, out_dtype == kF16 ? 1 : 0};
   const long npix = (long)B * H * W;
   if (npix == 0) return hipSuccess;
   if (r > 6) return hipErrorInvalidValue;

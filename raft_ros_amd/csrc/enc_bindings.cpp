@@ -31,9 +31,12 @@ void check(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, what, ": ", hipGetErrorString(e));
 }
 
+// activations are bf16, or fp16 under fp16 AMP (EncConvArgs::f16)
+bool is16(const at::Tensor& t) { return t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf; }
+
 void check_nhwc(const at::Tensor& t, const char* name) {
-  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4 && t.is_contiguous(), name,
-              ": expected a contiguous [B, H, W, C] bf16 CUDA tensor");
+  TORCH_CHECK(t.is_cuda() && is16(t) && t.dim() == 4 && t.is_contiguous(), name,
+              ": expected a contiguous [B, H, W, C] bf16 / fp16 CUDA tensor");
   TORCH_CHECK(t.size(3) % 8 == 0, name, ": channels must be a multiple of 8");
   TORCH_CHECK(t.numel() < (1L << 31), name, ": too large");
 }
@@ -140,9 +143,11 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
   TORCH_CHECK(Cin <= (split ? Cx / 3 : Cx), "weight has more input channels than x");
   TORCH_CHECK(!split || Cx % 3 == 0, "split x must hold three planes");
   TORCH_CHECK(N % 8 == 0 && N <= 1024, "out channels");
+  TORCH_CHECK(!split || x.scalar_type() == at::kBFloat16, "split planes are bf16");
   const int Ho = (H + 2 * (int)pad - KH) / (int)stride + 1, Wo = (W + 2 * (int)pad - KW) / (int)stride + 1;
   EncConvArgs a;
   init_args(a);
+  a.f16 = x.scalar_type() == at::kHalf ? 1 : 0;
   a.src[0] = {cbf(x), Cx, Cx, H, W, (int)stride};
   a.B = B;
   a.N = N;
@@ -212,8 +217,11 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
   init_args(a);
   a.B = B;
   a.N = Cin;
+  a.f16 = dys[0].scalar_type() == at::kHalf ? 1 : 0;
+  TORCH_CHECK(!split || !a.f16, "split planes are bf16");
   for (int j = 0; j < nconv; ++j) {
     check_nhwc(dys[j], "dy");
+    TORCH_CHECK(dys[j].scalar_type() == dys[0].scalar_type(), "dgrad: dys share one dtype");
     check_w(ws[j], "w");
     TORCH_CHECK(dys[j].size(0) == B && ws[j].size(1) == Cin && dys[j].size(3) == (split ? 3 : 1) * ws[j].size(0),
                 "dgrad shapes");
@@ -270,13 +278,13 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
   a.split_w = split ? (int)ws[0].size(0) : 0;
   if (res.has_value() && res->defined()) {
     check_nhwc(*res, "res");
-    TORCH_CHECK(res->sizes() == dx.sizes(), "res shape");
+    TORCH_CHECK(res->sizes() == dx.sizes() && res->scalar_type() == dx.scalar_type(), "res shape / dtype");
     a.res = cbf(*res);
     a.res_stride = rs;
   }
   if (mask.has_value() && mask->defined()) {
     check_nhwc(*mask, "mask");
-    TORCH_CHECK(mask->sizes() == dx.sizes(), "mask shape");
+    TORCH_CHECK(mask->sizes() == dx.sizes() && mask->scalar_type() == dx.scalar_type(), "mask shape / dtype");
     a.mask = cbf(*mask);
     a.mask_stride = rs;
   }
@@ -289,8 +297,8 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
 // x and dy may be channel slices of NHWC rows (a split tensor's [hi | lo] or hi planes):
 // unit channel stride, pixel pitch stride(2), rows of one image contiguous in pitch.
 void check_rows(const at::Tensor& t, const char* name) {
-  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4 && t.stride(3) == 1, name,
-              ": expected [B, H, W, C] bf16 rows with unit channel stride");
+  TORCH_CHECK(t.is_cuda() && is16(t) && t.dim() == 4 && t.stride(3) == 1, name,
+              ": expected [B, H, W, C] bf16 / fp16 rows with unit channel stride");
   TORCH_CHECK(t.size(3) % 8 == 0 && t.stride(2) % 8 == 0 && t.stride(2) >= t.size(3) &&
                   t.stride(1) == t.size(2) * t.stride(2) && t.stride(0) == t.size(1) * t.stride(1) &&
                   reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
@@ -303,6 +311,8 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
   check_rows(x, "x");
   check_rows(dy, "dy");
   const int xpitch = (int)x.stride(2), dypitch = (int)dy.stride(2);
+  TORCH_CHECK(x.scalar_type() == dy.scalar_type(), "wgrad: x and dy share one dtype");
+  const int f16 = x.scalar_type() == at::kHalf ? 1 : 0;
   TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == at::kFloat && dw.dim() == 4, "dw: fp32 4-D");
   const int B = (int)x.size(0), Hx = (int)x.size(1), Wx = (int)x.size(2), Cx = (int)x.size(3);
   const int N = (int)dw.size(0), Cin = (int)dw.size(1), KH = (int)dw.size(2), KW = (int)dw.size(3);
@@ -337,6 +347,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
     w.dy_stride = dypitch;
     w.N = N;
     w.P = (long)B * Hx * Wx;
+    w.f16 = f16;
     if (wgrad_supported(w)) {
       const WgradPlan pl = plan_conv_wgrad(w);
       const bool with_b = want_db && !db_zero;
@@ -379,6 +390,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
   a.dy = cbf(dy);
   a.dy_stride = dypitch;
   a.N = N;
+  a.f16 = f16;
   const int BM = (N % 128 == 0) ? 128 : 64;
   a.tilesM = (N + BM - 1) / BM;
   a.Npad = a.tilesM * BM;
@@ -412,7 +424,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
 }
 
 // [img0; img1] (fp32 0..255, [B,3,H,W] any strides) -> [nimg, H, W, 8] bf16 in [-1, 1]
-at::Tensor enc_prep(const at::Tensor& img0, const c10::optional<at::Tensor>& img1, bool split) {
+at::Tensor enc_prep(const at::Tensor& img0, const c10::optional<at::Tensor>& img1, bool split, bool f16) {
   TORCH_CHECK(img0.is_cuda() && img0.scalar_type() == at::kFloat && img0.dim() == 4 && img0.size(1) == 3,
               "images: fp32 [B, 3, H, W]");
   const int B = (int)img0.size(0), H = (int)img0.size(2), W = (int)img0.size(3);
@@ -423,10 +435,11 @@ at::Tensor enc_prep(const at::Tensor& img0, const c10::optional<at::Tensor>& img
                 "paired images must match");
     nimg = 2 * B;
   }
-  at::Tensor out = at::empty({nimg, H, W, split ? 24 : 8}, img0.options().dtype(at::kBFloat16));
+  TORCH_CHECK(!(split && f16), "enc_prep: split planes are bf16");
+  at::Tensor out = at::empty({nimg, H, W, split ? 24 : 8}, img0.options().dtype(f16 ? at::kHalf : at::kBFloat16));
   long st[4] = {img0.stride(0), img0.stride(1), img0.stride(2), img0.stride(3)};
   check(launch_enc_prep(img0.data_ptr<float>(), nimg > B ? img1->data_ptr<float>() : nullptr, st, B, H, W, nimg,
-                        out.data_ptr(), split ? 1 : 0, stream()),
+                        out.data_ptr(), (split ? 1 : 0) | (f16 ? 2 : 0), stream()),
         "enc_prep");
   return out;
 }
@@ -505,8 +518,9 @@ at::Tensor enc_apply(const at::Tensor& x, const at::Tensor& coef, bool relu_a, c
     }
   }
   at::Tensor out = at::empty_like(x);
+  if (r.has_value() && r->defined()) TORCH_CHECK(r->scalar_type() == x.scalar_type(), "residual dtype");
   check(launch_enc_apply(x.data_ptr(), coef.data_ptr<float>(), relu_a, rp, crp, relu_out, out.data_ptr(), B, HW, N,
-                         split ? 1 : 0, stream()),
+                         (split ? 1 : 0) | (x.scalar_type() == at::kHalf ? 2 : 0), stream()),
         "enc_apply");
   return out;
 }
@@ -545,6 +559,8 @@ std::vector<at::Tensor> enc_norm_bwd_impl(const at::Tensor& g, const at::Tensor&
   a.R = std::min(kNormChunks, std::max(1, HW / 256));
   a.kind = (int)kind;
   a.split = split ? 1 : 0;
+  a.f16 = g.scalar_type() == at::kHalf ? 1 : 0;
+  TORCH_CHECK(a0.scalar_type() == g.scalar_type(), "norm backward: g and a0 share one dtype");
   auto fo = g.options().dtype(at::kFloat);
   const long bf = stage == 2 ? (long)b_fin : (long)B;
   TORCH_CHECK(stage != 2 || (kind == 2 && bf >= B && part_in.has_value() && part_in->defined() &&
@@ -607,7 +623,7 @@ TORCH_LIBRARY_FRAGMENT(raft_amd, m) {
       "bool split=False) -> Tensor");
   m.def("enc_conv_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, Tensor(b!)? db, int stride, int pad, bool accumulate, "
         "bool db_zero=False) -> ()");
-  m.def("enc_prep(Tensor img0, Tensor? img1, bool split=False) -> Tensor");
+  m.def("enc_prep(Tensor img0, Tensor? img1, bool split=False, bool f16=False) -> Tensor");
   m.def(
       "enc_norm_stats(Tensor? stats, int B, int HW, int N, int kind, Tensor? gamma, Tensor? beta, Tensor(a!)? rmean, "
       "Tensor(b!)? rvar, Tensor(c!)? nbt, float momentum, float eps, int W=0) -> Tensor");

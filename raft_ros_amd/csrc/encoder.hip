@@ -45,15 +45,16 @@ namespace {
 
 constexpr int EBK = 64, ELDK = EBK + 8;
 
-__device__ __forceinline__ void load8(const __bf16* p, float* v) {
+// 8 channels of 16-bit storage: bf16, or fp16 under fp16 AMP (common.h st16 / ld16)
+__device__ __forceinline__ void load8(const __bf16* p, float* v, bool f16 = false) {
   const bf16x8 x = *reinterpret_cast<const bf16x8*>(p);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = static_cast<float>(x[i]);
+  for (int i = 0; i < 8; ++i) v[i] = ld16(x[i], f16);
 }
-__device__ __forceinline__ void store8(__bf16* p, const float* v) {
+__device__ __forceinline__ void store8(__bf16* p, const float* v, bool f16 = false) {
   bf16x8 x;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) x[i] = static_cast<__bf16>(v[i]);
+  for (int i = 0; i < 8; ++i) x[i] = st16(v[i], f16);
   *reinterpret_cast<bf16x8*>(p) = x;
 }
 // split-bf16 planes (kernel_abi.h EncConvArgs::split): hi at p, lo at p + S, hi again at p + 2S
@@ -119,7 +120,7 @@ struct EncCfg {
   static_assert(ACH * 256 * 8 == BM * EBK && BCH * 256 * 8 == BN * EBK, "staging shape");
 };
 
-template <int BM, int BN, int WM, int WN, int NSRC>
+template <int BM, int BN, int WM, int WN, int NSRC, bool F16 = false>
 __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
   using C = EncCfg<BM, BN, WM, WN>;
   constexpr int TM = C::TM, TN = C::TN, ACH = C::ACH, BCH = C::BCH, STAGE = C::STAGE;
@@ -269,7 +270,7 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mma16<F16>(af[i], bfr[j], acc[i][j]);
     }
   };
   // step t computes LDS buffer t&1; registers: set t&1 receives step t+2, set (t+1)&1 holds
@@ -368,20 +369,20 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
     if (a.res) {
       float r[8];
       if (a.split) load8_split(a.res + pix * a.res_stride + n, a.N, r);
-      else load8(a.res + pix * a.res_stride + n, r);
+      else load8(a.res + pix * a.res_stride + n, r, F16);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += r[e];
     }
     if (a.mask) {
       float m[8];
-      load8(a.mask + pix * a.mask_stride + n, m);
+      load8(a.mask + pix * a.mask_stride + n, m, F16);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = m[e] > 0.f ? v[e] : 0.f;
     }
     if (a.split)
       store8_split(a.out + pix * a.out_stride + n, a.N, v);
     else
-      store8(a.out + pix * a.out_stride + n, v);
+      store8(a.out + pix * a.out_stride + n, v, F16);
   }
 }
 
@@ -424,7 +425,7 @@ __global__ __launch_bounds__(256) void enc_pack_kernel(const EncConvArgs a, __bf
         v = wp[row * s0 + loc * s1 + ky * s2 + kx * s3];
       }
     }
-    out[cl.wofs + (long)row * cl.Kpad + k] = static_cast<__bf16>(v);
+    out[cl.wofs + (long)row * cl.Kpad + k] = st16(v, a.f16 != 0);
   }
 }
 
@@ -443,7 +444,7 @@ __device__ __forceinline__ int wswz(int row, int chunk) {
   return COLS == 128 ? (chunk ^ ((row & 3) << 2)) : (chunk ^ (((row >> 1) & 1) << 2));
 }
 
-template <int BM, int BN>
+template <int BM, int BN, bool F16 = false>
 __global__ __launch_bounds__(256) void enc_wgrad_kernel(const EncWgradArgs a) {
   // 2x2 waves of (BM/2) x (BN/2): TM x TN MFMA 32x32x16 tiles per wave
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -533,7 +534,7 @@ __global__ __launch_bounds__(256) void enc_wgrad_kernel(const EncWgradArgs a) {
       if (do_db) {
         const bf16x8 v = __builtin_bit_cast(bf16x8, ra[i]);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) dbacc[e] += static_cast<float>(v[e]);
+        for (int e = 0; e < 8; ++e) dbacc[e] += ld16(v[e], F16);
       }
     }
 #pragma unroll
@@ -583,7 +584,7 @@ __global__ __launch_bounds__(256) void enc_wgrad_kernel(const EncWgradArgs a) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mma16<F16>(af[i], bfr[j], acc[i][j]);
     }
     if (t + 1 < nsteps) store((t + 1) & 1);
     __syncthreads();
@@ -690,10 +691,10 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const float* __restrict__
   for (int c = 0; c < 3; ++c) v[c] = 2.f * (src[o + c * sc] / 255.f) - 1.f;
 #pragma unroll
   for (int c = 3; c < 8; ++c) v[c] = 0.f;
-  if (split)
+  if (split & 1)
     store8_split(out + p * 24, 8, v);
   else
-    store8(out + p * 8, v);
+    store8(out + p * 8, v, (split & 2) != 0);
 }
 
 // ============================================================================ norms
@@ -798,6 +799,8 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
                                                         const float* __restrict__ cr, int relu_out,
                                                         __bf16* __restrict__ out, int B, int HW, int N, int split) {
   const int G = N / 8;
+  const bool f16 = (split & 2) != 0;
+  split &= 1;
   const int rs = split ? 3 * N : N;  // row stride: split rows hold hi / lo / hi planes
   const PixWalk w = pix_walk(G);
   if (w.p < 0) return;
@@ -819,7 +822,7 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
     if (split)
       load8_split(a + (long)p * rs + n, N, v);
     else
-      load8(a + (long)p * N + n, v);
+      load8(a + (long)p * N + n, v, f16);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       v[e] = v[e] * s[e] + t[e];
@@ -830,7 +833,7 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
       if (split)
         load8_split(r + (long)p * rs + n, N, rv);
       else
-        load8(r + (long)p * N + n, rv);
+        load8(r + (long)p * N + n, rv, f16);
       if (cr)
 #pragma unroll
         for (int e = 0; e < 8; ++e) rv[e] = rv[e] * s2[e] + t2[e];
@@ -843,7 +846,7 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
     if (split)
       store8_split(out + (long)p * rs + n, N, v);
     else
-      store8(out + (long)p * N + n, v);
+      store8(out + (long)p * N + n, v, f16);
   }
 }
 
@@ -865,7 +868,7 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_reduce_kernel(const NormBwdA
   const int pb = r * chunk, pe = min(a.HW, pb + chunk);
   auto ld8 = [&](const __bf16* q, float* v) __attribute__((always_inline)) {
     if (a.split) load8_split(q, N, v);
-    else load8(q, v);
+    else load8(q, v, a.f16 != 0);
   };
   float S[4][8];
 #pragma unroll
@@ -995,11 +998,11 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_apply_kernel(const NormBwdAr
   const long rp = a.split ? 3L * N : N;  // row pitch (split rows: hi / lo / hi planes of N)
   auto ld8 = [&](const __bf16* q, float* v) __attribute__((always_inline)) {
     if (a.split) load8_split(q, N, v);
-    else load8(q, v);
+    else load8(q, v, a.f16 != 0);
   };
   auto st8 = [&](__bf16* q, const float* v) __attribute__((always_inline)) {
     if (a.split) store8_split(q, N, v);
-    else store8(q, v);
+    else store8(q, v, a.f16 != 0);
   };
   int bend = 0;
   float k1[8], k2[8], k3[8], rs[8], mu[8], sc[8], sh[8];
@@ -1107,6 +1110,7 @@ __device__ __forceinline__ void c3_dma16(__amdgpu_buffer_rsrc_t r, unsigned lds_
 
 __device__ __forceinline__ bf16x8 c3_read16(unsigned lds_byte) { return *(const c3_lds_bf16x8*)(uintptr_t)lds_byte; }
 
+template <bool F16 = false>
 __global__ __launch_bounds__(512) void enc_conv3_kernel(const EncConvArgs a, int ntiles, int tiles_x,
                                                         int tiles_img) {
   extern __shared__ __attribute__((aligned(1024))) char c3smem[];
@@ -1186,8 +1190,8 @@ __global__ __launch_bounds__(512) void enc_conv3_kernel(const EncConvArgs a, int
         const bf16x8 fa = c3_read16(abase + (unsigned)(((s2 * 2 + lh) ^ sw) << 4));
         const bf16x8 fb0 = c3_read16(wrow + t * 128 + bsw[s2]);
         const bf16x8 fb1 = c3_read16(wrow + 32 * 1152 + t * 128 + bsw[s2]);
-        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb0, acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb1, acc[1], 0, 0, 0);
+        acc[0] = mma16<F16>(fa, fb0, acc[0]);
+        acc[1] = mma16<F16>(fa, fb1, acc[1]);
       }
     }
 
@@ -1209,7 +1213,7 @@ __global__ __launch_bounds__(512) void enc_conv3_kernel(const EncConvArgs a, int
         const bool valid = (i >> 4) < vh && (i & 15) < vw;
         sm += valid ? v : 0.f;
         sq += valid ? v * v : 0.f;
-        stg[i * C3_SP + n0 + 32 * j] = static_cast<__bf16>(v);
+        stg[i * C3_SP + n0 + 32 * j] = st16(v, F16);
       }
       if (a.stats) {
         sm += __shfl_xor(sm, 32, 64);
@@ -1242,20 +1246,20 @@ __global__ __launch_bounds__(512) void enc_conv3_kernel(const EncConvArgs a, int
       const bf16x8 sv = *reinterpret_cast<const bf16x8*>(stg + i * C3_SP + c8);
       float v[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = static_cast<float>(sv[e]);
+      for (int e = 0; e < 8; ++e) v[e] = ld16(sv[e], F16);
       if (a.res) {
         float r8[8];
-        load8(a.res + pix * a.res_stride + c8, r8);
+        load8(a.res + pix * a.res_stride + c8, r8, F16);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += r8[e];
       }
       if (a.mask) {
         float m8[8];
-        load8(a.mask + pix * a.mask_stride + c8, m8);
+        load8(a.mask + pix * a.mask_stride + c8, m8, F16);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = m8[e] > 0.f ? v[e] : 0.f;
       }
-      store8(a.out + pix * a.out_stride + c8, v);
+      store8(a.out + pix * a.out_stride + c8, v, F16);
     }
   }
 }
@@ -1276,20 +1280,20 @@ hipError_t launch_enc_pack(const EncConvArgs& a, int rows, void* out, hipStream_
   return hipGetLastError();
 }
 
-template <int NSRC>
+template <int NSRC, bool F16>
 void launch_enc_conv_n(const EncConvArgs& a, int nblocks, hipStream_t s) {
   switch (enc_tile_bn(a.N)) {
     case 128:
-      hipLaunchKernelGGL((enc_conv_kernel<128, 128, 2, 2, NSRC>), dim3(nblocks), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((enc_conv_kernel<128, 128, 2, 2, NSRC, F16>), dim3(nblocks), dim3(256), 0, s, a);
       break;
     case 96:
-      hipLaunchKernelGGL((enc_conv_kernel<128, 96, 4, 1, NSRC>), dim3(nblocks), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((enc_conv_kernel<128, 96, 4, 1, NSRC, F16>), dim3(nblocks), dim3(256), 0, s, a);
       break;
     case 64:
-      hipLaunchKernelGGL((enc_conv_kernel<128, 64, 2, 2, NSRC>), dim3(nblocks), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((enc_conv_kernel<128, 64, 2, 2, NSRC, F16>), dim3(nblocks), dim3(256), 0, s, a);
       break;
     default:
-      hipLaunchKernelGGL((enc_conv_kernel<128, 32, 4, 1, NSRC>), dim3(nblocks), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((enc_conv_kernel<128, 32, 4, 1, NSRC, F16>), dim3(nblocks), dim3(256), 0, s, a);
       break;
   }
 }
@@ -1304,35 +1308,44 @@ hipError_t launch_enc_conv3(const EncConvArgs& a, hipStream_t s) {
       num_cu = 256;
   }
   if (!lds_set) {
-    (void)hipFuncSetAttribute((const void*)enc_conv3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, C3_LDS);
+    (void)hipFuncSetAttribute((const void*)enc_conv3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, C3_LDS);
+    (void)hipFuncSetAttribute((const void*)enc_conv3_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, C3_LDS);
     lds_set = true;
   }
   const int tiles_x = (a.Wo + C3_T - 1) / C3_T, tiles_img = tiles_x * ((a.Ho + C3_T - 1) / C3_T);
   const int ntiles = a.B * tiles_img;
   if (ntiles == 0) return hipSuccess;
   const int grid = std::min(ntiles, num_cu);
-  hipLaunchKernelGGL(enc_conv3_kernel, dim3(grid), dim3(512), C3_LDS, s, a, ntiles, tiles_x, tiles_img);
+  if (a.f16)
+    hipLaunchKernelGGL(enc_conv3_kernel<true>, dim3(grid), dim3(512), C3_LDS, s, a, ntiles, tiles_x, tiles_img);
+  else
+    hipLaunchKernelGGL(enc_conv3_kernel<false>, dim3(grid), dim3(512), C3_LDS, s, a, ntiles, tiles_x, tiles_img);
   return hipGetLastError();
 }
 
 hipError_t launch_enc_conv(const EncConvArgs& a, int nblocks, hipStream_t s) {
   if (a.src[1].ptr != nullptr)
-    launch_enc_conv_n<2>(a, nblocks, s);
+    a.f16 ? launch_enc_conv_n<2, true>(a, nblocks, s) : launch_enc_conv_n<2, false>(a, nblocks, s);
   else
-    launch_enc_conv_n<1>(a, nblocks, s);
+    a.f16 ? launch_enc_conv_n<1, true>(a, nblocks, s) : launch_enc_conv_n<1, false>(a, nblocks, s);
   return hipGetLastError();
 }
 
 hipError_t launch_enc_wgrad(const EncWgradArgs& a, int BM, int BN, hipStream_t s) {
   const int nwg = a.nsplit * a.tilesM * a.tilesN;
-  if (BM == 128 && BN == 128)
-    hipLaunchKernelGGL((enc_wgrad_kernel<128, 128>), dim3(nwg), dim3(256), 0, s, a);
-  else if (BM == 128)
-    hipLaunchKernelGGL((enc_wgrad_kernel<128, 64>), dim3(nwg), dim3(256), 0, s, a);
-  else if (BN == 128)
-    hipLaunchKernelGGL((enc_wgrad_kernel<64, 128>), dim3(nwg), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((enc_wgrad_kernel<64, 64>), dim3(nwg), dim3(256), 0, s, a);
+  auto go = [&](auto f16c) {
+    constexpr bool F = decltype(f16c)::value;
+    if (BM == 128 && BN == 128)
+      hipLaunchKernelGGL((enc_wgrad_kernel<128, 128, F>), dim3(nwg), dim3(256), 0, s, a);
+    else if (BM == 128)
+      hipLaunchKernelGGL((enc_wgrad_kernel<128, 64, F>), dim3(nwg), dim3(256), 0, s, a);
+    else if (BN == 128)
+      hipLaunchKernelGGL((enc_wgrad_kernel<64, 128, F>), dim3(nwg), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((enc_wgrad_kernel<64, 64, F>), dim3(nwg), dim3(256), 0, s, a);
+  };
+  if (a.f16) go(std::true_type{});
+  else go(std::false_type{});
   return hipGetLastError();
 }
 

@@ -117,6 +117,10 @@ struct ConvFwdArgs {
   int split_g3;    // > 0: out3 is split with group width split_g3
   int split_add;   // > 0: addsrc is split (lo plane offset)
   int split_cout;  // > 0: cout is split with group width split_cout
+  // fp16 AMP (the reference's --mixed_precision dtype): every 16-bit operand, epilogue operand
+  // and 16-bit output is IEEE fp16 (v_mfma_f32_32x32x16_f16) instead of bf16; the pointers
+  // keep their __bf16 type as 16-bit storage
+  int f16;
 };
 
 struct ConvWgradArgs {
@@ -133,6 +137,7 @@ struct ConvWgradArgs {
   float* dbslab;  // [nsplit][tilesN][Npad] fp32 bias partials (may be null)
   int Npad;       // slab rows (N rounded up to the row tile)
   int xcd_g;      // >0: XCD-grouped split mapping with xcd_g splits per XCD (set by the launcher)
+  int f16;        // fp16 operands (see ConvFwdArgs::f16)
 };
 
 // Plan of one weight-gradient launch (the caller sizes the slabs from it).
@@ -159,6 +164,7 @@ struct ConvParamDesc {
   // [W_hi | W_hi | W_lo]; split_dy = G > 0 -> the data-gradient operand runs over dY planes
   // [hi | lo | hi] of width G (k = tapflip * 3G + plane * G + n) against [W_hi | W_hi | W_lo]
   int split_fw, split_dy;
+  int f16;  // pack: fp16 operands instead of bf16 (fp16 AMP)
 };
 
 // ============================================================================ encoder convs
@@ -214,6 +220,7 @@ struct EncConvArgs {
   // tables of more than kEncTab entries: device copies [kEncTabMax] (null: the arrays above)
   const int* tab_ptr;
   const int* ptab_ptr;
+  int f16;  // 16-bit activations / packed weights are fp16 (fp16 AMP) instead of bf16
   // split-bf16 output (fp32-faithful inference, see ConvFwdArgs::split_g): out rows hold
   // [hi | lo | hi] planes of N channels each (out_stride = 3N).  A split data gradient (fp32
   // training) also reads res as split rows (res_stride = 3N, lo plane at +N) and the ReLU'
@@ -233,6 +240,7 @@ struct EncWgradArgs {
   int pix_per_split, nsplit;
   float* slab;    // [nsplit][Npad][Kpad]
   float* dbslab;  // [nsplit][Npad] or null
+  int f16;        // fp16 operands (fp16 AMP)
 };
 
 struct NormFinArgs {
@@ -264,6 +272,7 @@ struct NormBwdArgs {
   __bf16* out0;
   __bf16* out1;
   int split;  // g, a0, a1, out0, out1 are split-bf16 rows of 3N (hi / lo / hi planes; fp32 training)
+  int f16;    // g, a0, a1, out0, out1 are fp16 (fp16 AMP)
 };
 
 // 3x3 / stride-1 encoder convs with 64 input and 64 output channels (both encoders' stage-1

@@ -82,16 +82,17 @@ __global__ __launch_bounds__(256) void pack_flow_kernel(const float* __restrict_
   const int b = p / HW;
   const int s = p - (long)b * HW;
   float u = flow[(long)b * 2 * HW + s], v = flow[(long)b * 2 * HW + HW + s];
-  if (from_coords) {
+  const bool f16 = (from_coords & 2) != 0;  // bit 1: fp16 storage (fp16 AMP)
+  if (from_coords & 1) {
     const int y = s / W;
     u -= (float)(s - y * W);
     v -= (float)y;
   }
   bf16x8 o;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) o[k] = static_cast<__bf16>(0.f);
-  o[0] = static_cast<__bf16>(u);
-  o[1] = static_cast<__bf16>(v);
+  for (int k = 0; k < 8; ++k) o[k] = st16(0.f, false);
+  o[0] = st16(u, f16);
+  o[1] = st16(v, f16);
   *reinterpret_cast<bf16x8*>(flow8 + p * 8) = o;
   if (motion) {
     motion[p * smo] = o[0];

@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void pack_conv_weights_kernel(ConvParamDesc d,
         const int c = real_channel(d, k - tap * d.Cin_pad);
         if (c >= 0) v = d.scale * param_at(d, n, c, tap / d.KW, tap - (tap / d.KW) * d.KW);
       }
-      wf[i] = static_cast<__bf16>(v);
+      wf[i] = st16(v, d.f16 != 0);
     } else if (i < nf + nd) {
       const long j = i - nf;
       const int cp = (int)(j / Kd), k = (int)(j - (long)cp * Kd);
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void pack_conv_weights_kernel(ConvParamDesc d,
         const int kyf = tapf / d.KW, kxf = tapf - kyf * d.KW;
         if (c >= 0) v = d.scale * param_at(d, n, c, d.KH - 1 - kyf, d.KW - 1 - kxf);
       }
-      wd[j] = static_cast<__bf16>(v);
+      wd[j] = st16(v, d.f16 != 0);
     } else {
       const int n = (int)(i - nf - nd);
       const int which = n < d.rows[0] ? 0 : 1;

@@ -155,9 +155,11 @@ class RAFT(nn.Module):
             main = torch.cuda.current_stream(raw1.device)
             side.wait_stream(main)
             split = not amp  # fp32: split-bf16 (fp32-faithful) encoder kernels
+            f16 = amp and self.amp_dtype == torch.float16  # fp16 AMP: fp16 MFMA kernels
             with torch.cuda.stream(side):
-                cnet_native = encoder_native.encode(self.cnet, raw1, join_stream=main, split=split)
-            fmap1, fmap2 = encoder_native.encode(self.fnet, raw1, raw2, split=split).split(raw1.shape[0], dim=0)
+                cnet_native = encoder_native.encode(self.cnet, raw1, join_stream=main, split=split, f16=f16)
+            fmap1, fmap2 = encoder_native.encode(self.fnet, raw1, raw2, split=split,
+                                                 f16=f16).split(raw1.shape[0], dim=0)
         else:
             with self._autocast(dev):
                 fmap1, fmap2 = self.fnet([image1, image2])
@@ -230,14 +232,15 @@ class RAFT(nn.Module):
         return aux_stream(device, "side")
 
     def _use_native_encoders(self, image1, amp: bool) -> bool:
-        """bf16 AMP, or fp32 (training and inference) on the split-bf16 kernels."""
-        mode_ok = (self.amp_dtype == torch.bfloat16) if amp else True
+        """bf16 / fp16 AMP, or fp32 (training and inference) on the split-bf16 kernels."""
+        mode_ok = True
         return (mode_ok and _arg(self.args, "native_encoder", True)
                 and encoder_native.supported(self.fnet, image1) and encoder_native.supported(self.cnet, image1))
 
     # ------------------------------------------------------------------ fused (HIP) update path
     def _use_fused(self, image1, amp: bool) -> bool:
-        return (amp and self.amp_dtype == torch.bfloat16 and _arg(self.args, "fused_update", True)
+        """bf16 or fp16 AMP on the fused HIP step (fp16: v_mfma_f32_32x32x16_f16, GradScaler)."""
+        return (amp and _arg(self.args, "fused_update", True)
                 and (update_fused.supported(self.update_block) or update_fused_small.supported(self.update_block))
                 and use_native(image1))
 
@@ -307,7 +310,9 @@ class RAFT(nn.Module):
         small = update_fused_small.supported(self.update_block)
         fused = update_fused_small.FusedSmallUpdate if small else update_fused.FusedBasicUpdate
         pad = update_fused_small.CORR_PAD if small else update_fused.CORR_PAD
-        kw = {} if small else {"token": wtoken}
+        kw = {"dt16": self.amp_dtype}
+        if not small:
+            kw["token"] = wtoken
         upd = fused(self.update_block, inp, iters, pyramid=corr_fn.state if dense else None, **kw)
         flow_predictions = []
         flow_up = None
@@ -317,11 +322,11 @@ class RAFT(nn.Module):
             up = not test_mode or t == iters - 1
             if dense:
                 net, flow_up, coords1 = upd.step(t, net, coords1, ptoken=corr_fn.token, upsample=up)
-            elif getattr(corr_fn, "mfma", False):  # features already in the fused layout
-                corr = corr_fn.lookup_padded(coords1.detach(), pad)
+            elif getattr(corr_fn, "mfma", False) and self.amp_dtype == torch.bfloat16:
+                corr = corr_fn.lookup_padded(coords1.detach(), pad)  # features already in the fused layout
                 net, flow_up, coords1 = upd.step(t, net, coords1, corr=corr, upsample=up)
             else:
-                c = corr_fn(coords1.detach(), out_dtype=torch.bfloat16).permute(0, 2, 3, 1)
+                c = corr_fn(coords1.detach(), out_dtype=self.amp_dtype).permute(0, 2, 3, 1)
                 corr = torch.nn.functional.pad(c, (0, pad - c.shape[-1]))
                 net, flow_up, coords1 = upd.step(t, net, coords1, corr=corr, upsample=up)
             flow_predictions.append(flow_up)

@@ -111,11 +111,12 @@ def register() -> None:
         return wf, wd, w[0].new_empty((n,))
 
     @fake(lib + "pack_conv_weights")
-    def _(w, b, segs, scale, Kf, Kd, cout_pad):
+    def _(w, b, segs, scale, Kf, Kd, cout_pad, f16=False):
         n = sum(t.shape[0] for t in w)
         cin_pad = sum(segs[1::2])
-        wf = w[0].new_empty((n, Kf), dtype=torch.bfloat16)
-        wd = w[0].new_empty((cin_pad, Kd), dtype=torch.bfloat16) if Kd > 0 else None
+        dt = torch.float16 if f16 else torch.bfloat16
+        wf = w[0].new_empty((n, Kf), dtype=dt)
+        wd = w[0].new_empty((cin_pad, Kd), dtype=dt) if Kd > 0 else None
         return wf, wd, w[0].new_empty((n,))
 
     @fake(lib + "enc_conv_fwd")
@@ -142,9 +143,10 @@ def register() -> None:
         return dys[0].new_empty((dys[0].shape[0], H, W, (3 if split else 1) * ws[0].shape[1]))
 
     @fake(lib + "enc_prep")
-    def _(img0, img1, split=False):
+    def _(img0, img1, split=False, f16=False):
         n = img0.shape[0] * (2 if img1 is not None else 1)
-        return img0.new_empty((n, img0.shape[2], img0.shape[3], 24 if split else 8), dtype=torch.bfloat16)
+        return img0.new_empty((n, img0.shape[2], img0.shape[3], 24 if split else 8),
+                              dtype=torch.float16 if f16 else torch.bfloat16)
 
     @fake(lib + "enc_norm_stats")
     def _(stats, B, HW, N, kind, gamma, beta, rmean, rvar, nbt, momentum, eps, W=0):

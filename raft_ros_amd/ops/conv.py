@@ -197,10 +197,10 @@ def split_segments_by_source(source_segments) -> List[Tuple[int, int]]:
     return out
 
 
-def pack_weights(weights, biases, segments, scale: float = 1.0, dgrad: bool = True):
+def pack_weights(weights, biases, segments, scale: float = 1.0, dgrad: bool = True, f16: bool = False):
     """One HIP launch: fp32 parameters (1..2 stacked along Cout) -> (wf [N][Kpad] bf16,
     wd [Cin_pad][Kpad'] bf16 or None, bias fp32 [N]) -- the layouts of ``pack_fwd`` /
-    ``pack_dgrad``."""
+    ``pack_dgrad``; ``f16``: fp16 operands (fp16 AMP) instead of bf16."""
     cout = sum(w.shape[0] for w in weights)
     _, cin, kh, kw = weights[0].shape
     cin_p = sum(p for _, p in segments)
@@ -209,4 +209,4 @@ def pack_weights(weights, biases, segments, scale: float = 1.0, dgrad: bool = Tr
     kd = _round(kh * kw * cout_p, KBLK) if dgrad else 0
     w = [t.detach() for t in weights]
     b = [None if t is None else t.detach() for t in biases]
-    return ops().pack_conv_weights(w, b, flat_segments(segments), scale, kf, kd, cout_p)
+    return ops().pack_conv_weights(w, b, flat_segments(segments), scale, kf, kd, cout_p, f16)

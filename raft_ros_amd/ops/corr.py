@@ -405,8 +405,10 @@ class LocalCorrPyramid:
     def __call__(self, coords: torch.Tensor, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
         if self.mfma:
             win = (2 * self.radius + 1) ** 2
-            out = self.lookup_padded(coords, self.num_levels * win, out_dtype or torch.float32)
-            return out.permute(0, 3, 1, 2)
+            dt = out_dtype or torch.float32
+            kdt = dt if dt in (torch.float32, torch.bfloat16) else torch.float32  # the kernel writes fp32 / bf16
+            out = self.lookup_padded(coords, self.num_levels * win, kdt)
+            return (out if kdt == dt else out.to(dt)).permute(0, 3, 1, 2)
         outs = []
         for i in range(self.num_levels):
             ci = coords / (2 ** i)

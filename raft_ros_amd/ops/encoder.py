@@ -289,6 +289,7 @@ class _EncoderFn(torch.autograd.Function):
         ctx.params = params
         ctx.join = join
         ctx.split = split
+        ctx.dt16 = x0.dtype  # bf16, or fp16 under fp16 AMP
         # records hold only tensors created here (activations, statistics coefficients)
         ctx.stem_rec, ctx.recs = stem_rec, recs
         if split:
@@ -298,7 +299,7 @@ class _EncoderFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
-        gy = _split_rows(gy) if ctx.split else gy.contiguous().to(torch.bfloat16)
+        gy = _split_rows(gy) if ctx.split else gy.contiguous().to(ctx.dt16)
         grads = _backward(ctx.layout, ctx.params, gy, ctx.stem_rec, ctx.recs, ctx.split)
         ctx.stem_rec = ctx.recs = None
         if ctx.join is not None:
@@ -330,14 +331,15 @@ def _layout(enc):
 
 
 def encode(enc, image1: torch.Tensor, image2: torch.Tensor | None = None,
-           join_stream: torch.cuda.Stream | None = None, split: bool = False) -> torch.Tensor:
+           join_stream: torch.cuda.Stream | None = None, split: bool = False, f16: bool = False) -> torch.Tensor:
     """Run ``enc`` natively on raw 0..255 fp32 images (``image2``: second frame of a
     paired batch).  Returns the (n, C, H/8, W/8) bf16 feature map in channels-last
     layout (``n`` = 2B when paired).  ``join_stream``: when this runs on a side stream,
     the stream that must see the parameter gradients complete (see ``_EncoderFn.backward``).
-    ``split``: fp32-faithful mode (no AMP; training or inference): the fp32 feature map."""
+    ``split``: fp32-faithful mode (no AMP; training or inference): the fp32 feature map.
+    ``f16``: fp16 activations (fp16 AMP, v_mfma_f32_32x32x16_f16) instead of bf16."""
     L = _layout(enc)
-    x0 = ops().enc_prep(image1.float(), image2.float() if image2 is not None else None, split)
+    x0 = ops().enc_prep(image1.float(), image2.float() if image2 is not None else None, split, f16 and not split)
     if split and not torch.is_grad_enabled():
         y = _forward_split(L, x0, L.params)
         N = y.shape[3] // 3

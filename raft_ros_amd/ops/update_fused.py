@@ -90,11 +90,13 @@ class _Arena:
     (``keep=False``) ``take`` hands out per-call temporaries instead.
     """
 
-    def __init__(self, iters: int, P: int, device, keep: bool):
+    def __init__(self, iters: int, P: int, device, keep: bool, dtype=torch.bfloat16):
         self.iters, self.P, self.device, self.keep = iters, P, device, keep
+        self.dtype = dtype  # the 16-bit activation dtype (bf16, or fp16 under fp16 AMP)
         self.bufs: Dict[str, torch.Tensor] = {}
 
-    def take(self, name: str, t: int, C: int, dtype=torch.bfloat16, slots: Optional[int] = None) -> torch.Tensor:
+    def take(self, name: str, t: int, C: int, dtype=None, slots: Optional[int] = None) -> torch.Tensor:
+        dtype = dtype or self.dtype
         if not self.keep:
             return torch.empty(self.P, C, device=self.device, dtype=dtype)
         buf = self.bufs.get(name)
@@ -110,14 +112,16 @@ class _Arena:
 class _Run:
     """Everything one RAFT forward's fused steps share."""
 
-    def __init__(self, block, inp: torch.Tensor, iters: int, pyramid=None, keep: bool = True):
+    def __init__(self, block, inp: torch.Tensor, iters: int, pyramid=None, keep: bool = True,
+                 dt16=torch.bfloat16):
         B, _, H, W = inp.shape
+        self.dt16 = dt16  # 16-bit operand dtype: bf16, or fp16 (fp16 AMP, v_mfma_f32_32x32x16_f16)
         self.dims = (B, H, W)
         self.P = P = B * H * W
         self.iters = iters
         self.block = block
         self.pyr = pyramid  # ops.corr._PyramidState or None (local correlation supplies corr)
-        self.arena = _Arena(iters, P, inp.device, keep)
+        self.arena = _Arena(iters, P, inp.device, keep, dt16)
         self.done = set()  # steps whose backward stored their dY
         self.g_all: Optional[torch.Tensor] = None  # [iters, P, 3*HID] data-gradient rows (backward)
         self.tail: Optional[torch.cuda.Stream] = None  # stream of the motion-encoder backward
@@ -131,11 +135,12 @@ class _Run:
         self.cout: Dict[str, int] = {}
         for name, mods, segs, scale, dgrad in _LAYERS:
             ms = mods(block)
-            wf, wd, b = C.pack_weights([m.weight for m in ms], [m.bias for m in ms], segs, scale, dgrad=dgrad)
+            wf, wd, b = C.pack_weights([m.weight for m in ms], [m.bias for m in ms], segs, scale, dgrad=dgrad,
+                                       f16=dt16 == torch.float16)
             self.wf[name], self.wd[name], self.bias[name] = wf, wd, b
             self.cout[name] = sum(m.weight.shape[0] for m in ms)
         # context features: constant over the iterations -> one bf16 pixel-major copy
-        self.inp_bf = _pm(inp.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        self.inp_bf = _pm(inp.detach().to(dt16).contiguous(memory_format=torch.channels_last))
 
     def geom(self, kh, kw, T: int = 1):
         B, H, W = self.dims
@@ -348,7 +353,7 @@ class _Step(torch.autograd.Function):
         B, H, W = run.dims
         P = run.P
         dev = net.device
-        bf = torch.bfloat16
+        bf = run.dt16
         k = ops()
         ar = run.arena
         g = run.geom
@@ -447,7 +452,7 @@ class _Step(torch.autograd.Function):
         B, H, W = run.dims
         P = run.P
         dev = g_flow_up.device if g_flow_up is not None else run.inp_bf.device
-        bf = torch.bfloat16
+        bf = run.dt16
         k = ops()
         ar = run.arena
         gd = run.geom_d
@@ -578,9 +583,10 @@ class _Step(torch.autograd.Function):
 class FusedBasicUpdate:
     """Per-forward driver: packs the weights once, then runs fused refinement steps."""
 
-    def __init__(self, block, inp: torch.Tensor, iters: int, pyramid=None, token: Optional[WeightToken] = None):
+    def __init__(self, block, inp: torch.Tensor, iters: int, pyramid=None, token: Optional[WeightToken] = None,
+                 dt16=torch.bfloat16):
         keep = torch.is_grad_enabled()
-        self.run = _Run(block, inp, iters, pyramid=pyramid, keep=keep)
+        self.run = _Run(block, inp, iters, pyramid=pyramid, keep=keep, dt16=dt16)
         if token is not None and keep:
             token.run = self.run  # created before the encoders (see WeightToken)
             self.token = token.tensor

@@ -56,14 +56,16 @@ def _params(block) -> List[torch.Tensor]:
 
 
 class _Run:
-    def __init__(self, block, inp: torch.Tensor, iters: int, pyramid=None, keep: bool = True):
+    def __init__(self, block, inp: torch.Tensor, iters: int, pyramid=None, keep: bool = True,
+                 dt16=torch.bfloat16):
         B, _, H, W = inp.shape
+        self.dt16 = dt16  # 16-bit operand dtype: bf16, or fp16 (fp16 AMP)
         self.dims = (B, H, W)
         self.P = B * H * W
         self.iters = iters
         self.block = block
         self.pyr = pyramid
-        self.arena = _Arena(iters, self.P, inp.device, keep)
+        self.arena = _Arena(iters, self.P, inp.device, keep, dt16)
         self.done = set()
         self.g_all: Optional[torch.Tensor] = None  # [iters, P, GX] data-gradient rows (backward)
         self.coords = {}
@@ -71,8 +73,8 @@ class _Run:
         for name, mods, segs, dgrad in _LAYERS:
             ms = mods(block)
             self.wf[name], self.wd[name], self.bias[name] = C.pack_weights(
-                [m.weight for m in ms], [m.bias for m in ms], segs, 1.0, dgrad=dgrad)
-        self.inp_bf = _pm(inp.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+                [m.weight for m in ms], [m.bias for m in ms], segs, 1.0, dgrad=dgrad, f16=dt16 == torch.float16)
+        self.inp_bf = _pm(inp.detach().to(dt16).contiguous(memory_format=torch.channels_last))
         self._motion_zeroed = False
 
     def geom(self, kh, kw, T: int = 1):
@@ -235,8 +237,12 @@ class _Step(torch.autograd.Function):
             C.conv_fwd([dy], run.wd[name], gd(kh, kw), n, out, epi=C.EPI_GRAD, mask=mask, acc_c0=acc_c0)
 
         dd8 = ar.take("dd8", t, 8)
-        if g_flow_up is not None:
+        if g_flow_up is not None and run.dt16 == torch.bfloat16:
             k.upflow8_backward(g_flow_up.float().contiguous(), H, W, dd8)
+        elif g_flow_up is not None:  # fp16 rows: from the fp32 flow gradient
+            dflow = k.upflow8_backward(g_flow_up.float().contiguous(), H, W, None)
+            dd8.zero_()
+            dd8[:, :2] = _pm(dflow)
         else:
             dd8.zero_()
         hd = R("hd")
@@ -256,12 +262,12 @@ class _Step(torch.autograd.Function):
         dzr = ar.take("dzr", t, 2 * HID)
         C.conv_fwd([dhd], run.wd["fh1"], gd(3, 3), HID, carry, epi=C.EPI_GRU_BWD_A, h=h, z=zr[:, :HID], g0=q,
                    out2=dq, out3=dzr[:, :HID], carry=carry, gru_cols=HID,
-                   addsrc=_pm(g_net).to(torch.bfloat16).contiguous() if g_net is not None else None)
+                   addsrc=_pm(g_net).to(run.dt16).contiguous() if g_net is not None else None)
         C.conv_fwd([dq], run.wd["q"], gd(3, 3), GX, G, epi=C.EPI_GRU_BWD_B, h=h, g0=zr[:, HID:], carry=carry,
                    out3=dzr[:, HID:], gru_cols=HID)
         motion, cf, f1 = R("motion"), R("cf"), R("f1")
         dmo = ar.take("dmo", t, 80)
-        d_net = torch.empty(P, HID, device=dev, dtype=torch.bfloat16)
+        d_net = torch.empty(P, HID, device=dev, dtype=run.dt16)
         # relu' of the motion features; the flow channels -> coords (detached)
         C.conv_fwd([dzr], run.wd["zr"], gd(3, 3), GX, G, epi=C.EPI_GRU_BWD_LAST, acc_c0=0, out3=d_net, gru_cols=HID,
                    cout=dmo, cmask=motion, cm_c0=HID + CTX, cm_valid=80)
@@ -269,7 +275,7 @@ class _Step(torch.autograd.Function):
         # motion encoder
         dcf = ar.take("dcf", t, 128)
         dgrad("conv", dmo, 3, 3, dcf, 128, mask=cf)
-        dcorr = torch.empty(P, CORR_PAD, device=dev, dtype=torch.bfloat16)
+        dcorr = torch.empty(P, CORR_PAD, device=dev, dtype=run.dt16)
         dgrad("convc1", dcf[:, :96], 1, 1, dcorr, CORR_PAD)
         df1 = ar.take("df1", t, 64)
         dgrad("convf2", dcf[:, 96:], 3, 3, df1, 64, mask=f1)
@@ -280,7 +286,7 @@ class _Step(torch.autograd.Function):
             d_corr_in = dcorr.reshape(B, H, W, CORR_PAD)
         elif run.pyr is not None and run.pyr.levels:
             run.pyr.add_grad(run.coords[t], dcorr.reshape(B, H, W, CORR_PAD))
-        d_net = _nchw(d_net if ctx.net_dtype == torch.bfloat16 else d_net.to(ctx.net_dtype), B, H, W)
+        d_net = _nchw(d_net if ctx.net_dtype == run.dt16 else d_net.to(ctx.net_dtype), B, H, W)
         d_inp = None
         if t == 0:  # the last step backward to run (every other step's d net feeds it)
             done = sorted(run.done)
@@ -297,9 +303,9 @@ class FusedSmallUpdate:
 
     corr_pad = CORR_PAD
 
-    def __init__(self, block, inp: torch.Tensor, iters: int, pyramid=None):
+    def __init__(self, block, inp: torch.Tensor, iters: int, pyramid=None, dt16=torch.bfloat16):
         keep = torch.is_grad_enabled()
-        self.run = _Run(block, inp, iters, pyramid=pyramid, keep=keep)
+        self.run = _Run(block, inp, iters, pyramid=pyramid, keep=keep, dt16=dt16)
         self.token = _PackWeights.apply(self.run, *_params(block))
         self.inp32 = inp.float().contiguous(memory_format=torch.channels_last)
 
