@@ -32,7 +32,7 @@ hipError_t launch_pyramid_operand(const PyrOperandArgs& a, hipStream_t s);
 hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int W, hipStream_t s);
 hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void* out, int out_dtype,
                                   int B, int H, int W, int r, int out_ch, hipStream_t s, void* flow8 = nullptr,
-                                  void* motion = nullptr, long smo = 0);
+                                  void* motion = nullptr, long smo = 0, int split_m = 0);
 hipError_t launch_corr_lookup_bwd(const PyrDesc& dpyr, const float* coords, const void* gout,
                                   int g_dtype, int B, int H, int W, int r, int gstride, hipStream_t s);
 hipError_t launch_lookup_grad_rows(const GradRowsArgs& a, int g_dtype, hipStream_t s);
@@ -382,6 +382,41 @@ void corr_lookup_grad_rows(const at::Tensor& out, at::TensorList coords, at::Ten
   a.r = (int)radius;
   const c10::DeviceGuard guard(out.device());
   HIP_OK(launch_lookup_grad_rows(a, dtype_code(gt), cur_stream()));
+}
+
+// fp32-mode lookup (ops/update_split.py): the window features of every level as split-bf16 rows
+// [hi | lo | hi] of G >= L*(2r+1)^2 channels (zero padded) in out (P, >= 3G) bf16, from the fp32
+// pyramid; optionally the step's split flow operand: flow8 (P, 24) rows and the 2 flow channels
+// of the motion features (motion: a view starting at the flow's hi channel, lo plane G_m after)
+void corr_lookup_split_into(at::TensorList pyramid, const at::Tensor& coords, int64_t radius, const at::Tensor& out,
+                            int64_t G, const c10::optional<at::Tensor>& flow8, const c10::optional<at::Tensor>& motion,
+                            int64_t G_m) {
+  check_coords(coords);
+  const long B = coords.size(0), H = coords.size(2), W = coords.size(3);
+  std::vector<at::Tensor> lv(pyramid.begin(), pyramid.end());
+  PyrDesc d = make_desc(lv, B * H * W, false);
+  const long win = (2 * radius + 1) * (2 * radius + 1);
+  check_gpu(out, "out");
+  TORCH_CHECK(out.dim() == 2 && out.is_contiguous() && out.scalar_type() == at::kBFloat16 && out.size(0) == B * H * W &&
+                  out.size(1) == 3 * G && G >= d.levels * win,
+              "raft_amd::corr_lookup_split_into: out must be contiguous bf16 (P, 3G), G >= L*(2r+1)^2");
+  void* f8 = nullptr;
+  void* mo = nullptr;
+  long smo = 0;
+  if (flow8) {
+    TORCH_CHECK(flow8->is_contiguous() && flow8->scalar_type() == at::kBFloat16 && flow8->numel() == B * H * W * 24,
+                "raft_amd::corr_lookup_split_into: flow8 must be contiguous bf16 (P, 24) split rows");
+    f8 = flow8->data_ptr();
+    if (motion) {
+      pm_any(*motion, "motion", B * H * W, at::kBFloat16);
+      TORCH_CHECK(G_m > 0 && motion->size(1) >= 2 * G_m + 2, "raft_amd::corr_lookup_split_into: motion split slice");
+      mo = motion->data_ptr();
+      smo = motion->stride(0);
+    }
+  }
+  const c10::DeviceGuard guard(coords.device());
+  HIP_OK(launch_corr_lookup_fwd(d, coords.data_ptr<float>(), out.data_ptr(), 3, B, H, W, static_cast<int>(radius),
+                                static_cast<int>(G), cur_stream(), f8, mo, smo, static_cast<int>(G_m)));
 }
 
 // ---------------------------------------------------------------- convex upsampling
@@ -1306,6 +1341,8 @@ TORCH_LIBRARY(raft_amd, m) {
       "int ldc, int sC, float alpha, bool a_trans, bool split, int epi, int cfg=0) -> ()");
   m.def("pyramid_unpool(Tensor G, int H, int W, int[] segs, bool blocked=False) -> Tensor");
   m.def("pyramid_operand(Tensor fmap, int[] segs, int ld, bool blocked, bool nchw) -> Tensor");
+  m.def("corr_lookup_split_into(Tensor[] pyramid, Tensor coords, int radius, Tensor(a!) out, int G, Tensor(b!)? flow8, "
+        "Tensor(c!)? motion, int G_m) -> ()");
   m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");
   m.def("convex_upsample_backward(Tensor flow, Tensor mask, Tensor grad) -> (Tensor, Tensor)");
   m.def("seq_loss(Tensor[] preds, Tensor gt, Tensor valid, float gamma, float max_flow) -> Tensor");
@@ -1354,6 +1391,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("conv_wgrad_params", &raft_amd::conv_wgrad_params);
   m.impl("pack_conv_weights", &raft_amd::pack_conv_weights);
   m.impl("pack_conv_weights_split", &raft_amd::pack_conv_weights_split);
+  m.impl("corr_lookup_split_into", &raft_amd::corr_lookup_split_into);
   m.impl("gru_gates", &raft_amd::gru_gates);
   m.impl("gru_gates_backward", &raft_amd::gru_gates_backward);
   m.impl("gru_blend", &raft_amd::gru_blend);

@@ -554,14 +554,40 @@ struct FlowPack {
   __bf16* flow8;
   __bf16* motion;
   long smo;
-  int f16;  // 16-bit storage is fp16 (fp16 AMP)
+  int f16;      // 16-bit storage is fp16 (fp16 AMP)
+  int split_m;  // > 0: split-bf16 planes (fp32 mode): flow8 rows [hi | lo | hi] of 8, motion lo plane
+                // split_m channels after its hi plane (ops/update_split.py)
+};
+
+// Output rows of the lookup: out_ch channels of OutT, or (SplitOut) split-bf16 planes [hi | lo |
+// hi] of out_ch channels each -- the fp32 training / inference step's GEMM operand, written
+// straight from the fp32 blend (no fp32 row round trip)
+struct SplitOut {};
+template <typename OutT>
+struct OutRow {
+  OutT* o;
+  int G;
+  static constexpr int kPlanes = 1;
+  __device__ __forceinline__ void put(int ch, float v) const { o[ch] = from_f32<OutT>(v); }
+};
+template <>
+struct OutRow<SplitOut> {
+  __bf16* o;
+  int G;
+  static constexpr int kPlanes = 3;
+  __device__ __forceinline__ void put(int ch, float v) const {
+    const __bf16 hi = static_cast<__bf16>(v);
+    o[ch] = hi;
+    o[G + ch] = static_cast<__bf16>(v - static_cast<float>(hi));
+    o[2 * G + ch] = hi;
+  }
 };
 
 // RC > 0: the radius as a compile-time constant (RAFT's r = 4): the window index math divides by
 // constants (a runtime 32-bit division is ~30 VALU per use)
 template <typename OutT, int RC = 0>
 __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const float* __restrict__ coords,
-                                                         OutT* __restrict__ out, int B, int H, int W, int r_arg,
+                                                         void* __restrict__ out_, int B, int H, int W, int r_arg,
                                                          int out_ch, const FlowPack fp) {
   const int r = RC > 0 ? RC : r_arg;
   __shared__ float nb[4][NBMAX];
@@ -577,11 +603,27 @@ __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const floa
   if (fp.flow8 && live && lane < 8) {
     const int py = p / W;
     const float u = cx0 - (float)(p - py * W), v = cy0 - (float)py;
-    const __bf16 f = st16(lane == 0 ? u : (lane == 1 ? v : 0.f), fp.f16 != 0);
-    fp.flow8[pix * 8 + lane] = f;
-    if (fp.motion && lane < 2) fp.motion[pix * fp.smo + lane] = f;
+    const float fv = lane == 0 ? u : (lane == 1 ? v : 0.f);
+    if (fp.split_m > 0) {  // split planes: hi = bf16(f), lo = bf16(f - hi)
+      const __bf16 hi = static_cast<__bf16>(fv), lo = static_cast<__bf16>(fv - static_cast<float>(hi));
+      fp.flow8[pix * 24 + lane] = hi;
+      fp.flow8[pix * 24 + 8 + lane] = lo;
+      fp.flow8[pix * 24 + 16 + lane] = hi;
+      if (fp.motion && lane < 2) {
+        __bf16* m = fp.motion + pix * fp.smo + lane;
+        m[0] = hi;
+        m[fp.split_m] = lo;
+        m[2 * fp.split_m] = hi;
+      }
+    } else {
+      const __bf16 f = st16(fv, fp.f16 != 0);
+      fp.flow8[pix * 8 + lane] = f;
+      if (fp.motion && lane < 2) fp.motion[pix * fp.smo + lane] = f;
+    }
   }
-  OutT* o = out + pix * out_ch;
+  using Row = OutRow<OutT>;
+  using Elem = decltype(Row::o);
+  const Row o{static_cast<Elem>(out_) + pix * out_ch * Row::kPlanes, out_ch};
   // software pipeline over the levels: the neighbourhood loads of level l+1 are in flight
   // while level l is blended (the lookup is bound by the load round trips, not by bytes)
   float fx = 0.f, fy = 0.f, nfx = 0.f, nfy = 0.f;
@@ -623,14 +665,14 @@ __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const floa
         const float* n0 = nb[wave] + iy * nd + ix;
         const float val =
             (1.f - fy) * ((1.f - fx) * n0[0] + fx * n0[1]) + fy * ((1.f - fx) * n0[nd] + fx * n0[nd + 1]);
-        o[l * win + ch] = from_f32<OutT>(val);
+        o.put(l * win + ch, val);
       }
     wave_lds_sync();
     fx = nfx;
     fy = nfy;
   }
   if (live)
-    for (int ch = pyr.levels * win + lane; ch < out_ch; ch += 64) o[ch] = from_f32<OutT>(0.f);
+    for (int ch = pyr.levels * win + lane; ch < out_ch; ch += 64) o.put(ch, 0.f);
 }
 
 // dpyr[l][pix][y][x] += window gradient, transposed bilinear blend; one wave per query.
@@ -868,27 +910,35 @@ hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int 
 }
 
 hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void* out, int out_dtype, int B, int H,
-                                  int W, int r, int out_ch, hipStream_t s, void* flow8, void* motion, long smo) {
-  const FlowPack fp{static_cast<__bf16*>(flow8), static_cast<__bf16*>(motion), smo, out_dtype == kF16 ? 1 : 0};
+                                  int W, int r, int out_ch, hipStream_t s, void* flow8, void* motion, long smo,
+                                  int split_m) {
+  // out_dtype kSplitBF16 (= 3): split-bf16 rows of 3 * out_ch; the flow operand split too
+  // (motion lo plane ``smo_split`` channels after its hi plane)
+  const bool split = out_dtype == 3;
+  const FlowPack fp{static_cast<__bf16*>(flow8), static_cast<__bf16*>(motion), smo, out_dtype == kF16 ? 1 : 0,
+                    split ? split_m : 0};
   const long npix = (long)B * H * W;
   if (npix == 0) return hipSuccess;
-  if (r > 6) return hipErrorInvalidValue;
+  if (r > 6 || (split && flow8 && split_m <= 0 && motion)) return hipErrorInvalidValue;
   const dim3 g((unsigned)((npix + 3) / 4)), blk(256);
-  if (out_dtype == kBF16 && r == 4)
-    hipLaunchKernelGGL((lookup_fwd_kernel<__bf16, 4>), g, blk, 0, s, pyr, coords, static_cast<__bf16*>(out), B, H, W,
-                       r, out_ch, fp);
+  if (split && r == 4)
+    hipLaunchKernelGGL((lookup_fwd_kernel<SplitOut, 4>), g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
+  else if (split && r == 3)
+    hipLaunchKernelGGL((lookup_fwd_kernel<SplitOut, 3>), g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
+  else if (split)
+    hipLaunchKernelGGL((lookup_fwd_kernel<SplitOut>), g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
+  else if (out_dtype == kBF16 && r == 4)
+    hipLaunchKernelGGL((lookup_fwd_kernel<__bf16, 4>), g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
   else if (out_dtype == kF32 && r == 4)
-    hipLaunchKernelGGL((lookup_fwd_kernel<float, 4>), g, blk, 0, s, pyr, coords, static_cast<float*>(out), B, H, W, r,
-                       out_ch, fp);
+    hipLaunchKernelGGL((lookup_fwd_kernel<float, 4>), g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
+  else if (out_dtype == kF16 && r == 4)
+    hipLaunchKernelGGL((lookup_fwd_kernel<_Float16, 4>), g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
   else if (out_dtype == kBF16)
-    hipLaunchKernelGGL(lookup_fwd_kernel<__bf16>, g, blk, 0, s, pyr, coords, static_cast<__bf16*>(out), B, H, W, r,
-                       out_ch, fp);
+    hipLaunchKernelGGL(lookup_fwd_kernel<__bf16>, g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
   else if (out_dtype == kF16)
-    hipLaunchKernelGGL(lookup_fwd_kernel<_Float16>, g, blk, 0, s, pyr, coords, static_cast<_Float16*>(out), B, H, W,
-                       r, out_ch, fp);
+    hipLaunchKernelGGL(lookup_fwd_kernel<_Float16>, g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
   else
-    hipLaunchKernelGGL(lookup_fwd_kernel<float>, g, blk, 0, s, pyr, coords, static_cast<float*>(out), B, H, W, r,
-                       out_ch, fp);
+    hipLaunchKernelGGL(lookup_fwd_kernel<float>, g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
   return hipGetLastError();
 }
 

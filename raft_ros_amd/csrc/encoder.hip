@@ -927,10 +927,12 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_reduce_kernel(const NormBwdA
       for (int e = 0; e < 8; ++e) red[(e * PPB + pr) * G + cg] = S[qd][e];
     __syncthreads();
     if (tid < N) {
-      const int tc = tid >> 3, te = tid & 7;
+      // lane -> (chunk tc, element te) with the chunk fastest, so the 64 lanes of a read read
+      // consecutive words (the element-fastest order put 8 lanes 256 words apart on one bank)
+      const int tc = tid % G, te = tid / G;
       float s = 0.f;
       for (int k = 0; k < PPB; ++k) s += red[(te * PPB + k) * G + tc];
-      a.part[(((long)b * a.R + r) * 4 + qd) * N + tid] = s;
+      a.part[(((long)b * a.R + r) * 4 + qd) * N + tc * 8 + te] = s;
     }
     __syncthreads();
   }

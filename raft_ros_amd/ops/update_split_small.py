@@ -169,16 +169,19 @@ class _Step(torch.autograd.Function):
         if net.data_ptr() != h0.data_ptr():
             C.split_pack(_pm(net.float()).contiguous(), h0, HID)
         corr = run.take("corr", t, 3 * CORR_PAD)
-        if run.pyr is not None:
-            c = k.corr_lookup(run.pyr.levels, coords1, run.pyr.radius, torch.float32, CORR_PAD).view(P, CORR_PAD)
-        else:
-            c = corr_in.reshape(P, -1).float().contiguous()
-        C.split_pack(c, corr, CORR_PAD, 0, CORR_PAD)
-        flow = (coords1 - run.coords0).permute(0, 2, 3, 1).reshape(P, 2).contiguous()
         flow8 = run.take("flow8", t, 24)
         motion = run.take("motion", t, 3 * MOT_PAD)
-        C.split_pack(flow, flow8, 8, 0, 8)
-        C.split_pack(flow, motion, MOT_PAD, 80, 8)  # flow at 80..81, zeros 82..87
+        if run.pyr is not None:  # one launch: split features + the split flow operand
+            k.corr_lookup_split_into(run.pyr.levels, coords1, run.pyr.radius, corr, CORR_PAD, flow8, motion[:, 80:],
+                                     MOT_PAD)
+            motion[:, 82:MOT_PAD].zero_()
+            motion[:, MOT_PAD + 82:2 * MOT_PAD].zero_()
+            motion[:, 2 * MOT_PAD + 82:].zero_()
+        else:
+            C.split_pack(corr_in.reshape(P, -1).float().contiguous(), corr, CORR_PAD, 0, CORR_PAD)
+            flow = (coords1 - run.coords0).permute(0, 2, 3, 1).reshape(P, 2).contiguous()
+            C.split_pack(flow, flow8, 8, 0, 8)
+            C.split_pack(flow, motion, MOT_PAD, 80, 8)  # flow at 80..81, zeros 82..87
 
         cf = run.take("cf", t, 384)
         f1 = run.take("f1", t, 192)

@@ -147,3 +147,32 @@ def test_split_weight_packing_kernel_matches_python(cuda, small):
         torch.testing.assert_close(bias, bias_ref, rtol=0, atol=0)
         if gdy:
             assert torch.equal(wd, update_split.pack_dgrad_split(w, dsegs, dyg, scale)), name
+
+
+@pytest.mark.parametrize("radius,G,Gm,mo_c0", [(4, 328, 128, 126), (3, 200, 88, 80)])
+def test_split_lookup_matches_fp32_lookup(cuda, radius, G, Gm, mo_c0):
+    """corr_lookup_split_into == split_pack(fp32 corr_lookup) and the split flow operand, bitwise."""
+    from raft_ros_amd.ops import CorrPyramid
+    from raft_ros_amd.ops import conv as C
+    from raft_ros_amd.ops._ext import ops
+
+    torch.manual_seed(3)
+    B, Cf, H, W = 2, 64, 16, 24
+    f1, f2 = torch.randn(B, Cf, H, W, device=cuda), torch.randn(B, Cf, H, W, device=cuda)
+    pyr = CorrPyramid(f1, f2, radius=radius, split=True)
+    ys, xs = torch.meshgrid(torch.arange(H, device=cuda), torch.arange(W, device=cuda), indexing="ij")
+    coords = torch.stack([xs, ys]).float()[None].repeat(B, 1, 1, 1) + 3 * torch.randn(B, 2, H, W, device=cuda)
+    P = B * H * W
+    k = ops()
+    ref = k.corr_lookup(pyr.state.levels, coords, radius, torch.float32, G).view(P, G)
+    want = C.split_pack(ref, torch.zeros(P, 3 * G, device=cuda, dtype=torch.bfloat16), G, 0, G)
+    got = torch.zeros(P, 3 * G, device=cuda, dtype=torch.bfloat16)
+    flow8 = torch.zeros(P, 24, device=cuda, dtype=torch.bfloat16)
+    motion = torch.zeros(P, 3 * Gm, device=cuda, dtype=torch.bfloat16)
+    k.corr_lookup_split_into(pyr.state.levels, coords, radius, got, G, flow8, motion[:, mo_c0:], Gm)
+    assert torch.equal(got, want)
+    flow = (coords - torch.stack([xs, ys]).float()[None]).permute(0, 2, 3, 1).reshape(P, 2).contiguous()
+    want8 = C.split_pack(flow, torch.zeros(P, 24, device=cuda, dtype=torch.bfloat16), 8, 0, 8)
+    wantm = C.split_pack(flow, torch.zeros(P, 3 * Gm, device=cuda, dtype=torch.bfloat16), Gm, mo_c0, 2)
+    assert torch.equal(flow8, want8)
+    assert torch.equal(motion, wantm)
