@@ -225,7 +225,7 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
     check_w(ws[j], "w");
     TORCH_CHECK(dys[j].size(0) == B && ws[j].size(1) == Cin && dys[j].size(3) == (split ? 3 : 1) * ws[j].size(0),
                 "dgrad shapes");
-    TORCH_CHECK(!split || ws[j].size(0) == ws[0].size(0), "split dgrad: convs share Cout");
+
     TORCH_CHECK(S % strides[j] == 0, "strides must divide the largest stride");
     const int KH = (int)ws[j].size(2), KW = (int)ws[j].size(3);
     const int Ho = ((int)H + 2 * (int)pads[j] - KH) / (int)strides[j] + 1;
@@ -276,6 +276,7 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
   a.out_stride = rs;
   a.split = split ? 1 : 0;
   a.split_w = split ? (int)ws[0].size(0) : 0;
+  for (int j = 0; j < nconv; ++j) a.split_wd[j] = split ? (int)ws[j].size(0) : 0;
   if (res.has_value() && res->defined()) {
     check_nhwc(*res, "res");
     TORCH_CHECK(res->sizes() == dx.sizes() && res->scalar_type() == dx.scalar_type(), "res shape / dtype");

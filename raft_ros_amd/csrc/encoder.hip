@@ -408,7 +408,8 @@ __global__ __launch_bounds__(256) void enc_pack_kernel(const EncConvArgs a, __bf
       const long s2 = w ? a.ws[1][2] : a.ws[0][2], s3 = w ? a.ws[1][3] : a.ws[0][3];
       const int cin = w ? a.wcin[1] : a.wcin[0];
       if (a.pack_dgrad && a.split_w) {  // split dY rows [hi | lo | hi] of Cout: [W_hi | W_hi | W_lo]
-        const int plane = loc / a.split_w, co = loc - plane * a.split_w;
+        const int pw = a.split_wd[w] > 0 ? a.split_wd[w] : a.split_w;  // this conv's Cout
+        const int plane = loc / pw, co = loc - plane * pw;
         const float x = wp[co * s0 + row * s1 + ky * s2 + kx * s3];
         const float hi = static_cast<float>(static_cast<__bf16>(x));
         v = plane < 2 ? hi : x - hi;

@@ -221,6 +221,7 @@ struct EncConvArgs {
   const int* tab_ptr;
   const int* ptab_ptr;
   int f16;  // 16-bit activations / packed weights are fp16 (fp16 AMP) instead of bf16
+  int split_wd[2];  // split data gradient: the dY plane width (Cout) of conv 0 / 1 (0: split_w)
   // split-bf16 output (fp32-faithful inference, see ConvFwdArgs::split_g): out rows hold
   // [hi | lo | hi] planes of N channels each (out_stride = 3N).  A split data gradient (fp32
   // training) also reads res as split rows (res_stride = 3N, lo plane at +N) and the ReLU'
