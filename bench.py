@@ -60,7 +60,10 @@ def parse():
     ap.add_argument("--lr", type=float, default=4e-4)
     # ~10 MB buckets: the update-block gradients (12.5 MB, ready first -- batched wgrads run
     # before the encoders' backward) all-reduce over xGMI while the encoders backpropagate
-    ap.add_argument("--bucket_mb", type=float, default=10.0)
+    ap.add_argument("--bucket_mb", type=float, default=10.0, help="DDP bucket size (--dp_impl ddp)")
+    ap.add_argument("--dp_impl", choices=["sync", "ddp"], default="sync",
+                    help="N>1 gradient averaging: one packed all-reduce after the backward "
+                         "(parallel/grad_sync.py) or torch DistributedDataParallel")
     ap.add_argument("--no_fused", action="store_true", help="update block on PyTorch/MIOpen convs")
     ap.add_argument("--mode", choices=["train", "infer"], default="train",
                     help="infer: forward-only test_mode passes (BASELINE config #5: --image_size 1080 1920 --iters 32)")
@@ -186,12 +189,17 @@ def run(args):
     oargs = Namespace(lr=args.lr, wdecay=1e-4, epsilon=1e-8, num_steps=100000)
     train_graph = (bool(args.graph) and args.mode == "train" and args.impl == "native" and args.amp_dtype == "bf16"
                    and not args.fp32)
-    if distributed and not train_graph:
+    gsync = None
+    if distributed and not train_graph and args.dp_impl == "ddp":
         ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local] if device.type == "cuda" else None,
                                                         bucket_cap_mb=args.bucket_mb,
                                                         gradient_as_bucket_view=True, static_graph=True)
     else:
         ddp = model
+        if distributed and not train_graph:
+            from raft_ros_amd.parallel.grad_sync import GradSync
+
+            gsync = GradSync(model)
     optimizer, scheduler = fetch_optimizer(oargs, model, capturable=train_graph)
     scaler = torch.amp.GradScaler("cuda", enabled=args.amp_dtype == "fp16" and not args.fp32 and device.type == "cuda")
 
@@ -218,6 +226,8 @@ def run(args):
         preds = ddp(i1, i2, iters=args.iters)
         loss, metrics = sequence_loss(preds, flow, valid, gamma=0.8)
         scaler.scale(loss).backward()
+        if gsync is not None:
+            gsync.sync()
         scaler.unscale_(optimizer)
         torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
         scaler.step(optimizer)
@@ -294,6 +304,7 @@ def run(args):
                 "image_size": [H, W],
                 "iters": args.iters,
                 "parallelism": f"dp{world}",
+                "dp_impl": (args.dp_impl if world > 1 else None),
                 "impl": args.impl,
                 # the code paths that actually ran (decided by the model's own dispatch rules)
                 "fused_update": upd_path not in ("module", "reference"),

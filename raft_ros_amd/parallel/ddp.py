@@ -4,9 +4,10 @@ Replaces the reference's single-process ``nn.DataParallel`` (train.py:138), whic
 broadcasts all 5.26 M parameters to every replica, scatters inputs and gathers
 all 12 full-resolution flow predictions to GPU 0 *every step* (SURVEY.md 2.5).
 Here each rank keeps its own replica; the only per-step collective is the
-bucketed fp32 gradient all-reduce (~21 MB for RAFT-base), overlapped with the
-backward pass by DistributedDataParallel.  On ROCm the ``"nccl"`` backend is
-RCCL.  CPU runs (tests) use ``gloo``.
+fp32 gradient all-reduce (~21 MB for RAFT-base): by default one packed all-reduce
+after the backward (:func:`data_parallel`, parallel/grad_sync.py), or torch's
+DistributedDataParallel with bucketed all-reduces (``impl="ddp"``, :func:`wrap_model`).
+On ROCm the ``"nccl"`` backend is RCCL.  CPU runs (tests) use ``gloo``.
 
 Rendezvous always uses 127.0.0.1 unless MASTER_ADDR says otherwise.
 """
@@ -112,6 +113,25 @@ def wrap_model(model: torch.nn.Module, info: DistInfo, bucket_cap_mb: float = 10
 
         net.register_comm_hook(None, default_hooks.bf16_compress_hook)
     return net
+
+
+def data_parallel(model: torch.nn.Module, info: DistInfo, impl: str = "sync", bucket_cap_mb: float = 10.0,
+                  bf16_grads: bool = False):
+    """-> (module to call forward on, GradSync or None).
+
+    ``impl="sync"`` (default): the model itself plus a :class:`~.grad_sync.GradSync` whose
+    ``sync()`` the training step calls after ``backward()`` -- one packed all-reduce instead of
+    DDP's per-parameter bucket copies (see parallel/grad_sync.py for why that fits RAFT).
+    ``impl="ddp"``: torch's DistributedDataParallel (:func:`wrap_model`), no GradSync."""
+    if not info.distributed:
+        return model, None
+    if impl == "ddp":
+        return wrap_model(model, info, bucket_cap_mb=bucket_cap_mb, bf16_grads=bf16_grads), None
+    if impl != "sync":
+        raise ValueError(f"data-parallel impl {impl!r}: 'sync' or 'ddp'")
+    from .grad_sync import GradSync
+
+    return model, GradSync(model, bf16=bf16_grads)
 
 
 def all_reduce_mean(values: Dict[str, float], info: DistInfo) -> Dict[str, float]:

@@ -74,8 +74,9 @@ def train(args: Namespace) -> str:
         convert_sync_bn(model.cnet)
     if args.stage != "chairs":
         model.freeze_bn()
-    net = ddp.wrap_model(model, info, bucket_cap_mb=getattr(args, "bucket_mb", 10.0),
-                         bf16_grads=getattr(args, "ddp_bf16_grads", False))
+    net, gsync = ddp.data_parallel(model, info, impl=getattr(args, "dp_impl", "sync"),
+                                   bucket_cap_mb=getattr(args, "bucket_mb", 10.0),
+                                   bf16_grads=getattr(args, "ddp_bf16_grads", False))
 
     args.device = str(dev)  # batched augmentation runs on the rank's device
     train_loader = fetch_dataloader(args)
@@ -119,6 +120,9 @@ def train(args: Namespace) -> str:
             loss = injector.on_loss(total_steps, loss)
         with trace_range("backward"):
             scaler.scale(loss).backward()
+        if gsync is not None:
+            with trace_range("grad_sync"):
+                gsync.sync()
         scaler.unscale_(optimizer)
         gnorm = torch.nn.utils.clip_grad_norm_(model.parameters(), args.clip)
         if use_scaler:

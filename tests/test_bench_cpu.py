@@ -31,6 +31,7 @@ def test_bench_spawns_ranks_for_gpus_flag():
     assert KEYS <= set(r), set(KEYS) - set(r)
     assert r["n_gpus"] == 2
     assert r["config"]["parallelism"] == "dp2"
+    assert r["config"]["dp_impl"] == "sync"  # GradSync (parallel/grad_sync.py)
     assert r["config"]["global_batch"] == 2
     assert r["allreduce_ms"] > 0
 

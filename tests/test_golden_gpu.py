@@ -8,6 +8,8 @@ test_mode -- the demo.py / ROS node configuration).
 * native bf16 path (HIP encoders + fused update kernels): EPE delta <= 3x the delta of
   PyTorch's own bf16 autocast of the module path (the same computation on MIOpen).
 """
+import os
+
 import pytest
 import torch
 
@@ -61,8 +63,18 @@ def test_native_fp32_training_gradients_match_reference(cuda, small):
     """Native fp32 training (split-bf16 kernels: encoders + refinement step) vs the REAL
     reference's CPU fp32 gradients (tests/fixtures/golden_grads.npz), per parameter (16 fixed
     projections or the full tensor), anchored on the fp32 module path (MIOpen) measured the
-    same way: the native path must be within a small factor of MIOpen's own fp32 deviation."""
+    same way, and on the precision floor of the split number format itself: the fp32 module
+    path run on CPU with every conv operand / output / gradient rounded to hi + lo (a 16-bit
+    mantissa) -- scripts/emulate_split_precision.py, tests/fixtures/split_format_floor.json.
+    Gradients of the early encoder layers are sensitive to the 2^-17 operand perturbation
+    (RAFT-small's fnet.layer1 to ~4e-2 in that emulation), so no kernel on this format gets
+    below it; the native path must stay within 1.5x of the format's floor or 4x of MIOpen's
+    own deviation, whichever is larger."""
+    import json
+
     name = "small" if small else "base"
+    with open(os.path.join(os.path.dirname(__file__), "fixtures", "split_format_floor.json")) as f:
+        floor = json.load(f)[name]
     fix, loss, errs = _grad_errs(cuda, small, mixed_precision=False)
     _, _, emod = _grad_errs(cuda, small, mixed_precision=False, fused_update=False, native_encoder=False)
     rms = lambda e: (sum(v * v for v in e.values()) / len(e)) ** 0.5  # noqa: E731
@@ -71,8 +83,10 @@ def test_native_fp32_training_gradients_match_reference(cuda, small):
     print(f"\n{name}: fp32 training vs reference: loss {loss:.6f} (ref {float(fix[name + '/loss']):.6f}); "
           f"native worst {worst}, RMS {rms(errs):.2e}; MIOpen module path worst {wmod}, RMS {rms(emod):.2e}")
     assert abs(loss - float(fix[f"{name}/loss"])) <= 1e-4 * abs(float(fix[f"{name}/loss"]))
-    assert worst[0][1] <= max(4 * wmod[0][1], 1e-3), (worst, wmod)
-    assert rms(errs) <= 3 * rms(emod) + 1e-3, (rms(errs), rms(emod))
+    print(f"{name}: split-format floor (emulated): worst {floor['worst']:.2e} ({floor['worst_param']}), "
+          f"RMS {floor['rms']:.2e}")
+    assert worst[0][1] <= max(4 * wmod[0][1], 1.5 * floor["worst"], 1e-3), (worst, wmod, floor)
+    assert rms(errs) <= max(3 * rms(emod) + 1e-3, 1.5 * floor["rms"]), (rms(errs), rms(emod), floor)
 
 
 @pytest.mark.parametrize("small", [False, True])

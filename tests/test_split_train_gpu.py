@@ -5,8 +5,9 @@ native_encoder=False``: MIOpen fp32 convs, fp32 grid_sample-equivalent lookups).
 fp32 path (ops/update_split.py, ops/encoder.py split mode) computes every conv product as
 x_hi W_hi + x_lo W_hi + x_hi W_lo with fp32 accumulation over operands stored with a 16-bit
 mantissa (hi + lo), so predictions agree to ~1e-5 relative.  Weight gradients are sums with
-heavy cancellation (norm backward, softmax-mask gradients), where the 2^-16 operand precision
-shows up as ~1e-3 relative (worst ~1e-2) -- the same order as MIOpen's own fp32 deviation from
+heavy cancellation (norm backward, softmax-mask gradients), where the 2^-17 operand precision
+shows up as ~1e-3 relative (worst ~1e-2, RAFT-small's fnet.layer1 ~3e-2: the format's own floor,
+scripts/emulate_split_precision.py) -- the same order as MIOpen's own fp32 deviation from
 the REAL reference's CPU gradients (up to 4.5e-3, ``scripts/diag_split_grads.py``,
 profiles/r4_split_grad_precision.log; the reference-anchored bound is in test_golden_gpu.py).
 A real defect (a wrong plane, tap or gate) shows up as O(1e-1 .. 1) errors; bf16 AMP is ~1e-1.
@@ -35,6 +36,17 @@ def _run(m, batch, iters):
     loss.backward()
     torch.cuda.synchronize()
     return preds, {n: p.grad.float().clone() for n, p in m.named_parameters() if p.grad is not None}
+
+
+def _floor_tol(small: bool) -> float:
+    """1.5x the split format's own worst gradient error vs the reference (CPU emulation of the
+    storage layout, tests/fixtures/split_format_floor.json): the native path vs the MIOpen
+    module path can differ by that much without any kernel defect."""
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(__file__), "fixtures", "split_format_floor.json")) as f:
+        return 1.5 * json.load(f)["small" if small else "base"]["worst"]
 
 
 def _compare(cuda, shape, iters, tol, native_encoder, small=False, **kw):
@@ -77,11 +89,11 @@ def test_split_update_training_matches_fp32_module(cuda, shape):
 
 
 def test_split_training_native_encoders_matches_fp32_module(cuda):
-    _compare(cuda, (2, 128, 192), 3, 2e-2, native_encoder=True)
+    _compare(cuda, (2, 128, 192), 3, _floor_tol(False), native_encoder=True)
 
 
 def test_split_small_training_matches_fp32_module(cuda):
-    _compare(cuda, (2, 128, 192), 3, 2e-2, native_encoder=True, small=True)
+    _compare(cuda, (2, 128, 192), 3, _floor_tol(True), native_encoder=True, small=True)
 
 
 def test_split_small_inference_matches_fp32_module(cuda):
@@ -174,10 +186,10 @@ def test_split_lookup_matches_fp32_lookup(cuda, radius, G, Gm, mo_c0):
     flow8 = torch.zeros(P, 24, device=cuda, dtype=torch.bfloat16)
     motion = torch.zeros(P, 3 * Gm, device=cuda, dtype=torch.bfloat16)
     k.corr_lookup_split_into(pyr.state.levels, coords, radius, got, G, flow8, motion[:, mo_c0:], Gm)
-    # hi + lo reproduces the fp32 lookup (the blend may contract differently per instantiation:
-    # ulp-level differences), hi-again == hi
+    # hi + lo reproduces the fp32 lookup to the split format's 16-bit mantissa (relative
+    # 2^-17 per value; the blend may also contract differently per instantiation), hi-again == hi
     val = got[:, :G].float() + got[:, G:2 * G].float()
-    torch.testing.assert_close(val, ref, rtol=2e-6, atol=1e-7)
+    torch.testing.assert_close(val, ref, rtol=2e-5, atol=1e-6)
     assert torch.equal(got[:, :G], got[:, 2 * G:])
     flow = (coords - torch.stack([xs, ys]).float()[None]).permute(0, 2, 3, 1).reshape(P, 2).contiguous()
     want8 = C.split_pack(flow, torch.zeros(P, 24, device=cuda, dtype=torch.bfloat16), 8, 0, 8)

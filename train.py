@@ -54,9 +54,11 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--ckpt_dir", default="checkpoints")
     g.add_argument("--log_dir", default="runs")
     g.add_argument("--dataset_root", default=None, help="directory holding Sintel/, KITTI/, ... (default ./datasets)")
+    g.add_argument("--dp_impl", choices=["sync", "ddp"], default="sync",
+                   help="data-parallel gradient averaging: one packed all-reduce after the backward (sync, "
+                        "parallel/grad_sync.py) or torch DistributedDataParallel (ddp)")
     g.add_argument("--bucket_mb", type=float, default=10.0,
-                   help="DDP gradient bucket size (10 MB: the update-block gradients all-reduce while the "
-                        "encoders backpropagate)")
+                   help="DDP gradient bucket size (--dp_impl ddp)")
     g.add_argument("--seed", type=int, default=1234)
     g.add_argument("--deterministic", action="store_true",
                    help="bitwise-reproducible steps: torch.use_deterministic_algorithms + the native kernels' "
@@ -65,7 +67,7 @@ def build_parser() -> argparse.ArgumentParser:
                    help="synchronize the context encoder's BatchNorm statistics over the DDP ranks (default: "
                         "per-rank statistics, like the reference's DataParallel replicas)")
     g.add_argument("--ddp_bf16_grads", action="store_true",
-                   help="all-reduce gradients in bf16 (DDP compression hook; halves xGMI traffic)")
+                   help="all-reduce gradients in bf16 (halves xGMI traffic)")
     g.add_argument("--profile_dir", default=None, help="capture a torch.profiler trace of steps 5-7 here")
     return p
 
