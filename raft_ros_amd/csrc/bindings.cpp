@@ -1109,6 +1109,84 @@ std::tuple<at::Tensor, c10::optional<at::Tensor>, at::Tensor> pack_conv_weights_
   return {wf, wd, bias};
 }
 
+// Several layers' operands in ONE launch.  Per layer q: nw[q] stacked weights (and biases) from
+// the flat lists, nseg[q] (real, padded) segment pairs from ``segs``, scale[q], Kf[q], Kd[q]
+// (0: no data-gradient operand) and aux[q] (Cout_pad, or G_dy in split mode).  Returns
+// [wf_0, wd_0, bias_0, wf_1, ...] (wd_q empty when Kd[q] == 0): views of one 16-bit buffer and
+// one fp32 buffer.
+std::vector<at::Tensor> pack_conv_weights_multi(at::TensorList w, const c10::List<c10::optional<at::Tensor>>& b,
+                                                at::IntArrayRef nw, at::IntArrayRef segs, at::IntArrayRef nseg,
+                                                at::ArrayRef<double> scale, at::IntArrayRef Kf, at::IntArrayRef Kd,
+                                                at::IntArrayRef aux, bool f16, bool split) {
+  const int L = (int)nw.size();
+  TORCH_CHECK(L >= 1 && L <= kPackJobs && (int)nseg.size() == L && (int)scale.size() == L && (int)Kf.size() == L &&
+                  (int)Kd.size() == L && (int)aux.size() == L && (int)b.size() == (int)w.size(),
+              "raft_amd pack_conv_weights_multi: 1..", kPackJobs, " layers with one entry per list");
+  TORCH_CHECK(!(split && f16), "raft_amd pack_conv_weights_multi: split packs are bf16");
+  PackJobs js{};
+  js.n = L;
+  int wi = 0, si = 0;
+  long total = 0, n16 = 0, n32 = 0;
+  std::vector<long> off16(L), offd(L), off32(L);
+  for (int q = 0; q < L; ++q) {
+    TORCH_CHECK(nw[q] >= 1 && nw[q] <= 2 && wi + nw[q] <= (int)w.size(), "raft_amd pack_conv_weights_multi: nw");
+    TORCH_CHECK(nseg[q] >= 1 && si + 2 * nseg[q] <= (int)segs.size(), "raft_amd pack_conv_weights_multi: segs");
+    c10::List<c10::optional<at::Tensor>> bq;
+    for (int k = 0; k < nw[q]; ++k) bq.push_back(b.get(wi + k));
+    PackJob& jb = js.j[q];
+    jb.d = param_desc(w.slice(wi, nw[q]), bq, segs.slice(si, 2 * nseg[q]), scale[q], "pack_conv_weights_multi");
+    wi += (int)nw[q];
+    si += 2 * (int)nseg[q];
+    const int N = jb.d.rows[0] + jb.d.rows[1], taps = jb.d.KH * jb.d.KW;
+    jb.N = N;
+    jb.Kf = (int)Kf[q];
+    jb.Kd = (int)Kd[q];
+    jb.aux = (int)aux[q];
+    if (split) {
+      TORCH_CHECK(Kf[q] >= taps * 3 * jb.d.Cin_pad && Kf[q] % 64 == 0 &&
+                      (Kd[q] == 0 || (aux[q] >= N && aux[q] % 8 == 0 && Kd[q] >= taps * 3 * aux[q] && Kd[q] % 64 == 0)),
+                  "raft_amd pack_conv_weights_multi: bad split layout of layer ", q);
+      jb.d.split_fw = 1;
+      jb.d.split_dy = (int)aux[q];
+    } else {
+      TORCH_CHECK(Kf[q] >= taps * jb.d.Cin_pad && Kf[q] % 64 == 0 &&
+                      (Kd[q] == 0 || (aux[q] >= N && Kd[q] >= taps * aux[q] && Kd[q] % 64 == 0)),
+                  "raft_amd pack_conv_weights_multi: bad layout of layer ", q);
+      jb.d.f16 = f16 ? 1 : 0;
+    }
+    jb.begin = total;
+    total += (long)N * Kf[q] + (Kd[q] > 0 ? (long)jb.d.Cin_pad * Kd[q] : 0) + N;
+    off16[q] = n16;
+    auto r64 = [](long v) { return (v + 63) / 64 * 64; };  // 128-byte aligned views
+    n16 += r64((long)N * Kf[q]);
+    offd[q] = n16;
+    n16 += Kd[q] > 0 ? r64((long)jb.d.Cin_pad * Kd[q]) : 0;
+    off32[q] = n32;
+    n32 += r64((long)N);
+  }
+  TORCH_CHECK(wi == (int)w.size() && si == (int)segs.size(), "raft_amd pack_conv_weights_multi: unused list entries");
+  js.total = total;
+  const c10::DeviceGuard guard(w[0].device());
+  auto buf16 = at::empty({n16}, w[0].options().dtype(f16 ? at::kHalf : at::kBFloat16));
+  auto buf32 = at::empty({n32}, w[0].options().dtype(at::kFloat));
+  std::vector<at::Tensor> out;
+  for (int q = 0; q < L; ++q) {
+    PackJob& jb = js.j[q];
+    at::Tensor wf = buf16.narrow(0, off16[q], (long)jb.N * jb.Kf).view({jb.N, jb.Kf});
+    at::Tensor wd = jb.Kd > 0 ? buf16.narrow(0, offd[q], (long)jb.d.Cin_pad * jb.Kd).view({jb.d.Cin_pad, jb.Kd})
+                              : buf16.new_empty({0});
+    at::Tensor bias = buf32.narrow(0, off32[q], jb.N);
+    jb.wf = reinterpret_cast<__bf16*>(wf.data_ptr());
+    jb.wd = jb.Kd > 0 ? reinterpret_cast<__bf16*>(wd.data_ptr()) : nullptr;
+    jb.bias = bias.data_ptr<float>();
+    out.push_back(wf);
+    out.push_back(wd);
+    out.push_back(bias);
+  }
+  HIP_OK(launch_pack_conv_weights_multi(js, cur_stream()));
+  return out;
+}
+
 // ---------------------------------------------------------------- update-block elementwise
 void pm_any(const at::Tensor& t, const char* name, long P, at::ScalarType dt) {
   check_gpu(t, name);
@@ -1313,6 +1391,8 @@ TORCH_LIBRARY(raft_amd, m) {
         "float scale, bool accumulate) -> ()");
   m.def("pack_conv_weights_split(Tensor[] w, Tensor?[] b, int[] segs, float scale, int Kf, int Kd, int G_dy) -> "
         "(Tensor, Tensor?, Tensor)");
+  m.def("pack_conv_weights_multi(Tensor[] w, Tensor?[] b, int[] nw, int[] segs, int[] nseg, float[] scale, "
+        "int[] Kf, int[] Kd, int[] aux, bool f16=False, bool split=False) -> Tensor[]");
   m.def("pack_conv_weights(Tensor[] w, Tensor?[] b, int[] segs, float scale, int Kf, int Kd, int cout_pad, "
         "bool f16=False) -> "
         "(Tensor, Tensor?, Tensor)");
@@ -1390,6 +1470,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("conv_wgrad", &raft_amd::conv_wgrad);
   m.impl("conv_wgrad_params", &raft_amd::conv_wgrad_params);
   m.impl("pack_conv_weights", &raft_amd::pack_conv_weights);
+  m.impl("pack_conv_weights_multi", &raft_amd::pack_conv_weights_multi);
   m.impl("pack_conv_weights_split", &raft_amd::pack_conv_weights_split);
   m.impl("corr_lookup_split_into", &raft_amd::corr_lookup_split_into);
   m.impl("gru_gates", &raft_amd::gru_gates);

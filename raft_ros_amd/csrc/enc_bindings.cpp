@@ -307,8 +307,10 @@ void check_rows(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.size(0) * t.stride(0) < (1L << 31), name, ": too large");
 }
 
+// fold > 0 (split-bf16 training): x = [hi | lo] planes of ``fold`` channels each; the gradient of
+// the fp32 parameter is the sum of the hi- and lo-plane columns (folded in the reduction)
 void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, const c10::optional<at::Tensor>& db,
-                    int64_t stride, int64_t pad, bool accumulate, bool db_zero) {
+                    int64_t stride, int64_t pad, bool accumulate, bool db_zero, int64_t fold) {
   check_rows(x, "x");
   check_rows(dy, "dy");
   const int xpitch = (int)x.stride(2), dypitch = (int)dy.stride(2);
@@ -318,7 +320,8 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
   const int B = (int)x.size(0), Hx = (int)x.size(1), Wx = (int)x.size(2), Cx = (int)x.size(3);
   const int N = (int)dw.size(0), Cin = (int)dw.size(1), KH = (int)dw.size(2), KW = (int)dw.size(3);
   const int Ho = (int)dy.size(1), Wo = (int)dy.size(2);
-  TORCH_CHECK(dy.size(0) == B && dy.size(3) == N && Cin <= Cx, "wgrad shapes");
+  TORCH_CHECK(dy.size(0) == B && dy.size(3) == N && Cin <= (fold > 0 ? fold : Cx), "wgrad shapes");
+  TORCH_CHECK(fold == 0 || (fold % 8 == 0 && Cx == 2 * fold), "wgrad fold: x holds two planes of fold channels");
   TORCH_CHECK(Ho == (Hx + 2 * (int)pad - KH) / (int)stride + 1 && Wo == (Wx + 2 * (int)pad - KW) / (int)stride + 1,
               "wgrad spatial shapes");
   const bool want_db = db.has_value() && db->defined();
@@ -330,7 +333,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
   // halo block, two waves per SIMD) instead of the per-tap im2col kernel below, reduced
   // straight into the fp32 parameter layout (weights.hip).  scripts/bench_enc.py on MI355X:
   // 158 -> 122 us at 16 x 184 x 248; the 128-channel stage-3 conv is faster below (47 vs 55 us)
-  if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && Cin == Cx && Cin == 64 && N % 8 == 0) {
+  if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && Cin == Cx && Cin == 64 && N % 8 == 0 && fold == 0) {
     ConvWgradArgs w{};
     w.src[0] = ConvSrc{cbf(x), (long)xpitch, Cin, 0};
     w.nsrc = 1;
@@ -420,7 +423,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
   long wsd[4];
   for (int d = 0; d < 4; ++d) wsd[d] = dw.stride(d);
   check(launch_enc_wgrad_reduce(a.slab, a.nsplit, a.Npad, a.Kpad, a.dbslab, dw.data_ptr<float>(), wsd, N, Cin, Cx, KH,
-                                KW, want_db ? db->data_ptr<float>() : nullptr, accumulate, stream()),
+                                KW, want_db ? db->data_ptr<float>() : nullptr, accumulate, (int)fold, stream()),
         "enc_wgrad_reduce");
 }
 
@@ -623,7 +626,7 @@ TORCH_LIBRARY_FRAGMENT(raft_amd, m) {
       "enc_conv_dgrad(Tensor[] dys, Tensor[] ws, int[] strides, int[] pads, int H, int W, Tensor? res, Tensor? mask, "
       "bool split=False) -> Tensor");
   m.def("enc_conv_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, Tensor(b!)? db, int stride, int pad, bool accumulate, "
-        "bool db_zero=False) -> ()");
+        "bool db_zero=False, int fold=0) -> ()");
   m.def("enc_prep(Tensor img0, Tensor? img1, bool split=False, bool f16=False) -> Tensor");
   m.def(
       "enc_norm_stats(Tensor? stats, int B, int HW, int N, int kind, Tensor? gamma, Tensor? beta, Tensor(a!)? rmean, "

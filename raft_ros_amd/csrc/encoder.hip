@@ -626,7 +626,7 @@ __global__ __launch_bounds__(256) void enc_wgrad_reduce_kernel(const float* __re
                                                                int Kpad, const float* __restrict__ dbslab,
                                                                float* __restrict__ dw, long s0, long s1, long s2,
                                                                long s3, int Cout, int Cin, int Cx, int KW, int taps,
-                                                               float* __restrict__ db, int accumulate) {
+                                                               float* __restrict__ db, int accumulate, int fold) {
   __shared__ float red[16][17];
   const int o = threadIdx.x & 15, sub = threadIdx.x >> 4;
   const long total = (long)Cout * taps * Cin;
@@ -655,6 +655,12 @@ __global__ __launch_bounds__(256) void enc_wgrad_reduce_kernel(const float* __re
       s += (v0 + v1) + (v2 + v3);
     }
     for (; sp < nsplit; sp += 16) s += src[sp * sstride];
+    // split-bf16 weight gradient ([X_hi | X_lo]^T dY_hi): the lo-plane columns sit ``fold``
+    // channels after the hi-plane ones, the parameter gradient is their sum
+    if (fold > 0 && e < total) {
+      const float* s2 = src + fold;
+      for (sp = sub; sp < nsplit; sp += 16) s += s2[sp * sstride];
+    }
   }
   red[sub][o] = s;
   __syncthreads();
@@ -1354,11 +1360,11 @@ hipError_t launch_enc_wgrad(const EncWgradArgs& a, int BM, int BN, hipStream_t s
 
 hipError_t launch_enc_wgrad_reduce(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, float* dw,
                                    const long* ws, int Cout, int Cin, int Cx, int KH, int KW, float* db,
-                                   bool accumulate, hipStream_t s) {
+                                   bool accumulate, int fold, hipStream_t s) {
   const long total = (long)Cout * KH * KW * Cin + (db != nullptr ? Cout : 0);
   const int blocks = (int)std::max<long>((total + 15) / 16, 1);
   hipLaunchKernelGGL(enc_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, slab, nsplit, Npad, Kpad, dbslab, dw,
-                     ws[0], ws[1], ws[2], ws[3], Cout, Cin, Cx, KW, KH * KW, db, accumulate ? 1 : 0);
+                     ws[0], ws[1], ws[2], ws[3], Cout, Cin, Cx, KW, KH * KW, db, accumulate ? 1 : 0, fold);
   return hipGetLastError();
 }
 

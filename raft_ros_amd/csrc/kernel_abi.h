@@ -167,6 +167,25 @@ struct ConvParamDesc {
   int f16;  // pack: fp16 operands instead of bf16 (fp16 AMP)
 };
 
+// Several layers' packs in one launch (pack_conv_weights_multi): job q covers the element
+// range [begin, begin + N Kf + Cin_pad Kd + N) of the launch; split_fw in ``d`` selects the
+// split-bf16 layout (aux = unused) over the bf16 / fp16 one (aux = Cout_pad of the dgrad operand)
+struct PackJob {
+  ConvParamDesc d;
+  __bf16* wf;
+  __bf16* wd;
+  float* bias;
+  long begin;
+  int N, Kf, Kd, aux;
+};
+constexpr int kPackJobs = 14;
+struct PackJobs {
+  PackJob j[kPackJobs];
+  long total;
+  int n;
+};
+static_assert(sizeof(PackJobs) <= 4000, "pack jobs must fit the kernel-argument segment");
+
 // ============================================================================ encoder convs
 constexpr int kEncTab = 256;  // K/8 decode-table entries per launch (all classes) held in the arguments
 // deeper convs (the split-bf16 layout's 3x channels) read their tables from device memory
@@ -569,6 +588,7 @@ hipError_t launch_conv_wgrad(ConvWgradArgs a, const WgradPlan& pl, hipStream_t s
 // weights.hip
 hipError_t launch_pack_conv_weights(const ConvParamDesc& d, int N, void* wf, int Kf, void* wd, int Kd, int Cout_pad,
                                     float* bias, hipStream_t s);
+hipError_t launch_pack_conv_weights_multi(const PackJobs& js, hipStream_t s);
 hipError_t launch_wgrad_reduce_params(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, int ndb,
                                       const ConvParamDesc& d, int N, int accumulate, hipStream_t s);
 hipError_t launch_wgrad_reduce_packed(const float* slab, int nsplit, int Npad, int Kpad, int K, const float* dbslab,
@@ -581,7 +601,7 @@ hipError_t launch_enc_conv3(const EncConvArgs& a, hipStream_t s);
 hipError_t launch_enc_wgrad(const EncWgradArgs& a, int BM, int BN, hipStream_t s);
 hipError_t launch_enc_wgrad_reduce(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, float* dw,
                                    const long* ws, int Cout, int Cin, int Cx, int KH, int KW, float* db,
-                                   bool accumulate, hipStream_t s);
+                                   bool accumulate, int fold, hipStream_t s);
 hipError_t launch_enc_prep(const float* i0, const float* i1, const long* st, int B, int H, int W, int nimg,
                            void* out, int split, hipStream_t s);
 hipError_t launch_enc_norm_finalize(const NormFinArgs& a, hipStream_t s);

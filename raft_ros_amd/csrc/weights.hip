@@ -79,80 +79,108 @@ __device__ __forceinline__ int split_channel(const ConvParamDesc& d, int c3, int
   return -1;
 }
 
-__global__ __launch_bounds__(256) void pack_conv_weights_split_kernel(ConvParamDesc d, int N, __bf16* __restrict__ wf,
-                                                                      int Kf, __bf16* __restrict__ wd, int Kd,
-                                                                      float* __restrict__ bias) {
+// one element i < N Kf + Cin_pad Kd + N of a split-bf16 pack (see pack_conv_weights_split)
+__device__ __forceinline__ void pack_split_elem(const ConvParamDesc& d, int N, __bf16* __restrict__ wf, int Kf,
+                                                __bf16* __restrict__ wd, int Kd, float* __restrict__ bias, long i) {
   const int taps = d.KH * d.KW;
   const int Cin3 = 3 * d.Cin_pad, G = d.split_dy;
   const long nf = (long)N * Kf;
   const long nd = wd ? (long)d.Cin_pad * Kd : 0;
-  const long total = nf + nd + N;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    if (i < nf) {
-      const int n = (int)(i / Kf), k = (int)(i - (long)n * Kf);
-      const int tap = k / Cin3;
-      __bf16 v = static_cast<__bf16>(0.f);
-      if (tap < taps) {
-        int plane;
-        const int c = split_channel(d, k - tap * Cin3, plane);
-        if (c >= 0) v = plane_of(d.scale * param_at(d, n, c, tap / d.KW, tap - (tap / d.KW) * d.KW), plane);
-      }
-      wf[i] = v;
-    } else if (i < nf + nd) {
-      const long j = i - nf;
-      const int cp = (int)(j / Kd), k = (int)(j - (long)cp * Kd);
-      const int tapf = k / (3 * G), n3 = k - tapf * 3 * G;
-      const int plane = n3 / G, n = n3 - plane * G;
-      __bf16 v = static_cast<__bf16>(0.f);
-      if (tapf < taps && n < N) {
-        const int c = real_channel(d, cp);
-        const int kyf = tapf / d.KW, kxf = tapf - kyf * d.KW;
-        if (c >= 0) v = plane_of(d.scale * param_at(d, n, c, d.KH - 1 - kyf, d.KW - 1 - kxf), plane);
-      }
-      wd[j] = v;
-    } else {
-      const int n = (int)(i - nf - nd);
-      const int which = n < d.rows[0] ? 0 : 1;
-      const float* b = d.b[which];
-      bias[n] = b ? d.scale * b[which == 0 ? n : n - d.rows[0]] : 0.f;
+  if (i < nf) {
+    const int n = (int)(i / Kf), k = (int)(i - (long)n * Kf);
+    const int tap = k / Cin3;
+    __bf16 v = static_cast<__bf16>(0.f);
+    if (tap < taps) {
+      int plane;
+      const int c = split_channel(d, k - tap * Cin3, plane);
+      if (c >= 0) v = plane_of(d.scale * param_at(d, n, c, tap / d.KW, tap - (tap / d.KW) * d.KW), plane);
     }
+    wf[i] = v;
+  } else if (i < nf + nd) {
+    const long j = i - nf;
+    const int cp = (int)(j / Kd), k = (int)(j - (long)cp * Kd);
+    const int tapf = k / (3 * G), n3 = k - tapf * 3 * G;
+    const int plane = n3 / G, n = n3 - plane * G;
+    __bf16 v = static_cast<__bf16>(0.f);
+    if (tapf < taps && n < N) {
+      const int c = real_channel(d, cp);
+      const int kyf = tapf / d.KW, kxf = tapf - kyf * d.KW;
+      if (c >= 0) v = plane_of(d.scale * param_at(d, n, c, d.KH - 1 - kyf, d.KW - 1 - kxf), plane);
+    }
+    wd[j] = v;
+  } else {
+    const int n = (int)(i - nf - nd);
+    const int which = n < d.rows[0] ? 0 : 1;
+    const float* b = d.b[which];
+    bias[n] = b ? d.scale * b[which == 0 ? n : n - d.rows[0]] : 0.f;
   }
+}
+
+// one element i < N Kf + Cin_pad Kd + N of a bf16 / fp16 pack (see pack_conv_weights)
+__device__ __forceinline__ void pack_elem(const ConvParamDesc& d, int N, __bf16* __restrict__ wf, int Kf,
+                                          __bf16* __restrict__ wd, int Kd, int Cout_pad, float* __restrict__ bias,
+                                          long i) {
+  const int taps = d.KH * d.KW;
+  const long nf = (long)N * Kf;
+  const long nd = wd ? (long)d.Cin_pad * Kd : 0;
+  if (i < nf) {
+    const int n = (int)(i / Kf), k = (int)(i - (long)n * Kf);
+    float v = 0.f;
+    const int tap = k / d.Cin_pad;
+    if (tap < taps) {
+      const int c = real_channel(d, k - tap * d.Cin_pad);
+      if (c >= 0) v = d.scale * param_at(d, n, c, tap / d.KW, tap - (tap / d.KW) * d.KW);
+    }
+    wf[i] = st16(v, d.f16 != 0);
+  } else if (i < nf + nd) {
+    const long j = i - nf;
+    const int cp = (int)(j / Kd), k = (int)(j - (long)cp * Kd);
+    float v = 0.f;
+    const int tapf = k / Cout_pad, n = k - tapf * Cout_pad;
+    if (tapf < taps && n < N) {
+      const int c = real_channel(d, cp);
+      const int kyf = tapf / d.KW, kxf = tapf - kyf * d.KW;
+      if (c >= 0) v = d.scale * param_at(d, n, c, d.KH - 1 - kyf, d.KW - 1 - kxf);
+    }
+    wd[j] = st16(v, d.f16 != 0);
+  } else {
+    const int n = (int)(i - nf - nd);
+    const int which = n < d.rows[0] ? 0 : 1;
+    const float* b = d.b[which];
+    bias[n] = b ? d.scale * b[which == 0 ? n : n - d.rows[0]] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void pack_conv_weights_split_kernel(ConvParamDesc d, int N, __bf16* __restrict__ wf,
+                                                                      int Kf, __bf16* __restrict__ wd, int Kd,
+                                                                      float* __restrict__ bias) {
+  const long total = (long)N * Kf + (wd ? (long)d.Cin_pad * Kd : 0) + N;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256)
+    pack_split_elem(d, N, wf, Kf, wd, Kd, bias, i);
 }
 
 __global__ __launch_bounds__(256) void pack_conv_weights_kernel(ConvParamDesc d, int N, __bf16* __restrict__ wf,
                                                                 int Kf, __bf16* __restrict__ wd, int Kd,
                                                                 int Cout_pad, float* __restrict__ bias) {
-  const int taps = d.KH * d.KW;
-  const long nf = (long)N * Kf;
-  const long nd = wd ? (long)d.Cin_pad * Kd : 0;
-  const long total = nf + nd + N;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    if (i < nf) {
-      const int n = (int)(i / Kf), k = (int)(i - (long)n * Kf);
-      float v = 0.f;
-      const int tap = k / d.Cin_pad;
-      if (tap < taps) {
-        const int c = real_channel(d, k - tap * d.Cin_pad);
-        if (c >= 0) v = d.scale * param_at(d, n, c, tap / d.KW, tap - (tap / d.KW) * d.KW);
-      }
-      wf[i] = st16(v, d.f16 != 0);
-    } else if (i < nf + nd) {
-      const long j = i - nf;
-      const int cp = (int)(j / Kd), k = (int)(j - (long)cp * Kd);
-      float v = 0.f;
-      const int tapf = k / Cout_pad, n = k - tapf * Cout_pad;
-      if (tapf < taps && n < N) {
-        const int c = real_channel(d, cp);
-        const int kyf = tapf / d.KW, kxf = tapf - kyf * d.KW;
-        if (c >= 0) v = d.scale * param_at(d, n, c, d.KH - 1 - kyf, d.KW - 1 - kxf);
-      }
-      wd[j] = st16(v, d.f16 != 0);
-    } else {
-      const int n = (int)(i - nf - nd);
-      const int which = n < d.rows[0] ? 0 : 1;
-      const float* b = d.b[which];
-      bias[n] = b ? d.scale * b[which == 0 ? n : n - d.rows[0]] : 0.f;
-    }
+  const long total = (long)N * Kf + (wd ? (long)d.Cin_pad * Kd : 0) + N;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256)
+    pack_elem(d, N, wf, Kf, wd, Kd, Cout_pad, bias, i);
+}
+
+// Every layer of a refinement step in one launch (the step's weights are packed once per
+// forward; 12 single-layer launches left the GPU waiting on their host-side issue): the
+// element range of job q is [begin_q, begin_{q+1}); a grid-stride loop visits the ranges in
+// order, so the job index only moves forward.
+__global__ __launch_bounds__(256) void pack_conv_weights_multi_kernel(const PackJobs js) {
+  int q = 0;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < js.total; i += (long)gridDim.x * 256) {
+    while (q + 1 < js.n && i >= js.j[q + 1].begin) ++q;
+    const PackJob& jb = js.j[q];
+    const long e = i - jb.begin;
+    if (jb.d.split_fw)
+      pack_split_elem(jb.d, jb.N, jb.wf, jb.Kf, jb.wd, jb.Kd, jb.bias, e);
+    else
+      pack_elem(jb.d, jb.N, jb.wf, jb.Kf, jb.wd, jb.Kd, jb.aux, jb.bias, e);
   }
 }
 
@@ -262,6 +290,12 @@ hipError_t launch_pack_conv_weights(const ConvParamDesc& d, int N, void* wf, int
   }
   hipLaunchKernelGGL(pack_conv_weights_kernel, grid_of(total), dim3(256), 0, s, d, N, static_cast<__bf16*>(wf), Kf,
                      static_cast<__bf16*>(wd), Kd, Cout_pad, bias);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_conv_weights_multi(const PackJobs& js, hipStream_t s) {
+  if (js.n < 1 || js.n > kPackJobs) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_conv_weights_multi_kernel, grid_of(js.total), dim3(256), 0, s, js);
   return hipGetLastError();
 }
 

@@ -110,6 +110,19 @@ def register() -> None:
         wd = w[0].new_empty((cin_pad, Kd), dtype=torch.bfloat16) if Kd > 0 else None
         return wf, wd, w[0].new_empty((n,))
 
+    @fake(lib + "pack_conv_weights_multi")
+    def _(w, b, nw, segs, nseg, scale, Kf, Kd, aux, f16=False, split=False):
+        dt = torch.float16 if f16 else torch.bfloat16
+        out, wi, si = [], 0, 0
+        for q in range(len(nw)):
+            n = sum(t.shape[0] for t in w[wi:wi + nw[q]])
+            cin_pad = sum(segs[si:si + 2 * nseg[q]][1::2])
+            wi += nw[q]
+            si += 2 * nseg[q]
+            out += [w[0].new_empty((n, Kf[q]), dtype=dt),
+                    w[0].new_empty((cin_pad, Kd[q]) if Kd[q] > 0 else (0,), dtype=dt), w[0].new_empty((n,))]
+        return out
+
     @fake(lib + "pack_conv_weights")
     def _(w, b, segs, scale, Kf, Kd, cout_pad, f16=False):
         n = sum(t.shape[0] for t in w)

@@ -184,6 +184,39 @@ def pack_weights_split_native(weights, biases, segments, scale: float = 1.0, G_d
                                          flat_segments(segments), scale, kf, kd, G_dy)
 
 
+def pack_weights_multi(layers, f16: bool = False, split: bool = False):
+    """Every layer's operands in ONE launch (csrc/weights.hip pack_conv_weights_multi_kernel).
+
+    ``layers``: [(weights, biases, segments, scale, dgrad_arg)] with ``dgrad_arg`` the bool
+    ``dgrad`` of :func:`pack_weights` (bf16 / fp16) or the ``G_dy`` of
+    :func:`pack_weights_split_native` (``split=True``; 0 = no data-gradient operand).
+    Returns [(wf, wd or None, bias)] in the layouts of those two functions."""
+    w, b, nw, segs, nseg, scales, kfs, kds, aux = [], [], [], [], [], [], [], [], []
+    for weights, biases, segments, scale, darg in layers:
+        cout = sum(t.shape[0] for t in weights)
+        _, _, kh, kw = weights[0].shape
+        cin_p = sum(p for _, p in segments)
+        w += [t.detach() for t in weights]
+        b += [None if t is None else t.detach() for t in biases]
+        nw.append(len(weights))
+        fs = flat_segments(segments)
+        segs += fs
+        nseg.append(len(fs) // 2)
+        scales.append(float(scale))
+        if split:
+            kfs.append(_round(kh * kw * 3 * cin_p, KBLK))
+            kds.append(_round(kh * kw * 3 * darg, KBLK) if darg else 0)
+            aux.append(int(darg))
+        else:
+            cout_p = _round(cout, 8)
+            kfs.append(_round(kh * kw * cin_p, KBLK))
+            kds.append(_round(kh * kw * cout_p, KBLK) if darg else 0)
+            aux.append(cout_p)
+    out = ops().pack_conv_weights_multi(w, b, nw, segs, nseg, scales, kfs, kds, aux, f16, split)
+    return [(out[3 * i], out[3 * i + 1] if out[3 * i + 1].numel() else None, out[3 * i + 2])
+            for i in range(len(layers))]
+
+
 def split_segments_by_source(source_segments) -> List[Tuple[int, int]]:
     """Segments of the expanded weight [W_hi | W_hi | W_lo] per source, in K order (every
     source's (real, padded) channel groups appear three times: its hi, lo and hi planes)."""

@@ -198,15 +198,13 @@ def _wgrad(x, dy, cd, P, grads, nd=None, split: bool = False):
     zero = nd is not None and nd["kind"] in (_INSTANCE, _BATCH_TRAIN)
     has_b = cd["b"] >= 0
     if split:
-        N, Cin, KH, KW = w.shape
+        # [X_hi | X_lo]^T dY_hi (hi / lo columns folded in the reduction), then += X_hi^T dY_lo
+        N = w.shape[0]
         cx = x.shape[3] // 3
-        f32 = dict(device=w.device, dtype=torch.float32)
-        dwa, dwb = torch.empty(N, 2 * cx, KH, KW, **f32), torch.empty(N, cx, KH, KW, **f32)
-        dba, dbb = (torch.empty(N, **f32), torch.empty(N, **f32)) if has_b else (None, None)
-        ops().enc_conv_wgrad(x[..., :2 * cx], dy[..., :N], dwa, dba, cd["stride"], cd["pad"], False, zero)
-        ops().enc_conv_wgrad(x[..., :cx], dy[..., N:2 * N], dwb, dbb, cd["stride"], cd["pad"], False, zero)
-        dw = (dwa[:, :cx] + dwa[:, cx:] + dwb)[:, :Cin].contiguous()
-        db = dba + dbb if has_b else None
+        dw = torch.empty_like(w, dtype=torch.float32)
+        db = torch.empty(N, device=w.device, dtype=torch.float32) if has_b else None
+        ops().enc_conv_wgrad(x[..., :2 * cx], dy[..., :N], dw, db, cd["stride"], cd["pad"], False, zero, cx)
+        ops().enc_conv_wgrad(x[..., :cx], dy[..., N:2 * N], dw, db, cd["stride"], cd["pad"], True, zero)
     else:
         dw = torch.empty_like(w, dtype=torch.float32)
         db = torch.empty(w.shape[0], device=w.device, dtype=torch.float32) if has_b else None

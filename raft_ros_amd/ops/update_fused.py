@@ -133,10 +133,12 @@ class _Run:
         self.wd: Dict[str, Optional[torch.Tensor]] = {}
         self.bias: Dict[str, torch.Tensor] = {}
         self.cout: Dict[str, int] = {}
-        for name, mods, segs, scale, dgrad in _LAYERS:
-            ms = mods(block)
-            wf, wd, b = C.pack_weights([m.weight for m in ms], [m.bias for m in ms], segs, scale, dgrad=dgrad,
-                                       f16=dt16 == torch.float16)
+        # every layer's operands in one launch
+        mods_of = [(name, mods(block)) for name, mods, _, _, _ in _LAYERS]
+        packed = C.pack_weights_multi([([m.weight for m in ms], [m.bias for m in ms], segs, scale, dgrad)
+                                       for (_, ms), (_, _, segs, scale, dgrad) in zip(mods_of, _LAYERS)],
+                                      f16=dt16 == torch.float16)
+        for (name, ms), (wf, wd, b) in zip(mods_of, packed):
             self.wf[name], self.wd[name], self.bias[name] = wf, wd, b
             self.cout[name] = sum(m.weight.shape[0] for m in ms)
         # context features: constant over the iterations -> one bf16 pixel-major copy
@@ -654,10 +656,12 @@ class SplitBasicUpdate:
         self.pyr = pyramid
         dev = inp.device
         self.wf, self.bias = {}, {}
-        for name, mods, _, scale, _ in _LAYERS:
-            ms = mods(block)
-            self.wf[name], _, self.bias[name] = C.pack_weights_split_native(
-                [m.weight for m in ms], [m.bias for m in ms], [s for src in _SPLIT_SOURCES[name] for s in src], scale)
+        packed = C.pack_weights_multi(
+            [([m.weight for m in mods(block)], [m.bias for m in mods(block)],
+              [s for src in _SPLIT_SOURCES[name] for s in src], scale, 0) for name, mods, _, scale, _ in _LAYERS],
+            split=True)
+        for (name, _, _, _, _), (wf, _, b) in zip(_LAYERS, packed):
+            self.wf[name], self.bias[name] = wf, b
         bf = torch.bfloat16
         e = lambda n: torch.empty(P, n, device=dev, dtype=bf)  # noqa: E731
         self.inp = C.split_pack(_pm(inp.float()), e(384), HID)

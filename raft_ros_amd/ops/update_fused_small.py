@@ -70,10 +70,10 @@ class _Run:
         self.g_all: Optional[torch.Tensor] = None  # [iters, P, GX] data-gradient rows (backward)
         self.coords = {}
         self.wf, self.wd, self.bias = {}, {}, {}
-        for name, mods, segs, dgrad in _LAYERS:
-            ms = mods(block)
-            self.wf[name], self.wd[name], self.bias[name] = C.pack_weights(
-                [m.weight for m in ms], [m.bias for m in ms], segs, 1.0, dgrad=dgrad, f16=dt16 == torch.float16)
+        packed = C.pack_weights_multi([([m.weight for m in mods(block)], [m.bias for m in mods(block)], segs, 1.0, dgrad)
+                                       for name, mods, segs, dgrad in _LAYERS], f16=dt16 == torch.float16)
+        for (name, _, _, _), (wf, wd, b) in zip(_LAYERS, packed):
+            self.wf[name], self.wd[name], self.bias[name] = wf, wd, b
         self.inp_bf = _pm(inp.detach().to(dt16).contiguous(memory_format=torch.channels_last))
         self._motion_zeroed = False
 

@@ -179,12 +179,12 @@ class _SRun:
         self.wf: Dict[str, torch.Tensor] = {}
         self.bias: Dict[str, torch.Tensor] = {}
         self.wd: Dict[str, torch.Tensor] = {}
-        for name, mods, fsrc, dsegs, dyg, scale in _LAYERS:
-            ms = mods(block)
-            # one HIP launch per conv: forward + (training) data-gradient operands, bias
-            gdy = dyg[0][2] if (keep and dsegs is not None) else 0
-            wf, wd, b = C.pack_weights_split_native([m.weight for m in ms], [m.bias for m in ms],
-                                                    [s for src in fsrc for s in src], scale, gdy)
+        # one HIP launch for every conv: forward + (training) data-gradient operands, biases
+        gdys = [dyg[0][2] if (keep and dsegs is not None) else 0 for _, _, _, dsegs, dyg, _ in _LAYERS]
+        packed = C.pack_weights_multi(
+            [([m.weight for m in mods(block)], [m.bias for m in mods(block)], [s for src in fsrc for s in src], scale,
+              gdy) for (_, mods, fsrc, _, _, scale), gdy in zip(_LAYERS, gdys)], split=True)
+        for (name, *_), gdy, (wf, wd, b) in zip(_LAYERS, gdys, packed):
             self.wf[name], self.bias[name] = wf, b
             if gdy:
                 self.wd[name] = wd

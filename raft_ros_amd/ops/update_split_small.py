@@ -82,11 +82,11 @@ class _SRun:
         self.dnet: Dict[int, torch.Tensor] = {}
         self.coords: Dict[int, torch.Tensor] = {}
         self.wf, self.bias, self.wd = {}, {}, {}
-        for name, mods, fsrc, dsegs, dyg in _LAYERS:
-            ms = mods(block)
-            gdy = dyg[0][2] if (keep and dsegs is not None) else 0
-            wf, wd, b = C.pack_weights_split_native([m.weight for m in ms], [m.bias for m in ms],
-                                                    [s for src in fsrc for s in src], 1.0, gdy)
+        gdys = [dyg[0][2] if (keep and dsegs is not None) else 0 for _, _, _, dsegs, dyg in _LAYERS]
+        packed = C.pack_weights_multi(
+            [([m.weight for m in mods(block)], [m.bias for m in mods(block)], [s for src in fsrc for s in src], 1.0,
+              gdy) for (_, mods, fsrc, _, _), gdy in zip(_LAYERS, gdys)], split=True)
+        for (name, *_), gdy, (wf, wd, b) in zip(_LAYERS, gdys, packed):
             self.wf[name], self.bias[name] = wf, b
             if gdy:
                 self.wd[name] = wd
