@@ -248,15 +248,15 @@ def run(args):
 
         step = graph_step
     step = step or train_step
-    # RAFT_HP_MAIN=1 (experiment): issue the step on a high-priority stream, so the refinement
-    # loop's critical path is dispatched ahead of the side / tail streams' kernels
-    if os.environ.get("RAFT_HP_MAIN", "0") == "1" and device.type == "cuda":
-        hp = torch.cuda.Stream(device=device, priority=-1)
-        hp.wait_stream(torch.cuda.current_stream(device))
+    # the step on a high-priority stream (ops/streams.py step_stream; RAFT_HP_MAIN=0 disables):
+    # the refinement loop's critical path is dispatched ahead of the side / tail streams' kernels
+    if args.mode == "train" and not train_graph:
+        from raft_ros_amd.ops.streams import step_context
+
         plain_step = step
 
         def step(i):  # noqa: F811
-            with torch.cuda.stream(hp):
+            with step_context(device):
                 return plain_step(i)
     for i in range(args.warmup):
         loss, metrics = step(i)

@@ -276,6 +276,35 @@ def _backward(L, P, gy, stem_rec, recs, split: bool = False):
     return grads
 
 
+def _one_block(grads):
+    """The gradients packed into views of one fp32 allocation (one multi-tensor copy).
+
+    Gradients computed on a side stream and consumed on the main stream must be
+    ``record_stream``-ed; the caching allocator then records an event on the main stream for
+    every such block when it is freed (``optimizer.zero_grad``), and each event costs the main
+    stream GPU time (~7 us on MI355X).  Packed, the ~45 context-encoder gradients free as one
+    block: one event."""
+    live = [g for g in grads if g is not None]
+    if len(live) < 2 or any(g.dtype != torch.float32 for g in live):
+        return grads
+    flat = torch.empty(sum(g.numel() for g in live), device=live[0].device, dtype=torch.float32)
+    views, off = {}, 0
+    for i, g in enumerate(grads):
+        if g is None:
+            continue
+        dims = sorted((st, n) for st, n in zip(g.stride(), g.shape) if n != 1)
+        expect, dense = 1, True
+        for st, n in dims:
+            dense = dense and st == expect
+            expect *= n
+        stride = g.stride() if dense else torch.empty(g.shape).stride()
+        views[i] = torch.as_strided(flat, g.shape, stride, off)
+        off += g.numel()
+    idx = sorted(views)
+    torch._foreach_copy_([views[i] for i in idx], [grads[i] for i in idx])
+    return [views.get(i) for i in range(len(grads))]
+
+
 class _EncoderFn(torch.autograd.Function):
     """bf16 AMP (``split=False``: bf16 NHWC output) or fp32 training (``split=True``: the
     split-bf16 network, fp32 NHWC output = hi + lo planes)."""
@@ -308,10 +337,12 @@ class _EncoderFn(torch.autograd.Function):
             # shared with main-stream gradients must not see these still in flight
             cur = torch.cuda.current_stream(gy.device)
             if cur != ctx.join:
+                grads = _one_block(grads)
                 ctx.join.wait_stream(cur)
-                for g in grads:
+                for g in grads:  # views of one block: ONE allocator event when it is freed
                     if g is not None:
                         g.record_stream(ctx.join)
+                        break
         return (None, None, None, None, *grads)
 
 

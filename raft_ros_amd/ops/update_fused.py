@@ -126,6 +126,7 @@ class _Run:
         self.g_all: Optional[torch.Tensor] = None  # [iters, P, 3*HID] data-gradient rows (backward)
         self.tail: Optional[torch.cuda.Stream] = None  # stream of the motion-encoder backward
         self.wgrads: Optional[List[torch.Tensor]] = None  # weight gradients of iterations [wg_lo, iters)
+        self.grad_out: Optional[List[torch.Tensor]] = None  # preallocated (main-stream) parameter gradients
         self.wg_lo = iters
         self.coords: Dict[int, torch.Tensor] = {}
         self.flows: Dict[int, torch.Tensor] = {}
@@ -164,10 +165,19 @@ class _Run:
         return C.geom(B, H, W, kh, kw, kh - 1 - kh // 2, kw - 1 - kw // 2)
 
     # ------------------------------------------------------------ batched weight gradients
+    def alloc_weight_grads(self) -> List[torch.Tensor]:
+        """Empty parameter-gradient tensors in ``weight_grads`` order, on the current stream."""
+        out: List[torch.Tensor] = []
+        for _, mods, _, _, _ in _LAYERS:
+            for m in mods(self.block):
+                out += [torch.empty_like(m.weight), torch.empty_like(m.bias)]
+        return out
+
     def weight_grads(self, t_lo: int = 0, t_hi: Optional[int] = None,
-                     grads: Optional[List[torch.Tensor]] = None) -> List[Optional[torch.Tensor]]:
+                     grads: Optional[List[torch.Tensor]] = None,
+                     out_bufs: Optional[List[torch.Tensor]] = None) -> List[Optional[torch.Tensor]]:
         """Parameter gradients summed over iterations [t_lo, t_hi); ``grads``: the tensors of an
-        earlier range to accumulate into (None: fresh ones)."""
+        earlier range to accumulate into (None: fresh ones, or ``out_bufs`` to write)."""
         T, P, ar = self.iters, self.P, self.arena
         t_hi = T if t_hi is None else t_hi
         for t in range(t_lo, t_hi):  # steps whose outputs fed no loss: zero dY
@@ -207,12 +217,13 @@ class _Run:
         gi = 0
         for name, mods, segs, scale, _ in _LAYERS:
             ms = mods(self.block)
-            if grads is None:
+            dst = grads if grads is not None else out_bufs
+            if dst is None:
                 wg = [torch.empty_like(m.weight) for m in ms]
                 bg = [torch.empty_like(m.bias) for m in ms]
             else:
-                wg = [grads[gi + 2 * i] for i in range(len(ms))]
-                bg = [grads[gi + 2 * i + 1] for i in range(len(ms))]
+                wg = [dst[gi + 2 * i] for i in range(len(ms))]
+                bg = [dst[gi + 2 * i + 1] for i in range(len(ms))]
             gi += 2 * len(ms)
             kh, kw = ms[0].weight.shape[2:]
             # one launch over the range, unless an operand would exceed the kernels' 32-bit
@@ -318,12 +329,15 @@ class _PackWeights(torch.autograd.Function):
             ws = _tail_stream(cur.device)
             ws.wait_event(ev)  # the steps' backward on the main stream (the tail stream is ordered)
             with torch.cuda.stream(ws):
-                grads = run.weight_grads()
+                grads = run.weight_grads(out_bufs=run.grad_out)
             cur.wait_stream(ws)
-            for g in grads:
-                g.record_stream(cur)
-            for b in run.arena.bufs.values():
-                b.record_stream(ws)
+            # no record_stream: the gradients were allocated on this stream before the event the
+            # tail stream waited for, and the arena (this stream's memory too) is released only
+            # after this stream waited for the tail stream -- every later reuse of those blocks is
+            # ordered behind the weight gradients.  (A record_stream'ed block costs an event on
+            # the recorded stream when it is freed: ~70 of them, ~0.5 ms of GPU time, used to
+            # land on the main stream at every optimizer.zero_grad.)
+            run.grad_out = None
             run.arena.bufs.clear()
             run.tail = None
             return (None, *grads)
@@ -571,6 +585,9 @@ class _Step(torch.autograd.Function):
         d_inp = None
         if t == 0:  # the last step backward to run (every other step's d net feeds it)
             if EARLY_WGRAD and dev.type == "cuda" and ar.keep:
+                # the parameter gradients the tail stream will write: main-stream memory, taken
+                # before the event the tail stream waits for (see _PackWeights.backward)
+                run.grad_out = run.alloc_weight_grads()
                 run.steps_done = torch.cuda.Event()
                 run.steps_done.record(torch.cuda.current_stream(dev))
             done = sorted(run.done)

@@ -280,17 +280,26 @@ class _SplitToken(torch.autograd.Function):
             ws = aux_stream(cur.device, "tail")
             ws.wait_event(ev)
             with torch.cuda.stream(ws):
-                grads = run.weight_grads()
+                # packed into one block: one allocator event on this stream when it is freed
+                # (see ops/encoder.py _one_block) instead of one per layer
+                grads = _one_block(run.weight_grads())
             cur.wait_stream(ws)
             for g in grads:
                 g.record_stream(cur)
-            for b in run.arena.bufs.values():
-                b.record_stream(ws)
+                break
+            # the arena is this stream's memory, released after this stream waited for ws: no
+            # record_stream needed
         else:
             grads = run.weight_grads()
         run.arena.bufs.clear()
         run.dnet.clear()
         return (None, *grads)
+
+
+def _one_block(grads):
+    from .encoder import _one_block as ob
+
+    return ob(grads)
 
 
 def _sp(g=0, g2=0, h=0, z=0, g0=0, g3=0, add=0, cout=0):

@@ -29,6 +29,7 @@ import torch
 from ..data.datasets import fetch_dataloader
 from ..eval.validate import run_validation
 from ..models import RAFT
+from ..ops.streams import step_context
 from ..parallel import ddp
 from ..utils import checkpoint, fault
 from ..utils.profiling import maybe_profiler, trace_range
@@ -107,42 +108,44 @@ def train(args: Namespace) -> str:
     profiler = prof.__enter__()
     for data_blob in _infinite(train_loader, set_epoch):
         injector.before_step(total_steps)
-        optimizer.zero_grad(set_to_none=True)
-        image1, image2, flow, valid = [x.to(dev, non_blocking=True) for x in data_blob]
-        if args.add_noise:
-            stdv = np.random.uniform(0.0, 5.0)
-            image1 = (image1 + stdv * torch.randn_like(image1)).clamp(0.0, 255.0)
-            image2 = (image2 + stdv * torch.randn_like(image2)).clamp(0.0, 255.0)
+        # the step on the high-priority step stream (ops/streams.py; RAFT_HP_MAIN=0 disables)
+        with step_context(dev):
+            optimizer.zero_grad(set_to_none=True)
+            image1, image2, flow, valid = [x.to(dev, non_blocking=True) for x in data_blob]
+            if args.add_noise:
+                stdv = np.random.uniform(0.0, 5.0)
+                image1 = (image1 + stdv * torch.randn_like(image1)).clamp(0.0, 255.0)
+                image2 = (image2 + stdv * torch.randn_like(image2)).clamp(0.0, 255.0)
 
-        with trace_range("forward"):
-            flow_predictions = net(image1, image2, iters=args.iters)
-            loss, metrics = sequence_loss(flow_predictions, flow, valid, args.gamma)
-            loss = injector.on_loss(total_steps, loss)
-        with trace_range("backward"):
-            scaler.scale(loss).backward()
-        if gsync is not None:
-            with trace_range("grad_sync"):
-                gsync.sync()
-        scaler.unscale_(optimizer)
-        gnorm = torch.nn.utils.clip_grad_norm_(model.parameters(), args.clip)
-        if use_scaler:
-            scaler.step(optimizer)  # GradScaler already skips non-finite steps
-            scaler.update()
-        else:
-            # failure guard without a host sync: a non-finite gradient norm (identical on all
-            # ranks after the all-reduce) turns the fused AdamW update into a no-op on device
-            bad = (~torch.isfinite(gnorm)).float()
-            skipped += bad
-            if fused_opt:
-                optimizer.found_inf = bad
-                optimizer.step()
-                optimizer.found_inf = None
-            elif not bool(bad):
-                optimizer.step()
-        scheduler.step()
-        logger.push(metrics)
-        if profiler is not None:
-            profiler.step()
+            with trace_range("forward"):
+                flow_predictions = net(image1, image2, iters=args.iters)
+                loss, metrics = sequence_loss(flow_predictions, flow, valid, args.gamma)
+                loss = injector.on_loss(total_steps, loss)
+            with trace_range("backward"):
+                scaler.scale(loss).backward()
+            if gsync is not None:
+                with trace_range("grad_sync"):
+                    gsync.sync()
+            scaler.unscale_(optimizer)
+            gnorm = torch.nn.utils.clip_grad_norm_(model.parameters(), args.clip)
+            if use_scaler:
+                scaler.step(optimizer)  # GradScaler already skips non-finite steps
+                scaler.update()
+            else:
+                # failure guard without a host sync: a non-finite gradient norm (identical on all
+                # ranks after the all-reduce) turns the fused AdamW update into a no-op on device
+                bad = (~torch.isfinite(gnorm)).float()
+                skipped += bad
+                if fused_opt:
+                    optimizer.found_inf = bad
+                    optimizer.step()
+                    optimizer.found_inf = None
+                elif not bool(bad):
+                    optimizer.step()
+            scheduler.step()
+            logger.push(metrics)
+            if profiler is not None:
+                profiler.step()
 
         if total_steps % VAL_FREQ == VAL_FREQ - 1:
             path = os.path.join(args.ckpt_dir, "%d_%s.pth" % (total_steps + 1, args.name))
