@@ -258,8 +258,12 @@ def run(args):
         def step(i):  # noqa: F811
             with step_context(device):
                 return plain_step(i)
+    from raft_ros_amd.ops.streams import LeadLimiter
+
+XX
     for i in range(args.warmup):
         loss, metrics = step(i)
+        lead.step_done(device)
     _sync(device)
     if distributed:
         dist.barrier()
@@ -267,6 +271,7 @@ def run(args):
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss, metrics = step(args.warmup + i)
+        lead.step_done(device)
     _sync(device)
     if distributed:
         dist.barrier()

@@ -69,3 +69,29 @@ def aux_stream(device, name: str) -> torch.cuda.Stream:
     if key not in _STREAMS:
         _STREAMS[key] = torch.cuda.Stream(device=key[0])
     return _STREAMS[key]
+
+
+class LeadLimiter:
+    """Bound how far the host runs ahead of the GPU: ``step_done()`` after issuing a step
+    records an event on the current stream and waits for the one of ``max_lead`` steps ago.
+
+    The eager training step issues its ~17 ms of host work per ~20 ms GPU step, so left alone
+    the host drifts further ahead every step; the caching allocator then holds more and more
+    blocks whose last use is still queued and keeps mapping new memory (10.9 -> 17.1 GiB
+    reserved over 40 steps, host issue 12 -> 19 ms/step from allocator churn;
+    profiles/r4_host_lead_unthrottled.log vs r4_host_lead_before_fix.log).  One or two steps of
+    lead already keep the GPU fed (the step time is unchanged)."""
+
+    def __init__(self, max_lead: int = 2):
+        self.max_lead = max_lead
+        self._events = []
+
+    def step_done(self, device) -> None:
+        dev = torch.device(device)
+        if dev.type != "cuda" or self.max_lead <= 0:
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        self._events.append(ev)
+        if len(self._events) > self.max_lead:
+            self._events.pop(0).synchronize()

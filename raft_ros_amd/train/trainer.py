@@ -29,7 +29,7 @@ import torch
 from ..data.datasets import fetch_dataloader
 from ..eval.validate import run_validation
 from ..models import RAFT
-from ..ops.streams import step_context
+from ..ops.streams import LeadLimiter, step_context
 from ..parallel import ddp
 from ..utils import checkpoint, fault
 from ..utils.profiling import maybe_profiler, trace_range
@@ -104,6 +104,7 @@ def train(args: Namespace) -> str:
     fused_opt = bool(optimizer.defaults.get("fused"))
     injector = fault.Injector.from_env(info.rank)  # RAFT_FAULT_INJECT (tests only)
     t0 = time.perf_counter()
+    lead = LeadLimiter(max_lead=2)  # host at most 2 steps ahead of the GPU (ops/streams.py)
     prof = maybe_profiler(getattr(args, "profile_dir", None))
     profiler = prof.__enter__()
     for data_blob in _infinite(train_loader, set_epoch):
@@ -146,6 +147,7 @@ def train(args: Namespace) -> str:
             logger.push(metrics)
             if profiler is not None:
                 profiler.step()
+        lead.step_done(dev)
 
         if total_steps % VAL_FREQ == VAL_FREQ - 1:
             path = os.path.join(args.ckpt_dir, "%d_%s.pth" % (total_steps + 1, args.name))
