@@ -11,6 +11,7 @@
 #include <c10/core/DeviceGuard.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <vector>
 
@@ -966,7 +967,17 @@ ConvWgradArgs wgrad_args(at::TensorList srcs, const at::Tensor& dy, at::IntArray
 }
 
 // Runs the split weight-gradient GEMM into fresh partial slabs; returns (slab, dbslab, plan).
+// RAFT_WGRAD3_MT=2: 128-row workgroups for the 1x5 / 5x1 weight gradients (A/B experiments)
+int wgrad3_mt5() {
+  static const int v = [] {
+    const char* e = std::getenv("RAFT_WGRAD3_MT");
+    return (e && std::atoi(e) == 2) ? 2 : 1;
+  }();
+  return v;
+}
+
 std::tuple<at::Tensor, at::Tensor, WgradPlan> run_wgrad(ConvWgradArgs& a, bool with_bias, const at::Tensor& like) {
+  a.mt5 = wgrad3_mt5();
   const WgradPlan pl = plan_conv_wgrad(a);
   auto opts = like.options().dtype(at::kFloat);
   auto slab = at::empty({(long)pl.nsplit * pl.Npad * a.Kpad}, opts);

@@ -2238,8 +2238,12 @@ hipError_t conv_wgrad_dispatch(const ConvWgradArgs& a, const WgradPlan& pl, hipS
   if (pl.kind == 3) {
     if (a.KH == 3)
       hipLaunchKernelGGL((conv_wgrad3_kernel<3, 3, 8, 8, 1, 3, F16>), grid, dim3(256), 0, s, a);
+    else if (a.KH == 5 && pl.BM == 128)
+      hipLaunchKernelGGL((conv_wgrad3_kernel<5, 1, 16, 4, 2, 3, F16>), grid, dim3(256), 0, s, a);
     else if (a.KH == 5)
       hipLaunchKernelGGL((conv_wgrad3_kernel<5, 1, 16, 4, 1, 3, F16>), grid, dim3(256), 0, s, a);
+    else if (pl.BM == 128)
+      hipLaunchKernelGGL((conv_wgrad3_kernel<1, 5, 1, 64, 2, 3, F16>), grid, dim3(256), 0, s, a);
     else
       hipLaunchKernelGGL((conv_wgrad3_kernel<1, 5, 1, 64, 1, 3, F16>), grid, dim3(256), 0, s, a);
     return hipGetLastError();

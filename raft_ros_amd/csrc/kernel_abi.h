@@ -138,6 +138,7 @@ struct ConvWgradArgs {
   int Npad;       // slab rows (N rounded up to the row tile)
   int xcd_g;      // >0: XCD-grouped split mapping with xcd_g splits per XCD (set by the launcher)
   int f16;        // fp16 operands (see ConvFwdArgs::f16)
+  int mt5;        // wgrad v3 on 1x5 / 5x1 convs: output-channel rows per workgroup / 64 (1 or 2)
 };
 
 // Plan of one weight-gradient launch (the caller sizes the slabs from it).
@@ -467,7 +468,9 @@ inline WgradPlan plan_conv_wgrad3(const ConvWgradArgs& a) {
   // waves per SIMD (amdgpu_waves_per_eu(2)), which hides the DMA / transposed-read latency
   // that bound the one-wave 128-channel variant (scripts/bench_convs.py on MI355X: 3x3
   // wgrads 1.2-1.3x faster, 1x5/5x1 1.05-1.1x)
-  pl.BM = 64;
+  // 1x5 / 5x1 (a.mt5 == 2): 128 output channels per workgroup -- twice the MFMAs per staged
+  // dY tile and halo block for the 5-tap convs, whose 64-channel steps are short
+  pl.BM = (!sq && a.mt5 == 2) ? 128 : 64;
   pl.BN = 64 * a.KH * a.KW;
   pl.tilesM = (a.N + pl.BM - 1) / pl.BM;
   pl.tilesN = a.Cin / 64;

@@ -175,13 +175,15 @@ class _Run:
 
     def weight_grads(self, t_lo: int = 0, t_hi: Optional[int] = None,
                      grads: Optional[List[torch.Tensor]] = None,
-                     out_bufs: Optional[List[torch.Tensor]] = None) -> List[Optional[torch.Tensor]]:
+                     out_bufs: Optional[List[torch.Tensor]] = None,
+                     only: Optional[set] = None) -> List[Optional[torch.Tensor]]:
         """Parameter gradients summed over iterations [t_lo, t_hi); ``grads``: the tensors of an
-        earlier range to accumulate into (None: fresh ones, or ``out_bufs`` to write)."""
+        earlier range to accumulate into (None: fresh ones, or ``out_bufs`` to write);
+        ``only``: compute just these layers (the others' entries are passed through)."""
         T, P, ar = self.iters, self.P, self.arena
         t_hi = T if t_hi is None else t_hi
         for t in range(t_lo, t_hi):  # steps whose outputs fed no loss: zero dY
-            if t not in self.done:
+            if t not in self.done and only is None:
                 for name in ("dmask", "dd8", "dhd", "dq1", "dq2", "dzr1", "dzr2", "dmo", "dcf", "dc1", "df1"):
                     if name in ar.bufs:
                         ar.rows(name, t, t + 1).zero_()
@@ -225,6 +227,10 @@ class _Run:
                 wg = [dst[gi + 2 * i] for i in range(len(ms))]
                 bg = [dst[gi + 2 * i + 1] for i in range(len(ms))]
             gi += 2 * len(ms)
+            if only is not None and name not in only:
+                for w, b in zip(wg, bg):
+                    out += [w, b]
+                continue
             kh, kw = ms[0].weight.shape[2:]
             # one launch over the range, unless an operand would exceed the kernels' 32-bit
             # byte offsets (very large batches / resolutions): then chunks of iterations
@@ -269,6 +275,11 @@ WGRAD_SPLIT = int(os.environ.get("RAFT_WGRAD_SPLIT", "1"))  # 2: -1.5 % (gpurun_
 HEAD_STREAM = True  # upsampler / head backward ahead of the d-net chain (see _Step.backward)
 # batched weight gradients on the tail stream beside the encoders' backward (see WeightToken)
 EARLY_WGRAD = os.environ.get("RAFT_EARLY_WGRAD", "1") != "0"
+# the batched weight gradients on 1 (tail) or 2 (tail + wgrad) streams
+WGRAD_STREAMS = int(os.environ.get("RAFT_WGRAD_STREAMS", "1"))
+# cost-balanced halves (per-layer wgrad time at config #2, profiles/r2_bench_convs_v5_all.log)
+_WGRAD_GROUP_A = {"zr1", "zr2", "heads", "convc1", "fh2", "convf2"}
+_WGRAD_GROUP_B = {"q1", "q2", "convc2", "conv", "mask2", "convf1"}
 
 
 def _head_stream(device) -> torch.cuda.Stream:
@@ -328,8 +339,19 @@ class _PackWeights(torch.autograd.Function):
         if ev is not None and run.wgrads is None and cur is not None:
             ws = _tail_stream(cur.device)
             ws.wait_event(ev)  # the steps' backward on the main stream (the tail stream is ordered)
-            with torch.cuda.stream(ws):
-                grads = run.weight_grads(out_bufs=run.grad_out)
+            if WGRAD_STREAMS > 1 and len(run.done) == run.iters:
+                # the layers in two cost-balanced groups on two streams (tail, wgrad): after the
+                # encoders' backward the weight gradients are all that is left of the step
+                ws2 = aux_stream(cur.device, "wgrad")
+                ws2.wait_event(ev)
+                with torch.cuda.stream(ws):
+                    run.weight_grads(out_bufs=run.grad_out, only=_WGRAD_GROUP_A)
+                with torch.cuda.stream(ws2):
+                    grads = run.weight_grads(out_bufs=run.grad_out, only=_WGRAD_GROUP_B)
+                cur.wait_stream(ws2)
+            else:
+                with torch.cuda.stream(ws):
+                    grads = run.weight_grads(out_bufs=run.grad_out)
             cur.wait_stream(ws)
             # no record_stream: the gradients were allocated on this stream before the event the
             # tail stream waited for, and the arena (this stream's memory too) is released only

@@ -1,0 +1,16 @@
+#!/bin/bash
+S="python scripts/rocpd_summary.py"
+C="python scripts/rocpd_concurrency.py"
+bash scripts/gpu_step.sh \
+ "150 r4k_bench_a.json python bench.py --steps 30" \
+ "150 r4k_bench_nolead.json env RAFT_MAX_LEAD=0 python bench.py --steps 30" \
+ "150 r4k_bench_a2.json python bench.py --steps 30" \
+ "150 r4k_bench_nolead2.json env RAFT_MAX_LEAD=0 python bench.py --steps 30" \
+ "300 r4k_prof_bf16.log rocprofv3 --kernel-trace -d gpurun_out/pk -o run -- python3 bench.py --steps 4 --warmup 3" \
+ "120 r4k_bf16_kernels.txt $S gpurun_out/pk/run_results.db --boundary seq_loss_fwd --steps 3 --top 60" \
+ "120 r4k_bf16_concurrency.txt $C gpurun_out/pk/run_results.db --boundary seq_loss_fwd --steps 3 --top 30 --gaps 40" \
+ "30 r4k_rm.log rm -rf gpurun_out/pk" \
+ "300 r4k_prof_1080.log rocprofv3 --kernel-trace -d gpurun_out/p1 -o run -- python3 bench.py --mode infer --image_size 1080 1920 --iters 32 --batch 1 --steps 3 --warmup 2" \
+ "120 r4k_1080_kernels.txt $S gpurun_out/p1/run_results.db --boundary corr_volume --steps 3 --top 40" \
+ "30 r4k_rm2.log rm -rf gpurun_out/p1" \
+ "900 r4k_pmc.log bash scripts/pmc_step.sh"
