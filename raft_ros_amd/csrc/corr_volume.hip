@@ -546,6 +546,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // One wave per query pixel, looping over the levels; 4 waves per block.  LDS per wave:
 // the (2r+2)^2 neighbourhood (<= 14 x 14 for r <= 6) as fp32.
 constexpr int NBMAX = 14 * 14;
+constexpr int NBPITCHED = 10 * 25;  // >= NBMAX and the pitched r = 4 / 3 layouts (10 x 25, 8 x 23)
 
 // Optionally also packs the step's flow operand (the pack_flow op, folded in: the wave
 // already holds the query's coordinates): flow8[pix] = bf16 [u, v, 0 x 6] and
@@ -590,7 +591,11 @@ __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const floa
                                                          void* __restrict__ out_, int B, int H, int W, int r_arg,
                                                          int out_ch, const FlowPack fp) {
   const int r = RC > 0 ? RC : r_arg;
-  __shared__ float nb[4][NBMAX];
+  // neighbourhood rows at a pitch that makes the blend's four reads (x-offset-major window
+  // order: lane -> (ix, iy), address iy * np + ix) bank-conflict-free for r = 4 / 3 (an exhaustive
+  // search over pitches; the natural pitch nd costs 8 extra LDS cycles per level)
+  constexpr int NP = RC == 4 ? 25 : (RC == 3 ? 23 : 0);
+  __shared__ float nb[4][NBPITCHED];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int HW = H * W;
   const long pix0 = (long)blockIdx.x * 4 + wave;
@@ -598,6 +603,7 @@ __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const floa
   const long pix = live ? pix0 : 0;
   const int b = pix / HW, p = pix - (long)b * HW;
   const int rd = 2 * r + 1, nd = rd + 1, win = rd * rd, nn = nd * nd;
+  const int np = NP > 0 ? NP : nd;
   const float cx0 = coords[(long)b * 2 * HW + p], cy0 = coords[(long)b * 2 * HW + HW + p];
   const bool finite = isfinite(cx0) && isfinite(cy0);
   if (fp.flow8 && live && lane < 8) {
@@ -655,16 +661,18 @@ __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const floa
   issue(0, fx, fy);
   for (int l = 0; l < pyr.levels; ++l) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (lane + 64 * k < nn) nb[wave][lane + 64 * k] = v[k];
+    for (int k = 0; k < 4; ++k) {
+      const int e = lane + 64 * k;
+      if (e < nn) nb[wave][(e / nd) * np + e % nd] = v[k];
+    }
     wave_lds_sync();
     if (l + 1 < pyr.levels) issue(l + 1, nfx, nfy);
     if (live)
       for (int ch = lane; ch < win; ch += 64) {
         const int ix = ch / rd, iy = ch - ix * rd;  // x-offset-major window order
-        const float* n0 = nb[wave] + iy * nd + ix;
+        const float* n0 = nb[wave] + iy * np + ix;
         const float val =
-            (1.f - fy) * ((1.f - fx) * n0[0] + fx * n0[1]) + fy * ((1.f - fx) * n0[nd] + fx * n0[nd + 1]);
+            (1.f - fy) * ((1.f - fx) * n0[0] + fx * n0[1]) + fy * ((1.f - fx) * n0[np] + fx * n0[np + 1]);
         o.put(l * win + ch, val);
       }
     wave_lds_sync();

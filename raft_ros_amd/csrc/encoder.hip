@@ -1113,6 +1113,20 @@ typedef __attribute__((address_space(3))) bf16x8 c3_lds_bf16x8;
 
 __device__ __forceinline__ int c3swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+// MFMA row m (0..31) of a wave -> its pixel (0..31) of the wave's two tile rows.  ds_read_b128
+// serves a wave in four 16-lane groups, {0-3, 12-15, 20-27} and {4-11, 16-19, 28-31} (+ 32); with
+// the natural map (pixel = m) a group spans px 0-3 / 12-15 of one tile row and px 4-11 of the
+// next, whose halo rows collide modulo 16 (the swizzle's period) -- ~1 extra LDS cycle per A
+// read.  Mapping each group onto one tile row (16 consecutive halo rows) makes it conflict-free.
+__device__ __forceinline__ int c3_pix(int m) {
+  if (m < 4) return m;               // group 0: px 0-3
+  if (m < 12) return 16 + (m - 4);   // group 1: px 0-7 of the second row
+  if (m < 16) return 4 + (m - 12);   // group 0: px 4-7
+  if (m < 20) return 24 + (m - 16);  // group 1: px 8-11
+  if (m < 28) return 8 + (m - 20);   // group 0: px 8-15
+  return 28 + (m - 28);              // group 1: px 12-15
+}
+
 __device__ __forceinline__ void c3_dma16(__amdgpu_buffer_rsrc_t r, unsigned lds_byte, unsigned voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (c3_lds_void*)(uintptr_t)lds_byte, 16, voff, 0, 0, 0);
 }
@@ -1163,7 +1177,8 @@ __global__ __launch_bounds__(512) void enc_conv3_kernel(const EncConvArgs a, int
 
   // fragment geometry: this lane's pixel (py, px) of the tile and its 64-channel half
   const int lh = lane >> 5;
-  const int py = 2 * wave + ((lane >> 4) & 1), px = lane & 15;
+  const int pm = c3_pix(lane & 31);
+  const int py = 2 * wave + (pm >> 4), px = pm & 15;
   const int hb = py * C3_B + px;  // halo row of the pixel at tap (0, 0) offset (-1, -1)
   const int n0 = lane & 31;       // B columns n0 and n0 + 32
   const unsigned wrow = ldsW + n0 * 1152;
@@ -1217,7 +1232,7 @@ __global__ __launch_bounds__(512) void enc_conv3_kernel(const EncConvArgs a, int
       float sm = 0.f, sq = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int i = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;  // tile pixel of this element
+        const int i = wave * 32 + c3_pix((r & 3) + 8 * (r >> 2) + 4 * lh);  // tile pixel of this element
         const float v = acc[j][r] + bias[j];
         const bool valid = (i >> 4) < vh && (i & 15) < vw;
         sm += valid ? v : 0.f;

@@ -1,5 +1,6 @@
 #!/bin/bash
 bash scripts/gpu_step.sh \
+ "400 r4l_enc_lookup_tests.log python -u -m pytest tests/test_encoder_gpu.py tests/test_kernels_gpu.py tests/test_golden_gpu.py -x -q --timeout 180 --timeout-method thread" \
  "300 r4l_wgrad_mt2_tests.log env RAFT_WGRAD3_MT=2 python -u -m pytest tests/test_conv_gpu.py tests/test_update_fused_gpu.py -x -q -k wgrad --timeout 180 --timeout-method thread" \
  "300 r4l_streams2_tests.log env RAFT_WGRAD_STREAMS=2 python -u -m pytest tests/test_update_fused_gpu.py -x -q --timeout 180 --timeout-method thread" \
  "200 r4l_convs_mt1.log python scripts/bench_convs.py" \
