@@ -260,7 +260,8 @@ def run(args):
                 return plain_step(i)
     from raft_ros_amd.ops.streams import LeadLimiter
 
-XX
+    # the trainer's bound on how far the host runs ahead (RAFT_MAX_LEAD=0: unbounded)
+    lead = LeadLimiter(max_lead=int(os.environ.get("RAFT_MAX_LEAD", "2")))
     for i in range(args.warmup):
         loss, metrics = step(i)
         lead.step_done(device)
