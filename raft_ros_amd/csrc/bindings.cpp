@@ -967,11 +967,15 @@ ConvWgradArgs wgrad_args(at::TensorList srcs, const at::Tensor& dy, at::IntArray
 }
 
 // Runs the split weight-gradient GEMM into fresh partial slabs; returns (slab, dbslab, plan).
-// RAFT_WGRAD3_MT=2: 128-row workgroups for the 1x5 / 5x1 weight gradients (A/B experiments)
+// 128-row workgroups for the 1x5 / 5x1 weight gradients: 12 % slower per launch standalone
+// (scripts/bench_convs.py, profiles/r4_convs_wgrad_mt.log) but +0.4 % on the training step
+// (5 of 5 interleaved A/B pairs, profiles/r4_bench_wgrad_mt_ab.log): half the workgroups, so the
+// tail stream leaves more of the chip to the encoders' backward running beside it.
+// RAFT_WGRAD3_MT=1 restores 64-row workgroups.
 int wgrad3_mt5() {
   static const int v = [] {
     const char* e = std::getenv("RAFT_WGRAD3_MT");
-    return (e && std::atoi(e) == 2) ? 2 : 1;
+    return (e && std::atoi(e) == 1) ? 1 : 2;
   }();
   return v;
 }

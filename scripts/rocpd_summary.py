@@ -19,9 +19,17 @@ def main():
     ap.add_argument("--steps", type=int, default=3, help="summarise the last N steps")
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--by-grid", action="store_true", help="split each kernel by its launch grid (shapes)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
-    rows = c.execute("select name, start, end from kernels order by start").fetchall()
+    if a.by_grid:
+        cols = [r[1] for r in c.execute("pragma table_info(kernels)").fetchall()]
+        gx = next((x for x in ("grid_size_x", "grid_x", "grid_size") if x in cols), None)
+        gy = next((x for x in ("grid_size_y", "grid_y") if x in cols), None)
+        sel = (f"'grid=' || {gx}" + (f" || 'x' || {gy}" if gy else "") + " || ' ' || name") if gx else "name"
+        rows = c.execute(f"select {sel}, start, end from kernels order by start").fetchall()
+    else:
+        rows = c.execute("select name, start, end from kernels order by start").fetchall()
     if a.boundary:
         idx = [i for i, r in enumerate(rows) if a.boundary in r[0]]
         if len(idx) > a.steps:
