@@ -864,9 +864,13 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
 
 
 __global__ __launch_bounds__(256) void enc_norm_bwd_reduce_kernel(const NormBwdArgs a) {
-  __shared__ float red[2048];
+  __shared__ float red[8 * (256 + 32)];
   const int r = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int N = a.N, G = N / 8, PPB = 256 / G;
+  // element-e block pitch: the partials of one element occupy PPB x G words; padding the pitch
+  // to (a multiple of 64 banks) + G puts the G-lane groups of different elements read by one
+  // instruction on different banks (the unpadded 256-word pitch read N = 64 4-way conflicted)
+  const int EP = (PPB * G + 63) / 64 * 64 + G;
   const int cg = tid % G, pr = tid / G;
   const bool active = pr < PPB;
   const int n = cg * 8;
@@ -931,14 +935,14 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_reduce_kernel(const NormBwdA
     // layout [e][pr][cg]: consecutive lanes (consecutive cg) hit consecutive banks
     if (active)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) red[(e * PPB + pr) * G + cg] = S[qd][e];
+      for (int e = 0; e < 8; ++e) red[e * EP + pr * G + cg] = S[qd][e];
     __syncthreads();
     if (tid < N) {
       // lane -> (chunk tc, element te) with the chunk fastest, so the 64 lanes of a read read
       // consecutive words (the element-fastest order put 8 lanes 256 words apart on one bank)
       const int tc = tid % G, te = tid / G;
       float s = 0.f;
-      for (int k = 0; k < PPB; ++k) s += red[(te * PPB + k) * G + tc];
+      for (int k = 0; k < PPB; ++k) s += red[te * EP + k * G + tc];
       a.part[(((long)b * a.R + r) * 4 + qd) * N + tc * 8 + te] = s;
     }
     __syncthreads();

@@ -191,8 +191,10 @@ def test_encoder_matches_fp32_module(name):
             assert p.grad.abs().max() < 1e-3 * scale, n
             continue
         floor = _rel(a.grad, q.grad)
-        # BatchNorm affine gradients sum dy * xhat over whole batches (more cancellation)
-        factor = 1.5 if ".norm" in n else 1.25
+        # BatchNorm affine and conv bias gradients are sums of dy (* xhat) over whole batches:
+        # more cancellation, so bf16 noise is a larger fraction of them (a norm-free encoder's
+        # bias gradients measured 0.12-0.16 relative for both MIOpen autocast and native)
+        factor = 1.5 if (".norm" in n or n.endswith(".bias")) else 1.25
         assert _rel(p.grad, q.grad) <= factor * floor + 5e-3, (n, _rel(p.grad, q.grad), floor)
     for (n, b), (_, rb) in zip(enc.named_buffers(), ref.named_buffers()):
         if b.dtype.is_floating_point:
