@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <array>
 #include <cstring>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -24,6 +25,21 @@ namespace {
 
 constexpr int kBM = 128;  // conv M tile (pixels), fixed for every encoder conv
 constexpr int kNormChunks = 64;
+// chunking of the norm-backward reduction (experiments: RAFT_NORM_R / RAFT_NORM_PIX)
+int norm_chunks_max() {
+  static const int v = [] {
+    const char* e = std::getenv("RAFT_NORM_R");
+    return e ? std::max(1, std::atoi(e)) : kNormChunks;
+  }();
+  return v;
+}
+int norm_chunk_pixels() {
+  static const int v = [] {
+    const char* e = std::getenv("RAFT_NORM_PIX");
+    return e ? std::max(16, std::atoi(e)) : 256;
+  }();
+  return v;
+}
 
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
@@ -560,7 +576,7 @@ std::vector<at::Tensor> enc_norm_bwd_impl(const at::Tensor& g, const at::Tensor&
   a.B = B;
   a.HW = HW;
   a.N = N;
-  a.R = std::min(kNormChunks, std::max(1, HW / 256));
+  a.R = std::min(norm_chunks_max(), std::max(1, HW / norm_chunk_pixels()));
   a.kind = (int)kind;
   a.split = split ? 1 : 0;
   a.f16 = g.scalar_type() == at::kHalf ? 1 : 0;
