@@ -31,10 +31,13 @@ def test_native_fp32_matches_reference_fixture(cuda, small):
         assert d_lo <= 1e-2 and d_up <= 1e-2, (p, d_lo, d_up)
 
 
+@pytest.mark.parametrize("corr_fp32", [False, True], ids=["bf16_volume", "fp32_volume"])
 @pytest.mark.parametrize("small", [False, True])
-def test_native_bf16_within_3x_of_torch_autocast(cuda, small):
+def test_native_bf16_within_3x_of_torch_autocast(cuda, small, corr_fp32):
+    """bf16 AMP vs the reference fixture; ``corr_fp32``: the correlation volume kept fp32-faithful
+    under bf16 AMP as the reference does (core/raft.py:102-103, ``--corr_fp32``)."""
     fix = fixture()
-    nat = model(small, fix, mixed_precision=True, amp_dtype="bf16").to(cuda)
+    nat = model(small, fix, mixed_precision=True, amp_dtype="bf16", corr_fp32=corr_fp32).to(cuda)
     amp = model(small, fix, mixed_precision=True, amp_dtype="bf16", fused_update=False,
                 native_encoder=False).to(cuda)
     name = "small" if small else "base"
@@ -43,7 +46,8 @@ def test_native_bf16_within_3x_of_torch_autocast(cuda, small):
         _, up_a = run(amp, cuda, fix, p)
         ref = torch.from_numpy(fix[f"{name}/pair{p}/flow_up_sub"])
         dn, da = epe(up_n, ref), epe(up_a, ref)
-        print(f"\n{name} pair {p}: bf16 EPE vs reference  native {dn:.4f}  torch autocast {da:.4f} px "
+        print(f"\n{name} pair {p}: bf16 EPE vs reference ({'fp32' if corr_fp32 else 'bf16'} volume)  native {dn:.4f}  "
+              f"torch autocast {da:.4f} px "
               f"(mean |flow| {float(ref.norm(dim=1).mean()):.2f})")
         assert dn <= max(3 * da, 1e-3), (p, dn, da)
 
