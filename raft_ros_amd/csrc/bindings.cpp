@@ -1058,13 +1058,16 @@ ConvParamDesc param_desc(at::TensorList w, const c10::List<c10::optional<at::Ten
 
 // Weight gradient of all stacked parameters of one conv, written (or accumulated) into the
 // parameter gradients themselves: split GEMM -> fixed-order slab reduce (deterministic).
+// fold (split-bf16 training): the sources hold every segment as [hi | lo] planes (2 x seg_pad
+// channels each), and the parameter gradient is the sum of the two planes' columns.
 void conv_wgrad_params(at::TensorList srcs, const at::Tensor& dy, at::IntArrayRef geom, at::TensorList wgrad,
                        const c10::List<c10::optional<at::Tensor>>& bgrad, at::IntArrayRef segs, double scale,
-                       bool accumulate) {
+                       bool accumulate, bool fold) {
   ConvParamDesc d = param_desc(wgrad, bgrad, segs, scale, "conv_wgrad_params");
+  d.fold = fold ? 1 : 0;
   const int N = d.rows[0] + d.rows[1];
   ConvWgradArgs a = wgrad_args(srcs, dy, geom, N);
-  TORCH_CHECK(a.Cin == d.Cin_pad && a.KH == d.KH && a.KW == d.KW,
+  TORCH_CHECK(a.Cin == (fold ? 2 : 1) * d.Cin_pad && a.KH == d.KH && a.KW == d.KW,
               "raft_amd conv_wgrad_params: sources / geometry do not match the parameter layout");
   bool with_bias = false;
   for (size_t i = 0; i < bgrad.size(); ++i) with_bias = with_bias || bgrad.get(i).has_value();
@@ -1403,7 +1406,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("conv_wgrad(Tensor[] srcs, Tensor dy, int[] geom, int N, Tensor(a!) dw, Tensor(b!)? db, "
         "bool accumulate=True) -> ()");
   m.def("conv_wgrad_params(Tensor[] srcs, Tensor dy, int[] geom, Tensor(a!)[] wgrad, Tensor?[] bgrad, int[] segs, "
-        "float scale, bool accumulate) -> ()");
+        "float scale, bool accumulate, bool fold=False) -> ()");
   m.def("pack_conv_weights_split(Tensor[] w, Tensor?[] b, int[] segs, float scale, int Kf, int Kd, int G_dy) -> "
         "(Tensor, Tensor?, Tensor)");
   m.def("pack_conv_weights_multi(Tensor[] w, Tensor?[] b, int[] nw, int[] segs, int[] nseg, float[] scale, "

@@ -166,6 +166,9 @@ struct ConvParamDesc {
   // [hi | lo | hi] of width G (k = tapflip * 3G + plane * G + n) against [W_hi | W_hi | W_lo]
   int split_fw, split_dy;
   int f16;  // pack: fp16 operands instead of bf16 (fp16 AMP)
+  // reduce: the weight-gradient columns hold every segment as [hi | lo] planes of seg_pad
+  // channels (split-bf16 training, [X_hi | X_lo]^T dY_hi); the parameter gradient is their sum
+  int fold;
 };
 
 // Several layers' packs in one launch (pack_conv_weights_multi): job q covers the element

@@ -202,6 +202,23 @@ __device__ __forceinline__ float combine4(float v, float* red) {
   return ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
 }
 
+// fold layout (ConvParamDesc::fold): packed column kk of a tap -> real channel of its hi-plane
+// column (-1 for padding and for lo-plane columns, which the hi lane sums), lo = plane offset
+__device__ __forceinline__ int fold_channel(const ConvParamDesc& d, int kk, int& lo) {
+  int r0 = 0, p0 = 0;
+  for (int i = 0; i < d.nseg; ++i) {
+    if (kk < p0 + d.seg_pad[i]) {
+      const int o = kk - p0;
+      lo = d.seg_pad[i];
+      return o < d.seg_real[i] ? r0 + o : -1;
+    }
+    if (kk < p0 + 2 * d.seg_pad[i]) return -1;
+    r0 += d.seg_real[i];
+    p0 += 2 * d.seg_pad[i];
+  }
+  return -1;
+}
+
 // Parameter-layout output (scaled, un-padded, split into the stacked parameters).
 __global__ __launch_bounds__(256) void wgrad_reduce_params_kernel(const float* __restrict__ slab, int nsplit,
                                                                   int Npad, int Kpad,
@@ -209,18 +226,24 @@ __global__ __launch_bounds__(256) void wgrad_reduce_params_kernel(const float* _
                                                                   ConvParamDesc d, int N, int accumulate) {
   __shared__ float red[256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int kch = (d.KH * d.KW * d.Cin_pad + 63) / 64;
+  const int ktap = d.fold ? 2 * d.Cin_pad : d.Cin_pad;  // packed columns per tap
+  const int kch = (d.KH * d.KW * ktap + 63) / 64;
   const long blk = blockIdx.x;
   if (blk < (long)N * kch) {
     const int n = (int)(blk / kch);
     const int k = (int)(blk - (long)n * kch) * 64 + lane;
-    const int tap = k / d.Cin_pad;
+    const int tap = k / ktap;
     const bool live = tap < d.KH * d.KW;
-    const float v = combine4(live ? split_sum(slab + (long)n * Kpad + k, (long)Npad * Kpad, nsplit, wave) : 0.f,
-                             red);
-    if (wave != 0 || !live) return;
-    const int c = real_channel(d, k - tap * d.Cin_pad);
-    if (c < 0) return;
+    int lo = 0;
+    const int c = !live ? -1 : (d.fold ? fold_channel(d, k - tap * ktap, lo) : real_channel(d, k - tap * ktap));
+    const long ss = (long)Npad * Kpad;
+    float v0 = 0.f;
+    if (c >= 0) {
+      v0 = split_sum(slab + (long)n * Kpad + k, ss, nsplit, wave);
+      if (lo) v0 += split_sum(slab + (long)n * Kpad + k + lo, ss, nsplit, wave);
+    }
+    const float v = combine4(v0, red);
+    if (wave != 0 || c < 0) return;
     const int which = n < d.rows[0] ? 0 : 1;
     const int nn = which == 0 ? n : n - d.rows[0];
     const int ky = tap / d.KW, kx = tap - ky * d.KW;
@@ -301,7 +324,7 @@ hipError_t launch_pack_conv_weights_multi(const PackJobs& js, hipStream_t s) {
 
 hipError_t launch_wgrad_reduce_params(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, int ndb,
                                       const ConvParamDesc& d, int N, int accumulate, hipStream_t s) {
-  const long kch = (d.KH * d.KW * d.Cin_pad + 63) / 64;
+  const long kch = (d.KH * d.KW * (d.fold ? 2 : 1) * d.Cin_pad + 63) / 64;
   const long blocks = (long)N * kch + (dbslab ? (N + 63) / 64 : 0);
   hipLaunchKernelGGL(wgrad_reduce_params_kernel, dim3((unsigned)blocks), dim3(256), 0, s, slab, nsplit, Npad, Kpad,
                      dbslab, ndb, d, N, accumulate);

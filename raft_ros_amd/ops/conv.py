@@ -127,13 +127,15 @@ def flat_segments(segments: Sequence[Tuple[int, int]]) -> List[int]:
     return [v for rp in segments for v in rp]
 
 
-def conv_wgrad_params(srcs, dy, g, wgrads, bgrads, segments, scale: float = 1.0, accumulate: bool = False):
+def conv_wgrad_params(srcs, dy, g, wgrads, bgrads, segments, scale: float = 1.0, accumulate: bool = False,
+                      fold: bool = False):
     """Weight (+bias) gradients of 1..2 stacked conv parameters written straight into
     ``wgrads`` / ``bgrads`` (parameter layout, any strides).  A source with fewer rows
     than the pixel count is periodic (row p % rows), e.g. context features shared by
-    every refinement iteration of a batched update-block weight gradient."""
+    every refinement iteration of a batched update-block weight gradient.  ``fold``: every
+    source holds its segment as [hi | lo] split planes; their columns are summed."""
     ops().conv_wgrad_params(list(srcs), dy, g, list(wgrads), list(bgrads), flat_segments(segments), scale,
-                            accumulate)
+                            accumulate, fold)
 
 
 def split_planes(n: int, G: int) -> int:

@@ -157,6 +157,23 @@ def wgrad_split(srcs, dy: torch.Tensor, G_dy: int, geom, shape, segments, scale:
     return dW, db
 
 
+def wgrad_split_params(srcs, dy: torch.Tensor, G_dy: int, geom, wgrads, bgrads, segments, scale: float = 1.0,
+                       concat: bool = False, accumulate: bool = False) -> None:
+    """``wgrad_split`` reduced straight into the parameter gradients ``wgrads`` / ``bgrads``
+    (1..2 stacked parameters, any strides): [X_hi | X_lo]^T dY_hi with the hi / lo plane columns
+    summed by the reduction (csrc/weights.hip, ConvParamDesc::fold), then X_hi^T dY_lo
+    accumulated -- two GEMMs and two reductions per conv, no fold / unpack / add kernels."""
+    v1 = [t[:, :2 * w] for t, w in srcs]
+    v2 = [t[:, :w] for t, w in srcs]
+    if concat and len(srcs) > 1:
+        n = dy.shape[0]
+        rep = lambda v: v if v.shape[0] == n else v.repeat(n // v.shape[0], 1)  # noqa: E731
+        v1 = [torch.cat([rep(v) for v in v1], dim=1)]
+        v2 = [torch.cat([rep(v) for v in v2], dim=1)]
+    C.conv_wgrad_params(v1, dy[:, :G_dy], geom, wgrads, bgrads, segments, scale, accumulate=accumulate, fold=True)
+    C.conv_wgrad_params(v2, dy[:, G_dy:2 * G_dy], geom, wgrads, bgrads, segments, scale, accumulate=True)
+
+
 class _SRun:
     """Everything one RAFT forward's split steps share."""
 
@@ -173,6 +190,7 @@ class _SRun:
         self.coords0 = coords0
         self.done = set()
         self.g_all: Optional[torch.Tensor] = None
+        self.grad_out: Optional[List[torch.Tensor]] = None
         self.dnet: Dict[int, torch.Tensor] = {}  # step -> split d(hidden state in) rows
         self.coords: Dict[int, torch.Tensor] = {}
         self.flows: Dict[int, torch.Tensor] = {}
@@ -208,7 +226,15 @@ class _SRun:
         return self.arena.take(name, t, width, dtype=dtype, slots=slots)
 
     # ------------------------------------------------------------ batched weight gradients
-    def weight_grads(self) -> List[torch.Tensor]:
+    def alloc_weight_grads(self) -> List[torch.Tensor]:
+        """Empty parameter gradients in ``weight_grads`` order, on the current stream."""
+        out: List[torch.Tensor] = []
+        for _, mods, *_ in _LAYERS:
+            for m in mods(self.block):
+                out += [torch.empty_like(m.weight), torch.empty_like(m.bias)]
+        return out
+
+    def weight_grads(self, out_bufs: Optional[List[torch.Tensor]] = None) -> List[torch.Tensor]:
         T, P, ar = self.iters, self.P, self.arena
         for t in range(T):
             if t not in self.done:
@@ -226,27 +252,28 @@ class _SRun:
             return ar.rows(name, t0, t1)
 
         out: List[torch.Tensor] = []
+        gi = 0
         for name, mods, fsrc, _dsegs, _dyg, scale in _LAYERS:
             ms = mods(self.block)
+            if out_bufs is not None:
+                wg = [out_bufs[gi + 2 * i] for i in range(len(ms))]
+                bg = [out_bufs[gi + 2 * i + 1] for i in range(len(ms))]
+            else:
+                wg = [torch.empty_like(m.weight) for m in ms]
+                bg = [torch.empty_like(m.bias) for m in ms]
+            gi += 2 * len(ms)
             kh, kw = ms[0].weight.shape[2:]
-            cout = sum(m.weight.shape[0] for m in ms)
-            shape = (cout, ms[0].weight.shape[1], kh, kw)
             segs = [s for src in fsrc for s in src]
             srcs_spec, (dyn, gdy) = _WGRAD[name]
             per_iter = max([3 * w * 2 * P for _, w, _ in srcs_spec] + [3 * gdy * 2 * P, 1536 * 2 * P])
             chunk = max(1, min(T, _I32 // per_iter))
-            dW = db = None
             for t0 in range(0, T, chunk):
                 t1 = min(T, t0 + chunk)
                 srcs = [(rows(n, t0, t1)[:, c0:c0 + 3 * w], w) for n, w, c0 in srcs_spec]
-                g, b = wgrad_split(srcs, rows(dyn, t0, t1), gdy, self.geom(kh, kw, t1 - t0), shape, segs, scale)
-                dW = g if dW is None else dW + g
-                db = b if db is None else db + b
-            r0 = 0
-            for m in ms:
-                r1 = r0 + m.weight.shape[0]
-                out += [dW[r0:r1].to(m.weight.dtype), db[r0:r1].to(m.bias.dtype)]
-                r0 = r1
+                wgrad_split_params(srcs, rows(dyn, t0, t1), gdy, self.geom(kh, kw, t1 - t0), wg, bg, segs, scale,
+                                   accumulate=t0 > 0)
+            for w, b in zip(wg, bg):
+                out += [w, b]
         return out
 
 
@@ -280,15 +307,12 @@ class _SplitToken(torch.autograd.Function):
             ws = aux_stream(cur.device, "tail")
             ws.wait_event(ev)
             with torch.cuda.stream(ws):
-                # packed into one block: one allocator event on this stream when it is freed
-                # (see ops/encoder.py _one_block) instead of one per layer
-                grads = _one_block(run.weight_grads())
+                # straight into main-stream gradients allocated before the event ws waited for
+                # (ops/update_fused.py _PackWeights.backward): no record_stream, no copies
+                grads = run.weight_grads(out_bufs=run.grad_out)
             cur.wait_stream(ws)
-            for g in grads:
-                g.record_stream(cur)
-                break
-            # the arena is this stream's memory, released after this stream waited for ws: no
-            # record_stream needed
+            run.grad_out = None
+            # the arena is this stream's memory, released after this stream waited for ws
         else:
             grads = run.weight_grads()
         run.arena.bufs.clear()
@@ -470,6 +494,9 @@ class _SplitStep(torch.autograd.Function):
 
         d_net_out = d_inp = None
         if t == 0:  # the last step backward to run
+            # the parameter gradients the tail stream writes: main-stream memory taken before the
+            # event it waits for (ops/update_split.py _SplitToken.backward)
+            run.grad_out = run.alloc_weight_grads()
             run.steps_done = torch.cuda.Event()
             run.steps_done.record(torch.cuda.current_stream(dev))
             d_net_out = _nchw(d_net[:, :HID].float() + d_net[:, HID:2 * HID].float(), B, H, W)

@@ -24,7 +24,7 @@ import torch
 from . import conv as C
 from ._ext import ops
 from .update_fused import _Arena, _nchw, _pm
-from .update_split import _I32, SplitWeightToken, _SplitToken, _sp, wgrad_split
+from .update_split import _I32, SplitWeightToken, _SplitToken, _sp, wgrad_split_params
 
 HID, CTX = 96, 64
 MOT_PAD = 88
@@ -78,6 +78,7 @@ class _SRun:
         self.arena = _Arena(iters, P, inp.device, keep)
         self.coords0 = coords0
         self.done = set()
+        self.grad_out: Optional[List[torch.Tensor]] = None
         self.g_all: Optional[torch.Tensor] = None
         self.dnet: Dict[int, torch.Tensor] = {}
         self.coords: Dict[int, torch.Tensor] = {}
@@ -109,7 +110,15 @@ class _SRun:
             return ring[t % 2]
         return self.arena.take(name, t, width, dtype=dtype, slots=slots)
 
-    def weight_grads(self) -> List[torch.Tensor]:
+    def alloc_weight_grads(self) -> List[torch.Tensor]:
+        """Empty parameter gradients in ``weight_grads`` order, on the current stream."""
+        out: List[torch.Tensor] = []
+        for _, mods, *_ in _LAYERS:
+            for m in mods(self.block):
+                out += [torch.empty_like(m.weight), torch.empty_like(m.bias)]
+        return out
+
+    def weight_grads(self, out_bufs: Optional[List[torch.Tensor]] = None) -> List[torch.Tensor]:
         T, P, ar = self.iters, self.P, self.arena
         for t in range(T):
             if t not in self.done:
@@ -125,29 +134,29 @@ class _SRun:
             return ar.rows(name, t0, t1)
 
         out: List[torch.Tensor] = []
+        gi = 0
         for name, mods, fsrc, _dsegs, _dyg in _LAYERS:
             ms = mods(self.block)
+            if out_bufs is not None:
+                wg = [out_bufs[gi + 2 * i] for i in range(len(ms))]
+                bg = [out_bufs[gi + 2 * i + 1] for i in range(len(ms))]
+            else:
+                wg = [torch.empty_like(m.weight) for m in ms]
+                bg = [torch.empty_like(m.bias) for m in ms]
+            gi += 2 * len(ms)
             kh, kw = ms[0].weight.shape[2:]
-            cout = sum(m.weight.shape[0] for m in ms)
-            shape = (cout, ms[0].weight.shape[1], kh, kw)
             segs = [s for src in fsrc for s in src]
             srcs_spec, (dyn, gdy) = _WGRAD[name]
             multi = len(srcs_spec) > 1
             per_iter = 6 * P * (sum(w for _, w in srcs_spec) if multi else max(w for _, w in srcs_spec) + gdy)
             chunk = max(1, min(T, _I32 // max(per_iter, 1)))
-            dW = db = None
             for t0 in range(0, T, chunk):
                 t1 = min(T, t0 + chunk)
                 srcs = [(rows(n, t0, t1)[:, :3 * w], w) for n, w in srcs_spec]
-                g, b = wgrad_split(srcs, rows(dyn, t0, t1), gdy, self.geom(kh, kw, t1 - t0), shape, segs,
-                                   concat=multi)
-                dW = g if dW is None else dW + g
-                db = b if db is None else db + b
-            r0 = 0
-            for m in ms:
-                r1 = r0 + m.weight.shape[0]
-                out += [dW[r0:r1].to(m.weight.dtype), db[r0:r1].to(m.bias.dtype)]
-                r0 = r1
+                wgrad_split_params(srcs, rows(dyn, t0, t1), gdy, self.geom(kh, kw, t1 - t0), wg, bg, segs,
+                                   concat=multi, accumulate=t0 > 0)
+            for w, b in zip(wg, bg):
+                out += [w, b]
         return out
 
 
@@ -278,6 +287,9 @@ class _Step(torch.autograd.Function):
         run.done.add(t)
         d_net_out = d_inp = None
         if t == 0:
+            # the parameter gradients the tail stream writes: main-stream memory taken before the
+            # event it waits for (ops/update_split.py _SplitToken.backward)
+            run.grad_out = run.alloc_weight_grads()
             run.steps_done = torch.cuda.Event()
             run.steps_done.record(torch.cuda.current_stream(dev))
             d_net_out = _nchw(d_net[:, :HID].float() + d_net[:, HID:2 * HID].float(), B, H, W)
