@@ -31,6 +31,7 @@
 // Tiling: 256 threads = 4 wave64s in a 2x2 arrangement, v_mfma_f32_32x32x16_bf16,
 // BK = 64 per LDS stage, XCD-aware tile order.
 #include "common.h"
+#include <cstdlib>
 #include "kernel_abi.h"
 
 #include <algorithm>
@@ -2115,7 +2116,11 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
     // narrow output (flow-head conv2): register dot products, not a GEMM
     const int lpp = a.Cin / 8;
     const int ppb = 4 * (64 / lpp);
-    const long blocks = std::min<long>((a.P + ppb - 1) / ppb, 2048);
+    static const long max_blocks = [] {
+      const char* e = std::getenv("RAFT_N2_BLOCKS");  // experiments (scripts/bench_convs.py fh2 row)
+      return e ? std::max(64L, std::atol(e)) : 2048L;
+    }();
+    const long blocks = std::min<long>((a.P + ppb - 1) / ppb, max_blocks);
     if (lpp == 8) hipLaunchKernelGGL(conv_n2_fwd_kernel<8>, dim3(blocks), dim3(256), 0, s, a);
     else if (lpp == 16) hipLaunchKernelGGL(conv_n2_fwd_kernel<16>, dim3(blocks), dim3(256), 0, s, a);
     else if (lpp == 32) hipLaunchKernelGGL(conv_n2_fwd_kernel<32>, dim3(blocks), dim3(256), 0, s, a);
