@@ -120,10 +120,16 @@ static void test_wgrad_plans() {
         for (auto& d : dims)
           for (int nsrc = 1; nsrc <= 3; ++nsrc) {
             if (Cin % nsrc || (Cin / nsrc) % (nsrc > 1 ? 128 : 8)) continue;
-            const ConvWgradArgs a = make_args(d[0], d[1], d[2], s[0], s[1], Cin, N, nsrc);
+            ConvWgradArgs a = make_args(d[0], d[1], d[2], s[0], s[1], Cin, N, nsrc);
             if (!wgrad_supported(a)) continue;
-            check_plan(a);
-            ++n;
+            for (int mt5 = 1; mt5 <= 2; ++mt5) {  // 64- / 128-row workgroups of the 1x5 / 5x1 v3 kernel
+              a.mt5 = mt5;
+              check_plan(a);
+              if (s[0] * s[1] == 5 && plan_conv_wgrad(a).kind == 3)
+                EXPECT(plan_conv_wgrad(a).BM == 64 * mt5, "1x5 / 5x1 v3 rows %d for mt5 %d", plan_conv_wgrad(a).BM,
+                       mt5);
+              ++n;
+            }
           }
   EXPECT(n > 300, "only %d plans checked", n);
   std::printf("checked %d weight-gradient plans\n", n);
