@@ -82,10 +82,11 @@ void set_weight(EncConvArgs& a, int j, const at::Tensor& w) {
   a.wcin[j] = (int)w.size(1);
 }
 
-// Pack + run one planned conv launch (fwd or dgrad); classes and tables already filled.
-void run_conv(EncConvArgs& a, int rows, const at::TensorOptions& o) {
+// Packed-weight layout of a planned launch: per class, rows x Kpad (returns the total; sets the
+// classes' weight offsets and block ranges).
+long pack_layout(EncConvArgs& a, int rows, int& blocks) {
   long wtotal = 0;
-  int blocks = 0;
+  blocks = 0;
   a.tilesN = (a.N + enc_tile_bn(a.N) - 1) / enc_tile_bn(a.N);
   for (int c = 0; c < a.ncls; ++c) {
     EncClass& cl = a.cls[c];
@@ -95,9 +96,26 @@ void run_conv(EncConvArgs& a, int rows, const at::TensorOptions& o) {
     cl.blk0 = blocks;
     blocks += a.B * cl.tiles_img * a.tilesN;
   }
-  at::Tensor wt = at::empty({wtotal}, o.dtype(at::kBFloat16));
-  a.wt = cbf(wt);
-  check(launch_enc_pack(a, rows, wt.data_ptr(), stream()), "enc_pack");
+  return wtotal;
+}
+
+// Pack + run one planned conv launch (fwd or dgrad); classes and tables already filled.
+// ``prepacked``: the weights packed earlier by enc_pack_fwd / enc_pack_dgrad (same layout; the
+// packing launches then run off the encoder's critical path, ops/encoder.py).
+void run_conv(EncConvArgs& a, int rows, const at::TensorOptions& o,
+              const c10::optional<at::Tensor>& prepacked = c10::nullopt) {
+  int blocks = 0;
+  const long wtotal = pack_layout(a, rows, blocks);
+  at::Tensor wt;
+  if (prepacked.has_value() && prepacked->defined()) {
+    TORCH_CHECK(prepacked->numel() == wtotal && prepacked->is_contiguous() && is16(*prepacked),
+                "enc conv: prepacked weights do not match the launch's packed layout");
+    a.wt = cbf(*prepacked);
+  } else {
+    wt = at::empty({wtotal}, o.dtype(at::kBFloat16));
+    a.wt = cbf(wt);
+    check(launch_enc_pack(a, rows, wt.data_ptr(), stream()), "enc_pack");
+  }
   if (blocks == 0) return;
   if (enc_conv3_eligible(a))
     check(launch_enc_conv3(a, stream()), "enc_conv3");  // 3x3 64 -> 64: resident-weight kernel
@@ -148,10 +166,70 @@ void init_args(EncConvArgs& a) {
 
 }  // namespace
 
+namespace {
+// decode / packing tables of a KHxKW conv over Cx input channels (one class); returns Kpad
+int fwd_tables(EncConvArgs& a, int Cx, int KH, int KW, int pad, int device, const at::TensorOptions& o) {
+  std::vector<int> tab(kEncTabMax, -1), ptab(kEncTabMax, -1);
+  int e = 0;
+  for (int ky = 0; ky < KH; ++ky)
+    for (int kx = 0; kx < KW; ++kx)
+      for (int c = 0; c < Cx; c += 8) {
+        TORCH_CHECK(e < kEncTabMax, "conv too deep for the decode table");
+        tab[e] = enc_tab_entry(ky - pad, kx - pad, 0, c);
+        ptab[e] = enc_ptab_entry(0, ky, kx, c);
+        ++e;
+      }
+  const int K = e * 8, Kpad = round_up(K, 64);
+  set_tables(a, tab, ptab, Kpad / 8, device, o);
+  a.cls[0] = EncClass{0, 1, 1, 0, 0, K, Kpad, 0, 0, 0};
+  a.ncls = 1;
+  return Kpad;
+}
+}  // namespace
+
+// A packing job as bytes of its EncConvArgs, with its packed size and workgroup count
+std::tuple<at::Tensor, int64_t, int64_t> job_bytes(EncConvArgs& a, int rows) {
+  int blocks = 0;
+  const long wtotal = pack_layout(a, rows, blocks);
+  at::Tensor t = at::empty({(long)sizeof(EncConvArgs)}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(t.data_ptr(), &a, sizeof(EncConvArgs));
+  return {t, wtotal, (int64_t)rows * a.ncls};
+}
+
+// The forward weight operand of enc_conv_fwd for an input of Cx channels as a packing job of
+// enc_pack_multi (the layout run_conv would pack: N rows of round_up(KH*KW*Cx, 64))
+std::tuple<at::Tensor, int64_t, int64_t> enc_pack_fwd_job(const at::Tensor& w, int64_t Cx, int64_t pad, bool split,
+                                                          bool f16) {
+  check_w(w, "w");
+  EncConvArgs a;
+  init_args(a);
+  a.f16 = f16 ? 1 : 0;
+  a.B = 1;
+  a.N = (int)w.size(0);
+  fwd_tables(a, (int)Cx, (int)w.size(2), (int)w.size(3), (int)pad, w.get_device(), w.options());
+  a.split = split ? 1 : 0;
+  a.split_w = split ? (int)Cx / 3 : 0;
+  set_weight(a, 0, w);
+  a.pack_dgrad = 0;
+  return job_bytes(a, a.N);
+}
+
+// Pack the jobs of ``plan`` (device bytes: the jobs' EncConvArgs, their output offsets, their
+// first workgroups) into ``out`` with one launch
+void enc_pack_multi(const at::Tensor& plan, int64_t njobs, int64_t nblocks, at::Tensor out) {
+  TORCH_CHECK(plan.is_cuda() && plan.scalar_type() == at::kByte && plan.is_contiguous() &&
+                  plan.numel() >= njobs * (long)(sizeof(EncConvArgs) + sizeof(long) + sizeof(int)) + 4,
+              "enc_pack_multi: plan bytes");
+  TORCH_CHECK(out.is_cuda() && is16(out) && out.is_contiguous(), "enc_pack_multi: out");
+  if (njobs == 0 || nblocks == 0) return;
+  check(launch_enc_pack_multi(plan.data_ptr(), (int)njobs, (int)nblocks, out.data_ptr(), stream()), "enc_pack_multi");
+}
+
 // y[B,Ho,Wo,N] = conv(x[B,H,W,Cx], w[N,Cin,KH,KW]) + bias; stats [B, T, 2, N] (column sum, M2 per 128-pixel tile)
 std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::Tensor& w,
                                                 const c10::optional<at::Tensor>& bias, int64_t stride, int64_t pad,
-                                                bool want_stats, bool split) {
+                                                bool want_stats, bool split,
+                                                const c10::optional<at::Tensor>& prepacked) {
   check_nhwc(x, "x");
   check_w(w, "w");
   const int B = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), Cx = (int)x.size(3);
@@ -167,20 +245,9 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
   a.src[0] = {cbf(x), Cx, Cx, H, W, (int)stride};
   a.B = B;
   a.N = N;
-  std::vector<int> tab(kEncTabMax, -1), ptab(kEncTabMax, -1);
-  int e = 0;
-  for (int ky = 0; ky < KH; ++ky)
-    for (int kx = 0; kx < KW; ++kx)
-      for (int c = 0; c < Cx; c += 8) {
-        TORCH_CHECK(e < kEncTabMax, "conv too deep for the decode table");
-        tab[e] = enc_tab_entry(ky - (int)pad, kx - (int)pad, 0, c);
-        ptab[e] = enc_ptab_entry(0, ky, kx, c);
-        ++e;
-      }
-  const int K = e * 8, Kpad = round_up(K, 64);
-  set_tables(a, tab, ptab, Kpad / 8, x.get_device(), x.options());
-  a.cls[0] = EncClass{0, Ho, Wo, 0, 0, K, Kpad, 0, 0, 0};
-  a.ncls = 1;
+  fwd_tables(a, Cx, KH, KW, (int)pad, x.get_device(), x.options());
+  a.cls[0].Gh = Ho;
+  a.cls[0].Gw = Wo;
   at::Tensor y = at::empty({B, Ho, Wo, split ? 3 * N : N}, x.options());
   a.Ho = Ho;
   a.Wo = Wo;
@@ -207,7 +274,7 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
   if (want_stats) a.stats = st.data_ptr<float>();
   set_weight(a, 0, w);
   a.pack_dgrad = 0;
-  run_conv(a, N, x.options());
+  run_conv(a, N, x.options(), prepacked);
   return {y, st};
 }
 
@@ -217,57 +284,29 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
 // split (fp32 training): dys are split rows [hi | lo | hi] of 3 Cout channels, the weights are
 // packed [W_hi | W_hi | W_lo] along Cout, dx (and res) are split rows of 3 Cin, the ReLU' mask
 // is read from the hi plane of split rows.
-at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef strides, at::IntArrayRef pads,
-                          int64_t H, int64_t W, const c10::optional<at::Tensor>& res,
-                          const c10::optional<at::Tensor>& mask, bool split) {
-  const int nconv = (int)dys.size();
-  TORCH_CHECK(nconv >= 1 && nconv <= 2 && (int)ws.size() == nconv && (int)strides.size() == nconv &&
-                  (int)pads.size() == nconv,
-              "enc_conv_dgrad: 1 or 2 convs");
-  const int B = (int)dys[0].size(0);
-  const int Cin = (int)ws[0].size(1);
-  TORCH_CHECK(Cin % 8 == 0 && Cin <= 1024, "in channels");
-  int S = 1;
-  for (int j = 0; j < nconv; ++j) S = std::max<int>(S, (int)strides[j]);
-  EncConvArgs a;
-  init_args(a);
-  a.B = B;
-  a.N = Cin;
-  a.f16 = dys[0].scalar_type() == at::kHalf ? 1 : 0;
-  TORCH_CHECK(!split || !a.f16, "split planes are bf16");
-  for (int j = 0; j < nconv; ++j) {
-    check_nhwc(dys[j], "dy");
-    TORCH_CHECK(dys[j].scalar_type() == dys[0].scalar_type(), "dgrad: dys share one dtype");
-    check_w(ws[j], "w");
-    TORCH_CHECK(dys[j].size(0) == B && ws[j].size(1) == Cin && dys[j].size(3) == (split ? 3 : 1) * ws[j].size(0),
-                "dgrad shapes");
-
-    TORCH_CHECK(S % strides[j] == 0, "strides must divide the largest stride");
-    const int KH = (int)ws[j].size(2), KW = (int)ws[j].size(3);
-    const int Ho = ((int)H + 2 * (int)pads[j] - KH) / (int)strides[j] + 1;
-    const int Wo = ((int)W + 2 * (int)pads[j] - KW) / (int)strides[j] + 1;
-    TORCH_CHECK(dys[j].size(1) == Ho && dys[j].size(2) == Wo, "dy spatial shape does not match the conv");
-    const int C = (int)dys[j].size(3);
-    a.src[j] = {cbf(dys[j]), C, C, Ho, Wo, S / (int)strides[j]};
-    set_weight(a, j, ws[j]);
-  }
+namespace {
+// decode / packing tables of a dgrad launch: one class per output phase (py, px) of the largest
+// stride S, each gathering the taps of every conv that land on that phase (C[j]: dy channels)
+void dgrad_tables(EncConvArgs& a, at::TensorList ws, const std::vector<int>& C, at::IntArrayRef strides,
+                  at::IntArrayRef pads, int H, int W, int S, int device, const at::TensorOptions& o) {
+  const int nconv = (int)ws.size();
   std::vector<int> tab(kEncTabMax, -1), ptab(kEncTabMax, -1);
   int e = 0, ncls = 0;
   for (int py = 0; py < S; ++py)
     for (int px = 0; px < S; ++px) {
-      const int Gh = ((int)H - py + S - 1) / S, Gw = ((int)W - px + S - 1) / S;
+      const int Gh = (H - py + S - 1) / S, Gw = (W - px + S - 1) / S;
       if (Gh <= 0 || Gw <= 0) continue;
       const int t0 = e;
       for (int j = 0; j < nconv; ++j) {
         const int s = (int)strides[j], p = (int)pads[j];
-        const int KH = (int)ws[j].size(2), KW = (int)ws[j].size(3), C = (int)dys[j].size(3);
+        const int KH = (int)ws[j].size(2), KW = (int)ws[j].size(3);
         for (int ky = 0; ky < KH; ++ky) {
           const int vy = py + p - ky;
           if (((vy % s) + s) % s) continue;
           for (int kx = 0; kx < KW; ++kx) {
             const int vx = px + p - kx;
             if (((vx % s) + s) % s) continue;
-            for (int c = 0; c < C; c += 8) {
+            for (int c = 0; c < C[j]; c += 8) {
               TORCH_CHECK(e < kEncTabMax, "dgrad too deep for the decode table");
               tab[e] = enc_tab_entry(vy / s, vx / s, j, c);
               ptab[e] = enc_ptab_entry(j, ky, kx, c);
@@ -282,7 +321,81 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
       a.cls[ncls++] = EncClass{t0, Gh, Gw, py, px, K, Kpad, 0, 0, 0};
     }
   a.ncls = ncls;
-  set_tables(a, tab, ptab, e, dys[0].get_device(), dys[0].options());
+  set_tables(a, tab, ptab, e, device, o);
+}
+
+int largest_stride(at::IntArrayRef strides) {
+  int S = 1;
+  for (auto s : strides) S = std::max<int>(S, (int)s);
+  for (auto s : strides) TORCH_CHECK(S % s == 0, "strides must divide the largest stride");
+  return S;
+}
+}  // namespace
+
+// The dgrad weight operand of enc_conv_dgrad (convs ws over an H x W input) as a packing job of
+// enc_pack_multi: the weights do not change between the forward and the optimizer step
+std::tuple<at::Tensor, int64_t, int64_t> enc_pack_dgrad_job(at::TensorList ws, at::IntArrayRef strides,
+                                                            at::IntArrayRef pads, int64_t H, int64_t W, bool split,
+                                                            bool f16) {
+  const int nconv = (int)ws.size();
+  TORCH_CHECK(nconv >= 1 && nconv <= 2 && (int)strides.size() == nconv && (int)pads.size() == nconv,
+              "enc_pack_dgrad_job: 1 or 2 convs");
+  const int Cin = (int)ws[0].size(1);
+  EncConvArgs a;
+  init_args(a);
+  a.B = 1;
+  a.N = Cin;
+  a.f16 = f16 ? 1 : 0;
+  std::vector<int> C(nconv);
+  for (int j = 0; j < nconv; ++j) {
+    check_w(ws[j], "w");
+    TORCH_CHECK(ws[j].size(1) == Cin, "dgrad shapes");
+    C[j] = (split ? 3 : 1) * (int)ws[j].size(0);
+    set_weight(a, j, ws[j]);
+  }
+  dgrad_tables(a, ws, C, strides, pads, (int)H, (int)W, largest_stride(strides), ws[0].get_device(), ws[0].options());
+  a.split = split ? 1 : 0;
+  a.split_w = split ? (int)ws[0].size(0) : 0;
+  for (int j = 0; j < nconv; ++j) a.split_wd[j] = split ? (int)ws[j].size(0) : 0;
+  a.pack_dgrad = 1;
+  return job_bytes(a, Cin);
+}
+
+at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef strides, at::IntArrayRef pads,
+                          int64_t H, int64_t W, const c10::optional<at::Tensor>& res,
+                          const c10::optional<at::Tensor>& mask, bool split,
+                          const c10::optional<at::Tensor>& prepacked) {
+  const int nconv = (int)dys.size();
+  TORCH_CHECK(nconv >= 1 && nconv <= 2 && (int)ws.size() == nconv && (int)strides.size() == nconv &&
+                  (int)pads.size() == nconv,
+              "enc_conv_dgrad: 1 or 2 convs");
+  const int B = (int)dys[0].size(0);
+  const int Cin = (int)ws[0].size(1);
+  TORCH_CHECK(Cin % 8 == 0 && Cin <= 1024, "in channels");
+  const int S = largest_stride(strides);
+  EncConvArgs a;
+  init_args(a);
+  a.B = B;
+  a.N = Cin;
+  a.f16 = dys[0].scalar_type() == at::kHalf ? 1 : 0;
+  TORCH_CHECK(!split || !a.f16, "split planes are bf16");
+  std::vector<int> Cs(nconv);
+  for (int j = 0; j < nconv; ++j) {
+    check_nhwc(dys[j], "dy");
+    TORCH_CHECK(dys[j].scalar_type() == dys[0].scalar_type(), "dgrad: dys share one dtype");
+    check_w(ws[j], "w");
+    TORCH_CHECK(dys[j].size(0) == B && ws[j].size(1) == Cin && dys[j].size(3) == (split ? 3 : 1) * ws[j].size(0),
+                "dgrad shapes");
+    const int KH = (int)ws[j].size(2), KW = (int)ws[j].size(3);
+    const int Ho = ((int)H + 2 * (int)pads[j] - KH) / (int)strides[j] + 1;
+    const int Wo = ((int)W + 2 * (int)pads[j] - KW) / (int)strides[j] + 1;
+    TORCH_CHECK(dys[j].size(1) == Ho && dys[j].size(2) == Wo, "dy spatial shape does not match the conv");
+    const int C = (int)dys[j].size(3);
+    a.src[j] = {cbf(dys[j]), C, C, Ho, Wo, S / (int)strides[j]};
+    Cs[j] = C;
+    set_weight(a, j, ws[j]);
+  }
+  dgrad_tables(a, ws, Cs, strides, pads, (int)H, (int)W, S, dys[0].get_device(), dys[0].options());
   const int rs = split ? 3 * Cin : Cin;  // dx / res / mask row pitch
   at::Tensor dx = at::empty({B, H, W, rs}, dys[0].options());
   a.Ho = (int)H;
@@ -306,7 +419,7 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
     a.mask_stride = rs;
   }
   a.pack_dgrad = 1;
-  run_conv(a, Cin, dys[0].options());
+  run_conv(a, Cin, dys[0].options(), prepacked);
   return dx;
 }
 
@@ -636,11 +749,15 @@ std::vector<at::Tensor> enc_norm_bwd_finish(const at::Tensor& g, const at::Tenso
 }  // namespace raft_amd
 
 TORCH_LIBRARY_FRAGMENT(raft_amd, m) {
-  m.def("enc_conv_fwd(Tensor x, Tensor w, Tensor? bias, int stride, int pad, bool stats, bool split=False) -> "
-        "(Tensor, Tensor)");
+  m.def("enc_conv_fwd(Tensor x, Tensor w, Tensor? bias, int stride, int pad, bool stats, bool split=False, "
+        "Tensor? prepacked=None) -> (Tensor, Tensor)");
   m.def(
       "enc_conv_dgrad(Tensor[] dys, Tensor[] ws, int[] strides, int[] pads, int H, int W, Tensor? res, Tensor? mask, "
-      "bool split=False) -> Tensor");
+      "bool split=False, Tensor? prepacked=None) -> Tensor");
+  m.def("enc_pack_fwd_job(Tensor w, int Cx, int pad, bool split, bool f16) -> (Tensor, int, int)");
+  m.def("enc_pack_dgrad_job(Tensor[] ws, int[] strides, int[] pads, int H, int W, bool split, bool f16) -> "
+        "(Tensor, int, int)");
+  m.def("enc_pack_multi(Tensor plan, int njobs, int nblocks, Tensor(a!) out) -> ()");
   m.def("enc_conv_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, Tensor(b!)? db, int stride, int pad, bool accumulate, "
         "bool db_zero=False, int fold=0) -> ()");
   m.def("enc_prep(Tensor img0, Tensor? img1, bool split=False, bool f16=False) -> Tensor");
@@ -662,6 +779,9 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("enc_conv_fwd", &raft_amd::enc_conv_fwd);
   m.impl("enc_conv_dgrad", &raft_amd::enc_conv_dgrad);
   m.impl("enc_conv_wgrad", &raft_amd::enc_conv_wgrad);
+  m.impl("enc_pack_fwd_job", &raft_amd::enc_pack_fwd_job);
+  m.impl("enc_pack_dgrad_job", &raft_amd::enc_pack_dgrad_job);
+  m.impl("enc_pack_multi", &raft_amd::enc_pack_multi);
   m.impl("enc_prep", &raft_amd::enc_prep);
   m.impl("enc_norm_stats", &raft_amd::enc_norm_stats);
   m.impl("enc_apply", &raft_amd::enc_apply);

@@ -390,13 +390,7 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
 // out[wofs + row * Kpad + k] (bf16) from fp32 parameters (any strides):
 //   forward: row = out channel, column (tap, in channel)   -> W[row][local][ky][kx]
 //   dgrad:   row = in channel,  column (conv, tap, out ch) -> W_w[local][row][ky][kx]
-__global__ __launch_bounds__(256) void enc_pack_kernel(const EncConvArgs a, __bf16* out) {
-  const int ci = blockIdx.y;
-  EncClass cl = a.cls[0];
-  if (ci == 1) cl = a.cls[1];
-  if (ci == 2) cl = a.cls[2];
-  if (ci == 3) cl = a.cls[3];
-  const int row = blockIdx.x;
+__device__ __forceinline__ void pack_row(const EncConvArgs& a, const EncClass& cl, int row, __bf16* out) {
   const int* ptab = a.ptab_ptr ? a.ptab_ptr : a.ptab;
   for (int k = threadIdx.x; k < cl.Kpad; k += 256) {
     const int ent = (k < cl.K) ? ptab[cl.t0 + (k >> 3)] : -1;
@@ -428,6 +422,31 @@ __global__ __launch_bounds__(256) void enc_pack_kernel(const EncConvArgs a, __bf
     }
     out[cl.wofs + (long)row * cl.Kpad + k] = st16(v, a.f16 != 0);
   }
+}
+
+__global__ __launch_bounds__(256) void enc_pack_kernel(const EncConvArgs a, __bf16* out) {
+  const int ci = blockIdx.y;
+  EncClass cl = a.cls[0];
+  if (ci == 1) cl = a.cls[1];
+  if (ci == 2) cl = a.cls[2];
+  if (ci == 3) cl = a.cls[3];
+  pack_row(a, cl, blockIdx.x, out);
+}
+
+// Every conv of an encoder packed by one launch (ops/encoder.py _Prepack): ``plan`` holds
+// njobs EncConvArgs (packing fields only), then each job's output offset (long) and first
+// workgroup (int, njobs + 1 entries); workgroup = (job, class, row).
+__global__ __launch_bounds__(256) void enc_pack_multi_kernel(const unsigned char* plan, int njobs, __bf16* out) {
+  const EncConvArgs* jobs = reinterpret_cast<const EncConvArgs*>(plan);
+  const long* ofs = reinterpret_cast<const long*>(plan + sizeof(EncConvArgs) * njobs);
+  const int* blk0 = reinterpret_cast<const int*>(ofs + njobs);
+  const int b = blockIdx.x;
+  int j = 0;
+  while (j + 1 < njobs && blk0[j + 1] <= b) ++j;
+  const EncConvArgs& a = jobs[j];
+  const int rows = a.N;
+  const int local = b - blk0[j], ci = local / rows, row = local - ci * rows;
+  pack_row(a, a.cls[ci], row, out + ofs[j]);
 }
 
 // ============================================================================ wgrad
@@ -1305,6 +1324,12 @@ constexpr int kEncBM = 128;
 
 hipError_t launch_enc_pack(const EncConvArgs& a, int rows, void* out, hipStream_t s) {
   hipLaunchKernelGGL(enc_pack_kernel, dim3(rows, a.ncls), dim3(256), 0, s, a, static_cast<__bf16*>(out));
+  return hipGetLastError();
+}
+
+hipError_t launch_enc_pack_multi(const void* plan, int njobs, int nblocks, void* out, hipStream_t s) {
+  hipLaunchKernelGGL(enc_pack_multi_kernel, dim3(nblocks), dim3(256), 0, s, static_cast<const unsigned char*>(plan),
+                     njobs, static_cast<__bf16*>(out));
   return hipGetLastError();
 }
 

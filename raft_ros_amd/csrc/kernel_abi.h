@@ -602,6 +602,7 @@ hipError_t launch_wgrad_reduce_packed(const float* slab, int nsplit, int Npad, i
 // encoder.hip
 int enc_tile_bn(int N);
 hipError_t launch_enc_pack(const EncConvArgs& a, int rows, void* out, hipStream_t s);
+hipError_t launch_enc_pack_multi(const void* plan, int njobs, int nblocks, void* out, hipStream_t s);
 hipError_t launch_enc_conv(const EncConvArgs& a, int nblocks, hipStream_t s);
 hipError_t launch_enc_conv3(const EncConvArgs& a, hipStream_t s);
 hipError_t launch_enc_wgrad(const EncWgradArgs& a, int BM, int BN, hipStream_t s);

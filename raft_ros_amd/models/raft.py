@@ -157,7 +157,8 @@ class RAFT(nn.Module):
             split = not amp  # fp32: split-bf16 (fp32-faithful) encoder kernels
             f16 = amp and self.amp_dtype == torch.float16  # fp16 AMP: fp16 MFMA kernels
             with torch.cuda.stream(side):
-                cnet_native = encoder_native.encode(self.cnet, raw1, join_stream=main, split=split, f16=f16)
+                cnet_native = encoder_native.encode(self.cnet, raw1, join_stream=main, split=split, f16=f16,
+                                                    pack_stream="tail")
             fmap1, fmap2 = encoder_native.encode(self.fnet, raw1, raw2, split=split,
                                                  f16=f16).split(raw1.shape[0], dim=0)
         else:

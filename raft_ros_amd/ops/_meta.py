@@ -133,7 +133,7 @@ def register() -> None:
         return wf, wd, w[0].new_empty((n,))
 
     @fake(lib + "enc_conv_fwd")
-    def _(x, w, bias, stride, pad, stats, split=False):
+    def _(x, w, bias, stride, pad, stats, split=False, prepacked=None):
         B, H, W, Cx = x.shape
         N, Cin, KH, KW = w.shape
         Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
@@ -152,7 +152,7 @@ def register() -> None:
         return x.new_empty((B, Ho, Wo, N)), st
 
     @fake(lib + "enc_conv_dgrad")
-    def _(dys, ws, strides, pads, H, W, res, mask, split=False):
+    def _(dys, ws, strides, pads, H, W, res, mask, split=False, prepacked=None):
         return dys[0].new_empty((dys[0].shape[0], H, W, (3 if split else 1) * ws[0].shape[1]))
 
     @fake(lib + "enc_prep")
@@ -208,5 +208,5 @@ def register() -> None:
     for name in ("conv_fwd", "conv_wgrad", "conv_wgrad_params", "gru_bwd_a", "gru_bwd_b", "masked_cast",
                  "pack_flow", "apply_delta", "corr_lookup_into", "corr_lookup_split_into", "convex_upsample_backward_into",
                  "corr_lookup_backward_", "corr_lookup_grad_rows", "corr_gemm", "local_corr_mfma", "local_corr_mfma_backward",
-                 "enc_conv_wgrad"):
+                 "enc_conv_wgrad", "enc_pack_multi"):
         fake(lib + name)(lambda *args, **kwargs: None)

@@ -22,6 +22,8 @@ from the second replay of a captured training step.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -31,6 +33,12 @@ from .norm import InstanceNorm2dNHWC
 
 # norm kinds shared with csrc/encoder.hip
 _NONE, _INSTANCE, _BATCH_TRAIN, _BATCH_EVAL = 0, 1, 2, 3
+
+# pack every conv's weight operand (forward, and the data-gradient operands of the backward) with
+# two launches at the start of the encoder forward instead of one packing launch in front of each
+# conv (RAFT_ENC_PREPACK=0: per-conv packing; =fork: the two launches on an auxiliary stream)
+PREPACK = os.environ.get("RAFT_ENC_PREPACK", "1") != "0"
+_PREPACK_FORK = os.environ.get("RAFT_ENC_PREPACK", "1") == "fork"
 
 
 def _norm_kind(m: nn.Module):
@@ -122,20 +130,143 @@ def _stats(a, st, nd, P, split: bool = False):
     return ops().enc_norm_stats(st, B, H * W, N, k, None, None, None, None, None, 0.0, eps, W)
 
 
-def _conv(x, cd, P, stats, split: bool = False):
+def _conv(x, cd, P, stats, split: bool = False, pk=None):
     b = P[cd["b"]] if cd["b"] >= 0 else None
-    # split: the fp32 weight is split into [W_hi | W_hi | W_lo] by the per-call packing kernel (no
-    # cached copy: an optimizer step -- fused AdamW does not bump the parameter versions -- must
-    # never leave a stale split weight behind)
-    return ops().enc_conv_fwd(x, P[cd["w"]], b, cd["stride"], cd["pad"], stats, split)
+    # split: the fp32 weight is split into [W_hi | W_hi | W_lo] by the packing kernel, every step
+    # (no cached copy: an optimizer step -- fused AdamW does not bump the parameter versions --
+    # must never leave a stale split weight behind); ``pk``: the operands packed ahead (_Prepack)
+    packed = pk.fwd.get(id(cd)) if pk is not None else None
+    return ops().enc_conv_fwd(x, P[cd["w"]], b, cd["stride"], cd["pad"], stats, split, packed)
 
 
-def _forward(L, x0, P, split: bool = False):
+def _conv_hw(h, w, cd):
+    m = cd["module"]
+    s, p = cd["stride"], cd["pad"]
+    return (h + 2 * p - m.kernel_size[0]) // s + 1, (w + 2 * p - m.kernel_size[1]) // s + 1
+
+
+class _Prepack:
+    """Weight operands of one encoder packed ahead, in one persistent buffer per input shape.
+
+    ``issue()`` packs every conv's forward operand with ONE launch (csrc/encoder.hip
+    enc_pack_multi_kernel) at the start of the forward, and every data-gradient operand of
+    the backward with a second one (the weights do not change before the optimizer step),
+    instead of one small packing launch in front of each of the ~58 convs of the two encoders
+    (config #2: 761 -> ~705 kernels per step).  The stem conv still packs its own weights.
+    The job plans (the kernel arguments of every job, uploaded once) hold the parameters' data
+    pointers and are rebuilt when those change.
+
+    RAFT_ENC_PREPACK=fork issues the two launches on an auxiliary stream (the block convs
+    wait on ``fwd_ready``, the end of the forward joins ``bwd_ready``); measured no faster
+    than the consumer stream at config #2 (profiles/r4_enc_prepack_ab.log).  The buffer is
+    allocated on the consuming stream and kept, so no allocator event is recorded per step;
+    each step's packing follows the consumer's queued work, which includes every earlier read
+    of the buffer."""
+
+    _MAX_SHAPES = 4
+
+    def __init__(self, L, P, H, W, split, f16, need_bwd, device):
+        mul = 3 if split else 1
+        self.fwd_jobs, self.bwd_jobs = [], []  # (cd, Cx) / (cds, H, W)
+        h, w = _conv_hw(H, W, L.stem[0])
+        for units, down in L.blocks:
+            for ui, (cd, _nd) in enumerate(units):
+                self.fwd_jobs.append((cd, mul * P[cd["w"]].shape[1]))
+                cds = [cd] + ([down[0]] if ui == 0 and down is not None else [])
+                self.bwd_jobs.append((cds, h, w))
+                if ui == 0 and down is not None:
+                    self.fwd_jobs.append((down[0], mul * P[down[0]["w"]].shape[1]))
+                h, w = _conv_hw(h, w, cd)
+        self.fwd_jobs.append((L.out, mul * P[L.out["w"]].shape[1]))
+        self.bwd_jobs.append(([L.out], h, w))
+        if not need_bwd:
+            self.bwd_jobs = []
+        self.split, self.f16, self.need_bwd = split, f16, need_bwd
+        self.device = device
+        self.buf = None
+        self.ptrs = None
+        self.fwd_ready = self.bwd_ready = None
+
+    def _build(self, P):
+        """Job plans and the packed buffer (first use, and whenever a parameter moved)."""
+        o = ops()
+        fj = [o.enc_pack_fwd_job(P[cd["w"]], cx, cd["pad"], self.split, self.f16) for cd, cx in self.fwd_jobs]
+        bj = [o.enc_pack_dgrad_job([P[c["w"]] for c in cds], [c["stride"] for c in cds], [c["pad"] for c in cds],
+                                   h, w, self.split, self.f16) for cds, h, w in self.bwd_jobs]
+        offs, total = [], 0
+        for _, n, _ in fj + bj:
+            offs.append(total)
+            total += -(-n // 256) * 256
+        if self.buf is None or self.buf.numel() != total:
+            self.buf = torch.empty(total, device=self.device, dtype=torch.float16 if self.f16 else torch.bfloat16)
+
+        def plan(jobs, ofs):
+            blk = [0]
+            for _, _, nb in jobs:
+                blk.append(blk[-1] + nb)
+            raw = torch.cat([t for t, _, _ in jobs] + [torch.tensor(ofs, dtype=torch.int64).view(torch.uint8),
+                                                        torch.tensor(blk, dtype=torch.int32).view(torch.uint8)])
+            return raw.to(self.device), len(jobs), blk[-1]
+
+        self.fwd_plan = plan(fj, offs[:len(fj)])
+        self.fwd = {id(cd): self.buf[a:a + n] for (cd, _), a, (_, n, _) in zip(self.fwd_jobs, offs, fj)}
+        self.bwd = {}
+        if bj:
+            self.bwd_plan = plan(bj, offs[len(fj):])
+            self.bwd = {id(cds[0]): self.buf[a:a + n] for (cds, _, _), a, (_, n, _) in
+                        zip(self.bwd_jobs, offs[len(fj):], bj)}
+
+    def issue(self, P, stream):
+        o = ops()
+        ptrs = tuple(p.data_ptr() for p in P)
+        if ptrs != self.ptrs:
+            self._build(P)
+            self.ptrs = ptrs
+        if stream is None:  # on the consumer stream: ordered by the stream itself
+            o.enc_pack_multi(self.fwd_plan[0], self.fwd_plan[1], self.fwd_plan[2], self.buf)
+            if self.bwd_jobs:
+                o.enc_pack_multi(self.bwd_plan[0], self.bwd_plan[1], self.bwd_plan[2], self.buf)
+            return self
+        stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(stream):
+            o.enc_pack_multi(self.fwd_plan[0], self.fwd_plan[1], self.fwd_plan[2], self.buf)
+            self.fwd_ready = torch.cuda.Event()
+            self.fwd_ready.record(stream)
+            if self.bwd_jobs:
+                o.enc_pack_multi(self.bwd_plan[0], self.bwd_plan[1], self.bwd_plan[2], self.buf)
+                self.bwd_ready = torch.cuda.Event()
+                self.bwd_ready.record(stream)
+        return self
+
+
+def _prepack(L, x0, split: bool, f16: bool, stream_name: str):
+    """Issue the ahead-of-time packing of ``L``'s weight operands (None: disabled / too many
+    input shapes seen / inside a HIP-graph capture: launches cost nothing there, and the
+    forked packing stream (first design) crashed capture_end in
+    test_model_gpu.py::test_graphed_inference_matches_eager)."""
+    if not PREPACK or x0.device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+        return None
+    from .streams import aux_stream
+
+    need_bwd = torch.is_grad_enabled()
+    key = (x0.shape[1], x0.shape[2], split, f16, need_bwd)
+    cache = L.__dict__.setdefault("prepacks", {})
+    pk = cache.get(key)
+    if pk is None:
+        if len(cache) >= _Prepack._MAX_SHAPES:
+            return None
+        pk = cache[key] = _Prepack(L, L.params, x0.shape[1], x0.shape[2], split, f16, need_bwd, x0.device)
+    return pk.issue(L.params, aux_stream(x0.device, stream_name) if _PREPACK_FORK else None)
+
+
+def _forward(L, x0, P, split: bool = False, pk=None):
     """Run the encoder; returns (output NHWC, saved records).  ``split``: every activation as
-    split-bf16 planes (fp32-faithful, see below)."""
+    split-bf16 planes (fp32-faithful, see below).  ``pk``: weight operands packed ahead."""
     o = ops()
     sc, sn = L.stem
     a0, st = _conv(x0, sc, P, True, split)
+    if pk is not None and pk.fwd_ready is not None:
+        torch.cuda.current_stream(x0.device).wait_event(pk.fwd_ready)
     c0 = _stats(a0, st, sn, P, split)
     h = o.enc_apply(a0, c0, True, None, None, False, split)
     stem_rec = (x0, a0, c0, h)
@@ -145,7 +276,7 @@ def _forward(L, x0, P, split: bool = False):
         ins, acts, coefs = [], [], []
         cur = hin
         for ui, (cd, nd) in enumerate(units):
-            a, st = _conv(cur, cd, P, nd["kind"] != _BATCH_EVAL, split)
+            a, st = _conv(cur, cd, P, nd["kind"] != _BATCH_EVAL, split, pk)
             c = _stats(a, st, nd, P, split)
             ins.append(cur)
             acts.append(a)
@@ -155,14 +286,18 @@ def _forward(L, x0, P, split: bool = False):
         drec = None
         if down is not None:
             dcd, dnd = down
-            ad, st = _conv(hin, dcd, P, dnd["kind"] != _BATCH_EVAL, split)
+            ad, st = _conv(hin, dcd, P, dnd["kind"] != _BATCH_EVAL, split, pk)
             cdn = _stats(ad, st, dnd, P, split)
             h = o.enc_apply(acts[-1], coefs[-1], True, ad, cdn, True, split)
             drec = (ad, cdn)
         else:
             h = o.enc_apply(acts[-1], coefs[-1], True, hin, None, True, split)
         recs.append((ins, acts, coefs, drec, h))
-    y, _ = _conv(h, L.out, P, False, split)
+    y, _ = _conv(h, L.out, P, False, split, pk)
+    if pk is not None and pk.bwd_ready is not None:
+        # join the packing stream here (its data-gradient packs ran beside the blocks): nothing
+        # it writes is left in flight past the forward, whether or not a backward follows
+        torch.cuda.current_stream(x0.device).wait_event(pk.bwd_ready)
     return y, stem_rec, recs
 
 
@@ -176,9 +311,9 @@ def _forward(L, x0, P, split: bool = False):
 # apply / backward passes read and write the planes in fp32, and each weight gradient is two
 # GEMMs ([X_hi | X_lo]^T dY_hi + X_hi^T dY_lo) folded into the fp32 parameter layout.
 
-def _forward_split(L, x0, P):
+def _forward_split(L, x0, P, pk=None):
     """``_forward`` on split-bf16 planes without records (inference); the split output rows."""
-    return _forward(L, x0, P, True)[0]
+    return _forward(L, x0, P, True, pk)[0]
 
 
 def _split_rows(g: torch.Tensor) -> torch.Tensor:
@@ -229,15 +364,16 @@ def _norm_bwd(o, nd, g, a0, c0, relu0, a1, c1, split: bool = False):
     return o.enc_norm_bwd(g, a0, c0, relu0, a1, c1, nd["kind"], split)
 
 
-def _backward(L, P, gy, stem_rec, recs, split: bool = False):
+def _backward(L, P, gy, stem_rec, recs, split: bool = False, pk=None):
     o = ops()
     sp = split
     grads = [None] * len(P)
+    bp = pk.bwd if pk is not None else {}  # ordered before the backward by _forward
     last_h = recs[-1][4] if recs else stem_rec[3]
     _wgrad(last_h, gy, L.out, P, grads, split=sp)
     oc = L.out
     g = o.enc_conv_dgrad([gy], [P[oc["w"]]], [oc["stride"]], [oc["pad"]], last_h.shape[1], last_h.shape[2],
-                         None, last_h, sp)
+                         None, last_h, sp, bp.get(id(oc)))
     for (units, down), (ins, acts, coefs, drec, _h) in zip(reversed(L.blocks), reversed(recs)):
         dnd = down[1] if down is not None else None
         r = _norm_bwd(o, units[-1][1], g, acts[-1], coefs[-1], True, drec[0] if drec else None,
@@ -253,7 +389,7 @@ def _backward(L, P, gy, stem_rec, recs, split: bool = False):
             _wgrad(x, da, cd, P, grads, nd, split=sp)
             if u > 0:
                 dh = o.enc_conv_dgrad([da], [P[cd["w"]]], [cd["stride"]], [cd["pad"]], x.shape[1], x.shape[2],
-                                      None, x, sp)
+                                      None, x, sp, bp.get(id(cd)))
                 pnd = units[u - 1][1]
                 r = _norm_bwd(o, pnd, dh, acts[u - 1], coefs[u - 1], False, None, None, sp)
                 da = r[0]
@@ -267,7 +403,8 @@ def _backward(L, P, gy, stem_rec, recs, split: bool = False):
                     ss.append(dcd["stride"])
                     ps.append(dcd["pad"])
                     _wgrad(x, dad, dcd, P, grads, dnd, split=sp)
-                g = o.enc_conv_dgrad(dys, ws, ss, ps, x.shape[1], x.shape[2], None if down is not None else g, x, sp)
+                g = o.enc_conv_dgrad(dys, ws, ss, ps, x.shape[1], x.shape[2], None if down is not None else g, x, sp,
+                                     bp.get(id(cd)))
     x0, a0, c0, _h0 = stem_rec
     sc, sn = L.stem
     r = _norm_bwd(o, sn, g, a0, c0, False, None, None, sp)
@@ -310,8 +447,9 @@ class _EncoderFn(torch.autograd.Function):
     split-bf16 network, fp32 NHWC output = hi + lo planes)."""
 
     @staticmethod
-    def forward(ctx, layout, x0, join, split, *params):
-        y, stem_rec, recs = _forward(layout, x0, params, split)
+    def forward(ctx, layout, x0, join, split, pk, *params):
+        y, stem_rec, recs = _forward(layout, x0, params, split, pk)
+        ctx.pk = pk
         ctx.layout = layout
         ctx.params = params
         ctx.join = join
@@ -327,7 +465,8 @@ class _EncoderFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         gy = _split_rows(gy) if ctx.split else gy.contiguous().to(ctx.dt16)
-        grads = _backward(ctx.layout, ctx.params, gy, ctx.stem_rec, ctx.recs, ctx.split)
+        pk = ctx.pk if ctx.pk is not None and ctx.pk.need_bwd else None
+        grads = _backward(ctx.layout, ctx.params, gy, ctx.stem_rec, ctx.recs, ctx.split, pk)
         ctx.stem_rec = ctx.recs = None
         if ctx.join is not None:
             # the forward ran on a side stream, so autograd ran this backward there too: make
@@ -343,7 +482,7 @@ class _EncoderFn(torch.autograd.Function):
                     if g is not None:
                         g.record_stream(ctx.join)
                         break
-        return (None, None, None, None, *grads)
+        return (None, None, None, None, None, *grads)
 
 
 def _layout(enc):
@@ -360,18 +499,21 @@ def _layout(enc):
 
 
 def encode(enc, image1: torch.Tensor, image2: torch.Tensor | None = None,
-           join_stream: torch.cuda.Stream | None = None, split: bool = False, f16: bool = False) -> torch.Tensor:
+           join_stream: torch.cuda.Stream | None = None, split: bool = False, f16: bool = False,
+           pack_stream: str = "wgrad") -> torch.Tensor:
     """Run ``enc`` natively on raw 0..255 fp32 images (``image2``: second frame of a
     paired batch).  Returns the (n, C, H/8, W/8) bf16 feature map in channels-last
     layout (``n`` = 2B when paired).  ``join_stream``: when this runs on a side stream,
     the stream that must see the parameter gradients complete (see ``_EncoderFn.backward``).
     ``split``: fp32-faithful mode (no AMP; training or inference): the fp32 feature map.
-    ``f16``: fp16 activations (fp16 AMP, v_mfma_f32_32x32x16_f16) instead of bf16."""
+    ``f16``: fp16 activations (fp16 AMP, v_mfma_f32_32x32x16_f16) instead of bf16.
+    ``pack_stream``: the auxiliary stream (ops/streams.py) that packs the weights ahead."""
     L = _layout(enc)
     x0 = ops().enc_prep(image1.float(), image2.float() if image2 is not None else None, split, f16 and not split)
+    pk = _prepack(L, x0, bool(split), bool(f16 and not split), pack_stream)
     if split and not torch.is_grad_enabled():
-        y = _forward_split(L, x0, L.params)
+        y = _forward_split(L, x0, L.params, pk)
         N = y.shape[3] // 3
         return (y[..., :N].float() + y[..., N:2 * N].float()).permute(0, 3, 1, 2)
-    y = _EncoderFn.apply(L, x0, join_stream, bool(split), *L.params)
+    y = _EncoderFn.apply(L, x0, join_stream, bool(split), pk, *L.params)
     return y.permute(0, 3, 1, 2)

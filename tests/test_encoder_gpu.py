@@ -226,3 +226,48 @@ def test_split_encoder_inference_is_fp32_faithful(name):
     assert out.dtype == torch.float32 and out.shape == ref.shape
     err = _rel(out, ref)
     assert err < 2e-4, (name, err)  # measured 1e-5 (basic) .. 5.5e-5 (small)
+
+
+@pytest.mark.parametrize("mode", ["bf16", "f16", "split", "split_infer", "bf16_fork", "split_fork"])
+@pytest.mark.parametrize("name", ["basic_batch", "small_instance"])
+def test_prepacked_weights_match_per_conv_packing(name, mode, monkeypatch):
+    """Weights packed ahead by the one-launch multi-conv packing (ops/encoder.py _Prepack; _fork:
+    on an auxiliary stream) give bit-identical outputs and gradients to the per-conv packing,
+    also after an in-place weight update (the optimizer step the next forward's packing must
+    see)."""
+    from raft_ros_amd.ops import encoder as enc_native
+    monkeypatch.setattr(enc_native, "_PREPACK_FORK", mode.endswith("_fork"))
+    mode = mode.replace("_fork", "")
+    torch.manual_seed(0)
+    base = _encoders()[name]().to(cuda).to(memory_format=torch.channels_last).train()
+    nets = {flag: copy.deepcopy(base) for flag in (True, False)}
+    g = torch.Generator(device=cuda).manual_seed(3)
+    B, H, W = 2, 96, 128
+    ims = [torch.rand(B, 3, H, W, device=cuda, generator=g) * 255 for _ in range(2)]
+    gy = None
+    res = {}
+    for flag, enc in nets.items():
+        monkeypatch.setattr(enc_native, "PREPACK", flag)
+        outs, grads = [], []
+        for step in range(2):
+            if step == 1:
+                with torch.no_grad():
+                    for p in enc.parameters():
+                        p.mul_(1.01).add_(1e-3)
+            enc.zero_grad(set_to_none=True)
+            with torch.set_grad_enabled(mode != "split_infer"):
+                out = enc_native.encode(enc, ims[0], ims[1], split=mode.startswith("split"), f16=mode == "f16")
+            outs.append(out.float().clone())
+            if mode != "split_infer":
+                if gy is None:
+                    gy = torch.randn(out.shape, device=cuda, generator=g)
+                (out.float() * gy).sum().backward()
+                grads.append([p.grad.clone() for p in enc.parameters()])
+        torch.cuda.synchronize()
+        res[flag] = (outs, grads)
+    assert bool(enc_native._layout(nets[True]).__dict__.get("prepacks")), "prepacking did not run"
+    for a, b in zip(res[True][0], res[False][0]):
+        assert torch.equal(a, b)
+    for ga, gb in zip(res[True][1], res[False][1]):
+        for x, y in zip(ga, gb):
+            assert torch.equal(x, y)
