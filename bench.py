@@ -274,11 +274,22 @@ def run(args):
     if distributed:
         dist.barrier()
     _sync(device)
+    # RAFT_BENCH_STEP_TIMES=1: per-step GPU time (events on the current stream) to stderr
+    step_ev = [] if (os.environ.get("RAFT_BENCH_STEP_TIMES") == "1" and device.type == "cuda") else None
     t0 = time.perf_counter()
     for i in range(args.steps):
+        if step_ev is not None:
+            step_ev.append(torch.cuda.Event(enable_timing=True))
+            step_ev[-1].record()
         loss, metrics = step(args.warmup + i)
         lead.step_done(device)
+    if step_ev is not None:
+        step_ev.append(torch.cuda.Event(enable_timing=True))
+        step_ev[-1].record()
     _sync(device)
+    if step_ev is not None:
+        ms = [a.elapsed_time(b) for a, b in zip(step_ev, step_ev[1:])]
+        print("step ms: " + " ".join(f"{v:.2f}" for v in ms), file=sys.stderr, flush=True)
     if distributed:
         dist.barrier()
     _sync(device)
