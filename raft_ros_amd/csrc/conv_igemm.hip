@@ -1286,7 +1286,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   constexpr int HWD = TW + KW - 1;                  // 2-D halo block pitch (pixels)
   constexpr int HROWS = (TH + KH - 1) * HWD;        // 2-D halo block pixels
   constexpr int SPW2 = (HROWS + 8 * NW - 1) / (8 * NW);  // its DMA pieces per wave
-  static_assert(TW == 0 || (BM % TW == 0 && TW % 32 == 0 && SPW2 * 8 * NW <= CF::MAX_ROWS), "2-D tile");
+  static_assert(TW == 0 || (BM % TW == 0 && TW % 16 == 0 && SPW2 * 8 * NW <= CF::MAX_ROWS), "2-D tile");
   const int tilesN = (Nn + BN - 1) / BN;
   int tilesM;
   if constexpr (TW == 0) tilesM = (P + BM - 1) / BM;
@@ -2079,7 +2079,8 @@ bool launch_fwd6_t(const ConvFwdArgs& a, hipStream_t s) {
 }
 // v6 tiles (forced with cfg, chosen per shape by launch_conv_fwd): 41 = 256x64 flat strip (4x1
 // waves of 64x64; 3x3 / 1x5 / 5x1), 45 = 256x128 flat strip (2x2 waves of 128x64), 59 = 256x64
-// as 2-D 4 x 64 tiles (3x3, 1x5), 60 = 256x64 as 2-D 8 x 32 tiles (5x1).  (Measured and
+// as 2-D 4 x 64 tiles (3x3, 1x5), 60 = 256x64 as 2-D 8 x 32 tiles (5x1), 61 = 256x64 as 2-D
+// 16 x 16 tiles (3x3, 5x1).  (Measured and
 // dropped: 128x128 4-wave flat and 2-D tiles, cfg 40 / 57 / 58; all next-step reads before the
 // step's MFMAs, cfg 43 / 44 / 46: profiles/r3_bench_conv6_tiles.log, r3_bench_conv6_2d.log.)
 template <bool F16>
@@ -2099,6 +2100,9 @@ bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
       return t15 && launch_fwd6_t<256, 64, 4, 1, 1, 5, 64, F16>(a, s);
     case 60:
       return t51 && launch_fwd6_t<256, 64, 4, 1, 5, 1, 32, F16>(a, s);
+    case 61:  // 16 x 16 2-D tiles (less halo per output pixel than 8 x 32 / 4 x 64)
+      if (t33) return launch_fwd6_t<256, 64, 4, 1, 3, 3, 16, F16>(a, s);
+      return t51 && launch_fwd6_t<256, 64, 4, 1, 5, 1, 16, F16>(a, s);
     default:
       return false;
   }
@@ -2146,7 +2150,7 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
   bool ok5 = a.KH * a.KW > 1 && a.Cin % 64 == 0 && a.N >= 64 && a.P < (1L << 30);
   for (int i = 0; i < a.nsrc; ++i) ok5 = ok5 && a.src[i].C % 64 == 0;
   int v5 = cfg >= 20 ? cfg : 0;
-  if (cfg == 41 || cfg == 45 || cfg == 59 || cfg == 60) {  // v6 tiles (tests / microbenchmarks)
+  if (cfg == 41 || cfg == 45 || cfg == 59 || cfg == 60 || cfg == 61) {  // v6 tiles (tests / microbenchmarks)
     const bool shape6 = (a.KH == 3 && a.KW == 3) || (a.KH * a.KW == 5 && (a.KH == 1 || a.KW == 1));
     if (!ok5 || !shape6 || a.PH != a.KH / 2 || a.PW != a.KW / 2) return hipErrorInvalidValue;
     return launch_conv_fwd6<F16>(a, cfg, s) ? hipGetLastError() : hipErrorInvalidValue;

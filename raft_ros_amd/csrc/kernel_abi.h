@@ -540,9 +540,13 @@ RAFT_HD inline int fwd6_halo_rows(int TH, int TW, int KH, int KW, int NW) {
 }
 
 // v6 variant the forward dispatcher picks for a multi-tap stride-1 conv of N outputs over
-// B x H x W pixels (0: v5 / v4), from the measurements in profiles/r3_bench_conv6_*.log:
+// B x H x W pixels (0: v5 / v4), from the measurements in profiles/r3_bench_conv6_*.log and
+// r4_bench_conv6_16x16.log:
 //   41 = 256x64 flat strip, 45 = 256x128 flat strip, 59 = 256x64 as 4 x 64 2-D tiles (3x3,
-//   1x5), 60 = 256x64 as 8 x 32 2-D tiles (5x1).
+//   1x5), 60 = 256x64 as 8 x 32 2-D tiles (5x1).  (61 = 16 x 16 2-D tiles, the least halo per
+//   output pixel, wins alone -- 5x1 at config #2 40.7 -> 39.2 us, the Sintel-crop training 5x1
+//   v4 54.2 -> 39.5 us -- but lost in the step: config #2 even, Sintel crop -0.9 %,
+//   profiles/r4_bench_conv6_16x16.log; forced-variant only.)
 RAFT_HD inline int choose_fwd6(int KH, int KW, int N, int B, int H, int W) {
   const long P = (long)B * H * W;
   if (KH == 3 && KW == 3) {

@@ -157,7 +157,7 @@ static void test_fwd6_plan() {
   // Sintel inference (1 x 55 x 128): 2-D tiles
   EXPECT(choose_fwd6(3, 3, 126, 1, 55, 128) == 59, "sintel conv");
   EXPECT(choose_fwd6(5, 1, 128, 1, 55, 128) == 60, "sintel 5x1");
-  // fits: flat 41 / 45 need their strip, 2-D 59 / 60 their halo block (4 waves)
+  // fits: flat 41 / 45 need their strip, 2-D 59 / 60 / 61 their halo block (4 waves)
   const int taps[3][2] = {{3, 3}, {1, 5}, {5, 1}};
   for (int W = 1; W <= 400; ++W)
     for (int H = 1; H <= 140; H += 13)
@@ -169,7 +169,8 @@ static void test_fwd6_plan() {
           if (c == 45) EXPECT(fwd6_strip_rows(256, 4, kh, kw, W, fwd6_max_rows(128)) > 0, "45 W=%d", W);
           if (c == 59) EXPECT((kh == 3 || kh == 1) && fwd6_halo_rows(4, 64, kh, kw, 4) <= fwd6_max_rows(64), "59");
           if (c == 60) EXPECT(kh == 5 && fwd6_halo_rows(8, 32, kh, kw, 4) <= fwd6_max_rows(64), "60");
-          EXPECT(c == 0 || c == 41 || c == 45 || c == 59 || c == 60, "cfg %d", c);
+          if (c == 61) EXPECT(kh != 1 && fwd6_halo_rows(16, 16, kh, kw, 4) <= fwd6_max_rows(64), "61");
+          EXPECT(c == 0 || c == 41 || c == 45 || c == 59 || c == 60 || c == 61, "cfg %d", c);
         }
   EXPECT(2 * fwd6_sb(128) + 3 * 128 * 128 <= kFwd6Lds && fwd6_sb(64) <= 65408, "LDS layout");
 }
