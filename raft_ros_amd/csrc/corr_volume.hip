@@ -35,6 +35,8 @@
 //     per-lookup transpose kernel remains for rows too long for LDS.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace raft_amd {
 
 
@@ -586,7 +588,9 @@ struct OutRow<SplitOut> {
 
 // RC > 0: the radius as a compile-time constant (RAFT's r = 4): the window index math divides by
 // constants (a runtime 32-bit division is ~30 VALU per use)
-template <typename OutT, int RC = 0>
+// ALL: every level's neighbourhood loads issued up front (4 levels x 2 loads per lane for r = 4)
+// instead of one level ahead, so a wave waits for one load round trip rather than one per level
+template <typename OutT, int RC = 0, bool ALL = false>
 __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const float* __restrict__ coords,
                                                          void* __restrict__ out_, int B, int H, int W, int r_arg,
                                                          int out_ch, const FlowPack fp) {
@@ -634,7 +638,7 @@ __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const floa
   // while level l is blended (the lookup is bound by the load round trips, not by bytes)
   float fx = 0.f, fy = 0.f, nfx = 0.f, nfy = 0.f;
   float v[4];
-  auto issue = [&](int l, float& fxo, float& fyo) __attribute__((always_inline)) {
+  auto issue_to = [&](int l, float& fxo, float& fyo, float (&v)[4]) __attribute__((always_inline)) {
     const float s = 1.0f / float(1 << l);
     const float cx = finite ? cx0 * s : 0.f, cy = finite ? cy0 * s : 0.f;
     const float fx0 = safe_floor(cx), fy0 = safe_floor(cy);
@@ -655,6 +659,39 @@ __global__ __launch_bounds__(256) void lookup_fwd_kernel(PyrDesc pyr, const floa
       v[k] = in ? (pyr.vbf16 ? static_cast<float>(rowb[off]) : row[off]) : 0.f;
     }
   };
+  auto issue = [&](int l, float& fxo, float& fyo) __attribute__((always_inline)) { issue_to(l, fxo, fyo, v); };
+  if constexpr (ALL) {
+    static_assert(RC > 0 && (2 * RC + 2) * (2 * RC + 2) <= 128, "two loads per lane and level");
+    float va[4][4], fxa[4], fya[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      fxa[l] = fya[l] = 0.f;
+      va[l][0] = va[l][1] = va[l][2] = va[l][3] = 0.f;
+      if (l < pyr.levels) issue_to(l, fxa[l], fya[l], va[l]);
+    }
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      if (l >= pyr.levels) break;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int e = lane + 64 * k;
+        if (e < nn) nb[wave][(e / nd) * np + e % nd] = va[l][k];
+      }
+      wave_lds_sync();
+      if (live)
+        for (int ch = lane; ch < win; ch += 64) {
+          const int ix = ch / rd, iy = ch - ix * rd;  // x-offset-major window order
+          const float* n0 = nb[wave] + iy * np + ix;
+          const float val = (1.f - fya[l]) * ((1.f - fxa[l]) * n0[0] + fxa[l] * n0[1]) +
+                            fya[l] * ((1.f - fxa[l]) * n0[np] + fxa[l] * n0[np + 1]);
+          o.put(l * win + ch, val);
+        }
+      wave_lds_sync();
+    }
+    if (live)
+      for (int ch = pyr.levels * win + lane; ch < out_ch; ch += 64) o.put(ch, 0.f);
+    return;
+  }
   // the neighbourhood buffer is private to the wave: its LDS accesses execute in issue order,
   // so a wave-level fence (no workgroup barrier) orders the stores before the blend's reads
   // and those reads before the next level's stores; the 4 waves of a block run decoupled
@@ -917,6 +954,15 @@ hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int 
   return hipGetLastError();
 }
 
+// RAFT_LOOKUP_ALL=0: the one-level-ahead pipeline (A/B runs)
+static bool lookup_all_levels() {
+  static const bool v = [] {
+    const char* e = std::getenv("RAFT_LOOKUP_ALL");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void* out, int out_dtype, int B, int H,
                                   int W, int r, int out_ch, hipStream_t s, void* flow8, void* motion, long smo,
                                   int split_m) {
@@ -929,12 +975,21 @@ hipError_t launch_corr_lookup_fwd(const PyrDesc& pyr, const float* coords, void*
   if (npix == 0) return hipSuccess;
   if (r > 6 || (split && flow8 && split_m <= 0 && motion)) return hipErrorInvalidValue;
   const dim3 g((unsigned)((npix + 3) / 4)), blk(256);
-  if (split && r == 4)
+  const bool all = r == 4 && pyr.levels <= 4 && lookup_all_levels();
+  if (split && all)
+    hipLaunchKernelGGL((lookup_fwd_kernel<SplitOut, 4, true>), g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
+  else if (split && r == 4)
     hipLaunchKernelGGL((lookup_fwd_kernel<SplitOut, 4>), g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
   else if (split && r == 3)
     hipLaunchKernelGGL((lookup_fwd_kernel<SplitOut, 3>), g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
   else if (split)
     hipLaunchKernelGGL((lookup_fwd_kernel<SplitOut>), g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
+  else if (out_dtype == kBF16 && all)
+    hipLaunchKernelGGL((lookup_fwd_kernel<__bf16, 4, true>), g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
+  else if (out_dtype == kF32 && all)
+    hipLaunchKernelGGL((lookup_fwd_kernel<float, 4, true>), g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
+  else if (out_dtype == kF16 && all)
+    hipLaunchKernelGGL((lookup_fwd_kernel<_Float16, 4, true>), g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
   else if (out_dtype == kBF16 && r == 4)
     hipLaunchKernelGGL((lookup_fwd_kernel<__bf16, 4>), g, blk, 0, s, pyr, coords, out, B, H, W, r, out_ch, fp);
   else if (out_dtype == kF32 && r == 4)
