@@ -297,6 +297,7 @@ class AugmentedLoader:
         self.loader = loader
         self.augmentor = augmentor
         self.sampler = loader.sampler
+        self.batch_sampler = loader.batch_sampler
 
     def __len__(self):
         return len(self.loader)
@@ -308,19 +309,39 @@ class AugmentedLoader:
 
 def fetch_dataloader(args, TRAIN_DS: str = "C+T+K+S+H"):
     """Training batches for ``args.stage``.  ``args.batch_size`` is the GLOBAL batch (as in
-    the reference); under DDP each rank loads ``batch_size // world_size`` and augments with
-    its own generator (seeded by ``args.seed`` + rank) on ``args.device``."""
+    the reference): under DDP every rank draws the same shuffled global batch and loads its
+    own slice of it (``parallel/batching.py``: uneven splits such as 10 over 8 ranks are
+    exact; a rank with no sample gets an :class:`IdleLoader`), and augments with its own
+    generator (seeded by ``args.seed`` + rank) on ``args.device``."""
+    from ..parallel.batching import GlobalBatchSampler, IdleLoader, rank_batch_sizes
+
     world = int(getattr(args, "world_size", 1) or 1)
     rank = int(getattr(args, "rank", 0) or 0)
-    per_rank = max(1, args.batch_size // world)
+    if args.stage == "synthetic":  # device-resident pool (data/synthetic.py DeviceSyntheticLoader)
+        from .synthetic import DeviceSyntheticLoader
+
+        sizes = rank_batch_sizes(args.batch_size, world, getattr(args, "batch_split", "balanced"))
+        steps = 100000 // args.batch_size
+        if rank == 0:
+            print("Training with %d synthetic image pairs (device-resident pool)" % (steps * args.batch_size))
+        if sizes[rank] == 0:
+            return IdleLoader(GlobalBatchSampler(steps * args.batch_size, sizes, rank))
+        device = getattr(args, "device", None) or ("cuda" if torch.cuda.is_available() else "cpu")
+        return DeviceSyntheticLoader(sizes[rank], args.image_size, device,
+                                     seed=int(getattr(args, "seed", 1234)) + 1000 * rank, steps=steps)
     dataset, specs = build_train_dataset(args.stage, args.image_size, TRAIN_DS)
-    sampler = None
-    if world > 1:
-        sampler = data.distributed.DistributedSampler(dataset, num_replicas=world, rank=rank, shuffle=True,
-                                                      drop_last=True)
     workers = int(getattr(args, "num_workers", 4))
-    kw = dict(batch_size=per_rank, sampler=sampler, shuffle=sampler is None, num_workers=workers, drop_last=True,
-              pin_memory=torch.cuda.is_available(), persistent_workers=workers > 0)
+    kw = dict(num_workers=workers, pin_memory=torch.cuda.is_available(), persistent_workers=workers > 0)
+    if world > 1:
+        sizes = rank_batch_sizes(args.batch_size, world, getattr(args, "batch_split", "balanced"))
+        bs = GlobalBatchSampler(len(dataset), sizes, rank, seed=int(getattr(args, "seed", 1234)))
+        if sizes[rank] == 0:
+            if rank == 0:
+                print("Training with %d image pairs" % len(dataset))
+            return IdleLoader(bs)
+        kw["batch_sampler"] = bs
+    else:
+        kw.update(batch_size=args.batch_size, shuffle=True, drop_last=True)
     if rank == 0:
         print("Training with %d image pairs" % len(dataset))
     if specs is None:  # synthetic: already-final tensors

@@ -112,3 +112,34 @@ def demo_sequence(n_frames: int = 6, h: int = 436, w: int = 1024, seed: int = 16
 
 
 _demo_full = demo_sequence  # (tests substitute smaller frames through demo_sequence)
+
+
+class DeviceSyntheticLoader:
+    """``--stage synthetic`` batches generated ON the training device: ``pool`` batches of
+    ``batch`` pairs are made once (``synthetic_batch``, seeded by ``seed``) and replayed in a
+    per-epoch shuffled order, ``steps`` batches per epoch.  Generating on the CPU in DataLoader
+    workers costs ~20 ms per 368x496 pair and capped train.py at ~200 pairs/s on an MI355X
+    (profiles/r5a_train_synth.log) -- the synthetic stage is a pipeline / throughput check, so
+    its batches come from device memory, as bench.py's do (pairs are what a real stage's
+    decode + device augmentation would hand the model)."""
+
+    def __init__(self, batch: int, size, device, pool: int = 8, seed: int = 0, steps: int = 12500):
+        h, w = int(size[0]), int(size[1])
+        self.pool = [synthetic_batch(batch, h, w, seed=seed * 7919 + i, device=device) for i in range(pool)]
+        self.steps = int(steps)
+        self.seed = int(seed)
+        self.epoch = 0
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = int(epoch)
+
+    def __len__(self) -> int:
+        return self.steps
+
+    def __iter__(self):
+        g = torch.Generator()
+        g.manual_seed(self.seed + 104729 * self.epoch)
+        n = len(self.pool)
+        order = torch.randint(0, n, (self.steps,), generator=g).tolist()
+        for i in order:
+            yield self.pool[i]

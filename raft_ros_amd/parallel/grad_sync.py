@@ -18,6 +18,13 @@ hook, no copy), then after ``backward()``:
   2. one all-reduce of the flat buffer (RCCL ``AVG`` over xGMI; gloo: SUM + one scale);
   3. each ``p.grad`` becomes a view of its slice of the averaged buffer (no copy back).
 
+A parameter that no rank computed a gradient for keeps ``p.grad = None`` (so AdamW skips
+it, as in single-process training and DDP).  Which parameters receive gradients is found
+once, on the first ``sync()``: a per-parameter "had a gradient" count rides in the same
+all-reduce and is read back on the host that one time (RAFT uses every parameter in every
+step; a rank with no sample of the global batch -- parallel/batching.py -- has no gradient
+at all and sends zeros).
+
 At 21 MB the ring all-reduce over 8 MI355X is ~0.1-0.2 ms: one large collective is the cheap
 case on point-to-point xGMI links.  ``bf16=True`` halves the bytes on the wire (the buffer is
 cast to bf16 for the all-reduce; each rank's contribution is rounded to bf16).
@@ -44,7 +51,10 @@ class GradSync:
         dev = self.params[0].device
         self.backend = dist.get_backend(group)
         total = sum(p.numel() for p in self.params)
-        self.flat = torch.empty(total, device=dev, dtype=torch.float32)
+        self.total = total
+        # + one "had a gradient" slot per parameter (used by the first sync only)
+        self.flat = torch.empty(total + len(self.params), device=dev, dtype=torch.float32)
+        self.used: Optional[List[bool]] = None
         self.views: List[torch.Tensor] = []
         off = 0
         for p in self.params:
@@ -61,7 +71,13 @@ class GradSync:
     def sync(self) -> None:
         """Average ``p.grad`` over the ranks (call after ``backward()``, before unscale / clip /
         the optimizer).  A parameter without a gradient contributes zeros (every rank must
-        send the same buffer) and gets the averaged gradient of the others."""
+        send the same buffer) and gets the averaged gradient of the others; one that no rank
+        has a gradient for stays ``None``."""
+        first = self.used is None
+        if first:
+            flags = torch.tensor([0.0 if p.grad is None else 1.0 for p in self.params], dtype=torch.float32)
+            self.flat[self.total:].copy_(flags)
+        n = self.flat.numel() if first else self.total
         grads = []
         for p, v in zip(self.params, self.views):
             g = p.grad
@@ -76,18 +92,21 @@ class GradSync:
             for v, g in zip(self.views, grads):
                 v.copy_(g)
         if self.world > 1:
+            flat = self.flat[:n]
             if self.bf16:
-                buf = self.flat.to(torch.bfloat16)
+                buf = flat.to(torch.bfloat16)
                 dist.all_reduce(buf, group=self.group)
-                self.flat.copy_(buf)
-                self.flat.mul_(1.0 / self.world)
+                flat.copy_(buf)
+                flat.mul_(1.0 / self.world)
             elif self.backend == "nccl":
-                dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=self.group)
+                dist.all_reduce(flat, op=dist.ReduceOp.AVG, group=self.group)
             else:
-                dist.all_reduce(self.flat, group=self.group)
-                self.flat.mul_(1.0 / self.world)
-        for p, v in zip(self.params, self.views):
-            p.grad = v
+                dist.all_reduce(flat, group=self.group)
+                flat.mul_(1.0 / self.world)
+        if first:  # one host read, on the first step only
+            self.used = (self.flat[self.total:] > 0).tolist()
+        for p, v, u in zip(self.params, self.views, self.used):
+            p.grad = v if u else None
 
 
 def _dense(p: torch.Tensor) -> bool:

@@ -50,6 +50,9 @@ def _fused_ok(flow_preds, flow_gt) -> bool:
             and all(p.dtype == torch.float32 and p.shape == flow_gt.shape for p in flow_preds))
 
 
+METRIC_KEYS = ("epe", "1px", "3px", "5px")  # the metrics sequence_loss returns
+
+
 def sequence_loss(flow_preds: List[torch.Tensor], flow_gt: torch.Tensor, valid: torch.Tensor,
                   gamma: float = 0.8, max_flow: float = MAX_FLOW):
     if _fused_ok(flow_preds, flow_gt):

@@ -10,7 +10,10 @@ checkpoint every ``VAL_FREQ`` steps followed by validation, and a final
 MI355X-specific:
 
 * one process per GPU with DDP over RCCL (torchrun, or ``--gpus 0 1 ...``
-  which spawns the ranks itself); ``--batch_size`` stays the GLOBAL batch;
+  which spawns the ranks itself); ``--batch_size`` stays the GLOBAL batch, split
+  exactly over the ranks (``parallel/batching.py``: 10 over 8 ranks trains 10
+  samples per step, each rank's loss weighted by its share; idle ranks of a
+  batch smaller than the world contribute zero gradients);
 * bf16 autocast by default for ``--mixed_precision`` (``--amp_dtype fp16``
   restores the reference's fp16 + GradScaler);
 * channels-last model, fused AdamW, loss metrics kept on the device;
@@ -31,10 +34,11 @@ from ..eval.validate import run_validation
 from ..models import RAFT
 from ..ops.streams import LeadLimiter, step_context
 from ..parallel import ddp
+from ..parallel.batching import check_sync_bn, loss_weight, rank_batch_sizes
 from ..utils import checkpoint, fault
 from ..utils.profiling import maybe_profiler, trace_range
 from .logger import Logger
-from .loss import sequence_loss
+from .loss import METRIC_KEYS, sequence_loss
 from .optim import count_parameters, fetch_optimizer
 
 VAL_FREQ = 5000
@@ -50,13 +54,24 @@ def _infinite(loader, sampler_epoch=None):
         epoch += 1
 
 
-def train(args: Namespace) -> str:
+def _dummy_batch(image_size):
+    """One all-zero sample (weight 0): an idle rank's forward under torch DDP."""
+    h, w = int(image_size[0]), int(image_size[1])
+    return (torch.zeros(1, 3, h, w), torch.zeros(1, 3, h, w), torch.zeros(1, 2, h, w), torch.zeros(1, h, w))
+
+
+def train(args: Namespace, on_finish=None) -> str:
     info = ddp.init_distributed()
     args.rank, args.world_size = info.rank, info.world_size
     dev = info.device
-    if args.batch_size % info.world_size != 0 and info.is_main:
-        print(f"warning: global batch {args.batch_size} not divisible by {info.world_size} ranks; "
-              f"using {args.batch_size // info.world_size} per rank")
+    # the global batch split over the ranks, and this rank's loss weight (b_r * W / B: the
+    # AVG all-reduce of the weighted gradients is the full-batch gradient)
+    sizes = rank_batch_sizes(args.batch_size, info.world_size, getattr(args, "batch_split", "balanced"))
+    weight = loss_weight(sizes, info.rank)
+    if info.distributed and info.is_main:
+        print(f"global batch {args.batch_size} over {info.world_size} ranks: {sizes}")
+    if getattr(args, "sync_bn", False) and info.distributed:
+        check_sync_bn(sizes)
 
     model = RAFT(args)
     if info.is_main:
@@ -84,9 +99,8 @@ def train(args: Namespace) -> str:
     optimizer, scheduler = fetch_optimizer(args, model)
     use_scaler = bool(args.mixed_precision) and getattr(args, "amp_dtype", "bf16") == "fp16" and dev.type == "cuda"
     scaler = torch.amp.GradScaler("cuda", enabled=use_scaler)
-    per_rank = max(1, args.batch_size // info.world_size)
     logger = Logger(model, scheduler, log_dir=os.path.join(args.log_dir, args.name), enabled=info.is_main,
-                    pairs_per_step=per_rank * info.world_size,
+                    pairs_per_step=args.batch_size,
                     reduce_fn=(lambda m: ddp.all_reduce_mean(m, info)) if info.distributed else None)
 
     total_steps = 0
@@ -98,8 +112,11 @@ def train(args: Namespace) -> str:
             if info.is_main:
                 print(f"resumed at step {st}")
 
-    sampler = getattr(train_loader, "sampler", None)
-    set_epoch = sampler.set_epoch if hasattr(sampler, "set_epoch") else None
+    set_epoch = None
+    for smp in (train_loader, getattr(train_loader, "batch_sampler", None), getattr(train_loader, "sampler", None)):
+        if hasattr(smp, "set_epoch"):
+            set_epoch = smp.set_epoch
+            break
     skipped = torch.zeros((), device=dev)
     fused_opt = bool(optimizer.defaults.get("fused"))
     injector = fault.Injector.from_env(info.rank)  # RAFT_FAULT_INJECT (tests only)
@@ -112,18 +129,29 @@ def train(args: Namespace) -> str:
         # the step on the high-priority step stream (ops/streams.py; RAFT_HP_MAIN=0 disables)
         with step_context(dev):
             optimizer.zero_grad(set_to_none=True)
-            image1, image2, flow, valid = [x.to(dev, non_blocking=True) for x in data_blob]
+            idle = data_blob is None  # no sample of the global batch on this rank
+            if idle and gsync is None:
+                # torch DDP needs every rank in the backward: a zero-weight dummy sample
+                data_blob = _dummy_batch(args.image_size)
             if args.add_noise:
-                stdv = np.random.uniform(0.0, 5.0)
-                image1 = (image1 + stdv * torch.randn_like(image1)).clamp(0.0, 255.0)
-                image2 = (image2 + stdv * torch.randn_like(image2)).clamp(0.0, 255.0)
+                stdv = np.random.uniform(0.0, 5.0)  # drawn on every rank: same RNG stream
+            if idle and gsync is not None:
+                metrics = {k: torch.zeros((), device=dev) for k in METRIC_KEYS}
+            else:
+                image1, image2, flow, valid = [x.to(dev, non_blocking=True) for x in data_blob]
+                if args.add_noise:
+                    image1 = (image1 + stdv * torch.randn_like(image1)).clamp(0.0, 255.0)
+                    image2 = (image2 + stdv * torch.randn_like(image2)).clamp(0.0, 255.0)
 
-            with trace_range("forward"):
-                flow_predictions = net(image1, image2, iters=args.iters)
-                loss, metrics = sequence_loss(flow_predictions, flow, valid, args.gamma)
-                loss = injector.on_loss(total_steps, loss)
-            with trace_range("backward"):
-                scaler.scale(loss).backward()
+                with trace_range("forward"):
+                    flow_predictions = net(image1, image2, iters=args.iters)
+                    loss, metrics = sequence_loss(flow_predictions, flow, valid, args.gamma)
+                    loss = injector.on_loss(total_steps, loss)
+                    if weight != 1.0 or idle:
+                        loss = loss * (0.0 if idle else weight)
+                        metrics = {k: v * (0.0 if idle else weight) for k, v in metrics.items()}
+                with trace_range("backward"):
+                    scaler.scale(loss).backward()
             if gsync is not None:
                 with trace_range("grad_sync"):
                     gsync.sync()
@@ -168,13 +196,15 @@ def train(args: Namespace) -> str:
     prof.__exit__(None, None, None)
     if info.is_main:
         dt = time.perf_counter() - t0
-        print(f"trained {total_steps} steps in {dt:.1f}s ({per_rank * info.world_size * total_steps / dt:.2f} "
+        print(f"trained {total_steps} steps in {dt:.1f}s ({args.batch_size * total_steps / dt:.2f} "
               f"pairs/s, {int(skipped.item())} non-finite steps skipped)")
     logger.close()
     path = os.path.join(args.ckpt_dir, "%s.pth" % args.name)
     if info.is_main:
         checkpoint.save_weights(model, path)
         checkpoint.save_state(checkpoint.state_path(path), optimizer, scheduler, scaler, total_steps)
+    if on_finish is not None:  # test hook: inspect every rank's final model
+        on_finish(model, info)
     ddp.barrier(info)
     ddp.cleanup()
     return path

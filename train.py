@@ -47,6 +47,12 @@ def build_parser() -> argparse.ArgumentParser:
                    help="with --mixed_precision bf16: keep the correlation volume fp32-faithful (split-bf16 GEMM, "
                         "fp32 storage) like the reference (core/raft.py:102-103) instead of the bf16 volume")
     g.add_argument("--no_channels_last", dest="channels_last", action="store_false")
+    g.add_argument("--no_native_encoder", dest="native_encoder", action="store_false",
+                   help="encoders on PyTorch/MIOpen convs (exact fp32 training without AMP; the native fp32 "
+                        "encoder runs split-bf16 GEMMs)")
+    g.add_argument("--batch_split", default="balanced", choices=["balanced", "chunk"],
+                   help="how the global --batch_size splits over the ranks: balanced (10 over 8 = 2,2,1,1,1,1,1,1) "
+                        "or chunk (DataParallel's torch.chunk grouping: 2,2,2,2,2,0,0,0)")
     g.add_argument("--no_fused_update", dest="fused_update", action="store_false",
                    help="run the update block on PyTorch convs instead of the fused HIP kernels")
     g.add_argument("--resume", action="store_true", help="also restore optimizer/scheduler/step from <ckpt>.state.pt")
@@ -77,7 +83,9 @@ def _main(args) -> str:
 
     rank = int(os.environ.get("RANK", "0"))
     torch.manual_seed(args.seed + rank)
-    np.random.seed(args.seed + rank)
+    # the same numpy stream on every rank: --add_noise draws ONE sigma per global batch, as the
+    # reference does (train.py:167-170); per-rank augmentation has its own generators
+    np.random.seed(args.seed)
     if getattr(args, "deterministic", False):
         torch.use_deterministic_algorithms(True, warn_only=True)
         torch.backends.cudnn.benchmark = False
