@@ -1214,17 +1214,27 @@ inline long fwd5_lds_bytes(int BM, int BN, int strip_rows) {
 // SB bytes; the last 128-B row of each strip buffer is a zero row.
 constexpr int kLdsMax = 160 * 1024;
 
-template <int BN, int WGN, int NT>
+// Flat strips (TW == 0) take the whole 160 KB (their strip length depends on the image width);
+// 2-D tiles size the strip buffers to their halo block, so a small tile (BM = 128) fits two
+// workgroups per CU -- two waves per SIMD, and a grid quantised over 512 slots instead of 256.
+template <int BM, int BN, int NW, int KH, int KW, int TW>
 struct Fwd6Cfg {
+  static constexpr int NT = KH * KW;
   static constexpr int NS = 3;                        // weight ring stages
   static constexpr int U = (NT % 3 == 0) ? 2 : 6;     // chunks per unrolled block: U * NT % 6 == 0,
                                                       // so stage (step % 3), register set (step & 1)
                                                       // and strip parity (chunk & 1) are compile-time
   static constexpr int RING = NS * BN * 128;
-  static constexpr int SB = fwd6_sb(BN);              // odd-chunk strip = +SB immediate offset
-  static constexpr int MAX_ROWS = fwd6_max_rows(BN);  // strip rows (the last row is the zero row)
-  static constexpr int LDS = RING + 2 * SB;
-  static_assert(LDS <= kLdsMax, "LDS budget");
+  // strip rows: a 2-D tile's halo block; a flat 1 x KW strip's BM + KW - 1 pixels (independent of
+  // the image width); other flat strips take what the 160 KB leave
+  static constexpr int HALO = TW > 0   ? fwd6_halo_rows(BM / (TW > 0 ? TW : 1), TW, KH, KW, NW)
+                              : KH == 1 ? (BM + KW - 1 + 8 * NW - 1) / (8 * NW) * (8 * NW)
+                                        : 0;
+  static constexpr int SB = HALO > 0 && BM <= 128 ? (HALO + 1) * 128 : fwd6_sb(BN);  // odd strip = +SB
+  static constexpr int MAX_ROWS = SB / 128 - 1;       // strip rows (the last row is the zero row)
+  static constexpr int EPI = BM * (BN + 4) * 4;       // the epilogue's fp32 staging tile
+  static constexpr int LDS = (RING + 2 * SB) > EPI ? (RING + 2 * SB) : EPI;
+  static_assert(LDS <= kLdsMax && SB <= 65408, "LDS budget");
 };
 
 template <class F, int... I>
@@ -1258,7 +1268,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   constexpr int WM = BM / WGM, WN = BN / WGN;  // wave tile
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int NT = KH * KW;
-  using CF = Fwd6Cfg<BN, WGN, NT>;
+  using CF = Fwd6Cfg<BM, BN, WGM * WGN, KH, KW, TW>;
   constexpr int NS = CF::NS, SB = CF::SB, RING = CF::RING;
   constexpr int BI = BN / (8 * NW);  // weight pieces (8 rows x 128 B) per wave per step
   constexpr int BSTAGE = BN * 128;
@@ -1286,7 +1296,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   constexpr int HWD = TW + KW - 1;                  // 2-D halo block pitch (pixels)
   constexpr int HROWS = (TH + KH - 1) * HWD;        // 2-D halo block pixels
   constexpr int SPW2 = (HROWS + 8 * NW - 1) / (8 * NW);  // its DMA pieces per wave
-  static_assert(TW == 0 || (BM % TW == 0 && TW % 16 == 0 && SPW2 * 8 * NW <= CF::MAX_ROWS), "2-D tile");
+  static_assert(TW == 0 || (BM % TW == 0 && TW % 8 == 0 && SPW2 * 8 * NW <= CF::MAX_ROWS), "2-D tile");
   const int tilesN = (Nn + BN - 1) / BN;
   int tilesM;
   if constexpr (TW == 0) tilesM = (P + BM - 1) / BM;
@@ -2060,7 +2070,7 @@ __global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
 namespace {
 template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW, bool F16>
 bool launch_fwd6_t(const ConvFwdArgs& a, hipStream_t s) {
-  using CF = Fwd6Cfg<BN, WGN, KH * KW>;
+  using CF = Fwd6Cfg<BM, BN, WGM * WGN, KH, KW, TW>;
   constexpr int NW = WGM * WGN;
   int rows = 0;
   long tiles;
@@ -2103,6 +2113,20 @@ bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
     case 61:  // 16 x 16 2-D tiles (less halo per output pixel than 8 x 32 / 4 x 64)
       if (t33) return launch_fwd6_t<256, 64, 4, 1, 3, 3, 16, F16>(a, s);
       return t51 && launch_fwd6_t<256, 64, 4, 1, 5, 1, 16, F16>(a, s);
+    // 128 x 64 2-D tiles, two workgroups (8 waves) per CU: 62 = 4x1 waves of 32 x 64, 63 = 2x2
+    // waves of 64 x 32; 3x3 as 8 x 16, 1x5 as 2 x 64, 5x1 as 16 x 8 (64: 5x1 as 8 x 16)
+    case 62:
+      if (t33) return launch_fwd6_t<128, 64, 4, 1, 3, 3, 16, F16>(a, s);
+      if (t15) return launch_fwd6_t<128, 64, 4, 1, 1, 5, 64, F16>(a, s);
+      return t51 && launch_fwd6_t<128, 64, 4, 1, 5, 1, 8, F16>(a, s);
+    case 63:
+      if (t33) return launch_fwd6_t<128, 64, 2, 2, 3, 3, 16, F16>(a, s);
+      if (t15) return launch_fwd6_t<128, 64, 2, 2, 1, 5, 64, F16>(a, s);
+      return t51 && launch_fwd6_t<128, 64, 2, 2, 5, 1, 8, F16>(a, s);
+    case 64:
+      return t51 && launch_fwd6_t<128, 64, 4, 1, 5, 1, 16, F16>(a, s);
+    case 65:  // 1x5 as a flat 128-pixel strip (132 halo rows at any width), two workgroups per CU
+      return t15 && launch_fwd6_t<128, 64, 4, 1, 1, 5, 0, F16>(a, s);
     default:
       return false;
   }
@@ -2150,25 +2174,16 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
   bool ok5 = a.KH * a.KW > 1 && a.Cin % 64 == 0 && a.N >= 64 && a.P < (1L << 30);
   for (int i = 0; i < a.nsrc; ++i) ok5 = ok5 && a.src[i].C % 64 == 0;
   int v5 = cfg >= 20 ? cfg : 0;
-  if (cfg == 41 || cfg == 45 || cfg == 59 || cfg == 60 || cfg == 61) {  // v6 tiles (tests / microbenchmarks)
+  if (cfg == 41 || cfg == 45 || (cfg >= 59 && cfg <= 65)) {  // v6 tiles (tests / microbenchmarks)
     const bool shape6 = (a.KH == 3 && a.KW == 3) || (a.KH * a.KW == 5 && (a.KH == 1 || a.KW == 1));
     if (!ok5 || !shape6 || a.PH != a.KH / 2 || a.PW != a.KW / 2) return hipErrorInvalidValue;
     return launch_conv_fwd6<F16>(a, cfg, s) ? hipGetLastError() : hipErrorInvalidValue;
   }
   if (ok5 && cfg == 0 && a.PH == a.KH / 2 && a.PW == a.KW / 2) {
-    // v6 where it measured faster than v5 at config #2 (scripts/bench_conv6.py,
-    // profiles/r3_bench_conv6_tiles.log; bitwise-equal results): 3x3 with N <= 128 or N > 256
-    // (conv 32.0 -> 27.2 us, head data gradients 29.8 -> 25.1, heads 51.7 -> 45.6) and 1x5 with
-    // N <= 128 (q 26.4 -> 23.8) on 256x64 tiles; the 192-wide 3x3 on 256x128 (43.1 -> 41.8);
-    // every 5x1 (z||r 52.4 -> 46.9, q 27.9 -> 25.5, data gradient 58.5 -> 53.9) on 128x128.
-    // Shapes whose strip does not fit (wide images) fall through to v5 / v4.
-    // Wide images (the flat strip does not fit: Sintel / KITTI / 1080p widths) take the 2-D
-    // tiles (profiles/r3_bench_conv6_2d.log): 4 x 64 for a 3x3 when its grid is one round of
-    // the 256 CUs or v4 would pad N (N = 64, 192, > 256: 1080p convc2 63.0 -> 41.8 us, Sintel
-    // conv 28.5 -> 23.0), otherwise v5 / v4 (1080p conv 37.1 v4 vs 45.6 with 272 workgroups);
-    // 8 x 32 for every 5x1 up to ~24k pixels (config #2 z||r 43.9 -> 38.9, Sintel q 22.8 -> 20.0;
-    // v4 keeps 1080p's 32k pixels: 29.5 vs 39.1 us).  The rule: choose_fwd6 (kernel_abi.h,
-    // unit-tested on the host).
+    // v6 on 128 x 64 tiles, two workgroups per CU, for every 3x3 / 1x5 / 5x1 update-block
+    // shape (the rule and its measurements: choose_fwd6 in kernel_abi.h, unit-tested on the
+    // host; profiles/r5b_conv6_*.log).  Before round 5: 256 x 64 / 256 x 128 one-workgroup
+    // tiles (profiles/r3_bench_conv6_*.log, r4_bench_conv6_16x16.log), now forced variants.
     const int v6 = choose_fwd6(a.KH, a.KW, a.N, a.B, a.H, a.W);
     if (v6 && launch_conv_fwd6<F16>(a, v6, s)) return hipGetLastError();
   }

@@ -534,37 +534,35 @@ RAFT_HD inline int fwd6_strip_rows(int BM, int NW, int KH, int KW, int W, int ma
 
 // 2-D tile of TH x TW output pixels: its halo block of (TH + KH - 1) x (TW + KW - 1) pixels,
 // padded to whole DMA pieces
-RAFT_HD inline int fwd6_halo_rows(int TH, int TW, int KH, int KW, int NW) {
+RAFT_HD constexpr int fwd6_halo_rows(int TH, int TW, int KH, int KW, int NW) {
   const int rows = (TH + KH - 1) * (TW + KW - 1);
   return (rows + 8 * NW - 1) / (8 * NW) * (8 * NW);
 }
 
 // v6 variant the forward dispatcher picks for a multi-tap stride-1 conv of N outputs over
-// B x H x W pixels (0: v5 / v4), from the measurements in profiles/r3_bench_conv6_*.log and
-// r4_bench_conv6_16x16.log:
-//   41 = 256x64 flat strip, 45 = 256x128 flat strip, 59 = 256x64 as 4 x 64 2-D tiles (3x3,
-//   1x5), 60 = 256x64 as 8 x 32 2-D tiles (5x1).  (61 = 16 x 16 2-D tiles, the least halo per
-//   output pixel, wins alone -- 5x1 at config #2 40.7 -> 39.2 us, the Sintel-crop training 5x1
-//   v4 54.2 -> 39.5 us -- but lost in the step: config #2 even, Sintel crop -0.9 %,
-//   profiles/r4_bench_conv6_16x16.log; forced-variant only.)
+// B x H x W pixels (0: v5 / v4).  Since round 5 every update-block shape takes a 128 x 64 tile
+// whose LDS (halo block + 3-stage weight ring, <= 74 KB) lets two workgroups share a CU: two
+// waves per SIMD hide each other's DMA / barrier waits, and the grid is quantised over 512
+// workgroup slots instead of 256 (scripts/bench_conv6.py, profiles/r5b_conv6_*.log: config #2
+// 3x3 / 1x5 / 5x1 forward and data-gradient shapes 10-29 % faster than the round-4 choice,
+// 1080p 5x1 z||r 54.3 -> 36.5 us, 3x3 conv 37.2 -> 24.0 us):
+//   62 = 2-D tiles: 3x3 as 8 x 16, 1x5 as 2 x 64, 5x1 as 16 x 8;  64 = 5x1 as 8 x 16;
+//   65 = 1x5 as a flat 128-pixel strip (132 halo rows at any width: wide images).
+// The 5x1 tile is the one with fewer 512-slot rounds of workgroups (16 x 8: less halo per
+// pixel, 8 x 16: fewer tiles on 1080p's 135-row planes).  The round-3/4 one-workgroup tiles
+// (41 / 45 / 59 / 60 / 61, 256 x 64 / 256 x 128) remain as forced variants (tests, benches).
+RAFT_HD inline int fwd6_tiles2d(int B, int H, int W, int TH, int TW) {
+  return B * ((H + TH - 1) / TH) * ((W + TW - 1) / TW);
+}
 RAFT_HD inline int choose_fwd6(int KH, int KW, int N, int B, int H, int W) {
-  const long P = (long)B * H * W;
-  if (KH == 3 && KW == 3) {
-    if (fwd6_strip_rows(256, 4, 3, 3, W, fwd6_max_rows(64)) > 0) {
-      if (N <= 128 || N > 256) return 41;
-      if (N <= 192) return fwd6_strip_rows(256, 4, 3, 3, W, fwd6_max_rows(128)) > 0 ? 45 : 0;
-      return 0;
-    }
-    // wide images: 2-D tiles when the grid is one round of the 256 CUs or v4 would pad N
-    const long wg = (long)B * ((H + 3) / 4) * ((W + 63) / 64) * ((N + 63) / 64);
-    const int np = (N + 63) / 64 * 64;
-    return (wg <= 256 || (np != 128 && np != 256)) ? 59 : 0;
+  const int tn = (N + 63) / 64;
+  if (KH == 3 && KW == 3) return 62;
+  if (KH == 1 && KW == 5) return W <= 64 ? 62 : 65;
+  if (KH == 5 && KW == 1) {
+    const long r62 = ((long)fwd6_tiles2d(B, H, W, 16, 8) * tn + 511) / 512;
+    const long r64 = ((long)fwd6_tiles2d(B, H, W, 8, 16) * tn + 511) / 512;
+    return r64 < r62 ? 64 : 62;
   }
-  if (KH == 1 && KW == 5) {
-    if (N > 128) return 0;
-    return P <= 24576 ? 59 : 41;
-  }
-  if (KH == 5 && KW == 1) return P <= 24576 ? 60 : 0;
   return 0;
 }
 

@@ -47,7 +47,7 @@ SHAPES = {
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cfgs", default="41,45,59,60")
+    ap.add_argument("--cfgs", default="41,45,59,60,62,63,64")
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--hw", type=int, nargs=2, default=[46, 62])
     ap.add_argument("--only", default="")

@@ -118,11 +118,12 @@ def run(small, variants, scope):
             loss, _, grads = grad_step(m, torch.device("cpu"))
         finally:
             nn.Conv2d._conv_forward = orig
-        e = grad_errors(grads, gfix, name)
-        e = {k: v for k, v in e.items() if k.startswith(scope)}
+        e_all = grad_errors(grads, gfix, name)
+        rms_all = (sum(v * v for v in e_all.values()) / len(e_all)) ** 0.5
+        e = {k: v for k, v in e_all.items() if k.startswith(scope)}
         worst = sorted(e.items(), key=lambda kv: -kv[1])[:3]
         rms = (sum(v * v for v in e.values()) / len(e)) ** 0.5
-        print(f"{name} {var:14s} loss {loss:.6f}  RMS {rms:.2e}  worst " +
+        print(f"{name} {var:14s} loss {loss:.6f}  RMS {rms:.2e} (all params {rms_all:.2e})  worst " +
               ", ".join(f"{k} {v:.2e}" for k, v in worst), flush=True)
         res.append({"variant": var, "worst": worst[0][1], "worst_param": worst[0][0], "rms": rms})
     return res

@@ -138,26 +138,22 @@ static void test_wgrad_plans() {
 // conv_fwd6 selection: the measured choices at the benchmark shapes, and every chosen variant's
 // strip / halo block fits the LDS the kernel allocates, at any image width
 static void test_fwd6_plan() {
-  // config #2 (8 x 46 x 62): conv 126 / convc2 192 / flow+mask head 256 / heads 512 / 1x5 q /
-  // 1x5 z||r / 5x1
-  EXPECT(choose_fwd6(3, 3, 126, 8, 46, 62) == 41, "conv");
-  EXPECT(choose_fwd6(3, 3, 192, 8, 46, 62) == 45, "convc2");
-  EXPECT(choose_fwd6(3, 3, 256, 8, 46, 62) == 0, "fh1");
-  EXPECT(choose_fwd6(3, 3, 512, 8, 46, 62) == 41, "heads");
-  EXPECT(choose_fwd6(1, 5, 128, 8, 46, 62) == 59, "q 1x5");
-  EXPECT(choose_fwd6(1, 5, 256, 8, 46, 62) == 0, "z||r 1x5");
-  EXPECT(choose_fwd6(5, 1, 256, 8, 46, 62) == 60, "z||r 5x1");
-  EXPECT(choose_fwd6(5, 1, 384, 8, 46, 62) == 60, "5x1 data gradient");
-  // 1080p (1 x 135 x 240): v4 for N = 126 / 256 and the 5x1s, 2-D tiles for 64 / 192 / 512
-  EXPECT(choose_fwd6(3, 3, 126, 1, 135, 240) == 0, "1080p conv");
-  EXPECT(choose_fwd6(3, 3, 192, 1, 135, 240) == 59, "1080p convc2");
-  EXPECT(choose_fwd6(3, 3, 64, 1, 135, 240) == 59, "1080p convf2");
-  EXPECT(choose_fwd6(3, 3, 256, 1, 135, 240) == 0, "1080p fh1");
-  EXPECT(choose_fwd6(5, 1, 128, 1, 135, 240) == 0, "1080p 5x1");
-  // Sintel inference (1 x 55 x 128): 2-D tiles
-  EXPECT(choose_fwd6(3, 3, 126, 1, 55, 128) == 59, "sintel conv");
-  EXPECT(choose_fwd6(5, 1, 128, 1, 55, 128) == 60, "sintel 5x1");
-  // fits: flat 41 / 45 need their strip, 2-D 59 / 60 / 61 their halo block (4 waves)
+  // every update-block shape on the 128 x 64 two-workgroups-per-CU tiles: config #2 (8 x 46 x
+  // 62): 3x3 -> 62, 1x5 (W <= 64) -> 62, 5x1 -> 62 (16 x 8 and 8 x 16 tie on rounds)
+  EXPECT(choose_fwd6(3, 3, 126, 8, 46, 62) == 62, "conv");
+  EXPECT(choose_fwd6(3, 3, 192, 8, 46, 62) == 62, "convc2");
+  EXPECT(choose_fwd6(3, 3, 512, 8, 46, 62) == 62, "heads");
+  EXPECT(choose_fwd6(1, 5, 128, 8, 46, 62) == 62, "q 1x5");
+  EXPECT(choose_fwd6(1, 5, 256, 8, 46, 62) == 62, "z||r 1x5");
+  EXPECT(choose_fwd6(5, 1, 256, 8, 46, 62) == 62, "z||r 5x1");
+  EXPECT(choose_fwd6(5, 1, 384, 8, 46, 62) == 62, "5x1 data gradient");
+  // 1080p (1 x 135 x 240): flat 1x5 strips; the 5x1 z||r on 8 x 16 (1020 vs 1080 workgroups)
+  EXPECT(choose_fwd6(1, 5, 256, 1, 135, 240) == 65, "1080p 1x5");
+  EXPECT(choose_fwd6(5, 1, 256, 1, 135, 240) == 64, "1080p 5x1 z||r");
+  EXPECT(choose_fwd6(5, 1, 128, 1, 135, 240) == 64, "1080p 5x1 q");
+  EXPECT(choose_fwd6(3, 3, 126, 1, 135, 240) == 62, "1080p conv");
+  EXPECT(choose_fwd6(7, 7, 128, 1, 135, 240) == 0, "7x7 -> v4");
+  // every choice fits: 2-D halo blocks / the flat 1x5 strip within the two-workgroup budget
   const int taps[3][2] = {{3, 3}, {1, 5}, {5, 1}};
   for (int W = 1; W <= 400; ++W)
     for (int H = 1; H <= 140; H += 13)
@@ -165,12 +161,14 @@ static void test_fwd6_plan() {
         for (int N = 64; N <= 576; N += 64) {
           const int kh = t[0], kw = t[1];
           const int c = choose_fwd6(kh, kw, N, 2, H, W);
-          if (c == 41) EXPECT(fwd6_strip_rows(256, 4, kh, kw, W, fwd6_max_rows(64)) > 0, "41 W=%d", W);
-          if (c == 45) EXPECT(fwd6_strip_rows(256, 4, kh, kw, W, fwd6_max_rows(128)) > 0, "45 W=%d", W);
-          if (c == 59) EXPECT((kh == 3 || kh == 1) && fwd6_halo_rows(4, 64, kh, kw, 4) <= fwd6_max_rows(64), "59");
-          if (c == 60) EXPECT(kh == 5 && fwd6_halo_rows(8, 32, kh, kw, 4) <= fwd6_max_rows(64), "60");
-          if (c == 61) EXPECT(kh != 1 && fwd6_halo_rows(16, 16, kh, kw, 4) <= fwd6_max_rows(64), "61");
-          EXPECT(c == 0 || c == 41 || c == 45 || c == 59 || c == 60 || c == 61, "cfg %d", c);
+          EXPECT(c == 62 || c == 64 || c == 65, "cfg %d", c);
+          if (c == 64) EXPECT(kh == 5, "64 is a 5x1 tile");
+          if (c == 65) EXPECT(kh == 1 && W > 64, "65: wide 1x5");
+          const int halo = c == 65 ? (128 + 4 + 31) / 32 * 32
+                           : c == 64 ? fwd6_halo_rows(8, 16, kh, kw, 4)
+                           : kh == 3 ? fwd6_halo_rows(8, 16, 3, 3, 4)
+                           : kh == 1 ? fwd6_halo_rows(2, 64, 1, 5, 4) : fwd6_halo_rows(16, 8, 5, 1, 4);
+          EXPECT(3 * 64 * 128 + 2 * (halo + 1) * 128 <= kFwd6Lds / 2, "two workgroups per CU: halo %d", halo);
         }
   EXPECT(2 * fwd6_sb(128) + 3 * 128 * 128 <= kFwd6Lds && fwd6_sb(64) <= 65408, "LDS layout");
 }
