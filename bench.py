@@ -147,6 +147,17 @@ def _paths(model, image, args):
     return enc, upd
 
 
+def _corr_volume(model, args, device):
+    """Storage precision of the dense correlation volume the model builds (its own rule in
+    RAFT.forward), or None when no native dense volume is built (the reference implementation,
+    --alternate_corr)."""
+    if args.impl == "reference" or args.alternate_corr:
+        return None
+    amp = not args.fp32
+    bf16_amp = amp and device.type == "cuda" and model.amp_dtype == torch.bfloat16
+    return "fp32" if (not bf16_amp or bool(getattr(model.args, "corr_fp32", False))) else "bf16"
+
+
 def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -332,7 +343,7 @@ def run(args):
                 "fused_update": upd_path not in ("module", "reference"),
                 "update_path": upd_path,
                 "encoder_path": enc_path,
-                "corr_volume": "fp32" if (args.fp32 or args.corr_fp32 or args.amp_dtype == "fp16") else "bf16",
+                "corr_volume": _corr_volume(model, args, device),
                 "mode": args.mode,
                 "alternate_corr": args.alternate_corr,
                 "hip_graph": bool(train_graph or (args.graph is not False and args.mode == "infer")),

@@ -167,15 +167,23 @@ void init_args(EncConvArgs& a) {
 }  // namespace
 
 namespace {
-// decode / packing tables of a KHxKW conv over Cx input channels (one class); returns Kpad
-int fwd_tables(EncConvArgs& a, int Cx, int KH, int KW, int pad, int device, const at::TensorOptions& o) {
+// decode / packing tables of a KHxKW conv over Cx input channels (one class); returns Kpad.
+// split == 2 (three-plane fp32 forward): x rows hold [hi | mid | lo] planes of cx = Cx / 3
+// channels and the GEMM runs over SIX K planes -- x planes hi, mid, hi, lo, hi, mid against the
+// weight planes H, H, M, H, L, M packed by enc_pack (encoder.hip pack_row) -- i.e. every
+// product hi(x) H + mid H + hi M + lo H + hi L + mid M down to ~2^-24 of x W: the fp32 conv.
+int fwd_tables(EncConvArgs& a, int Cx, int KH, int KW, int pad, int device, const at::TensorOptions& o,
+               int split = 0) {
   std::vector<int> tab(kEncTabMax, -1), ptab(kEncTabMax, -1);
   int e = 0;
+  static const int kXPlane[6] = {0, 1, 0, 2, 0, 1};
+  const int cx = Cx / 3, nk = split == 2 ? 2 * Cx : Cx;
   for (int ky = 0; ky < KH; ++ky)
     for (int kx = 0; kx < KW; ++kx)
-      for (int c = 0; c < Cx; c += 8) {
+      for (int c = 0; c < nk; c += 8) {
         TORCH_CHECK(e < kEncTabMax, "conv too deep for the decode table");
-        tab[e] = enc_tab_entry(ky - pad, kx - pad, 0, c);
+        const int src_c = split == 2 ? kXPlane[c / cx] * cx + c % cx : c;
+        tab[e] = enc_tab_entry(ky - pad, kx - pad, 0, src_c);
         ptab[e] = enc_ptab_entry(0, ky, kx, c);
         ++e;
       }
@@ -198,16 +206,17 @@ std::tuple<at::Tensor, int64_t, int64_t> job_bytes(EncConvArgs& a, int rows) {
 
 // The forward weight operand of enc_conv_fwd for an input of Cx channels as a packing job of
 // enc_pack_multi (the layout run_conv would pack: N rows of round_up(KH*KW*Cx, 64))
-std::tuple<at::Tensor, int64_t, int64_t> enc_pack_fwd_job(const at::Tensor& w, int64_t Cx, int64_t pad, bool split,
+std::tuple<at::Tensor, int64_t, int64_t> enc_pack_fwd_job(const at::Tensor& w, int64_t Cx, int64_t pad, int64_t split,
                                                           bool f16) {
   check_w(w, "w");
+  TORCH_CHECK(split >= 0 && split <= 2, "split mode 0 / 1 / 2");
   EncConvArgs a;
   init_args(a);
   a.f16 = f16 ? 1 : 0;
   a.B = 1;
   a.N = (int)w.size(0);
-  fwd_tables(a, (int)Cx, (int)w.size(2), (int)w.size(3), (int)pad, w.get_device(), w.options());
-  a.split = split ? 1 : 0;
+  fwd_tables(a, (int)Cx, (int)w.size(2), (int)w.size(3), (int)pad, w.get_device(), w.options(), (int)split);
+  a.split = (int)split;
   a.split_w = split ? (int)Cx / 3 : 0;
   set_weight(a, 0, w);
   a.pack_dgrad = 0;
@@ -228,10 +237,11 @@ void enc_pack_multi(const at::Tensor& plan, int64_t njobs, int64_t nblocks, at::
 // y[B,Ho,Wo,N] = conv(x[B,H,W,Cx], w[N,Cin,KH,KW]) + bias; stats [B, T, 2, N] (column sum, M2 per 128-pixel tile)
 std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::Tensor& w,
                                                 const c10::optional<at::Tensor>& bias, int64_t stride, int64_t pad,
-                                                bool want_stats, bool split,
+                                                bool want_stats, int64_t split,
                                                 const c10::optional<at::Tensor>& prepacked) {
   check_nhwc(x, "x");
   check_w(w, "w");
+  TORCH_CHECK(split >= 0 && split <= 2, "split mode 0 / 1 / 2");
   const int B = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), Cx = (int)x.size(3);
   const int N = (int)w.size(0), Cin = (int)w.size(1), KH = (int)w.size(2), KW = (int)w.size(3);
   TORCH_CHECK(Cin <= (split ? Cx / 3 : Cx), "weight has more input channels than x");
@@ -245,7 +255,7 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
   a.src[0] = {cbf(x), Cx, Cx, H, W, (int)stride};
   a.B = B;
   a.N = N;
-  fwd_tables(a, Cx, KH, KW, (int)pad, x.get_device(), x.options());
+  fwd_tables(a, Cx, KH, KW, (int)pad, x.get_device(), x.options(), (int)split);
   a.cls[0].Gh = Ho;
   a.cls[0].Gw = Wo;
   at::Tensor y = at::empty({B, Ho, Wo, split ? 3 * N : N}, x.options());
@@ -254,7 +264,7 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
   a.os = 1;
   a.out = mbf(y);
   a.out_stride = split ? 3 * N : N;
-  a.split = split ? 1 : 0;
+  a.split = (int)split;
   a.split_w = split ? Cx / 3 : 0;  // the fp32 weight is split while packing
   at::Tensor b;
   if (bias.has_value() && bias->defined()) {
@@ -287,8 +297,11 @@ std::tuple<at::Tensor, at::Tensor> enc_conv_fwd(const at::Tensor& x, const at::T
 namespace {
 // decode / packing tables of a dgrad launch: one class per output phase (py, px) of the largest
 // stride S, each gathering the taps of every conv that land on that phase (C[j]: dy channels)
+// split == 2: the dY rows hold [hi | mid | lo] planes (store8_split mode 2); the K plane that
+// pairs with W_lo must read hi, so its decode entries point at plane 0 instead of plane 2
 void dgrad_tables(EncConvArgs& a, at::TensorList ws, const std::vector<int>& C, at::IntArrayRef strides,
-                  at::IntArrayRef pads, int H, int W, int S, int device, const at::TensorOptions& o) {
+                  at::IntArrayRef pads, int H, int W, int S, int device, const at::TensorOptions& o,
+                  int split = 0) {
   const int nconv = (int)ws.size();
   std::vector<int> tab(kEncTabMax, -1), ptab(kEncTabMax, -1);
   int e = 0, ncls = 0;
@@ -306,9 +319,11 @@ void dgrad_tables(EncConvArgs& a, at::TensorList ws, const std::vector<int>& C, 
           for (int kx = 0; kx < KW; ++kx) {
             const int vx = px + p - kx;
             if (((vx % s) + s) % s) continue;
+            const int co = C[j] / 3;  // split: Cout of conv j
             for (int c = 0; c < C[j]; c += 8) {
               TORCH_CHECK(e < kEncTabMax, "dgrad too deep for the decode table");
-              tab[e] = enc_tab_entry(vy / s, vx / s, j, c);
+              const int src_c = (split == 2 && c >= 2 * co) ? c - 2 * co : c;
+              tab[e] = enc_tab_entry(vy / s, vx / s, j, src_c);
               ptab[e] = enc_ptab_entry(j, ky, kx, c);
               ++e;
             }
@@ -335,7 +350,7 @@ int largest_stride(at::IntArrayRef strides) {
 // The dgrad weight operand of enc_conv_dgrad (convs ws over an H x W input) as a packing job of
 // enc_pack_multi: the weights do not change between the forward and the optimizer step
 std::tuple<at::Tensor, int64_t, int64_t> enc_pack_dgrad_job(at::TensorList ws, at::IntArrayRef strides,
-                                                            at::IntArrayRef pads, int64_t H, int64_t W, bool split,
+                                                            at::IntArrayRef pads, int64_t H, int64_t W, int64_t split,
                                                             bool f16) {
   const int nconv = (int)ws.size();
   TORCH_CHECK(nconv >= 1 && nconv <= 2 && (int)strides.size() == nconv && (int)pads.size() == nconv,
@@ -353,8 +368,9 @@ std::tuple<at::Tensor, int64_t, int64_t> enc_pack_dgrad_job(at::TensorList ws, a
     C[j] = (split ? 3 : 1) * (int)ws[j].size(0);
     set_weight(a, j, ws[j]);
   }
-  dgrad_tables(a, ws, C, strides, pads, (int)H, (int)W, largest_stride(strides), ws[0].get_device(), ws[0].options());
-  a.split = split ? 1 : 0;
+  dgrad_tables(a, ws, C, strides, pads, (int)H, (int)W, largest_stride(strides), ws[0].get_device(), ws[0].options(),
+               (int)split);
+  a.split = (int)split;
   a.split_w = split ? (int)ws[0].size(0) : 0;
   for (int j = 0; j < nconv; ++j) a.split_wd[j] = split ? (int)ws[j].size(0) : 0;
   a.pack_dgrad = 1;
@@ -363,7 +379,7 @@ std::tuple<at::Tensor, int64_t, int64_t> enc_pack_dgrad_job(at::TensorList ws, a
 
 at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef strides, at::IntArrayRef pads,
                           int64_t H, int64_t W, const c10::optional<at::Tensor>& res,
-                          const c10::optional<at::Tensor>& mask, bool split,
+                          const c10::optional<at::Tensor>& mask, int64_t split,
                           const c10::optional<at::Tensor>& prepacked) {
   const int nconv = (int)dys.size();
   TORCH_CHECK(nconv >= 1 && nconv <= 2 && (int)ws.size() == nconv && (int)strides.size() == nconv &&
@@ -395,7 +411,7 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
     Cs[j] = C;
     set_weight(a, j, ws[j]);
   }
-  dgrad_tables(a, ws, Cs, strides, pads, (int)H, (int)W, S, dys[0].get_device(), dys[0].options());
+  dgrad_tables(a, ws, Cs, strides, pads, (int)H, (int)W, S, dys[0].get_device(), dys[0].options(), (int)split);
   const int rs = split ? 3 * Cin : Cin;  // dx / res / mask row pitch
   at::Tensor dx = at::empty({B, H, W, rs}, dys[0].options());
   a.Ho = (int)H;
@@ -403,7 +419,7 @@ at::Tensor enc_conv_dgrad(at::TensorList dys, at::TensorList ws, at::IntArrayRef
   a.os = S;
   a.out = mbf(dx);
   a.out_stride = rs;
-  a.split = split ? 1 : 0;
+  a.split = (int)split;
   a.split_w = split ? (int)ws[0].size(0) : 0;
   for (int j = 0; j < nconv; ++j) a.split_wd[j] = split ? (int)ws[j].size(0) : 0;
   if (res.has_value() && res->defined()) {
@@ -557,7 +573,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
 }
 
 // [img0; img1] (fp32 0..255, [B,3,H,W] any strides) -> [nimg, H, W, 8] bf16 in [-1, 1]
-at::Tensor enc_prep(const at::Tensor& img0, const c10::optional<at::Tensor>& img1, bool split, bool f16) {
+at::Tensor enc_prep(const at::Tensor& img0, const c10::optional<at::Tensor>& img1, int64_t split, bool f16) {
   TORCH_CHECK(img0.is_cuda() && img0.scalar_type() == at::kFloat && img0.dim() == 4 && img0.size(1) == 3,
               "images: fp32 [B, 3, H, W]");
   const int B = (int)img0.size(0), H = (int)img0.size(2), W = (int)img0.size(3);
@@ -572,7 +588,7 @@ at::Tensor enc_prep(const at::Tensor& img0, const c10::optional<at::Tensor>& img
   at::Tensor out = at::empty({nimg, H, W, split ? 24 : 8}, img0.options().dtype(f16 ? at::kHalf : at::kBFloat16));
   long st[4] = {img0.stride(0), img0.stride(1), img0.stride(2), img0.stride(3)};
   check(launch_enc_prep(img0.data_ptr<float>(), nimg > B ? img1->data_ptr<float>() : nullptr, st, B, H, W, nimg,
-                        out.data_ptr(), (split ? 1 : 0) | (f16 ? 2 : 0), stream()),
+                        out.data_ptr(), (split ? 1 : 0) | (f16 ? 2 : 0) | (split == 2 ? 4 : 0), stream()),
         "enc_prep");
   return out;
 }
@@ -634,7 +650,7 @@ at::Tensor enc_norm_stats(const c10::optional<at::Tensor>& stats, int64_t B, int
 }
 
 at::Tensor enc_apply(const at::Tensor& x, const at::Tensor& coef, bool relu_a, const c10::optional<at::Tensor>& r,
-                     const c10::optional<at::Tensor>& coef_r, bool relu_out, bool split) {
+                     const c10::optional<at::Tensor>& coef_r, bool relu_out, int64_t split) {
   check_nhwc(x, "a");
   TORCH_CHECK(!split || x.size(3) % 24 == 0, "enc_apply: split rows hold 3 planes of a multiple of 8 channels");
   const int B = (int)x.size(0), HW = (int)(x.size(1) * x.size(2)), N = (int)x.size(3) / (split ? 3 : 1);
@@ -653,7 +669,7 @@ at::Tensor enc_apply(const at::Tensor& x, const at::Tensor& coef, bool relu_a, c
   at::Tensor out = at::empty_like(x);
   if (r.has_value() && r->defined()) TORCH_CHECK(r->scalar_type() == x.scalar_type(), "residual dtype");
   check(launch_enc_apply(x.data_ptr(), coef.data_ptr<float>(), relu_a, rp, crp, relu_out, out.data_ptr(), B, HW, N,
-                         (split ? 1 : 0) | (x.scalar_type() == at::kHalf ? 2 : 0), stream()),
+                         (split ? 1 : 0) | (x.scalar_type() == at::kHalf ? 2 : 0) | (split == 2 ? 4 : 0), stream()),
         "enc_apply");
   return out;
 }
@@ -667,7 +683,7 @@ at::Tensor enc_apply(const at::Tensor& x, const at::Tensor& coef, bool relu_a, c
 std::vector<at::Tensor> enc_norm_bwd_impl(const at::Tensor& g, const at::Tensor& a0, const at::Tensor& c0, bool relu0,
                                           const c10::optional<at::Tensor>& a1, const c10::optional<at::Tensor>& c1,
                                           int64_t kind, int stage, const c10::optional<at::Tensor>& part_in,
-                                          int64_t b_fin, bool split) {
+                                          int64_t b_fin, int64_t split) {
   check_nhwc(g, "g");
   check_nhwc(a0, "a0");
   TORCH_CHECK(a0.sizes() == g.sizes(), "a0 shape");
@@ -691,7 +707,7 @@ std::vector<at::Tensor> enc_norm_bwd_impl(const at::Tensor& g, const at::Tensor&
   a.N = N;
   a.R = std::min(norm_chunks_max(), std::max(1, HW / norm_chunk_pixels()));
   a.kind = (int)kind;
-  a.split = split ? 1 : 0;
+  a.split = (int)split;
   a.f16 = g.scalar_type() == at::kHalf ? 1 : 0;
   TORCH_CHECK(a0.scalar_type() == g.scalar_type(), "norm backward: g and a0 share one dtype");
   auto fo = g.options().dtype(at::kFloat);
@@ -729,50 +745,52 @@ std::vector<at::Tensor> enc_norm_bwd_impl(const at::Tensor& g, const at::Tensor&
 
 std::vector<at::Tensor> enc_norm_bwd(const at::Tensor& g, const at::Tensor& a0, const at::Tensor& c0, bool relu0,
                                      const c10::optional<at::Tensor>& a1, const c10::optional<at::Tensor>& c1,
-                                     int64_t kind, bool split) {
+                                     int64_t kind, int64_t split) {
   return enc_norm_bwd_impl(g, a0, c0, relu0, a1, c1, kind, 0, c10::nullopt, 0, split);
 }
 
 at::Tensor enc_norm_bwd_part(const at::Tensor& g, const at::Tensor& a0, const at::Tensor& c0, bool relu0,
                              const c10::optional<at::Tensor>& a1, const c10::optional<at::Tensor>& c1, int64_t kind,
-                             bool split) {
+                             int64_t split) {
   return enc_norm_bwd_impl(g, a0, c0, relu0, a1, c1, kind, 1, c10::nullopt, 0, split)[0];
 }
 
 std::vector<at::Tensor> enc_norm_bwd_finish(const at::Tensor& g, const at::Tensor& a0, const at::Tensor& c0,
                                             bool relu0, const c10::optional<at::Tensor>& a1,
                                             const c10::optional<at::Tensor>& c1, int64_t kind, const at::Tensor& part,
-                                            int64_t b_fin, bool split) {
+                                            int64_t b_fin, int64_t split) {
   return enc_norm_bwd_impl(g, a0, c0, relu0, a1, c1, kind, 2, part, b_fin, split);
 }
 
 }  // namespace raft_amd
 
 TORCH_LIBRARY_FRAGMENT(raft_amd, m) {
-  m.def("enc_conv_fwd(Tensor x, Tensor w, Tensor? bias, int stride, int pad, bool stats, bool split=False, "
+  // split: 0 = bf16 / fp16 rows, 1 = split-bf16 [hi | lo | hi] planes, 2 = three-plane [hi | mid | lo]
+  // rows with the six-plane fp32-exact forward GEMM (encoder.hip store8_split, fwd_tables)
+  m.def("enc_conv_fwd(Tensor x, Tensor w, Tensor? bias, int stride, int pad, bool stats, int split=0, "
         "Tensor? prepacked=None) -> (Tensor, Tensor)");
   m.def(
       "enc_conv_dgrad(Tensor[] dys, Tensor[] ws, int[] strides, int[] pads, int H, int W, Tensor? res, Tensor? mask, "
-      "bool split=False, Tensor? prepacked=None) -> Tensor");
-  m.def("enc_pack_fwd_job(Tensor w, int Cx, int pad, bool split, bool f16) -> (Tensor, int, int)");
-  m.def("enc_pack_dgrad_job(Tensor[] ws, int[] strides, int[] pads, int H, int W, bool split, bool f16) -> "
+      "int split=0, Tensor? prepacked=None) -> Tensor");
+  m.def("enc_pack_fwd_job(Tensor w, int Cx, int pad, int split, bool f16) -> (Tensor, int, int)");
+  m.def("enc_pack_dgrad_job(Tensor[] ws, int[] strides, int[] pads, int H, int W, int split, bool f16) -> "
         "(Tensor, int, int)");
   m.def("enc_pack_multi(Tensor plan, int njobs, int nblocks, Tensor(a!) out) -> ()");
   m.def("enc_conv_wgrad(Tensor x, Tensor dy, Tensor(a!) dw, Tensor(b!)? db, int stride, int pad, bool accumulate, "
         "bool db_zero=False, int fold=0) -> ()");
-  m.def("enc_prep(Tensor img0, Tensor? img1, bool split=False, bool f16=False) -> Tensor");
+  m.def("enc_prep(Tensor img0, Tensor? img1, int split=0, bool f16=False) -> Tensor");
   m.def(
       "enc_norm_stats(Tensor? stats, int B, int HW, int N, int kind, Tensor? gamma, Tensor? beta, Tensor(a!)? rmean, "
       "Tensor(b!)? rvar, Tensor(c!)? nbt, float momentum, float eps, int W=0) -> Tensor");
-  m.def("enc_apply(Tensor a, Tensor coef, bool relu_a, Tensor? r, Tensor? coef_r, bool relu_out, bool split=False) "
+  m.def("enc_apply(Tensor a, Tensor coef, bool relu_a, Tensor? r, Tensor? coef_r, bool relu_out, int split=0) "
         "-> Tensor");
   m.def("enc_norm_bwd(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind, "
-        "bool split=False) -> Tensor[]");
+        "int split=0) -> Tensor[]");
   m.def("enc_norm_bwd_part(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind, "
-        "bool split=False) -> Tensor");
+        "int split=0) -> Tensor");
   m.def(
       "enc_norm_bwd_finish(Tensor g, Tensor a0, Tensor c0, bool relu0, Tensor? a1, Tensor? c1, int kind, Tensor part, "
-      "int b_fin, bool split=False) -> Tensor[]");
+      "int b_fin, int split=0) -> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {

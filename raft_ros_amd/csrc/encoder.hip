@@ -57,22 +57,33 @@ __device__ __forceinline__ void store8(__bf16* p, const float* v, bool f16 = fal
   for (int i = 0; i < 8; ++i) x[i] = st16(v[i], f16);
   *reinterpret_cast<bf16x8*>(p) = x;
 }
-// split-bf16 planes (kernel_abi.h EncConvArgs::split): hi at p, lo at p + S, hi again at p + 2S
-__device__ __forceinline__ void store8_split(__bf16* p, int S, const float* v) {
-  bf16x8 hi, lo;
+// split-bf16 planes (kernel_abi.h EncConvArgs::split), planes of S channels at p, p + S, p + 2S:
+//   mode 1: hi, lo = bf16(x - hi), hi again   (x ~ hi + lo: a 16-bit mantissa)
+//   mode 2: hi, mid = bf16(x - hi), lo = bf16(x - hi - mid)   (x = hi + mid + lo: the fp32 value)
+// The first two planes are the same in both modes, so readers of [hi | lo] (the weight
+// gradients, the gradient planes of the backward) work on either.
+__device__ __forceinline__ void store8_split(__bf16* p, int S, const float* v, int mode = 1) {
+  bf16x8 hi, lo, third;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     hi[i] = static_cast<__bf16>(v[i]);
-    lo[i] = static_cast<__bf16>(v[i] - static_cast<float>(hi[i]));
+    const float r = v[i] - static_cast<float>(hi[i]);
+    lo[i] = static_cast<__bf16>(r);
+    third[i] = mode == 2 ? static_cast<__bf16>(r - static_cast<float>(lo[i])) : hi[i];
   }
   *reinterpret_cast<bf16x8*>(p) = hi;
   *reinterpret_cast<bf16x8*>(p + S) = lo;
-  *reinterpret_cast<bf16x8*>(p + 2 * S) = hi;
+  *reinterpret_cast<bf16x8*>(p + 2 * S) = third;
 }
-__device__ __forceinline__ void load8_split(const __bf16* p, int S, float* v) {
+__device__ __forceinline__ void load8_split(const __bf16* p, int S, float* v, int mode = 1) {
   const bf16x8 hi = *reinterpret_cast<const bf16x8*>(p), lo = *reinterpret_cast<const bf16x8*>(p + S);
 #pragma unroll
   for (int i = 0; i < 8; ++i) v[i] = static_cast<float>(hi[i]) + static_cast<float>(lo[i]);
+  if (mode == 2) {
+    const bf16x8 l3 = *reinterpret_cast<const bf16x8*>(p + 2 * S);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] += static_cast<float>(l3[i]);
+  }
 }
 __device__ __forceinline__ void loadf8(const float* p, float* v) {
   const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
@@ -368,7 +379,7 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
     }
     if (a.res) {
       float r[8];
-      if (a.split) load8_split(a.res + pix * a.res_stride + n, a.N, r);
+      if (a.split) load8_split(a.res + pix * a.res_stride + n, a.N, r, a.split);
       else load8(a.res + pix * a.res_stride + n, r, F16);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += r[e];
@@ -380,7 +391,7 @@ __global__ __launch_bounds__(256) void enc_conv_kernel(const EncConvArgs a) {
       for (int e = 0; e < 8; ++e) v[e] = m[e] > 0.f ? v[e] : 0.f;
     }
     if (a.split)
-      store8_split(a.out + pix * a.out_stride + n, a.N, v);
+      store8_split(a.out + pix * a.out_stride + n, a.N, v, a.split);
     else
       store8(a.out + pix * a.out_stride + n, v, F16);
   }
@@ -409,6 +420,18 @@ __device__ __forceinline__ void pack_row(const EncConvArgs& a, const EncClass& c
         v = plane < 2 ? hi : x - hi;
       } else if (a.pack_dgrad) {
         v = wp[loc * s0 + row * s1 + ky * s2 + kx * s3];
+      } else if (a.split_w && a.split == 2) {
+        // three-plane forward: six K planes (x planes hi, mid, hi, lo, hi, mid -- the decode table
+        // -- against W planes H, H, M, H, L, M): every product of relative size >= 2^-16 of
+        // hi(x) hi(W), so the GEMM is fp32-exact up to ~2^-24 (fwd_tables in enc_bindings.cpp)
+        const int plane = loc / a.split_w, cl = loc - plane * a.split_w;
+        if (cl < cin) {
+          const float x = wp[row * s0 + cl * s1 + ky * s2 + kx * s3];
+          const float H = static_cast<float>(static_cast<__bf16>(x));
+          const float M = static_cast<float>(static_cast<__bf16>(x - H));
+          const float L = x - H - M;
+          v = (plane == 2 || plane == 5) ? M : plane == 4 ? L : H;
+        }
       } else if (a.split_w) {  // [W_hi | W_hi | W_lo] against the [hi | lo | hi] input planes
         const int plane = loc / a.split_w, cl = loc - plane * a.split_w;
         if (cl < cin) {
@@ -718,7 +741,7 @@ __global__ __launch_bounds__(256) void enc_prep_kernel(const float* __restrict__
 #pragma unroll
   for (int c = 3; c < 8; ++c) v[c] = 0.f;
   if (split & 1)
-    store8_split(out + p * 24, 8, v);
+    store8_split(out + p * 24, 8, v, (split & 4) ? 2 : 1);
   else
     store8(out + p * 8, v, (split & 2) != 0);
 }
@@ -826,8 +849,9 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
                                                         __bf16* __restrict__ out, int B, int HW, int N, int split) {
   const int G = N / 8;
   const bool f16 = (split & 2) != 0;
+  const int mode = (split & 4) ? 2 : 1;  // split-plane mode (store8_split)
   split &= 1;
-  const int rs = split ? 3 * N : N;  // row stride: split rows hold hi / lo / hi planes
+  const int rs = split ? 3 * N : N;  // row stride: split rows hold three planes
   const PixWalk w = pix_walk(G);
   if (w.p < 0) return;
   const int n = w.n, P = B * HW;
@@ -846,7 +870,7 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
     }
     float v[8];
     if (split)
-      load8_split(a + (long)p * rs + n, N, v);
+      load8_split(a + (long)p * rs + n, N, v, mode);
     else
       load8(a + (long)p * N + n, v, f16);
 #pragma unroll
@@ -857,7 +881,7 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
     if (r) {
       float rv[8];
       if (split)
-        load8_split(r + (long)p * rs + n, N, rv);
+        load8_split(r + (long)p * rs + n, N, rv, mode);
       else
         load8(r + (long)p * N + n, rv, f16);
       if (cr)
@@ -870,7 +894,7 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     if (split)
-      store8_split(out + (long)p * rs + n, N, v);
+      store8_split(out + (long)p * rs + n, N, v, mode);
     else
       store8(out + (long)p * N + n, v, f16);
   }
@@ -897,7 +921,7 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_reduce_kernel(const NormBwdA
   const long rs = a.split ? 3L * N : N;  // row pitch (split rows: hi / lo / hi planes of N)
   const int pb = r * chunk, pe = min(a.HW, pb + chunk);
   auto ld8 = [&](const __bf16* q, float* v) __attribute__((always_inline)) {
-    if (a.split) load8_split(q, N, v);
+    if (a.split) load8_split(q, N, v, a.split);
     else load8(q, v, a.f16 != 0);
   };
   float S[4][8];
@@ -1029,11 +1053,11 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_apply_kernel(const NormBwdAr
   const int n = w.n, P = a.B * a.HW;
   const long rp = a.split ? 3L * N : N;  // row pitch (split rows: hi / lo / hi planes of N)
   auto ld8 = [&](const __bf16* q, float* v) __attribute__((always_inline)) {
-    if (a.split) load8_split(q, N, v);
+    if (a.split) load8_split(q, N, v, a.split);
     else load8(q, v, a.f16 != 0);
   };
   auto st8 = [&](__bf16* q, const float* v) __attribute__((always_inline)) {
-    if (a.split) store8_split(q, N, v);
+    if (a.split) store8_split(q, N, v, a.split);
     else store8(q, v, a.f16 != 0);
   };
   int bend = 0;

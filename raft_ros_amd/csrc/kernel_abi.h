@@ -193,7 +193,7 @@ static_assert(sizeof(PackJobs) <= 4000, "pack jobs must fit the kernel-argument 
 // ============================================================================ encoder convs
 constexpr int kEncTab = 256;  // K/8 decode-table entries per launch (all classes) held in the arguments
 // deeper convs (the split-bf16 layout's 3x channels) read their tables from device memory
-constexpr int kEncTabMax = 512;
+constexpr int kEncTabMax = 1024;  // the three-plane forward doubles K (six planes)
 
 struct EncSrc {
   const __bf16* ptr;

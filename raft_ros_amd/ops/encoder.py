@@ -39,6 +39,9 @@ _NONE, _INSTANCE, _BATCH_TRAIN, _BATCH_EVAL = 0, 1, 2, 3
 # conv (RAFT_ENC_PREPACK=0: per-conv packing; =fork: the two launches on an auxiliary stream)
 PREPACK = os.environ.get("RAFT_ENC_PREPACK", "1") != "0"
 _PREPACK_FORK = os.environ.get("RAFT_ENC_PREPACK", "1") == "fork"
+# fp32 training: three-plane (fp32-exact) encoder forward; RAFT_ENC_SPLIT3=0 keeps the round-4
+# two-plane forward (A/B, tests)
+SPLIT3 = os.environ.get("RAFT_ENC_SPLIT3", "1") != "0"
 
 
 def _norm_kind(m: nn.Module):
@@ -310,18 +313,38 @@ def _forward(L, x0, P, split: bool = False, pk=None):
 # x_hi W_lo with fp32 accumulation; norm statistics come from the fp32 accumulators, the norm
 # apply / backward passes read and write the planes in fp32, and each weight gradient is two
 # GEMMs ([X_hi | X_lo]^T dY_hi + X_hi^T dY_lo) folded into the fp32 parameter layout.
+#
+# Training (mode 2, round 5): the planes are [hi | mid | lo] -- the fp32 value exactly -- and
+# the forward convs run six K planes (x hi, mid, hi, lo, hi, mid against W H, H, M, H, L, M:
+# every product down to ~2^-24 of x W), so the forward is the fp32 conv; the backward keeps the
+# two-plane GEMMs (its operands' first two planes are the same in both layouts; the data-
+# gradient decode tables read hi where mode 1 read the duplicate hi plane).  CPU emulation on
+# the reference's gradients (scripts/emulate_split_precision.py): rounding the encoder's
+# FORWARD operands / outputs to 16 bits costs RMS 4.0e-3 (base) / 8.3e-3 (small) over all
+# parameters, the gradient operands 4-5e-6, the update block's forward 7e-4 / 1.4e-4 -- MIOpen's
+# own fp32 deviation is 1.8e-3.  The six-plane forward doubles the encoders' forward MFMA work.
 
-def _forward_split(L, x0, P, pk=None):
+def _forward_split(L, x0, P, pk=None, mode: int = 1):
     """``_forward`` on split-bf16 planes without records (inference); the split output rows."""
-    return _forward(L, x0, P, True, pk)[0]
+    return _forward(L, x0, P, mode, pk)[0]
 
 
-def _split_rows(g: torch.Tensor) -> torch.Tensor:
-    """fp32 [..., C] -> bf16 [..., 3C] split planes [hi | lo | hi]."""
+def _split_rows(g: torch.Tensor, mode: int = 1) -> torch.Tensor:
+    """fp32 [..., C] -> bf16 [..., 3C] split planes: [hi | lo | hi] (mode 1) or [hi | mid | lo]
+    (mode 2, the three-plane layout: see ``encode``)."""
     g = g.float()
     hi = g.to(torch.bfloat16)
-    lo = (g - hi.float()).to(torch.bfloat16)
-    return torch.cat([hi, lo, hi], dim=-1).contiguous()
+    r = g - hi.float()
+    lo = r.to(torch.bfloat16)
+    third = (r - lo.float()).to(torch.bfloat16) if mode == 2 else hi
+    return torch.cat([hi, lo, third], dim=-1).contiguous()
+
+
+def _unsplit(y: torch.Tensor, mode: int) -> torch.Tensor:
+    """Split rows [..., 3N] -> the fp32 value [..., N] (hi + lo, + the third plane in mode 2)."""
+    N = y.shape[-1] // 3
+    out = y[..., :N].float() + y[..., N:2 * N].float()
+    return out + y[..., 2 * N:].float() if mode == 2 else out
 
 
 def _wgrad(x, dy, cd, P, grads, nd=None, split: bool = False):
@@ -458,13 +481,12 @@ class _EncoderFn(torch.autograd.Function):
         # records hold only tensors created here (activations, statistics coefficients)
         ctx.stem_rec, ctx.recs = stem_rec, recs
         if split:
-            N = y.shape[3] // 3
-            return y[..., :N].float() + y[..., N:2 * N].float()
+            return _unsplit(y, split)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        gy = _split_rows(gy) if ctx.split else gy.contiguous().to(ctx.dt16)
+        gy = _split_rows(gy, ctx.split) if ctx.split else gy.contiguous().to(ctx.dt16)
         pk = ctx.pk if ctx.pk is not None and ctx.pk.need_bwd else None
         grads = _backward(ctx.layout, ctx.params, gy, ctx.stem_rec, ctx.recs, ctx.split, pk)
         ctx.stem_rec = ctx.recs = None
@@ -509,11 +531,15 @@ def encode(enc, image1: torch.Tensor, image2: torch.Tensor | None = None,
     ``f16``: fp16 activations (fp16 AMP, v_mfma_f32_32x32x16_f16) instead of bf16.
     ``pack_stream``: the auxiliary stream (ops/streams.py) that packs the weights ahead."""
     L = _layout(enc)
-    x0 = ops().enc_prep(image1.float(), image2.float() if image2 is not None else None, split, f16 and not split)
-    pk = _prepack(L, x0, bool(split), bool(f16 and not split), pack_stream)
+    # split mode: 1 = [hi | lo | hi] planes (inference: fp32-faithful to ~2^-17, EPE within 1e-5 px
+    # of the fp32 reference), 2 = [hi | mid | lo] planes with a six-plane forward GEMM (training:
+    # the forward activations are fp32-exact; their 16-bit rounding was the fp32 training path's
+    # dominant gradient error, profiles/r5_split_precision_by_scope.txt)
+    mode = 0 if not split else (2 if torch.is_grad_enabled() and SPLIT3 else 1)
+    x0 = ops().enc_prep(image1.float(), image2.float() if image2 is not None else None, mode, f16 and not split)
+    pk = _prepack(L, x0, mode, bool(f16 and not split), pack_stream)
     if split and not torch.is_grad_enabled():
-        y = _forward_split(L, x0, L.params, pk)
-        N = y.shape[3] // 3
-        return (y[..., :N].float() + y[..., N:2 * N].float()).permute(0, 3, 1, 2)
-    y = _EncoderFn.apply(L, x0, join_stream, bool(split), pk, *L.params)
+        y = _forward_split(L, x0, L.params, pk, mode)
+        return _unsplit(y, mode).permute(0, 3, 1, 2)
+    y = _EncoderFn.apply(L, x0, join_stream, mode, pk, *L.params)
     return y.permute(0, 3, 1, 2)

@@ -62,18 +62,21 @@ def _grad_errs(cuda, small, **kw):
     return fix, loss, grad_errors(grads, fix, "small" if small else "base")
 
 
+# verdict targets of round 4 (the reference-anchored fp32 gradient RMS of the native path)
+_FP32_RMS_ABS = {"base": 2.7e-3, "small": 1.4e-3}
+
+
 @pytest.mark.parametrize("small", [False, True])
 def test_native_fp32_training_gradients_match_reference(cuda, small):
-    """Native fp32 training (split-bf16 kernels: encoders + refinement step) vs the REAL
-    reference's CPU fp32 gradients (tests/fixtures/golden_grads.npz), per parameter (16 fixed
-    projections or the full tensor), anchored on the fp32 module path (MIOpen) measured the
-    same way, and on the precision floor of the split number format itself: the fp32 module
-    path run on CPU with every conv operand / output / gradient rounded to hi + lo (a 16-bit
-    mantissa) -- scripts/emulate_split_precision.py, tests/fixtures/split_format_floor.json.
-    Gradients of the early encoder layers are sensitive to the 2^-17 operand perturbation
-    (RAFT-small's fnet.layer1 to ~4e-2 in that emulation), so no kernel on this format gets
-    below it; the native path must stay within 1.5x of the format's floor or 4x of MIOpen's
-    own deviation, whichever is larger."""
+    """Native fp32 training (three-plane encoder forward + split-bf16 refinement step) vs the
+    REAL reference's CPU fp32 gradients (tests/fixtures/golden_grads.npz), per parameter (16
+    fixed projections or the full tensor), anchored on the fp32 module path (MIOpen) measured
+    the same way: RMS over parameters within 1.5x of MIOpen's own deviation (or the absolute
+    targets 2.7e-3 base / 1.4e-3 small, since MIOpen's deviation itself varies ~2x between
+    boxes: 0.87e-3 .. 1.81e-3 for base), worst parameter within 2x of MIOpen's worst.
+    Measured on MI355X (profiles/r5e_tests.log): base RMS 1.38e-3 vs MIOpen 0.87e-3, small
+    1.08e-3 vs 0.94e-3; the two-plane forward of round 4 (RAFT_ENC_SPLIT3=0) was 4.2e-3 / 6.3e-3,
+    the floor of its number format (tests/fixtures/split_format_floor.json)."""
     import json
 
     name = "small" if small else "base"
@@ -86,11 +89,14 @@ def test_native_fp32_training_gradients_match_reference(cuda, small):
     wmod = sorted(emod.items(), key=lambda kv: -kv[1])[:3]
     print(f"\n{name}: fp32 training vs reference: loss {loss:.6f} (ref {float(fix[name + '/loss']):.6f}); "
           f"native worst {worst}, RMS {rms(errs):.2e}; MIOpen module path worst {wmod}, RMS {rms(emod):.2e}")
+    print(f"{name}: two-plane split-format floor (emulated, RAFT_ENC_SPLIT3=0): worst {floor['worst']:.2e} "
+          f"({floor['worst_param']}), RMS {floor['rms']:.2e}")
     assert abs(loss - float(fix[f"{name}/loss"])) <= 1e-4 * abs(float(fix[f"{name}/loss"]))
-    print(f"{name}: split-format floor (emulated): worst {floor['worst']:.2e} ({floor['worst_param']}), "
-          f"RMS {floor['rms']:.2e}")
-    assert worst[0][1] <= max(4 * wmod[0][1], 1.5 * floor["worst"], 1e-3), (worst, wmod, floor)
-    assert rms(errs) <= max(3 * rms(emod) + 1e-3, 1.5 * floor["rms"]), (rms(errs), rms(emod), floor)
+    if os.environ.get("RAFT_ENC_SPLIT3", "1") == "0":  # the round-4 format: its own floor
+        assert rms(errs) <= max(3 * rms(emod) + 1e-3, 1.5 * floor["rms"]), (rms(errs), rms(emod), floor)
+        return
+    assert rms(errs) <= max(1.5 * rms(emod), _FP32_RMS_ABS[name]), (rms(errs), rms(emod))
+    assert worst[0][1] <= max(2 * wmod[0][1], 2e-3), (worst, wmod)
 
 
 @pytest.mark.parametrize("small", [False, True])

@@ -4,7 +4,8 @@ Oracle: the same RAFT without AMP on the PyTorch module path (``fused_update=Fal
 native_encoder=False``: MIOpen fp32 convs, fp32 grid_sample-equivalent lookups).  The native
 fp32 path (ops/update_split.py, ops/encoder.py split mode) computes every conv product as
 x_hi W_hi + x_lo W_hi + x_hi W_lo with fp32 accumulation over operands stored with a 16-bit
-mantissa (hi + lo), so predictions agree to ~1e-5 relative.  Weight gradients are sums with
+mantissa (hi + lo), so predictions agree to ~1e-5 relative.  The encoders' forward runs the
+three-plane (fp32-exact) GEMMs in training (ops/encoder.py, split mode 2).  Weight gradients are sums with
 heavy cancellation (norm backward, softmax-mask gradients), where the 2^-17 operand precision
 shows up as ~1e-3 relative (worst ~1e-2, RAFT-small's fnet.layer1 ~3e-2: the format's own floor,
 scripts/emulate_split_precision.py) -- the same order as MIOpen's own fp32 deviation from
@@ -39,12 +40,16 @@ def _run(m, batch, iters):
 
 
 def _floor_tol(small: bool) -> float:
-    """1.5x the split format's own worst gradient error vs the reference (CPU emulation of the
-    storage layout, tests/fixtures/split_format_floor.json): the native path vs the MIOpen
-    module path can differ by that much without any kernel defect."""
+    """Worst parameter-gradient tolerance of the native-encoder paths vs the MIOpen module path.
+    With the three-plane (fp32-exact) encoder forward the measured worst is 2.5e-3 (base) /
+    5.2e-3 (small) (profiles/r5e_tests.log): 1e-2.  The round-4 two-plane forward
+    (RAFT_ENC_SPLIT3=0) sits at its format's floor: 1.5x the emulated worst
+    (tests/fixtures/split_format_floor.json)."""
     import json
     import os
 
+    if os.environ.get("RAFT_ENC_SPLIT3", "1") != "0":
+        return 1e-2
     with open(os.path.join(os.path.dirname(__file__), "fixtures", "split_format_floor.json")) as f:
         return 1.5 * json.load(f)["small" if small else "base"]["worst"]
 
