@@ -28,6 +28,9 @@ enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s);
 hipError_t launch_fixed_to_float(const long long* in, float* out, long n, const float* fix_scale, hipStream_t s);
 hipError_t launch_local_corr_mfma(const LocalCorrArgs& a, bool backward, hipStream_t s);
+bool local_corr_gather_ok(const LocalCorrArgs& a);
+long local_corr_gather_scratch(const LocalCorrArgs& a);
+hipError_t launch_local_corr_mfma_bwd_gather(const LocalCorrArgs& a, int* scratch, hipStream_t s);
 hipError_t launch_pyramid_unpool(const UnpoolArgs& u, hipStream_t s);
 hipError_t launch_pyramid_operand(const PyrOperandArgs& a, hipStream_t s);
 hipError_t launch_avgpool2x2(const float* in, float* out, long rows, int H, int W, hipStream_t s);
@@ -687,6 +690,17 @@ void local_corr_mfma_backward(const at::Tensor& f1, const at::Tensor& f2, const 
     fs = fixed_point_scale(gout, f1, scale,
                            (double)a.H * a.W * a.levels * 4.0 * (2 * radius + 2) * (2 * radius + 2));
     a.fix_scale = fs.data_ptr<float>();
+  }
+  static const bool gather_env = [] {
+    const char* e = std::getenv("RAFT_LC_GATHER");  // 0: the round-4 window-atomic backward (A/B)
+    return !(e && e[0] == '0');
+  }();
+  if (!deterministic && gather_env && local_corr_gather_ok(a)) {
+    // dF2 by binning the queries per 8 x 8 level block and gathering (local_corr_mfma.hip):
+    // plain stores instead of ~0.4 GB of overlapping window atomics per lookup at KITTI size
+    at::Tensor scratch = at::empty({local_corr_gather_scratch(a)}, g2.options().dtype(at::kInt));
+    HIP_OK(launch_local_corr_mfma_bwd_gather(a, scratch.data_ptr<int>(), cur_stream()));
+    return;
   }
   HIP_OK(launch_local_corr_mfma(a, true, cur_stream()));
   if (deterministic) HIP_OK(launch_fixed_to_float(a.g2fix, a.g2, g2.numel(), a.fix_scale, cur_stream()));

@@ -2243,7 +2243,8 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
   }
   // v4 (scripts/bench_convs.py on MI355X): 64x128 tiles for N > 64 (the 576-wide mask-head 1x1:
   // 34.3 -> 30.0 us, profiles/r2_bench_convs_cfg8.log), 64x64 otherwise; 128x128 tiles (one
-  // workgroup per CU) measured 21-30% slower on every 1x1 shape (profiles/r3_conv_1x1_tiles.log)
+  // workgroup per CU) measured 21-30% slower on every 1x1 shape (profiles/r3_conv_1x1_tiles.log),
+  // full-width 64x256 / 128x256 tiles 0-60 % slower (profiles/r5h_conv1x1*.log)
   const bool wide = cfg == 8 || (cfg != 9 && a.N > 64);
   if (wide)
     hipLaunchKernelGGL((conv_fwd4_kernel<64, 128, 3, F16>), dim3(tiles(64, 128)), dim3(256), 0, s, a);

@@ -101,9 +101,11 @@ __device__ __forceinline__ void tile_level_geometry(const LocalCorrArgs& a, Tile
 }
 
 // Stage one 64-channel slice: query tile rows (32 x 64) and window chunk rows (256 x 64).
+// F1 = false: the window rows only (the dF1-only backward does not read the query tile).
+template <bool F1 = true>
 __device__ __forceinline__ void stage_tiles(const LocalCorrArgs& a, const TileGeo& g, int b, int l, int chunk, int c0,
                                             __bf16* sF1, __bf16* sW, int tid) {
-  {  // 32 rows x 8 chunks of 16 B = 256 pieces, one per thread
+  if constexpr (F1) {  // 32 rows x 8 chunks of 16 B = 256 pieces, one per thread
     const int row = tid >> 3, pc = tid & 7;
     bf16x8_t v{};
     if (g.pix[row] >= 0) v = *reinterpret_cast<const bf16x8_t*>(a.f1 + (long)g.pix[row] * a.C + c0 + pc * 8);
@@ -234,7 +236,8 @@ __global__ __launch_bounds__(256) void local_corr_mfma_fwd_kernel(const LocalCor
   }
 }
 
-template <int RC = 0>
+// DF2 = false: dF1 only (dF2 by the gather kernels below, lc_gather_df2_kernel)
+template <int RC = 0, bool DF2 = true>
 __global__ __launch_bounds__(256) void local_corr_mfma_bwd_kernel(const LocalCorrArgs a) {
   __shared__ TileGeo g;
   __shared__ float cx[NQ], cy[NQ];
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(256) void local_corr_mfma_bwd_kernel(const LocalCor
       }
       __syncthreads();
       for (int s = 0; s < nkc; ++s) {
-        stage_tiles(a, g, b, l, chunk, s * KC, sF1, sW, tid);
+        stage_tiles<DF2>(a, g, b, l, chunk, s * KC, sF1, sW, tid);
         __syncthreads();
         // dF1[q][c] += sum_n G[q][n] F2win[n][c]: M = 32 q (2 x 16), N = 16 channels (wave),
         // K = 256 window pixels.  A = G rows (k contiguous); B[k = n][col = c] = F2win column
@@ -313,6 +316,10 @@ __global__ __launch_bounds__(256) void local_corr_mfma_bwd_kernel(const LocalCor
             for (int j = 0; j < 8; ++j) bfr[j] = sW[(ks * 32 + (lane >> 4) * 8 + j) * FP + col];
             acc1[s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc1[s][m], 0, 0, 0);
           }
+        }
+        if constexpr (!DF2) {
+          __syncthreads();
+          continue;
         }
         // dF2win[n][c] = sum_q G[q][n] F1[q][c]: M = 256 n (wave: 64 = 2 tiles), N = 64 c
         // (2 tiles), K = 32 q.  A[row n][k = q] = G column -> transposed read of G [q][n];
@@ -387,6 +394,306 @@ __global__ __launch_bounds__(256) void local_corr_mfma_bwd_kernel(const LocalCor
   }
 }
 
+// ---------------------------------------------------------------- dF2 by gathering (no atomics)
+// The tile-window backward above adds every tile's window gradient into the level gradient with
+// fp32 atomics: the windows of neighbouring 8 x 4 query tiles overlap ~7x at level 0, so a
+// KITTI-size step (3 x 376 x 1248) issues ~0.44 GB of atomic adds per lookup, which the memory
+// side retires at ~1.3 TB/s -- 3/4 of the kernel's 552 us (profiles/r5a_pmc_alt_summary.txt:
+// 0.17 L2 hit, 5.6 M write requests).  Instead, per level, the queries are binned by the 8 x 8
+// blocks of level pixels their (2r+2)^2 neighbourhood touches (count / scan / fill), and one
+// workgroup per (block, segment of <= LC_SEG queries) computes
+//     dF2[block px][c] = sum_q G[q][px] F1[q][c]     (M = 64 px, N = 256 c, K = the queries)
+// with G built from the tap gradients in LDS -- each level pixel is written by its block's
+// workgroup (a plain store when the block has one segment; segments of longer lists -- the
+// coarse levels, where ~100 x 4^l queries touch a pixel -- are added with atomics, ~10x fewer
+// bytes than the windows).  Query order inside a list follows the fill atomics, so the fp32
+// sums are not bitwise reproducible: deterministic mode keeps the fixed-point window path.
+constexpr int LC_B = 8;      // block side (level pixels)
+constexpr int LC_Q = 32;     // queries per chunk (MFMA K)
+constexpr int LC_SEG = 512;  // queries per workgroup item
+constexpr int LC_FP = 256 + 8;  // F1 chunk pitch (bf16): C <= 256
+constexpr int LC_GP = 64 + 8;   // G chunk pitch (bf16): 64 block pixels
+constexpr int LC_SH = 16;       // counter shards per block (workgroup index % LC_SH): at level 3
+                                // every wave of an image adds to the same few blocks
+
+struct LcBin {
+  int levels, B, H, W, r;
+  int w[4], h[4], nbx[4], nby[4], blk0[5];  // blk0[levels] = total blocks
+};
+
+__device__ __forceinline__ bool lc_box(const LcBin& bn, const float* coords, long q, int l, int& bx0, int& bx1,
+                                       int& by0, int& by1, int& x0, int& y0, float& fx, float& fy) {
+  const long HW = (long)bn.H * bn.W;
+  const long b = q / HW, p = q - b * HW;
+  const float cx = coords[b * 2 * HW + p], cy = coords[b * 2 * HW + HW + p];
+  if (!isfinite(cx) || !isfinite(cy)) return false;
+  const float s = 1.0f / float(1 << l);
+  const float x = clampc(cx * s), y = clampc(cy * s);
+  const float fx0 = floorf(x), fy0 = floorf(y);
+  fx = x - fx0;
+  fy = y - fy0;
+  x0 = (int)fx0 - bn.r;
+  y0 = (int)fy0 - bn.r;
+  const int nd = 2 * bn.r + 2;
+  const int xa = max(x0, 0), xb = min(x0 + nd - 1, bn.w[l] - 1);
+  const int ya = max(y0, 0), yb = min(y0 + nd - 1, bn.h[l] - 1);
+  if (xa > xb || ya > yb) return false;
+  bx0 = xa / LC_B;
+  bx1 = xb / LC_B;
+  by0 = ya / LC_B;
+  by1 = yb / LC_B;
+  return true;
+}
+
+// pass 1 / 3: count (fill == false) or fill the per-block query lists.  Neighbouring queries
+// touch the same few blocks (at level 3 thousands of queries share one block), so one atomic
+// per counter per WAVE: the lanes holding the same block key are matched by ballot and their
+// leader adds the group's count (per-lane atomics on one counter serialised: 0.7 ms a pass)
+template <bool FILL>
+__global__ __launch_bounds__(256) void lc_bin_kernel(const LcBin bn, const float* __restrict__ coords,
+                                                     int* __restrict__ cnt, const int* __restrict__ off,
+                                                     int* __restrict__ list) {
+  const long P = (long)bn.B * bn.H * bn.W;
+  const long q = (long)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool in = q < P;
+  const int b = in ? (int)(q / ((long)bn.H * bn.W)) : 0;
+  for (int l = 0; l < bn.levels; ++l) {
+    int bx0 = 0, bx1 = -1, by0 = 0, by1 = -1, x0, y0;
+    float fx, fy;
+    if (!(in && lc_box(bn, coords, q, l, bx0, bx1, by0, by1, x0, y0, fx, fy))) bx1 = by1 = -1, bx0 = by0 = 0;
+    // up to 3 x 3 blocks per query: slot k = (dy, dx) relative to (by0, bx0)
+    for (int k = 0; k < 9; ++k) {
+      const int by = by0 + k / 3, bx = bx0 + k % 3;
+      int key = (by <= by1 && bx <= bx1) ? bn.blk0[l] + (b * bn.nby[l] + by) * bn.nbx[l] + bx : -1;
+      for (;;) {
+        const unsigned long long active = __ballot(key >= 0);
+        if (active == 0) break;
+        const int src = __ffsll((long long)active) - 1;
+        const int lead = __shfl(key, src, 64);
+        const unsigned long long m = __ballot(key == lead);
+        const int first = __ffsll((long long)m) - 1;
+        const int slot = lead * LC_SH + (int)(blockIdx.x & (LC_SH - 1));
+        if constexpr (FILL) {
+          // the leader fetches the list offset beside its cursor add: one dependent round trip
+          int base = 0;
+          if (lane == first) base = off[slot] + atomicAdd(cnt + slot, __popcll(m));
+          base = __shfl(base, first, 64);
+          if (key == lead) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int)q;
+        } else {
+          if (lane == first) atomicAdd(cnt + slot, __popcll(m));  // no return value needed
+        }
+        if (key == lead) key = -1;
+      }
+    }
+  }
+}
+
+// pass 2 (one workgroup): off = exclusive scan of the (block, shard) counts -- a block's list is
+// its shards back to back, [off[blk * LC_SH], off[(blk + 1) * LC_SH]) -- the work items (block,
+// segment), and the counts reset to 0 for the fill pass's cursors.  hdr = {items, next item}
+__global__ __launch_bounds__(1024) void lc_scan_kernel(int* __restrict__ cnt, int* __restrict__ off, int nb,
+                                                       int* __restrict__ items, int* __restrict__ hdr) {
+  __shared__ int sa[1024], sb[1024];
+  __shared__ int carry[2];
+  const int tid = threadIdx.x;
+  if (tid == 0) carry[0] = carry[1] = 0;
+  __syncthreads();
+  for (int base = 0; base < nb; base += 1024) {
+    const int i = base + tid;
+    int sh[LC_SH], c = 0;
+#pragma unroll
+    for (int k = 0; k < LC_SH; ++k) {
+      sh[k] = i < nb ? cnt[i * LC_SH + k] : 0;
+      c += sh[k];
+    }
+    const int ns = (c + LC_SEG - 1) / LC_SEG;
+    sa[tid] = c;
+    sb[tid] = ns;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scans
+      const int va = tid >= d ? sa[tid - d] : 0, vb = tid >= d ? sb[tid - d] : 0;
+      __syncthreads();
+      sa[tid] += va;
+      sb[tid] += vb;
+      __syncthreads();
+    }
+    if (i < nb) {
+      int o = carry[0] + sa[tid] - c;
+      const int io = carry[1] + sb[tid] - ns;
+#pragma unroll
+      for (int k = 0; k < LC_SH; ++k) {
+        off[i * LC_SH + k] = o;
+        o += sh[k];
+        cnt[i * LC_SH + k] = 0;
+      }
+      for (int sgi = 0; sgi < ns; ++sgi) items[io + sgi] = i * 1024 + sgi;
+    }
+    __syncthreads();
+    if (tid == 1023) {
+      carry[0] += sa[1023];
+      carry[1] += sb[1023];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    off[nb * LC_SH] = carry[0];
+    hdr[0] = carry[1];
+    hdr[1] = 0;
+  }
+}
+
+// pass 4: persistent workgroups pull (block, segment) items; dF2 rows of the block.  Every
+// wave covers the block's 64 pixels and NJ 32-channel tiles (C = 128 NJ: 4 waves x NJ x 32)
+template <int RC, int NJ>
+__global__ __launch_bounds__(256) void lc_gather_df2_kernel(const LocalCorrArgs a, const LcBin bn,
+                                                            const int* __restrict__ off,
+                                                            const int* __restrict__ list,
+                                                            const int* __restrict__ items, int* __restrict__ hdr) {
+  __shared__ __attribute__((aligned(16))) __bf16 sF1[LC_Q * LC_FP];
+  __shared__ __attribute__((aligned(16))) __bf16 G[LC_Q * LC_GP];
+  __shared__ int qpix[LC_Q], qx0[LC_Q], qy0[LC_Q];
+  __shared__ float qfx[LC_Q], qfy[LC_Q];
+  __shared__ float sg[LC_Q * 84];  // the chunk's level-l tap gradients ((2r+1)^2 <= 81 per query)
+  __shared__ int s_item;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rd = 2 * (RC > 0 ? RC : a.r) + 1, nd = rd + 1, win = rd * rd;
+  const int nitems = hdr[0];
+  const int hh = lane >> 5, gi = (lane >> 4) & 1, qq = (lane & 15) >> 2, pq = lane & 3;
+  const int C = a.C;
+  for (;;) {
+    if (tid == 0) s_item = atomicAdd(hdr + 1, 1);
+    __syncthreads();
+    const int item = s_item;
+    __syncthreads();  // s_item read by every wave before the next dequeue
+    if (item >= nitems) break;
+    const int blk = items[item] >> 10, seg = items[item] & 1023;
+    int l = 0;
+    while (l + 1 < bn.levels && blk >= bn.blk0[l + 1]) ++l;
+    const int lb = blk - bn.blk0[l];
+    const int b = lb / (bn.nbx[l] * bn.nby[l]);
+    const int rem = lb - b * bn.nbx[l] * bn.nby[l];
+    const int by = rem / bn.nbx[l], bx = rem - (rem / bn.nbx[l]) * bn.nbx[l];
+    const int lb0 = off[blk * LC_SH], lb1 = off[(blk + 1) * LC_SH];
+    const int lbeg = lb0 + seg * LC_SEG, lend = min(lb1, lbeg + LC_SEG);
+    const bool single = lb1 - lb0 <= LC_SEG;
+    f32x16 acc[2][NJ];  // [32-pixel tile][32-channel tile of the wave]
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    constexpr int cw = NJ * 32;  // channels per wave
+    for (int q0 = lbeg; q0 < lend; q0 += LC_Q) {
+      if (tid < LC_Q) {
+        const int li = q0 + tid;
+        int pix = -1, x0 = 0, y0 = 0;
+        float fx = 0.f, fy = 0.f;
+        if (li < lend) {
+          pix = list[li];
+          int t0, t1, t2, t3;
+          if (!lc_box(bn, a.coords, pix, l, t0, t1, t2, t3, x0, y0, fx, fy)) pix = -1;
+        }
+        qpix[tid] = pix;
+        qx0[tid] = x0;
+        qy0[tid] = y0;
+        qfx[tid] = fx;
+        qfy[tid] = fy;
+      }
+      __syncthreads();
+      // the chunk's tap gradients (coalesced rows of win values) -> sg [q][t]
+      for (int i = tid; i < LC_Q * win; i += 256) {
+        const int qi = i / win, t = i - (i / win) * win;
+        const int pix = qpix[qi];
+        float v = 0.f;
+        if (pix >= 0) {
+          const long gi_ = (long)pix * a.gstride + l * win + t;
+          v = a.gout_bf16 ? static_cast<float>(static_cast<const __bf16*>(a.gout)[gi_])
+                          : static_cast<const float*>(a.gout)[gi_];
+        }
+        sg[qi * 84 + t] = v;
+      }
+      // F1 rows of the chunk -> sF1 [q][c]
+      for (int i = tid; i < LC_Q * (C / 8); i += 256) {
+        const int row = i / (C / 8), pc = i - (i / (C / 8)) * (C / 8);
+        bf16x8_t v{};
+        if (qpix[row] >= 0) v = *reinterpret_cast<const bf16x8_t*>(a.f1 + (long)qpix[row] * C + pc * 8);
+        *reinterpret_cast<bf16x8_t*>(sF1 + row * LC_FP + pc * 8) = v;
+      }
+      __syncthreads();
+      // G[q][px]: the gradient of block pixel px through query q's bilinear taps (the transpose
+      // of the forward blend, as in local_corr_mfma_bwd_kernel); thread = (query, block row)
+      {
+        const int q = tid & 31, ry = tid >> 5;
+        const int pix = qpix[q];
+        const int y = by * LC_B + ry;
+        const float fx = qfx[q], fy = qfy[q];
+        const float* gq = sg + q * 84;
+        auto gv = [&](int t) { return gq[t]; };
+#pragma unroll
+        for (int rx = 0; rx < LC_B; ++rx) {
+          const int x = bx * LC_B + rx;
+          const int aa = y - qy0[q], cc = x - qx0[q];
+          float v = 0.f;
+          if (pix >= 0 && y < bn.h[l] && x < bn.w[l] && (unsigned)aa < (unsigned)nd && (unsigned)cc < (unsigned)nd) {
+            if (aa < rd) {
+              if (cc < rd) v += (1.f - fx) * (1.f - fy) * gv(cc * rd + aa);
+              if (cc > 0) v += fx * (1.f - fy) * gv((cc - 1) * rd + aa);
+            }
+            if (aa > 0) {
+              if (cc < rd) v += (1.f - fx) * fy * gv(cc * rd + aa - 1);
+              if (cc > 0) v += fx * fy * gv((cc - 1) * rd + aa - 1);
+            }
+          }
+          G[q * LC_GP + ry * LC_B + rx] = static_cast<__bf16>(v * a.scale);
+        }
+      }
+      __syncthreads();
+      // acc[i][j] += G^T[px tile i][q] F1[q][c tile j]: A = transposed read of G [q][px],
+      // B = transposed read of sF1 [q][c] (the k permutation of both reads is the same)
+#pragma unroll
+      for (int ks = 0; ks < LC_Q / 16; ++ks) {
+        const int r0 = ks * 16 + hh * 8 + qq;
+        bf16x8 af[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int col = i * 32 + gi * 16 + 4 * pq;
+          const s16x4 lo = tr_read(G + r0 * LC_GP + col);
+          const s16x4 hi = tr_read(G + (r0 + 4) * LC_GP + col);
+          af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int col = wave * cw + j * 32 + gi * 16 + 4 * pq;
+          const s16x4 lo = tr_read(sF1 + r0 * LC_FP + col);
+          const s16x4 hi = tr_read(sF1 + (r0 + 4) * LC_FP + col);
+          const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+          for (int i = 0; i < 2; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+        }
+      }
+      __syncthreads();
+    }
+    // store / add the block's rows: C/D map row = px (e), col = channel (lane & 31)
+    float* g2l = a.g2 + (long)b * a.f2_bstride + (long)a.off[l] * C;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int px = i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        const int y = by * LC_B + px / LC_B, x = bx * LC_B + px % LC_B;
+        if (y >= bn.h[l] || x >= bn.w[l]) continue;
+        float* dst = g2l + ((long)y * bn.w[l] + x) * C + wave * cw + (lane & 31);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          if (single) dst[j * 32] = acc[i][j][e];
+          else atomicAdd(dst + j * 32, acc[i][j][e]);
+        }
+      }
+  }
+}
+
 __global__ __launch_bounds__(256) void fixed_to_float_kernel(const long long* __restrict__ in, float* __restrict__ out,
                                                              long n, const float* __restrict__ fix_scale) {
   const double inv = 1.0 / static_cast<double>(*fix_scale);
@@ -423,6 +730,76 @@ hipError_t launch_local_corr_mfma(const LocalCorrArgs& a, bool backward, hipStre
     hipLaunchKernelGGL((local_corr_mfma_fwd_kernel<__bf16, 4>), dim3((unsigned)tiles), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL((local_corr_mfma_fwd_kernel<__bf16, 0>), dim3((unsigned)tiles), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---- gather backward: dF1 by the tile kernel (no dF2 part), dF2 by binning + gathering
+namespace {
+LcBin lc_bin(const LocalCorrArgs& a) {
+  LcBin bn{};
+  bn.levels = a.levels;
+  bn.B = a.B;
+  bn.H = a.H;
+  bn.W = a.W;
+  bn.r = a.r;
+  int tot = 0;
+  for (int l = 0; l < a.levels; ++l) {
+    bn.w[l] = a.w[l];
+    bn.h[l] = a.h[l];
+    bn.nbx[l] = (a.w[l] + LC_B - 1) / LC_B;
+    bn.nby[l] = (a.h[l] + LC_B - 1) / LC_B;
+    bn.blk0[l] = tot;
+    tot += a.B * bn.nbx[l] * bn.nby[l];
+  }
+  bn.blk0[a.levels] = tot;
+  return bn;
+}
+// a neighbourhood of 2r + 2 <= 10 pixels touches at most 3 blocks of 8 per axis
+constexpr int kLcMaxBlocksPerQuery = 9;
+long lc_list_bound(const LocalCorrArgs& a) { return (long)a.B * a.H * a.W * a.levels * kLcMaxBlocksPerQuery; }
+}  // namespace
+
+bool local_corr_gather_ok(const LocalCorrArgs& a) { return (a.C == 128 || a.C == 256) && a.r <= 4 && a.levels <= 4; }
+
+long local_corr_gather_scratch(const LocalCorrArgs& a) {
+  const LcBin bn = lc_bin(a);
+  const long nb = bn.blk0[a.levels];
+  const long lists = lc_list_bound(a);
+  return nb * LC_SH + (nb * LC_SH + 1) + 2 + (nb + lists / LC_SEG + 1) + lists;
+}
+
+hipError_t launch_local_corr_mfma_bwd_gather(const LocalCorrArgs& a, int* scratch, hipStream_t s) {
+  if (!local_corr_gather_ok(a)) return hipErrorInvalidValue;
+  const long tiles = (long)a.B * ((a.H + TY - 1) / TY) * ((a.W + TX - 1) / TX);
+  if (tiles == 0) return hipSuccess;
+  const LcBin bn = lc_bin(a);
+  const int nb = bn.blk0[a.levels];
+  const long lists = lc_list_bound(a);
+  int* cnt = scratch;
+  int* off = cnt + nb * LC_SH;
+  int* hdr = off + nb * LC_SH + 1;
+  int* items = hdr + 2;
+  int* list = items + (nb + lists / LC_SEG + 1);
+  const long P = (long)a.B * a.H * a.W;
+  const unsigned pblocks = (unsigned)((P + 255) / 256);
+  if (hipMemsetAsync(cnt, 0, (size_t)nb * LC_SH * sizeof(int), s) != hipSuccess) return hipGetLastError();
+  hipLaunchKernelGGL(lc_bin_kernel<false>, dim3(pblocks), dim3(256), 0, s, bn, a.coords, cnt, off, list);
+  hipLaunchKernelGGL(lc_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, off, nb, items, hdr);
+  hipLaunchKernelGGL(lc_bin_kernel<true>, dim3(pblocks), dim3(256), 0, s, bn, a.coords, cnt, off, list);
+  // dF1 (the tile kernel without its window-gradient atomics)
+  if (a.r == 4)
+    hipLaunchKernelGGL((local_corr_mfma_bwd_kernel<4, false>), dim3((unsigned)tiles), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((local_corr_mfma_bwd_kernel<0, false>), dim3((unsigned)tiles), dim3(256), 0, s, a);
+  // dF2: persistent workgroups over the (block, segment) items
+  const unsigned wgs = (unsigned)std::min<long>(1024, nb + lists / LC_SEG + 1);
+  if (a.C == 256) {
+    if (a.r == 4) hipLaunchKernelGGL((lc_gather_df2_kernel<4, 2>), dim3(wgs), dim3(256), 0, s, a, bn, off, list, items, hdr);
+    else hipLaunchKernelGGL((lc_gather_df2_kernel<0, 2>), dim3(wgs), dim3(256), 0, s, a, bn, off, list, items, hdr);
+  } else {
+    if (a.r == 4) hipLaunchKernelGGL((lc_gather_df2_kernel<4, 1>), dim3(wgs), dim3(256), 0, s, a, bn, off, list, items, hdr);
+    else hipLaunchKernelGGL((lc_gather_df2_kernel<0, 1>), dim3(wgs), dim3(256), 0, s, a, bn, off, list, items, hdr);
+  }
   return hipGetLastError();
 }
 

@@ -27,6 +27,7 @@ SHAPES = {
     "convf2": (128, 64, 3, 3),
     "heads": (128, 512, 3, 3),
     "fh1": (128, 256, 3, 3),
+    "fh2": (256, 2, 3, 3),
     "zr": (384, 256, 1, 5),
     "q15": (384, 128, 1, 5),
     "zr51": (384, 256, 5, 1),
