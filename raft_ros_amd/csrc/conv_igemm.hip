@@ -1516,6 +1516,147 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
 }
 
 
+// ============================================================================ 1x1 GEMM (v7)
+// The update block's 1x1 convs (convc1 324 -> 256, mask.2 256 -> 576 and their data gradients)
+// are plain GEMMs with a short K (256-576): on v4 each 64x128 tile ran 4-9 K steps whose issue
+// recomputed the im2col tap / bounds state per piece (~19 VALU per MFMA, r4_pmc_summary_final)
+// and read its fragments in front of the MFMAs.  v7: a single source row per pixel, so every
+// lane's DMA offsets are computed once and the K step rides in the scalar soffset; the
+// fwd6 pipeline (3-stage ring, fragments of step t+1 read behind the MFMAs of step t, raw
+// barriers, counted vmcnt); 128 x 64 tiles in 72 KB so two workgroups share a CU.
+template <int BM, int BN, int WGM, int WGN, bool F16 = false>
+__global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd7_kernel(const ConvFwdArgs a) {
+  constexpr int NW = WGM * WGN;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);  // DMA pieces per wave per step
+  constexpr int STAGE = (BM + BN) * 128;                 // bytes
+  constexpr int NS = 3;
+  static_assert(AI >= 1 && BI >= 1 && TM >= 1 && TN >= 1, "tile");
+  static_assert(NS * STAGE >= BM * (BN + 4) * 4, "epilogue tile must fit the ring");
+  extern __shared__ __attribute__((aligned(1024))) __bf16 dsm[];
+  char* const lds = reinterpret_cast<char*>(dsm);
+  const unsigned lds0 = (unsigned)(reinterpret_cast<uintptr_t>(dsm) & 0xffffffffu);
+
+  const int P = (int)a.P, Nn = a.N, Kpad = a.Kpad;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.src[0].ptr, (unsigned)(a.P * a.src[0].stride * 2));
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.wt, (unsigned)((long)Nn * Kpad * 2));
+  const unsigned xst = (unsigned)a.src[0].stride * 2;
+  const int tilesN = (Nn + BN - 1) / BN, tilesM = (P + BM - 1) / BM;
+  const int wg = xcd_remap(blockIdx.x, tilesM * tilesN);
+  const int tm = wg / tilesN, tn = wg - (wg / tilesN) * tilesN;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int lrow = lane >> 3, lpc = lane & 7;
+  const int fr = lane & 31, fh = lane >> 5;
+  unsigned avoff[AI], bvoff[BI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = (wave * AI + i) * 8 + lrow;
+    avoff[i] = (m0 + row < P) ? (unsigned)(m0 + row) * xst + (unsigned)(swz(row, lpc) * 16) : kOOB;
+  }
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int row = (wave * BI + i) * 8 + lrow;
+    bvoff[i] = (n0 + row < Nn) ? (unsigned)((n0 + row) * Kpad * 2 + swz(row, lpc) * 16) : kOOB;
+  }
+  // per-lane LDS fragment addresses (XOR-ready: sub-step s reads addr ^ (s << 5))
+  unsigned aaddr[TM], baddr[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int row = wm * WM + i * 32 + fr;
+    aaddr[i] = lds0 + (unsigned)row * 128u + ((((row >> 1) & 7) ^ fh) << 4);
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int row = BM + wn * WN + j * 32 + fr;
+    baddr[j] = lds0 + (unsigned)row * 128u + ((((row >> 1) & 7) ^ fh) << 4);
+  }
+  const int nk = Kpad / 64;
+  auto issue = [&](int t, int st) __attribute__((always_inline)) {
+    const unsigned soff = (unsigned)t * 128u;  // 64 channels = 128 bytes per step
+    char* sa = lds + st * STAGE;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) bload16(rx, reinterpret_cast<__bf16*>(sa + (wave * AI + i) * 1024), avoff[i], soff);
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      bload16(rw, reinterpret_cast<__bf16*>(sa + BM * 128 + (wave * BI + i) * 1024), bvoff[i], soff);
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  bf16x8 fa[2][TM][4], fb[2][TN][4];
+  auto read = [&](auto rc, int st) __attribute__((always_inline)) {
+    constexpr int R = decltype(rc)::value;
+    const unsigned off = (unsigned)(st * STAGE);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[R][i][s] = lds_read16((aaddr[i] ^ (unsigned)(s << 5)) + off);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[R][j][s] = lds_read16((baddr[j] ^ (unsigned)(s << 5)) + off);
+    }
+  };
+  constexpr int G = AI + BI;
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  if (nk > 2) issue(2, 2);
+  if (nk > 2) wait_vmcnt<2 * G>();
+  else if (nk > 1) wait_vmcnt<G>();
+  else wait_vmcnt<0>();
+  __syncthreads();
+  read(std::integral_constant<int, 0>{}, 0);
+  auto step = [&](int t, auto rc) __attribute__((always_inline)) {
+    constexpr int R = decltype(rc)::value;
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < nk) {
+      if (t + 2 < nk) wait_vmcnt<G>();  // step t+1 landed, t+2 may stay in flight
+      else wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 3 < nk) issue(t + 3, t % NS);  // into the stage step t was read from
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned off = (unsigned)(((t + 1) % NS) * STAGE);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mma16<F16>(fa[R][i][s], fb[R][j][s], acc[i][j]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[R ^ 1][i][s] = lds_read16((aaddr[i] ^ (unsigned)(s << 5)) + off);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[R ^ 1][j][s] = lds_read16((baddr[j] ^ (unsigned)(s << 5)) + off);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mma16<F16>(fa[R][i][s], fb[R][j][s], acc[i][j]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  for (int t = 0; t < nk; t += 2) {
+    step(t, std::integral_constant<int, 0>{});
+    if (t + 1 < nk) step(t + 1, std::integral_constant<int, 1>{});
+  }
+  wait_vmcnt<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  fwd_epilogue<BM, BN, TM, TN, NW, WGN, 0, F16>(a, reinterpret_cast<float*>(dsm), acc, m0, n0, P, Nn);
+}
+
 // ============================================================================ wgrad helpers
 constexpr int WBK = kWgradBK;
 
@@ -2127,11 +2268,18 @@ bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
       return t51 && launch_fwd6_t<128, 64, 4, 1, 5, 1, 16, F16>(a, s);
     case 65:  // 1x5 as a flat 128-pixel strip (132 halo rows at any width), two workgroups per CU
       return t15 && launch_fwd6_t<128, 64, 4, 1, 1, 5, 0, F16>(a, s);
+
     default:
       return false;
   }
 }
 }  // namespace
+
+// v7 for the automatic 1x1 choice (RAFT_CONV_V7=0: back to v4 for A/B runs)
+static const bool kUseV7 = [] {
+  const char* e = std::getenv("RAFT_CONV_V7");
+  return !(e && e[0] == '0');
+}();
 
 template <bool F16>
 hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
@@ -2175,6 +2323,7 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
   for (int i = 0; i < a.nsrc; ++i) ok5 = ok5 && a.src[i].C % 64 == 0;
   int v5 = cfg >= 20 ? cfg : 0;
   if (cfg == 41 || cfg == 45 || (cfg >= 59 && cfg <= 65)) {  // v6 tiles (tests / microbenchmarks)
+    // (a strip buffer pair per chunk needs >= 3 taps per chunk: no 1x1 variant)
     const bool shape6 = (a.KH == 3 && a.KW == 3) || (a.KH * a.KW == 5 && (a.KH == 1 || a.KW == 1));
     if (!ok5 || !shape6 || a.PH != a.KH / 2 || a.PW != a.KW / 2) return hipErrorInvalidValue;
     return launch_conv_fwd6<F16>(a, cfg, s) ? hipGetLastError() : hipErrorInvalidValue;
@@ -2245,6 +2394,16 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
   // 34.3 -> 30.0 us, profiles/r2_bench_convs_cfg8.log), 64x64 otherwise; 128x128 tiles (one
   // workgroup per CU) measured 21-30% slower on every 1x1 shape (profiles/r3_conv_1x1_tiles.log),
   // full-width 64x256 / 128x256 tiles 0-60 % slower (profiles/r5h_conv1x1*.log)
+  // v7 (lean 1x1 GEMM, 128 x 64 tiles, two workgroups per CU) for single-source 1x1 convs
+  const bool v7ok = a.KH == 1 && a.KW == 1 && a.nsrc == 1 && a.src[0].C == a.Cin && a.N >= 64 &&
+                    (a.src[0].stride % 8) == 0 && a.P * a.src[0].stride * 2 < (1L << 31);
+  if (cfg == 67 || (cfg == 0 && v7ok && kUseV7)) {
+    if (!v7ok) return hipErrorInvalidValue;
+    constexpr int lds7 = 3 * (128 + 64) * 128;
+    set_lds_limit((const void*)conv_fwd7_kernel<128, 64, 4, 1, F16>, lds7);
+    hipLaunchKernelGGL((conv_fwd7_kernel<128, 64, 4, 1, F16>), dim3(tiles(128, 64)), dim3(256), lds7, s, a);
+    return hipGetLastError();
+  }
   const bool wide = cfg == 8 || (cfg != 9 && a.N > 64);
   if (wide)
     hipLaunchKernelGGL((conv_fwd4_kernel<64, 128, 3, F16>), dim3(tiles(64, 128)), dim3(256), 0, s, a);
