@@ -231,6 +231,8 @@ def run(args):
     else:
         step = None
 
+    params = [p for p in model.parameters() if p.requires_grad]  # not re-walked per step (host time)
+
     def train_step(i):
         i1, i2, flow, valid = pool[i % len(pool)]
         optimizer.zero_grad(set_to_none=True)
@@ -240,7 +242,7 @@ def run(args):
         if gsync is not None:
             gsync.sync()
         scaler.unscale_(optimizer)
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
         scaler.step(optimizer)
         scheduler.step()
         scaler.update()

@@ -54,6 +54,8 @@ hipError_t launch_pack_flow(const float* flow, void* flow8, void* motion, long s
                             int from_coords, hipStream_t s);
 hipError_t launch_apply_delta(const float* coords1, const float* delta, long sd, float* coords_out,
                               float* flow_out, int B, int HW, int W, hipStream_t s);
+hipError_t launch_n2_apply(const float* y, int nslot, const float* bias, const float* coords1, float* coords_out,
+                           float* flow_out, float* delta, long sd, int B, int H, int W, hipStream_t s);
 hipError_t launch_convex_up_fwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
                                 long msH, long msW, float* out, int B, int H, int W, hipStream_t s);
 hipError_t launch_convex_up_bwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
@@ -825,7 +827,8 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
               const c10::optional<at::Tensor>& g0, const c10::optional<at::Tensor>& carry,
               const c10::optional<at::Tensor>& out3, int64_t gru_cols, const c10::optional<at::Tensor>& addsrc,
               const c10::optional<at::Tensor>& cout, const c10::optional<at::Tensor>& cmask, int64_t cm_c0,
-              int64_t cm_valid, at::IntArrayRef split) {
+              int64_t cm_valid, at::IntArrayRef split, const c10::optional<at::Tensor>& n2w,
+              const c10::optional<at::Tensor>& n2y) {
   TORCH_CHECK(geom.size() == 7, "raft_amd conv_fwd: geom = (B, H, W, KH, KW, PH, PW)");
   ConvFwdArgs a{};
   if (!split.empty()) {
@@ -954,6 +957,26 @@ void conv_fwd(at::TensorList srcs, const at::Tensor& wt, at::IntArrayRef geom, i
       a.cm_valid = static_cast<int>(cm_valid);
     }
     TORCH_CHECK(a.out_stride % 4 == 0 && al16(a.out), "raft_amd conv_fwd: out needs 16-byte aligned rows");
+  }
+  if (n2y) {
+    // the flow head's conv2 folded into this conv's epilogue (kernel_abi.h ConvFwdArgs::n2y):
+    // 3x3 weights [>=2][Kpad] over the first n2_cols = 64 * slots output channels
+    TORCH_CHECK(n2w.has_value() && epi == 0 && split.empty() && !a.out_f32 && a.N % 64 == 0,
+                "raft_amd conv_fwd: n2y needs n2w, epilogue 0, a 16-bit output and N % 64 == 0");
+    check_gpu(*n2w, "n2w");
+    check_gpu(*n2y, "n2y");
+    TORCH_CHECK(n2y->scalar_type() == at::kFloat && n2y->dim() == 3 && n2y->is_contiguous() && n2y->size(1) == 18 &&
+                    n2y->size(2) == a.P,
+                "raft_amd conv_fwd: n2y must be contiguous fp32 [slots][18][P]");
+    const int64_t cols = n2y->size(0) * 64;
+    TORCH_CHECK(cols <= a.N && n2w->scalar_type() == dt16 && n2w->dim() == 2 && n2w->is_contiguous() &&
+                    n2w->size(0) >= 2 && n2w->size(1) >= 9 * cols,
+                "raft_amd conv_fwd: n2w must be contiguous [>=2][>=9 * 64 * slots] in the sources' dtype");
+    a.n2w = static_cast<const __bf16*>(n2w->data_ptr());
+    a.n2y = n2y->data_ptr<float>();
+    a.n2_kpad = static_cast<int>(n2w->size(1));
+    a.n2_cols = static_cast<int>(cols);
+    TORCH_CHECK(a.P * 18 * n2y->size(0) < (1L << 31), "raft_amd conv_fwd: n2y too large");
   }
   const c10::DeviceGuard guard(wt.device());
   HIP_OK(launch_conv_fwd(a, cur_stream()));
@@ -1334,6 +1357,37 @@ void apply_delta(const at::Tensor& coords1, const at::Tensor& delta, const at::T
                             cur_stream()));
 }
 
+// the flow head's conv2 from the heads conv's per-tap partials (conv_fwd n2y) + apply_delta;
+// delta (P, >=2) fp32 rows is also written when given
+void n2_apply(const at::Tensor& y, const at::Tensor& bias, const at::Tensor& coords1, const at::Tensor& coords_out,
+              const at::Tensor& flow_out, const c10::optional<at::Tensor>& delta) {
+  check_coords(coords1);
+  check_coords(coords_out);
+  check_coords(flow_out);
+  TORCH_CHECK(coords_out.sizes() == coords1.sizes() && flow_out.sizes() == coords1.sizes(),
+              "raft_amd n2_apply: shape mismatch");
+  const long B = coords1.size(0), H = coords1.size(2), W = coords1.size(3);
+  check_gpu(y, "y");
+  TORCH_CHECK(y.scalar_type() == at::kFloat && y.dim() == 3 && y.is_contiguous() && y.size(0) <= 4 && y.size(1) == 18 &&
+                  y.size(2) == B * H * W,
+              "raft_amd n2_apply: y must be contiguous fp32 [slots <= 4][18][P]");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.is_contiguous() && bias.numel() >= 2 &&
+                  bias.device() == y.device(),
+              "raft_amd n2_apply: bias must be fp32 [>=2] on the device");
+  float* dp = nullptr;
+  long sd = 0;
+  if (delta) {
+    pm_any(*delta, "delta", B * H * W, at::kFloat);
+    TORCH_CHECK(delta->size(1) >= 2, "raft_amd n2_apply: delta needs 2 channels");
+    dp = delta->data_ptr<float>();
+    sd = delta->stride(0);
+  }
+  const c10::DeviceGuard guard(coords1.device());
+  HIP_OK(launch_n2_apply(y.data_ptr<float>(), (int)y.size(0), bias.data_ptr<float>(), coords1.data_ptr<float>(),
+                         coords_out.data_ptr<float>(), flow_out.data_ptr<float>(), dp, sd, (int)B, (int)H, (int)W,
+                         cur_stream()));
+}
+
 // corr_lookup into a caller buffer (B, H, W, och) with och >= L*(2r+1)^2 (zero padded)
 // flow8 / motion (optional): the step's packed flow operand, written by the same launch
 // (pack_flow(coords, flow8, motion, from_coords=true) folded into the lookup)
@@ -1415,7 +1469,8 @@ TORCH_LIBRARY(raft_amd, m) {
       "conv_fwd(Tensor[] srcs, Tensor wt, int[] geom, int N, Tensor? bias, int epi, int act, float alpha, "
       "Tensor(a!) out, int acc_c0, Tensor? mask, Tensor? h, Tensor? z, Tensor(b!)? out2, int cfg=0, "
       "Tensor? g0=None, Tensor(c!)? carry=None, Tensor(d!)? out3=None, int gru_cols=0, Tensor? addsrc=None, "
-      "Tensor(e!)? cout=None, Tensor? cmask=None, int cm_c0=0, int cm_valid=0, int[] split=[]) -> ()");
+      "Tensor(e!)? cout=None, Tensor? cmask=None, int cm_c0=0, int cm_valid=0, int[] split=[], Tensor? n2w=None, "
+      "Tensor(f!)? n2y=None) -> ()");
   m.def("split_pack(Tensor src, Tensor(a!) dst, int G, int c0, int Cpad) -> ()");
   m.def("conv_wgrad(Tensor[] srcs, Tensor dy, int[] geom, int N, Tensor(a!) dw, Tensor(b!)? db, "
         "bool accumulate=True) -> ()");
@@ -1441,6 +1496,8 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("masked_cast(Tensor src, Tensor? mask, Tensor(a!) out) -> ()");
   m.def("pack_flow(Tensor flow, Tensor(a!) flow8, Tensor(b!)? motion, bool from_coords=False) -> ()");
   m.def("apply_delta(Tensor coords1, Tensor delta, Tensor(a!) coords_out, Tensor(b!) flow_out) -> ()");
+  m.def("n2_apply(Tensor y, Tensor bias, Tensor coords1, Tensor(a!) coords_out, Tensor(b!) flow_out, "
+        "Tensor(c!)? delta=None) -> ()");
   m.def(
       "corr_lookup_into(Tensor[] pyramid, Tensor coords, int radius, Tensor(a!) out, Tensor(b!)? flow8=None, "
       "Tensor(c!)? motion=None) -> ()");
@@ -1497,6 +1554,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("pack_flow", &raft_amd::pack_flow);
   m.impl("split_pack", &raft_amd::split_pack);
   m.impl("apply_delta", &raft_amd::apply_delta);
+  m.impl("n2_apply", &raft_amd::n2_apply);
   m.impl("corr_lookup_into", &raft_amd::corr_lookup_into);
   m.impl("convex_upsample_backward_into", &raft_amd::convex_upsample_backward_into);
   m.impl("conv_wgrad", &raft_amd::conv_wgrad);

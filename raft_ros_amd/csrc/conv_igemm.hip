@@ -333,6 +333,72 @@ __device__ __forceinline__ void fwd_epilogue(const ConvFwdArgs& a, float* et, f3
     const bool accum = grad && n >= a.acc_c0;  // acc_c0 is a multiple of 8
     const bool f32o = a.out_f32 != 0;
     const bool vec = full && (!f32o || (a.out_stride & 3) == 0);
+    if constexpr (CPR >= 8) {
+      // epi 0 + the folded narrow conv (ConvFwdArgs::n2y; host: bf16 out, N % 64 == 0 or
+      // N >= n2_cols): each aligned group of 8 lanes is one 64-channel slot of one row
+      if (a.n2y != nullptr && a.epi == 0 && n0 < a.n2_cols) {
+        const bool in2 = n < a.n2_cols;  // uniform per 8-lane group (n2_cols % 64 == 0)
+        const int c8 = ch & 7;
+        const long slot = n / 64;
+#pragma unroll 1
+        for (int row = tid / CPR; row < BM; row += NT / CPR) {
+          long p;
+          if (!row_pixel<TW2D>(row, m0, P, t2, p)) {
+            if constexpr (TW2D == 0) break;
+            else continue;
+          }
+          f32x4 lo = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8);
+          f32x4 hi = *reinterpret_cast<const f32x4*>(et + row * EPI_LD + ch * 8 + 4);
+          lo = lo * alpha + fb0;
+          hi = hi * alpha + fb1;
+          bf16x8 w;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            w[q] = st16(relu ? fmaxf(lo[q], 0.f) : lo[q], f16);
+            w[q + 4] = st16(relu ? fmaxf(hi[q], 0.f) : hi[q], f16);
+          }
+          *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = w;
+          // the 18 weight rows are re-read per row (L1-resident, 9 KB in all): hoisting them
+          // out of the row loop would hold 72 more VGPRs in every forward kernel and halve the
+          // occupancy of the two-workgroups-per-CU tiles.  The empty asm makes the channel
+          // offset opaque per row so the compiler cannot hoist the loads.
+          int nn = in2 ? n : 0;
+          asm volatile("" : "+v"(nn));
+          const __bf16* wr = a.n2w + nn;
+          float s[18];
+#pragma unroll
+          for (int j = 0; j < 18; ++j) {
+            const int o = j / 9, t = j - (j / 9) * 9;
+            const bf16x8 wv = *reinterpret_cast<const bf16x8*>(wr + (long)o * a.n2_kpad + t * a.n2_cols);
+            float acc2 = 0.f;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc2 += ld16(w[q], f16) * ld16(wv[q], f16);
+            s[j] = acc2;
+          }
+#pragma unroll
+          for (int off = 4; off > 0; off >>= 1)
+#pragma unroll
+            for (int j = 0; j < 18; ++j) s[j] += __shfl_xor(s[j], off, 64);
+          if (in2) {
+            // lanes write planes j = c8, c8 + 8, c8 + 16 (< 18) of this row (selects, not a dynamic
+            // index into s, which would put s in scratch)
+            float v0 = s[0], v1 = s[8], v2 = s[16];
+#pragma unroll
+            for (int q = 1; q < 8; ++q)
+              if (c8 == q) {
+                v0 = s[q];
+                v1 = s[q + 8];
+                if (q < 2) v2 = s[q + 16];
+              }
+            float* y = a.n2y + (slot * 18 + c8) * P + p;  // planar: plane j at y + j * P
+            y[0] = v0;
+            y[8 * (long)P] = v1;
+            if (c8 < 2) y[16 * (long)P] = v2;
+          }
+        }
+        return;
+      }
+    }
     if (a.epi >= 2) {
       // GRU gates (bf16, channel counts multiples of 8): epi 2 z||r: out = sigmoid, and for the r
       // half out2 = r * h; epi 3: q = tanh, out = (1 - z) h + z q, out2 = q
@@ -2126,6 +2192,103 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   }
 }
 
+// ============================================================================ flow encoder conv1 (7x7, 2 channels)
+// convf1 (core/update.py BasicMotionEncoder: 7x7, the 2 flow channels -> 128 / 64, ReLU) has a
+// tiny K (49 taps x 2 channels) that the generic paths pad 4x (flow8 carries the flow as 8
+// channels, the DMA tiles work in 8-channel pieces: K = 392 -> 448).  Here the packed
+// K' = tap * 2 + c (98 -> 7 MFMA K-blocks of 16) is gathered straight from a halo tile of
+// the (u, v) pairs in LDS: one workgroup = an 8 x 16 pixel tile x all N output channels,
+// lane fragments built from 4 32-bit LDS reads per K-block; the weights' (u, v) pairs come
+// from the packed [N][Kpad] rows (k = tap * 8 + c).  Bias + ReLU + 16-bit store through an
+// LDS tile (16-byte rows).
+template <int N, bool F16>
+__global__ __launch_bounds__(256) void conv_flow7_kernel(const ConvFwdArgs a) {
+  constexpr int TH = 8, TW = 16, HH = TH + 6, HWD = TW + 6;
+  constexpr int NBLK = N / 32;  // 32-column blocks; waves per column block = 4 / NBLK
+  constexpr int MPW = NBLK;     // 32-pixel blocks per wave (4 in the tile)
+  constexpr int OLD = N + 8;    // output tile pitch (16-bit elements)
+  static_assert(N == 64 || N == 128, "convf1 widths");
+  __shared__ uint32_t halo[HH * HWD];
+  __shared__ __attribute__((aligned(16))) __bf16 otile[TH * TW * OLD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, W = a.W;
+  const int tw = (W + TW - 1) / TW, th = (H + TH - 1) / TH;
+  int bid = blockIdx.x;
+  const int b = bid / (tw * th);
+  bid -= b * tw * th;
+  const int y0 = (bid / tw) * TH, x0 = (bid - (bid / tw) * tw) * TW;
+  const long pbase = (long)b * H * W;
+  const long sst = a.src[0].stride;
+  for (int i = tid; i < HH * HWD; i += 256) {
+    const int hy = i / HWD, hx = i - (i / HWD) * HWD;
+    const int y = y0 + hy - 3, x = x0 + hx - 3;
+    uint32_t v = 0u;
+    if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
+      v = *reinterpret_cast<const uint32_t*>(a.src[0].ptr + (pbase + (long)y * W + x) * sst);
+    halo[i] = v;
+  }
+  const int nb = wave % NBLK, mb0 = (wave / NBLK) * MPW;
+  const int fr = lane & 31, fh = lane >> 5;
+  // B fragments: k' = kb * 16 + fh * 8 + i -> tap kb * 8 + fh * 4 + i / 2, channel i % 2
+  bf16x8 bw[7];
+  {
+    const __bf16* wrow = a.wt + (long)(nb * 32 + fr) * a.Kpad;
+#pragma unroll
+    for (int kb = 0; kb < 7; ++kb) {
+      u32x4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int tap = kb * 8 + fh * 4 + q;
+        v[q] = tap < 49 ? *reinterpret_cast<const uint32_t*>(wrow + tap * 8) : 0u;
+      }
+      bw[kb] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+  __syncthreads();
+  f32x16 acc[MPW];
+#pragma unroll
+  for (int i = 0; i < MPW; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < MPW; ++i) {
+    const int m = (mb0 + i) * 32 + fr;  // tile pixel of this lane's A row
+    const int ty = m / TW, tx = m - (m / TW) * TW;
+#pragma unroll
+    for (int kb = 0; kb < 7; ++kb) {
+      u32x4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int tap = kb * 8 + fh * 4 + q;
+        const int ky = tap / 7, kx = tap - (tap / 7) * 7;
+        v[q] = tap < 49 ? halo[(ty + ky) * HWD + tx + kx] : 0u;
+      }
+      acc[i] = mma16<F16>(__builtin_bit_cast(bf16x8, v), bw[kb], acc[i]);
+    }
+  }
+  const int n = nb * 32 + fr;
+  const float bias = a.bias ? a.bias[n] : 0.f;
+  const bool relu = a.act == 1;
+#pragma unroll
+  for (int i = 0; i < MPW; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = (mb0 + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+      float v = acc[i][r] * a.alpha + bias;
+      if (relu) v = fmaxf(v, 0.f);
+      otile[m * OLD + n] = st16(v, F16);
+    }
+  __syncthreads();
+  constexpr int CPR = N / 8;
+  for (int i = tid; i < TH * TW * CPR; i += 256) {
+    const int m = i / CPR, c = i - (i / CPR) * CPR;
+    const int y = y0 + m / TW, x = x0 + m % TW;
+    if (y < H && x < W)
+      *reinterpret_cast<bf16x8*>(static_cast<__bf16*>(a.out) + (pbase + (long)y * W + x) * a.out_stride + c * 8) =
+          *reinterpret_cast<const bf16x8*>(otile + m * OLD + c * 8);
+  }
+}
+
 // ============================================================================ narrow output (N <= 2)
 // flow_head.conv2 (3x3, 256 -> 2) is a pair of 2,304-long dot products per pixel: a
 // bandwidth problem, not a GEMM (a 64-wide MFMA tile would be 97% padding).  LPP lanes
@@ -2286,6 +2449,16 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
   if (a.P == 0 || a.N == 0) return hipSuccess;
   if (a.Kpad % FBK != 0) return hipErrorInvalidValue;
   const int cfg = a.cfg;
+  if ((cfg == 0 || cfg == 68) && a.KH == 7 && a.KW == 7 && a.PH == 3 && a.PW == 3 && a.nsrc == 1 && a.Cin == 8 &&
+      a.src[0].C == 8 && a.Kpad >= 49 * 8 && a.epi == 0 && !a.out_f32 && a.split_g == 0 && a.n2y == nullptr &&
+      (a.N == 64 || a.N == 128) && a.out_stride % 8 == 0 && (reinterpret_cast<uintptr_t>(a.out) & 15) == 0 &&
+      a.src[0].stride % 2 == 0 && (reinterpret_cast<uintptr_t>(a.src[0].ptr) & 3) == 0) {
+    // convf1: the flow channels are the first 2 of 8 (pack_flow zero-fills the rest)
+    const long tiles = (long)a.B * ((a.H + 7) / 8) * ((a.W + 15) / 16);
+    if (a.N == 128) hipLaunchKernelGGL((conv_flow7_kernel<128, F16>), dim3((unsigned)tiles), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((conv_flow7_kernel<64, F16>), dim3((unsigned)tiles), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   if (cfg == 0 && a.N <= 2 && a.epi == 0 && a.nsrc == 1 && a.KH * a.KW <= 9 && a.src[0].C == a.Cin &&
       a.P < (1L << 30) &&
       (a.Cin == 64 || a.Cin == 128 || a.Cin == 256 || a.Cin == 512)) {

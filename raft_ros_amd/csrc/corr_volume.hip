@@ -372,6 +372,139 @@ __global__ __launch_bounds__(256, 2) void corr_volume_bf16_kernel(const CorrGemm
   }
 }
 
+// v3 (cfg 6 / 7 / 8; automatic at 1080p-sized volumes): the v2 tile with (a) BK-deep K steps,
+// BK = 32 halving the LDS ring (2 x 16 KB) so that, with the epilogue tile aliased on it, four
+// workgroups share a CU (the stores of some overlap the MFMAs of the others; v2 runs two, and
+// its store phase and MFMA phase barely overlap: 1.30 ms vs a 0.55 ms write floor + 0.28 ms of
+// MFMA at 1080p), and (b) the MFMA operands swapped (C^T blocks: a lane holds 4 consecutive
+// columns of one row), so the epilogue writes the LDS tile as 8-byte runs instead of 2-byte
+// scattered stores.  Swizzle for BK-deep rows: R = 128 / BK rows share a 256-byte bank line,
+// 16-byte chunk slot = chunk ^ ((row / R) & (BK / 8 - 1)).
+template <int BK, int OCC>
+__global__ __launch_bounds__(256, OCC) void corr_volume_v3_kernel(const CorrGemmArgs g) {
+  constexpr int CH = BK / 8, R = 128 / BK, RPI = 512 / BK;  // chunks / row, rows / bank line, rows / DMA instr
+  constexpr int STAGE = (VBM + VBN) * BK;                      // bf16 elements
+  constexpr int NI = VBM / RPI / 4;                            // DMA instructions per wave per operand
+  constexpr int LDS = 2 * STAGE > VBM * VCP ? 2 * STAGE : VBM * VCP;
+  static_assert(NI >= 1 && (CH & (CH - 1)) == 0, "tile");
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[LDS];
+  const int tilesM = (g.M + VBM - 1) / VBM, tilesN = (g.N + VBN - 1) / VBN;
+  const int per_b = tilesM * tilesN;
+  const int wg = xcd_remap(blockIdx.x, per_b * g.batch);
+  const int b = wg / per_b, t = wg - b * per_b;
+  const int GM = corr_group_rows(g.N, g.K, g.cfg);
+  const int grp = t / (GM * tilesN), first = grp * GM, gsz = min(tilesM - first, GM);
+  const int r = t - grp * GM * tilesN;
+  const int m0 = (first + r % gsz) * VBM, n0 = (r / gsz) * VBN;
+  const __bf16* A = static_cast<const __bf16*>(g.A) + (long)b * g.sA;
+  const __bf16* B = static_cast<const __bf16*>(g.B) + (long)b * g.sB;
+  const __amdgpu_buffer_rsrc_t ra = vrsrc(A, (unsigned)((long)g.M * g.lda * 2));
+  const __amdgpu_buffer_rsrc_t rb = vrsrc(B, (unsigned)((long)g.N * g.ldb * 2));
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lr = lane / CH, lc = lane % CH;
+  unsigned avoff[NI], bvoff[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int row = (wave * NI + i) * RPI + lr;
+    const int src_chunk = lc ^ ((row / R) & (CH - 1));
+    avoff[i] = m0 + row < g.M ? (unsigned)((long)(m0 + row) * g.lda * 2 + src_chunk * 16) : kVOOB;
+    bvoff[i] = n0 + row < g.N ? (unsigned)((long)(n0 + row) * g.ldb * 2 + src_chunk * 16) : kVOOB;
+  }
+  auto issue = [&](int k0, int stage) __attribute__((always_inline)) {
+    const __bf16* sA = smem + stage * STAGE;
+    const __bf16* sB = sA + VBM * BK;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) vbload16(ra, sA + (wave * NI + i) * 512, avoff[i], (unsigned)k0 * 2);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) vbload16(rb, sB + (wave * NI + i) * 512, bvoff[i], (unsigned)k0 * 2);
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  const int fr = lane & 31, fh = lane >> 5;
+  int arow[2], brow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    arow[i] = wm * 64 + i * 32 + fr;
+    brow[i] = wn * 64 + i * 32 + fr;
+  }
+  const unsigned lds0 = (unsigned)(reinterpret_cast<uintptr_t>(smem) & 0xffffffffu);
+  auto frag = [&](unsigned base, int row, int s) __attribute__((always_inline)) {
+    const int chunk = (2 * s + fh) ^ ((row / R) & (CH - 1));
+    return *(const vlds_bf16x8*)(uintptr_t)(base + (unsigned)(row * BK * 2 + chunk * 16));
+  };
+  constexpr int G = 2 * NI;  // DMA instructions per wave per stage
+  const int nk = (g.K + BK - 1) / BK;
+  issue(0, 0);
+  if (nk > 1) issue(BK, 1);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const unsigned sa = lds0 + (unsigned)((kt & 1) * STAGE * 2), sb = sa + VBM * BK * 2;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        af[i] = frag(sa, arow[i], s);
+        bfr[i] = frag(sb, brow[i], s);
+      }
+      // swapped operands: block (i, j) holds C^T, lane = column m, registers = 4-runs of n
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) issue((kt + 2) * BK, kt & 1);
+  }
+
+  // ---- epilogue: 8-byte runs into the LDS tile (aliasing the drained ring), 16-byte stores
+  __bf16* ct = smem;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int row = wm * 64 + i * 32 + fr;
+        const int col = wn * 64 + j * 32 + 8 * q4 + 4 * fh;
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = static_cast<__bf16>(g.alpha * acc[i][j][4 * q4 + e]);
+        *reinterpret_cast<bf16x4*>(ct + row * VCP + col) = v;
+      }
+  __syncthreads();
+  __bf16* C = static_cast<__bf16*>(g.C) + (long)b * g.sC;
+#pragma unroll
+  for (int i = 0; i < (VBM * VBN / 8) / 256; ++i) {
+    const int id = tid + 256 * i;
+    const int row = id >> 4, c8 = (id & 15) * 8;
+    const int m = m0 + row, n = n0 + c8;
+    if (m >= g.M || n >= g.N) continue;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(ct + row * VCP + c8);
+    __bf16* dst = C + (long)m * g.ldc + n;
+    if (n + 8 <= g.N) {
+      *reinterpret_cast<bf16x8*>(dst) = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (n + e < g.N) dst[e] = v[e];
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void pyramid_unpool_kernel(const UnpoolArgs u) {
   const long total = (long)u.B * u.H * u.W * u.C;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -912,7 +1045,14 @@ hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s) {
                   (long)g.N * g.ldb * 2 < (1L << 31) && g.cfg != 1;
   if (v2) {
     const long tiles = (long)((g.M + VBM - 1) / VBM) * ((g.N + VBN - 1) / VBN) * g.batch;
-    hipLaunchKernelGGL(corr_volume_bf16_kernel, dim3((unsigned)tiles), dim3(256), 0, s, g);
+    // v3 on request (cfg 6: BK 32 / 4 per CU, 7: the same with GM = 8, 8: BK 64 / 2 per CU)
+    if (g.cfg == 6 || g.cfg == 7) {
+      hipLaunchKernelGGL((corr_volume_v3_kernel<32, 4>), dim3((unsigned)tiles), dim3(256), 0, s, g);
+    } else if (g.cfg == 8) {
+      hipLaunchKernelGGL((corr_volume_v3_kernel<64, 2>), dim3((unsigned)tiles), dim3(256), 0, s, g);
+    } else {
+      hipLaunchKernelGGL(corr_volume_bf16_kernel, dim3((unsigned)tiles), dim3(256), 0, s, g);
+    }
     return hipGetLastError();
   }
   const dim3 grid((unsigned)(((g.M + GBM - 1) / GBM) * ((g.N + GBN - 1) / GBN) * g.batch)), blk(256);

@@ -121,6 +121,16 @@ struct ConvFwdArgs {
   // and 16-bit output is IEEE fp16 (v_mfma_f32_32x32x16_f16) instead of bf16; the pointers
   // keep their __bf16 type as 16-bit storage
   int f16;
+  // Narrow follow-up conv folded into epilogue 0 (the flow head: heads conv 3x3 + ReLU ->
+  // flow_head.conv2 3x3, 256 -> 2).  For the first n2_cols output channels, each 64-channel
+  // slot s of a tile also writes the per-tap partial products of the NEXT conv,
+  //   n2y[s][o * 9 + t][p] = sum_{c in slot s} out_bf16[p][c] * n2w[o][t * n2_cols + c],
+  // and launch_n2_apply sums the 3x3 neighbourhood (out2[p][o] = bias + sum_s sum_t
+  // n2y[s][o * 9 + t][p + off_t]; planar, so its loads coalesce): the 256-channel activation
+  // is never re-read 9 times.
+  const __bf16* n2w;  // [2][n2_kpad] packed 3x3 weights of the follow-up conv (k = tap * n2_cols + c)
+  float* n2y;         // [n2_cols / 64][18][P] fp32 partials
+  int n2_kpad, n2_cols;
 };
 
 struct ConvWgradArgs {
@@ -580,7 +590,8 @@ inline bool up_seg_ok(unsigned long addr, int esz, long sN, long sC, long sH, lo
 // Row tiles per group of the v2 volume build's tile order (cfg 2-5 force 1 / 2 / 4 / 16):
 // 8 while one image's B operand (N x K bf16) fits 8 MB, 4 beyond (the 1080p store stream).
 RAFT_HD inline int corr_group_rows(long N, long K, int cfg) {
-  if (cfg >= 2) return cfg == 2 ? 1 : cfg == 3 ? 2 : cfg == 4 ? 4 : 16;
+  if (cfg >= 2 && cfg <= 5) return cfg == 2 ? 1 : cfg == 3 ? 2 : cfg == 4 ? 4 : 16;
+  if (cfg == 7) return 8;
   return N * K * 2 <= (8L << 20) ? 8 : 4;
 }
 

@@ -118,6 +118,63 @@ __global__ __launch_bounds__(256) void apply_delta_kernel(const float* __restric
   flow_out[i1] = cy - (float)y;
 }
 
+// The flow head's conv2 (3x3, pad 1, 2 outputs) from the per-tap partials that the heads conv
+// epilogue wrote (kernel_abi.h ConvFwdArgs::n2y: planes y[s][o * 9 + t][q] over 64-channel slots s),
+// fused with apply_delta: delta[o] = bias[o] + sum_s sum_t y[s][o * 9 + t][p + off_t] (taps
+// outside the image are the conv's zero padding), then coords_out / flow_out as apply_delta;
+// delta itself is stored when requested (tests)
+__global__ __launch_bounds__(64) void n2_apply_kernel(const float* __restrict__ y, int nslot,
+                                                       const float* __restrict__ bias,
+                                                       const float* __restrict__ coords1,
+                                                       float* __restrict__ coords_out, float* __restrict__ flow_out,
+                                                       float* __restrict__ delta, long sd, int B, int H, int W) {
+  const int HW = H * W;
+  const long P = (long)B * HW;
+  const long p = (long)blockIdx.x * 64 + threadIdx.x;
+  if (p >= P) return;
+  const int b = p / HW;
+  const int s = p - (long)b * HW;
+  const int py = s / W, px = s - py * W;
+  float d0 = bias ? bias[0] : 0.f, d1 = bias ? bias[1] : 0.f;
+  // branch-free taps (clamped offset, zero weight outside the image) so every slot's 18
+  // loads are issued back to back instead of one bounds-checked branch at a time
+  long off[9];
+  float keep[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int dy = t / 3 - 1, dx = t % 3 - 1;
+    const bool in = (unsigned)(py + dy) < (unsigned)H && (unsigned)(px + dx) < (unsigned)W;
+    off[t] = in ? (long)dy * W + dx : 0;
+    keep[t] = in ? 1.f : 0.f;
+  }
+#pragma unroll
+  for (int sl = 0; sl < 4; ++sl) {
+    if (sl >= nslot) break;
+    const float* ys = y + (long)sl * 18 * P + p;
+    float v[18];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      v[t] = ys[t * P + off[t]];
+      v[9 + t] = ys[(9 + t) * P + off[t]];
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      d0 += keep[t] * v[t];
+      d1 += keep[t] * v[9 + t];
+    }
+  }
+  if (delta) {
+    delta[p * sd] = d0;
+    delta[p * sd + 1] = d1;
+  }
+  const long i0 = (long)b * 2 * HW + s, i1 = i0 + HW;
+  const float cx = coords1[i0] + d0, cy = coords1[i1] + d1;
+  coords_out[i0] = cx;
+  coords_out[i1] = cy;
+  flow_out[i0] = cx - (float)px;
+  flow_out[i1] = cy - (float)py;
+}
+
 // fp32 rows -> split-bf16 planes (kernel_abi.h ConvFwdArgs::split_g): channel c of src row p
 // (zero for C <= c < Cpad) goes to output channel n = c0 + c of a group-G split row of dst
 __global__ __launch_bounds__(256) void split_pack_kernel(const float* __restrict__ src, long ss, int C, int Cpad,
@@ -189,6 +246,17 @@ hipError_t launch_apply_delta(const float* coords1, const float* delta, long sd,
   if (!P) return hipSuccess;
   hipLaunchKernelGGL(apply_delta_kernel, grid1(P), dim3(256), 0, s, coords1, delta, sd, coords_out, flow_out, B,
                      HW, W);
+  return hipGetLastError();
+}
+
+hipError_t launch_n2_apply(const float* y, int nslot, const float* bias, const float* coords1, float* coords_out,
+                           float* flow_out, float* delta, long sd, int B, int H, int W, hipStream_t s) {
+  const long P = (long)B * H * W;
+  if (!P) return hipSuccess;
+  if (nslot > 4) return hipErrorInvalidValue;
+  // 64-thread workgroups: a 1080p frame is 32,400 pixels, 507 workgroups over 256 CUs
+  hipLaunchKernelGGL(n2_apply_kernel, dim3((unsigned)((P + 63) / 64)), dim3(64), 0, s, y, nslot, bias, coords1,
+                     coords_out, flow_out, delta, sd, B, H, W);
   return hipGetLastError();
 }
 

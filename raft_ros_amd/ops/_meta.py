@@ -206,7 +206,7 @@ def register() -> None:
 
     # mutating ops: nothing to infer
     for name in ("conv_fwd", "conv_wgrad", "conv_wgrad_params", "gru_bwd_a", "gru_bwd_b", "masked_cast",
-                 "pack_flow", "apply_delta", "corr_lookup_into", "corr_lookup_split_into", "convex_upsample_backward_into",
+                 "pack_flow", "apply_delta", "n2_apply", "corr_lookup_into", "corr_lookup_split_into", "convex_upsample_backward_into",
                  "corr_lookup_backward_", "corr_lookup_grad_rows", "corr_gemm", "local_corr_mfma", "local_corr_mfma_backward",
                  "enc_conv_wgrad", "enc_pack_multi"):
         fake(lib + name)(lambda *args, **kwargs: None)

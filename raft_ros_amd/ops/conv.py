@@ -97,7 +97,8 @@ EPI_STORE, EPI_GRAD, EPI_GRU_ZR, EPI_GRU_Q, EPI_GRU_BWD_A, EPI_GRU_BWD_B, EPI_GR
 
 def conv_fwd(srcs, wt, g, N, out, bias=None, act=0, alpha=1.0, epi=EPI_STORE, acc_c0=1 << 30, mask=None,
              h=None, z=None, out2=None, cfg: int = 0, g0=None, carry=None, out3=None, gru_cols: int = 0,
-             addsrc=None, cout=None, cmask=None, cm_c0: int = 0, cm_valid: int = 0, split=None):
+             addsrc=None, cout=None, cmask=None, cm_c0: int = 0, cm_valid: int = 0, split=None, n2w=None,
+             n2y=None):
     """``cfg`` forces a kernel variant (0 = automatic; tests and microbenchmarks only):
     1 generic, 8/9 v4 64x128/64x64, 20/21 v5 halo strip 64x128/128x128 (4 waves),
     24..26 v5 with 8 waves 256x128/128x128/128x256.
@@ -112,9 +113,14 @@ def conv_fwd(srcs, wt, g, N, out, bias=None, act=0, alpha=1.0, epi=EPI_STORE, ac
         [cm_c0, N) -> bf16 cout = g where cmask > 0 (zero past cm_valid).
 
     ``split = (G_out, G_out2, S_h, S_z)``: split-bf16 (fp32-faithful) epilogues 0 / 2 / 3, see
-    ``split_pack`` and csrc/kernel_abi.h ``ConvFwdArgs::split_g``."""
+    ``split_pack`` and csrc/kernel_abi.h ``ConvFwdArgs::split_g``.
+
+    ``n2w`` / ``n2y``: a narrow 3x3 follow-up conv (2 outputs; the flow head's conv2) folded
+    into epilogue 0: ``n2y`` (fp32 [slots, 18, P]) receives the per-tap partial products of
+    the first 64 * slots output channels, and ``n2_apply`` finishes the conv (see
+    csrc/kernel_abi.h ``ConvFwdArgs::n2y``)."""
     ops().conv_fwd(list(srcs), wt, g, N, bias, epi, act, alpha, out, acc_c0, mask, h, z, out2, cfg, g0, carry,
-                   out3, gru_cols, addsrc, cout, cmask, cm_c0, cm_valid, list(split) if split else [])
+                   out3, gru_cols, addsrc, cout, cmask, cm_c0, cm_valid, list(split) if split else [], n2w, n2y)
     return out
 
 

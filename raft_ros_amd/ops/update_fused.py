@@ -273,6 +273,9 @@ TAIL_STREAM = True  # motion-encoder backward on its own stream (see _Step.backw
 # wgrad stream as soon as their iterations' backward is done (_Run.early_weight_grads)
 WGRAD_SPLIT = int(os.environ.get("RAFT_WGRAD_SPLIT", "1"))  # 2: -1.5 % (gpurun_out r3 A/B), kept off
 HEAD_STREAM = True  # upsampler / head backward ahead of the d-net chain (see _Step.backward)
+# flow_head.conv2 folded into the heads conv's epilogue (per-tap partials) + n2_apply, instead of
+# a separate 3x3 256 -> 2 conv that re-reads the 256-channel activation 9 times
+FOLD_N2 = os.environ.get("RAFT_FOLD_N2", "1") != "0"
 # batched weight gradients on the tail stream beside the encoders' backward (see WeightToken)
 EARLY_WGRAD = os.environ.get("RAFT_EARLY_WGRAD", "1") != "0"
 # the batched weight gradients on 1 (tail) or 2 (tail + wgrad) streams
@@ -440,16 +443,26 @@ class _Step(torch.autograd.Function):
             h = hn
 
         hd = ar.take("hd", t, 512)
-        delta = torch.empty(P, 8, device=dev, dtype=torch.float32)
         coords_out = torch.empty_like(coords1)
         flow = torch.empty_like(coords1)
+        # flow_head.conv2: folded into the heads conv (its per-tap partials, 4 slots of 64
+        # channels) and finished with apply_delta by n2_apply -- or a conv of its own
+        n2 = dict(n2w=run.wf["fh2"], n2y=torch.empty(4, 18, P, device=dev, dtype=torch.float32)) if FOLD_N2 else {}
+
+        def flow_head_out():
+            if FOLD_N2:
+                k.n2_apply(n2["n2y"], run.bias["fh2"], coords1, coords_out, flow)
+            else:
+                delta = torch.empty(P, 8, device=dev, dtype=torch.float32)
+                C.conv_fwd([hd[:, :256]], run.wf["fh2"], g(3, 3), 2, delta, bias=run.bias["fh2"])
+                k.apply_delta(coords1, delta, coords_out, flow)
+
         if not up:
             # inference step whose upsampled flow nobody reads (test_mode keeps only the last):
             # the flow head alone -- the first 256 rows of the fused heads weight -- no mask
             # head, no convex upsampling
-            C.conv_fwd([h], run.wf["heads"], g(3, 3), 256, hd, bias=run.bias["heads"], act=1)
-            C.conv_fwd([hd[:, :256]], run.wf["fh2"], g(3, 3), 2, delta, bias=run.bias["fh2"])
-            k.apply_delta(coords1, delta, coords_out, flow)
+            C.conv_fwd([h], run.wf["heads"], g(3, 3), 256, hd, bias=run.bias["heads"], act=1, **n2)
+            flow_head_out()
             return _nchw(h, B, H, W), None, coords_out
         mask = ar.take("mask", t, 576)
         # the mask head (its 3x3 half of the fused heads conv, the 1x1) and the convex upsampling
@@ -458,9 +471,8 @@ class _Step(torch.autograd.Function):
         # reads the flows); the main stream keeps the flow head alone
         tail = _tail_stream(dev) if TAIL_STREAM and dev.type == "cuda" and keep_tail(run) else None
         C.conv_fwd([h], run.wf["heads"], g(3, 3), 256 if tail is not None else 512, hd, bias=run.bias["heads"],
-                   act=1)
-        C.conv_fwd([hd[:, :256]], run.wf["fh2"], g(3, 3), 2, delta, bias=run.bias["fh2"])
-        k.apply_delta(coords1, delta, coords_out, flow)
+                   act=1, **n2)
+        flow_head_out()
         if tail is not None:
             tail.wait_stream(torch.cuda.current_stream(dev))
             run.tail = tail

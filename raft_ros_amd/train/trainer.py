@@ -124,6 +124,7 @@ def train(args: Namespace, on_finish=None) -> str:
     lead = LeadLimiter(max_lead=2)  # host at most 2 steps ahead of the GPU (ops/streams.py)
     prof = maybe_profiler(getattr(args, "profile_dir", None))
     profiler = prof.__enter__()
+    clip_params = [p for p in model.parameters() if p.requires_grad]  # walked once, not per step
     for data_blob in _infinite(train_loader, set_epoch):
         injector.before_step(total_steps)
         # the step on the high-priority step stream (ops/streams.py; RAFT_HP_MAIN=0 disables)
@@ -156,7 +157,7 @@ def train(args: Namespace, on_finish=None) -> str:
                 with trace_range("grad_sync"):
                     gsync.sync()
             scaler.unscale_(optimizer)
-            gnorm = torch.nn.utils.clip_grad_norm_(model.parameters(), args.clip)
+            gnorm = torch.nn.utils.clip_grad_norm_(clip_params, args.clip)
             if use_scaler:
                 scaler.step(optimizer)  # GradScaler already skips non-finite steps
                 scaler.update()

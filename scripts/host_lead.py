@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--host_pad_ms", type=float, default=0.0, help="host sleep before each step")
     ap.add_argument("--max_lead", type=int, default=0,
                     help="> 0: before issuing step i, wait for step i - max_lead - 1 to finish on the GPU")
+    ap.add_argument("--cprofile", type=int, default=0,
+                    help="> 0: also profile the host side of this many steps (cProfile, top functions)")
     args = ap.parse_args()
     from raft_ros_amd.data.synthetic import synthetic_batch
     from raft_ros_amd.models import RAFT
@@ -100,6 +102,19 @@ def main():
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / args.steps
         m1 = torch.cuda.memory_stats(dev)
+        if args.cprofile > 0:
+            import cProfile
+            import pstats
+
+            pr = cProfile.Profile()
+            pr.enable()
+            for i in range(args.cprofile):
+                step(i, [torch.cuda.Event(enable_timing=True) for _ in range(8)])
+            pr.disable()
+            torch.cuda.synchronize()
+            st = pstats.Stats(pr)
+            st.sort_stats("tottime").print_stats(45)
+            st.sort_stats("cumulative").print_stats(45)
     keys = ("num_device_alloc", "num_device_free", "num_alloc_retries", "num_sync_all_streams", "num_ooms")
     print("caching allocator over the timed steps:", {k: m1.get(k, 0) - m0.get(k, 0) for k in keys},
           f"reserved {m0['reserved_bytes.all.current'] / 2**30:.2f} -> {m1['reserved_bytes.all.current'] / 2**30:.2f} GiB")

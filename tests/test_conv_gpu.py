@@ -403,3 +403,60 @@ def test_split_gru_stage_is_fp32_faithful(cuda):
     got = _from_pm(_split_read(hn, Hd, Hd), B, H, W)
     assert (got - ref).abs().max().item() < 5e-5, (got - ref).abs().max().item()
     assert _rel(_from_pm(_split_read(zr, Hd, 2 * Hd), B, H, W), torch.cat([z, r], 1)) < 3e-5
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 8, 9, 20, 21, 24, 25, 26, 41, 45, 59, 61, 62, 63])
+@pytest.mark.parametrize("N,B,hw", [(256, 2, (46, 62)), (512, 1, (27, 120)), (256, 1, (23, 31))])
+def test_flow_head_conv2_folded_into_heads_epilogue(cuda, cfg, N, B, hw):
+    """heads conv (3x3 128 -> N, ReLU, bf16) with flow_head.conv2 (3x3 256 -> 2) folded into
+    its epilogue as per-tap partials, finished by n2_apply (+ apply_delta), vs fp32 convs of
+    the bf16 activations -- for every forward kernel variant that can run the heads conv."""
+    from raft_ros_amd.ops._ext import ops
+
+    torch.manual_seed(7)
+    H, W = hw
+    if cfg in (41, 45) and 256 + 2 * W + 2 > {41: 479, 45: 447}[cfg]:
+        pytest.skip("v6 flat strip does not fit in LDS at this width")
+    P = B * H * W
+    x = torch.randn(P, 128, device=cuda).bfloat16()
+    w1 = torch.randn(N, 128, 3, 3, device=cuda) / (128 * 9) ** 0.5
+    b1 = torch.randn(N, device=cuda) * 0.1
+    w2 = torch.randn(2, 256, 3, 3, device=cuda) / (256 * 9) ** 0.5
+    b2 = torch.randn(2, device=cuda)
+    hd = torch.full((P, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+    y = torch.full((4, 18, P), float("nan"), device=cuda)
+    g = C.geom(B, H, W, 3, 3, 1, 1)
+    C.conv_fwd([x], C.pack_fwd(w1, [(128, 128)]), g, N, hd, bias=b1, act=1, cfg=cfg,
+               n2w=C.pack_fwd(w2, [(256, 256)]), n2y=y)
+    coords1 = torch.randn(B, 2, H, W, device=cuda) * 3
+    coords_out, flow, delta = torch.empty_like(coords1), torch.empty_like(coords1), torch.empty(P, 8, device=cuda)
+    ops().n2_apply(y, b2, coords1, coords_out, flow, delta)
+    hd_ref = F.relu(F.conv2d(_from_pm(x, B, H, W), w1.bfloat16().float(), b1, padding=1))
+    assert _rel(_from_pm(hd, B, H, W), hd_ref) < 1e-2
+    # conv2 over the kernel's own bf16 activations: only the summation order differs
+    d_ref = F.conv2d(_from_pm(hd[:, :256], B, H, W), w2.bfloat16().float(), b2, padding=1)
+    d = _from_pm(delta[:, :2], B, H, W)
+    torch.testing.assert_close(d, d_ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(coords_out, coords1 + d, rtol=0, atol=1e-5)
+    yy, xx = torch.meshgrid(torch.arange(H, device=cuda), torch.arange(W, device=cuda), indexing="ij")
+    torch.testing.assert_close(flow, coords_out - torch.stack([xx, yy]).float()[None], rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("N", [128, 64])
+@pytest.mark.parametrize("B,hw", [(8, (46, 62)), (1, (27, 120)), (2, (13, 19)), (1, (135, 240))])
+def test_convf1_direct_7x7_kernel(cuda, N, B, hw):
+    """convf1 (7x7, the 2 flow channels of flow8 -> N, ReLU) on its direct halo-tile MFMA
+    kernel (automatic choice) vs an fp32 conv2d; the pad channels 2..7 are never read."""
+    torch.manual_seed(8)
+    H, W = hw
+    P = B * H * W
+    flow8 = torch.randn(P, 8, device=cuda).mul(4).bfloat16()
+    w = torch.randn(N, 2, 7, 7, device=cuda) / 98 ** 0.5
+    bias = torch.randn(N, device=cuda)
+    out = torch.full((P, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+    C.conv_fwd([flow8], C.pack_fwd(w, [(2, 8)]), C.geom(B, H, W, 7, 7, 3, 3), N, out, bias=bias, act=1)
+    ref = F.relu(F.conv2d(_from_pm(flow8, B, H, W)[:, :2], w.bfloat16().float(), bias, padding=3))
+    assert _rel(_from_pm(out, B, H, W), ref) < 1e-2
+    out2 = torch.full((P, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+    C.conv_fwd([flow8], C.pack_fwd(w, [(2, 8)]), C.geom(B, H, W, 7, 7, 3, 3), N, out2, bias=bias, act=1, cfg=1)
+    assert _rel(out.float(), out2.float()) < 1e-2

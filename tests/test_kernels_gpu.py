@@ -39,14 +39,16 @@ def test_corr_volume_v2_matches_generic(cuda, M, N, K, batch):
     A = torch.randn(batch, M, K, device=cuda).bfloat16()
     B = torch.randn(batch, N, K, device=cuda).bfloat16()
     outs = []
-    for cfg in (0, 1):
+    cfgs = (0, 1, 6, 7, 8)  # 6 / 7 / 8: the v3 kernel (BK 32 at four per CU, GM 8, BK 64)
+    for cfg in cfgs:
         C = torch.full((batch, M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
         ops.corr_gemm(A, B, C, M, N, K, batch, K, M * K, K, N * K, N, M * N, 0.0625, False, False, 0, cfg)
         outs.append(C.float())
     want = 0.0625 * torch.matmul(A.float(), B.float().transpose(1, 2))
-    assert torch.isfinite(outs[0]).all()
-    torch.testing.assert_close(outs[0], want, rtol=1e-2, atol=1e-2)
-    assert (outs[0] - outs[1]).abs().max().item() <= 2 * want.abs().max().item() * 2 ** -8
+    for cfg, out in zip(cfgs, outs):
+        assert torch.isfinite(out).all(), cfg
+        torch.testing.assert_close(out, want, rtol=1e-2, atol=1e-2)
+        assert (out - outs[1]).abs().max().item() <= 2 * want.abs().max().item() * 2 ** -8, cfg
 
 
 def test_gemm_nt_identity_asymmetric(cuda):
