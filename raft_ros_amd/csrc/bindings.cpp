@@ -8,9 +8,12 @@
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPCachingAllocator.h>
 #include <c10/core/DeviceGuard.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cmath>
 #include <vector>
@@ -54,6 +57,7 @@ hipError_t launch_pack_flow(const float* flow, void* flow8, void* motion, long s
                             int from_coords, hipStream_t s);
 hipError_t launch_apply_delta(const float* coords1, const float* delta, long sd, float* coords_out,
                               float* flow_out, int B, int HW, int W, hipStream_t s);
+hipError_t launch_probe(int kind, hipStream_t s);
 hipError_t launch_n2_apply(const float* y, int nslot, const float* bias, const float* coords1, float* coords_out,
                            float* flow_out, float* delta, long sd, int B, int H, int W, hipStream_t s);
 hipError_t launch_convex_up_fwd(const float* flow, const void* mask, int m_dtype, long msN, long msC,
@@ -1008,11 +1012,14 @@ ConvWgradArgs wgrad_args(at::TensorList srcs, const at::Tensor& dy, at::IntArray
 // (scripts/bench_convs.py, profiles/r4_convs_wgrad_mt.log) but +0.4 % on the training step
 // (5 of 5 interleaved A/B pairs, profiles/r4_bench_wgrad_mt_ab.log): half the workgroups, so the
 // tail stream leaves more of the chip to the encoders' backward running beside it.
-// RAFT_WGRAD3_MT=1 restores 64-row workgroups.
+// RAFT_WGRAD3_MT=1: 64-row workgroups; 3: the 128-row tile on 8 waves (two per SIMD, where the
+// default 4-wave one holds 274 registers per lane, one wave per SIMD) -- measured 1.3 % slower
+// on the training step (451.1 / 451.2 vs 457.3 / 457.0 pairs/s, profiles/r5o_bench_*.json).
 int wgrad3_mt5() {
   static const int v = [] {
     const char* e = std::getenv("RAFT_WGRAD3_MT");
-    return (e && std::atoi(e) == 1) ? 1 : 2;
+    const int m = e ? std::atoi(e) : 2;
+    return (m == 1 || m == 3) ? m : 2;
   }();
   return v;
 }
@@ -1459,6 +1466,152 @@ at::Tensor instance_norm_bwd(const at::Tensor& x, const at::Tensor& dy, const at
   return dx;
 }
 
+
+// ============================================================================ step executor
+// One refinement iteration of the fused RAFT-base update (ops/update_fused.py _Step.forward,
+// reference core/raft.py:122-139 + core/update.py:79-136) issued from C++ in one op call: the
+// ~17 launches, the side-stream fork / join of the flow branch and the tail-stream mask head,
+// with the arena slot views, packed weights and stream handles handed in by the caller.  The
+// Python body it replaces spent ~0.35 ms of host time per iteration (op dispatch with ~27
+// boxed arguments per conv, views, stream context managers) -- the training forward was
+// host-bound (6.6 ms host vs 5.9 ms GPU, profiles/r5j_host_lead.log).
+namespace step_exec {
+enum Buf {
+  B_H0, B_CORR, B_FLOW8, B_MOTION, B_C1, B_CF, B_F1, B_ZR1, B_RH1, B_Q1, B_H1, B_ZR2, B_RH2, B_Q2, B_H2,
+  B_HD, B_MASK, B_N2Y, B_COORDS1, B_INP, B_COUNT
+};
+enum Layer { L_CONVC1, L_CONVC2, L_CONVF1, L_CONVF2, L_CONV, L_ZR1, L_Q1, L_ZR2, L_Q2, L_HEADS, L_FH2, L_MASK2, L_COUNT };
+constexpr int kHid = 128, kCorrPad = 328;
+
+// fork / join events: a ring per process, each record is waited on immediately after
+hipEvent_t next_event() {
+  static std::vector<hipEvent_t> ring;
+  static size_t i = 0;
+  if (ring.empty()) {
+    ring.resize(64);
+    for (auto& e : ring) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  return ring[i++ % ring.size()];
+}
+void order(hipStream_t after, hipStream_t before) {  // `after` waits for the work queued on `before`
+  if (after == before) return;
+  hipEvent_t e = next_event();
+  HIP_OK(hipEventRecord(e, before));
+  HIP_OK(hipStreamWaitEvent(after, e, 0));
+}
+}  // namespace step_exec
+
+std::vector<at::Tensor> fused_step_fwd(at::TensorList bufs, at::TensorList wf, at::TensorList bias, at::TensorList levels,
+                                       const c10::optional<at::Tensor>& corr_in, at::IntArrayRef cfg) {
+  using namespace step_exec;
+  TORCH_CHECK(bufs.size() == B_COUNT && wf.size() == L_COUNT && bias.size() == L_COUNT && cfg.size() == 9,
+              "raft_amd fused_step_fwd: bufs / weights / cfg layout");
+  const int64_t B = cfg[0], H = cfg[1], W = cfg[2], radius = cfg[3];
+  const bool up = cfg[4] != 0, fold = cfg[7] != 0;
+  const at::Tensor &h0 = bufs[B_H0], &corr = bufs[B_CORR], &flow8 = bufs[B_FLOW8], &motion = bufs[B_MOTION];
+  const at::Tensor &c1 = bufs[B_C1], &cf = bufs[B_CF], &f1 = bufs[B_F1], &hd = bufs[B_HD], &mask = bufs[B_MASK];
+  const at::Tensor &coords1 = bufs[B_COORDS1], &inp = bufs[B_INP];
+  const c10::DeviceGuard guard(coords1.device());
+  const auto dev = coords1.device().index();
+  auto main_s = c10::hip::getCurrentHIPStream();
+  const hipStream_t hm = main_s.stream();
+  const hipStream_t hs = cfg[5] ? reinterpret_cast<hipStream_t>(cfg[5]) : hm;
+  const hipStream_t ht = (cfg[6] && up) ? reinterpret_cast<hipStream_t>(cfg[6]) : nullptr;
+  auto side_s = c10::hip::getStreamFromExternal(hs, dev);
+  const c10::optional<at::Tensor> none;
+  auto geom = [&](int64_t kh, int64_t kw) { return std::vector<int64_t>{B, H, W, kh, kw, kh / 2, kw / 2}; };
+  // the plain conv launch (epilogue 0: bias + optional ReLU)
+  auto conv = [&](std::vector<at::Tensor> srcs, const at::Tensor& w, int64_t kh, int64_t kw, int64_t N,
+                  const at::Tensor& out, const at::Tensor& b, int64_t act, const c10::optional<at::Tensor>& n2w = {},
+                  const c10::optional<at::Tensor>& n2y = {}) {
+    conv_fwd(srcs, w, geom(kh, kw), N, b, 0, act, 1.0, out, 1 << 30, none, none, none, none, 0, none, none, none, 0,
+             none, none, none, 0, 0, {}, n2w, n2y);
+  };
+
+  // correlation features (+ the step's flow operand)
+  if (levels.size() > 0) {
+    corr_lookup_into(levels, coords1, radius, corr.view({B, H, W, kCorrPad}), flow8, motion.narrow(1, 126, 2));
+  } else {
+    TORCH_CHECK(corr_in.has_value(), "raft_amd fused_step_fwd: no pyramid and no correlation rows");
+    corr.copy_(corr_in->reshape({B * H * W, kCorrPad}));
+    pack_flow(coords1, flow8, motion.narrow(1, 126, 2), true);
+  }
+  // motion encoder: the flow branch on the side stream beside the correlation branch
+  order(hs, hm);
+  {
+    c10::hip::HIPStreamGuard sg(side_s);
+    conv({flow8}, wf[L_CONVF1], 7, 7, 128, f1, bias[L_CONVF1], 1);
+    conv({f1}, wf[L_CONVF2], 3, 3, 64, cf.narrow(1, 192, 64), bias[L_CONVF2], 1);
+  }
+  conv({corr}, wf[L_CONVC1], 1, 1, 256, c1, bias[L_CONVC1], 1);
+  conv({c1}, wf[L_CONVC2], 3, 3, 192, cf.narrow(1, 0, 192), bias[L_CONVC2], 1);
+  order(hm, hs);
+  conv({cf}, wf[L_CONV], 3, 3, 126, motion, bias[L_CONV], 1);
+  // SepConvGRU: 1x5 then 5x1; gates in the epilogues
+  at::Tensor h = h0;
+  const Buf zrb[2] = {B_ZR1, B_ZR2}, rhb[2] = {B_RH1, B_RH2}, qb[2] = {B_Q1, B_Q2}, hb[2] = {B_H1, B_H2};
+  const Layer zrl[2] = {L_ZR1, L_ZR2}, ql[2] = {L_Q1, L_Q2};
+  for (int st = 0; st < 2; ++st) {
+    const int64_t kh = st == 0 ? 1 : 5, kw = st == 0 ? 5 : 1;
+    const at::Tensor &zr = bufs[zrb[st]], &rh = bufs[rhb[st]], &q = bufs[qb[st]], &hn = bufs[hb[st]];
+    conv_fwd({h, inp, motion}, wf[zrl[st]], geom(kh, kw), 2 * kHid, bias[zrl[st]], 2, 0, 1.0, zr, 1 << 30, none, h,
+             none, rh, 0, none, none, none, 0, none, none, none, 0, 0, {}, none, none);
+    conv_fwd({rh, inp, motion}, wf[ql[st]], geom(kh, kw), kHid, bias[ql[st]], 3, 0, 1.0, hn, 1 << 30, none, h,
+             zr.narrow(1, 0, kHid), q, 0, none, none, none, 0, none, none, none, 0, 0, {}, none, none);
+    h = hn;
+  }
+  // flow head (+ conv2 folded into its epilogue) and the coordinate update
+  auto coords_out = at::empty_like(coords1), flow = at::empty_like(coords1);
+  const at::Tensor& n2y = bufs[B_N2Y];
+  const int64_t nh = (up && !ht) ? 512 : 256;
+  if (fold) {
+    conv({h}, wf[L_HEADS], 3, 3, nh, hd, bias[L_HEADS], 1, wf[L_FH2], n2y);
+    n2_apply(n2y, bias[L_FH2], coords1, coords_out, flow, none);
+  } else {
+    conv({h}, wf[L_HEADS], 3, 3, nh, hd, bias[L_HEADS], 1);
+    auto delta = at::empty({B * H * W, 8}, coords1.options());
+    conv({hd.narrow(1, 0, 256)}, wf[L_FH2], 3, 3, 2, delta, bias[L_FH2], 0);
+    apply_delta(coords1, delta, coords_out, flow);
+  }
+  if (!up) return {coords_out, flow};
+  // mask head + convex upsampling: they feed only the loss, so on the tail stream beside the
+  // next step (the caller joins it before the loss reads the flows)
+  at::Tensor flow_up;
+  {
+    c10::optional<c10::hip::HIPStreamGuard> tg;
+    if (ht) {
+      order(ht, hm);
+      tg.emplace(c10::hip::getStreamFromExternal(ht, dev));
+      conv({h}, wf[L_HEADS].narrow(0, 256, 256), 3, 3, 256, hd.narrow(1, 256, 256), bias[L_HEADS].narrow(0, 256, 256), 1);
+    }
+    conv({hd.narrow(1, 256, 256)}, wf[L_MASK2], 1, 1, 576, mask, bias[L_MASK2], 0);
+    flow_up = convex_upsample(flow, mask.reshape({B, H, W, 576}).permute({0, 3, 1, 2}));
+  }
+  if (ht) c10::hip::HIPCachingAllocator::recordStream(flow_up.storage().data_ptr(), main_s);
+  return {coords_out, flow, flow_up};
+}
+
+// Host cost of the runtime pieces a training step is made of (scripts/launch_probe.py): mean
+// microseconds per operation over n repetitions.  kind 0 / 1: kernel launch with an 8-byte /
+// ConvFwdArgs-sized (sizeof = kind 1's bytes) argument block; 2: an event record + a wait on
+// another stream (the fork / join of the update step); 3: at::empty of 1 MB.
+double probe_host_cost(int64_t n, int64_t kind, int64_t other_stream) {
+  const hipStream_t s = cur_stream();
+  const hipStream_t o = other_stream ? reinterpret_cast<hipStream_t>(other_stream) : s;
+  const auto opts = at::TensorOptions().device(at::kCUDA, c10::hip::current_device()).dtype(at::kFloat);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int64_t i = 0; i < n; ++i) {
+    if (kind <= 1) {
+      HIP_OK(launch_probe(static_cast<int>(kind), s));
+    } else if (kind == 2) {
+      step_exec::order(o, s);
+    } else {
+      auto t = at::empty({1 << 18}, opts);
+    }
+  }
+  const auto t1 = std::chrono::steady_clock::now();
+  return std::chrono::duration<double, std::micro>(t1 - t0).count() / std::max<int64_t>(n, 1);
+}
 }  // namespace
 }  // namespace raft_amd
 
@@ -1498,6 +1651,9 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("apply_delta(Tensor coords1, Tensor delta, Tensor(a!) coords_out, Tensor(b!) flow_out) -> ()");
   m.def("n2_apply(Tensor y, Tensor bias, Tensor coords1, Tensor(a!) coords_out, Tensor(b!) flow_out, "
         "Tensor(c!)? delta=None) -> ()");
+  m.def("launch_probe(int n, int kind, int other_stream=0) -> float", &raft_amd::probe_host_cost);  // no tensors: catch-all
+  m.def("fused_step_fwd(Tensor[] bufs, Tensor[] wf, Tensor[] bias, Tensor[] levels, Tensor? corr_in, int[] cfg) "
+        "-> Tensor[]");
   m.def(
       "corr_lookup_into(Tensor[] pyramid, Tensor coords, int radius, Tensor(a!) out, Tensor(b!)? flow8=None, "
       "Tensor(c!)? motion=None) -> ()");
@@ -1555,6 +1711,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("split_pack", &raft_amd::split_pack);
   m.impl("apply_delta", &raft_amd::apply_delta);
   m.impl("n2_apply", &raft_amd::n2_apply);
+  m.impl("fused_step_fwd", &raft_amd::fused_step_fwd);
   m.impl("corr_lookup_into", &raft_amd::corr_lookup_into);
   m.impl("convex_upsample_backward_into", &raft_amd::convex_upsample_backward_into);
   m.impl("conv_wgrad", &raft_amd::conv_wgrad);

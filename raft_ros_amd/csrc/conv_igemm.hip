@@ -1972,24 +1972,31 @@ __global__ __launch_bounds__(256) void conv_wgrad2_kernel(const ConvWgradArgs a)
 // Pixel tiles never cross an image; the (T*B, H, W) image stack is tiled, the tile list is
 // split over workgroups (XCD-grouped like v2) and each split writes its own fp32 slab.
 // Periodic sources: image i reads source image i % (period / HW).
-template <int KH, int KW, int TH, int TW>
+template <int KH, int KW, int TH, int TW, int NW = 4>
 struct WG3Geo {
   static constexpr int BH = TH + KH - 1, BW = TW + KW - 1;
-  static constexpr int ROWS = (BH * BW + 31) / 32 * 32;  // halo-block rows, a multiple of 4 waves x 8
+  static constexpr int ROWS = (BH * BW + NW * 8 - 1) / (NW * 8) * (NW * 8);  // halo-block rows, whole DMA pieces
   static constexpr int TAPS = KH * KW;
 };
 
-template <int KH, int KW, int TH, int TW, int MT, int S, bool F16 = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv_wgrad3_kernel(const ConvWgradArgs a) {
-  using G3 = WG3Geo<KH, KW, TH, TW>;
+// NW = 8 (8 waves as 4 x 2, MT = 1): the 128-channel tile of the 5-tap convs with half the
+// accumulators per wave (80 + 16 instead of 160 + 32 registers), so one workgroup per CU still
+// gives every SIMD two waves; NW = 4 with MT = 2 holds 274 registers per lane: one wave per
+// SIMD, the DMA / transposed-read latency exposed (r5 profile: 376-381 us per dispatch).
+template <int KH, int KW, int TH, int TW, int MT, int S, bool F16 = false, int NW = 4>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void conv_wgrad3_kernel(const ConvWgradArgs a) {
+  using G3 = WG3Geo<KH, KW, TH, TW, NW>;
   static_assert(TH * TW == 64, "64-pixel tiles");
   static_assert(TW % 4 == 0, "4 consecutive tile pixels share a tile row (transposed-read rows)");
-  constexpr int BM = 64 * MT;          // 2 wave rows x MT 32-row tiles
+  static_assert(NW == 4 || NW == 8, "2 wave columns x 2 or 4 wave rows");
+  constexpr int WR = NW / 2;           // wave rows
+  constexpr int BM = 32 * WR * MT;     // WR wave rows x MT 32-row tiles
   constexpr int NT = G3::TAPS;         // 32-column tiles per wave: 2 wave columns x NT = TAPS x 64
   constexpr int ACPR = BM / 8;         // dY chunks per row
   constexpr int ARPI = 64 / ACPR;      // dY rows per wave-instruction
-  constexpr int AI = 64 / (4 * ARPI);  // dY wave-instructions per wave per step
-  constexpr int SI = G3::ROWS / 32;    // halo-block wave-instructions per wave per step
+  constexpr int AI = 64 / (NW * ARPI);  // dY wave-instructions per wave per step
+  constexpr int SI = G3::ROWS / (NW * 8);  // halo-block wave-instructions per wave per step
+  static_assert(AI >= 1 && AI * NW * ARPI == 64, "dY tile DMA pieces");
   constexpr int G = AI + SI;
   constexpr int STAGE = 64 * BM + G3::ROWS * 64;  // bf16 elements
   __shared__ __attribute__((aligned(1024))) __bf16 smem[S * STAGE];
@@ -2134,7 +2141,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       bf16x8 af[MT];
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
-        const int col = wm * (BM / 2) + i * 32 + gi * 16 + 4 * pq;
+        const int col = wm * (BM / WR) + i * 32 + gi * 16 + 4 * pq;
         const int r0 = s * 16 + hh * 8 + q, r1 = r0 + 4;
         const s16x4 lo = tr_read(sA + r0 * BM + wswz<BM>(r0, col >> 3) * 8 + (col & 7));
         const s16x4 hi = tr_read(sA + r1 * BM + wswz<BM>(r1, col >> 3) * 8 + (col & 7));
@@ -2171,7 +2178,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          sdb[wn * BM + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)] = accb[i][r];
+          sdb[wn * BM + wm * (BM / WR) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)] = accb[i][r];
     }
     __syncthreads();
     if (tid < BM) a.dbslab[((long)split * nchunk + cc) * a.Npad + m0 + tid] = sdb[tid] + sdb[BM + tid];
@@ -2186,7 +2193,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int row = m0 + wm * (BM / WR) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         slab[(long)row * a.Kpad + col] = acc[i][j][r];
       }
   }
@@ -2595,10 +2602,14 @@ hipError_t conv_wgrad_dispatch(const ConvWgradArgs& a, const WgradPlan& pl, hipS
   if (pl.kind == 3) {
     if (a.KH == 3)
       hipLaunchKernelGGL((conv_wgrad3_kernel<3, 3, 8, 8, 1, 3, F16>), grid, dim3(256), 0, s, a);
+    else if (a.KH == 5 && pl.BM == 128 && a.mt5 == 3)
+      hipLaunchKernelGGL((conv_wgrad3_kernel<5, 1, 16, 4, 1, 3, F16, 8>), grid, dim3(512), 0, s, a);
     else if (a.KH == 5 && pl.BM == 128)
       hipLaunchKernelGGL((conv_wgrad3_kernel<5, 1, 16, 4, 2, 3, F16>), grid, dim3(256), 0, s, a);
     else if (a.KH == 5)
       hipLaunchKernelGGL((conv_wgrad3_kernel<5, 1, 16, 4, 1, 3, F16>), grid, dim3(256), 0, s, a);
+    else if (pl.BM == 128 && a.mt5 == 3)
+      hipLaunchKernelGGL((conv_wgrad3_kernel<1, 5, 1, 64, 1, 3, F16, 8>), grid, dim3(512), 0, s, a);
     else if (pl.BM == 128)
       hipLaunchKernelGGL((conv_wgrad3_kernel<1, 5, 1, 64, 2, 3, F16>), grid, dim3(256), 0, s, a);
     else

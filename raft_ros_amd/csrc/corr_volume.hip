@@ -1045,8 +1045,10 @@ hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s) {
                   (long)g.N * g.ldb * 2 < (1L << 31) && g.cfg != 1;
   if (v2) {
     const long tiles = (long)((g.M + VBM - 1) / VBM) * ((g.N + VBN - 1) / VBN) * g.batch;
-    // v3 on request (cfg 6: BK 32 / 4 per CU, 7: the same with GM = 8, 8: BK 64 / 2 per CU)
-    if (g.cfg == 6 || g.cfg == 7) {
+    // v3 BK 32 at four per CU by default (cfg 0 / 6; 7: GM = 8): train shape 81 -> 69-73 us,
+    // Sintel 56.5 -> 50.1 us, 1080p unchanged (1.26 ms, store-bound; profiles/r5n_bench_corr.log).
+    // cfg 8: v3 BK 64, two per CU; cfg 2-5 / 9: v2 (GM overrides / automatic)
+    if (g.cfg == 0 || g.cfg == 6 || g.cfg == 7) {
       hipLaunchKernelGGL((corr_volume_v3_kernel<32, 4>), dim3((unsigned)tiles), dim3(256), 0, s, g);
     } else if (g.cfg == 8) {
       hipLaunchKernelGGL((corr_volume_v3_kernel<64, 2>), dim3((unsigned)tiles), dim3(256), 0, s, g);

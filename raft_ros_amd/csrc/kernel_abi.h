@@ -148,7 +148,7 @@ struct ConvWgradArgs {
   int Npad;       // slab rows (N rounded up to the row tile)
   int xcd_g;      // >0: XCD-grouped split mapping with xcd_g splits per XCD (set by the launcher)
   int f16;        // fp16 operands (see ConvFwdArgs::f16)
-  int mt5;        // wgrad v3 on 1x5 / 5x1 convs: output-channel rows per workgroup / 64 (1 or 2)
+  int mt5;        // wgrad v3 on 1x5 / 5x1 convs: 1 = 64-row workgroups, 2 = 128 rows on 4 waves, 3 = 128 rows on 8 waves
 };
 
 // Plan of one weight-gradient launch (the caller sizes the slabs from it).
@@ -483,7 +483,8 @@ inline WgradPlan plan_conv_wgrad3(const ConvWgradArgs& a) {
   // wgrads 1.2-1.3x faster, 1x5/5x1 1.05-1.1x)
   // 1x5 / 5x1 (a.mt5 == 2): 128 output channels per workgroup -- twice the MFMAs per staged
   // dY tile and halo block for the 5-tap convs, whose 64-channel steps are short
-  pl.BM = (!sq && a.mt5 == 2) ? 128 : 64;
+  // (a.mt5 == 3: the 128-row tile on 8 waves, one 96 KB workgroup per CU: one round of 256)
+  pl.BM = (!sq && a.mt5 >= 2) ? 128 : 64;
   pl.BN = 64 * a.KH * a.KW;
   pl.tilesM = (a.N + pl.BM - 1) / pl.BM;
   pl.tilesN = a.Cin / 64;
@@ -491,7 +492,7 @@ inline WgradPlan plan_conv_wgrad3(const ConvWgradArgs& a) {
   const int TH = sq ? 8 : (a.KH == 5 ? 16 : 1), TW = 64 / TH;
   const long ntiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
   long splits, g;
-  choose_splits((long)pl.tilesM * pl.tilesN, ntiles, splits, g, 512);
+  choose_splits((long)pl.tilesM * pl.tilesN, ntiles, splits, g, (!sq && a.mt5 == 3) ? 256 : 512);
   long per = (ntiles + splits - 1) / splits;
   if ((ntiles + per - 1) / per != splits) g = 0;
   pl.nsplit = (int)((ntiles + per - 1) / per);

@@ -194,7 +194,26 @@ __global__ __launch_bounds__(256) void split_pack_kernel(const float* __restrict
 
 inline dim3 grid1(long n) { return dim3((unsigned)((n + 255) / 256)); }
 
+// host-overhead probes (scripts/launch_probe.py): empty kernels with an 8-byte and a
+// ConvFwdArgs-sized argument block
+__global__ void probe_small_kernel(int* p) {
+  if (p != nullptr && threadIdx.x == 1024) p[0] = 1;  // never true: an empty body the compiler keeps
+}
+__global__ void probe_big_kernel(const ConvFwdArgs a) {
+  if (a.out != nullptr && threadIdx.x == 1024) static_cast<int*>(a.out)[0] = 1;
+}
+
 }  // namespace
+
+hipError_t launch_probe(int kind, hipStream_t s) {
+  if (kind == 0) {
+    hipLaunchKernelGGL(probe_small_kernel, dim3(1), dim3(64), 0, s, nullptr);
+  } else {
+    ConvFwdArgs a{};
+    hipLaunchKernelGGL(probe_big_kernel, dim3(1), dim3(64), 0, s, a);
+  }
+  return hipGetLastError();
+}
 
 hipError_t launch_split_pack(const float* src, long ss, int C, int Cpad, void* dst, long sd, int G, int c0, long P,
                              hipStream_t s) {

@@ -134,6 +134,7 @@ class _Run:
         self.wd: Dict[str, Optional[torch.Tensor]] = {}
         self.bias: Dict[str, torch.Tensor] = {}
         self.cout: Dict[str, int] = {}
+        self.n2y: Optional[torch.Tensor] = None  # folded flow-head partials (native step), per run
         # every layer's operands in one launch
         mods_of = [(name, mods(block)) for name, mods, _, _, _ in _LAYERS]
         packed = C.pack_weights_multi([([m.weight for m in ms], [m.bias for m in ms], segs, scale, dgrad)
@@ -276,6 +277,10 @@ HEAD_STREAM = True  # upsampler / head backward ahead of the d-net chain (see _S
 # flow_head.conv2 folded into the heads conv's epilogue (per-tap partials) + n2_apply, instead of
 # a separate 3x3 256 -> 2 conv that re-reads the 256-channel activation 9 times
 FOLD_N2 = os.environ.get("RAFT_FOLD_N2", "1") != "0"
+# the step's forward issued by one native op (csrc/bindings.cpp fused_step_fwd) instead of ~17
+# Python-side op calls; RAFT_NATIVE_STEP=0 keeps the Python body (A/B, and the reference for the
+# native path's tests)
+NATIVE_STEP = os.environ.get("RAFT_NATIVE_STEP", "1") != "0"
 # batched weight gradients on the tail stream beside the encoders' backward (see WeightToken)
 EARLY_WGRAD = os.environ.get("RAFT_EARLY_WGRAD", "1") != "0"
 # the batched weight gradients on 1 (tail) or 2 (tail + wgrad) streams
@@ -404,6 +409,8 @@ class _Step(torch.autograd.Function):
         net_pm = _pm(net)
         if net_pm.data_ptr() != h0.data_ptr():
             h0.copy_(net_pm)
+        if NATIVE_STEP and dev.type == "cuda":
+            return _Step._native_forward(ctx, run, t, up, h0, coords1, corr_in, net.dtype)
         # correlation features
         corr = ar.take("corr", t, CORR_PAD)
         flow8 = ar.take("flow8", t, 8)
@@ -494,6 +501,45 @@ class _Step(torch.autograd.Function):
         # no zero fills for the gradients that never arrive (coords_out; the last step's net)
         ctx.set_materialize_grads(False)
         return _nchw(h, B, H, W), flow_up, coords_out
+
+    @staticmethod
+    def _native_forward(ctx, run, t, up, h0, coords1, corr_in, net_dtype):
+        """The forward above as one native op call (csrc/bindings.cpp fused_step_fwd): the same
+        launches, streams and arena slots, issued from C++."""
+        B, H, W = run.dims
+        ar = run.arena
+        take = ar.take
+        dev = h0.device
+        if run.n2y is None:
+            run.n2y = torch.empty(4, 18, run.P, device=dev, dtype=torch.float32)
+            run.wf_list = [run.wf[name] for name, _, _, _, _ in _LAYERS]
+            run.bias_list = [run.bias[name] for name, _, _, _, _ in _LAYERS]
+            run.none16 = torch.empty(0, device=dev, dtype=run.dt16)
+        h_out = take("h", t + 1, HID, slots=run.iters + 1)
+        bufs = [h0, take("corr", t, CORR_PAD), take("flow8", t, 8), take("motion", t, HID), take("c1", t, 256),
+                take("cf", t, 256), take("f1", t, 128), take("zr1", t, 2 * HID), take("rh1", t, HID),
+                take("q1", t, HID), take("h1", t, HID), take("zr2", t, 2 * HID), take("rh2", t, HID),
+                take("q2", t, HID), h_out, take("hd", t, 512), take("mask", t, 576) if up else run.none16, run.n2y,
+                coords1, run.inp_bf]
+        tail = _tail_stream(dev) if TAIL_STREAM and up and keep_tail(run) else None
+        cfg = [B, H, W, run.pyr.radius if run.pyr is not None else 0, int(up),
+               _side_stream(dev).cuda_stream if CONCURRENT else 0, tail.cuda_stream if tail is not None else 0,
+               int(FOLD_N2), 0]
+        res = ops().fused_step_fwd(bufs, run.wf_list, run.bias_list, run.pyr.levels if run.pyr is not None else [],
+                                   corr_in if run.pyr is None else None, cfg)
+        coords_out, flow = res[0], res[1]
+        if not up:
+            return _nchw(h_out, B, H, W), None, coords_out
+        if tail is not None:
+            run.tail = tail
+        ctx.run, ctx.t = run, t
+        ctx.net_dtype = net_dtype
+        ctx.has_corr_in = corr_in is not None
+        run.coords[t] = coords1
+        run.flows[t] = flow
+        ctx.mark_non_differentiable(coords_out)
+        ctx.set_materialize_grads(False)
+        return _nchw(h_out, B, H, W), res[2], coords_out
 
     @staticmethod
     def backward(ctx, g_net, g_flow_up, _g_coords):

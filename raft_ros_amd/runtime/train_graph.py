@@ -27,10 +27,20 @@ that the next replay overwrites.
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
+
+# one process: the gradients are the tensors the captured backward allocates (autograd steals
+# them: no accumulate kernels -- a pre-bound flat buffer costs one add kernel per parameter,
+# ~0.5 ms/step at config #2); RAFT_GRAPH_FLAT=1 binds the flat buffer anyway (A/B)
+_FLAT_1 = os.environ.get("RAFT_GRAPH_FLAT", "0") == "1"
+# RAFT_GRAPH_HP=1: capture and replay on the high-priority step stream (ops/streams.py
+# step_stream), as the eager step runs.  Off: it made the replay much slower on MI355X
+# (284-292 vs 402 pairs/s default-priority, profiles/r5n_bench_graph*.json)
+_GRAPH_HP = os.environ.get("RAFT_GRAPH_HP", "0") == "1"
 
 
 class GraphedTrainStep:
@@ -73,8 +83,18 @@ class GraphedTrainStep:
             p.grad = self.flat.as_strided(p.shape, p.stride(), o)
             o += n
 
+    def _use_flat(self) -> bool:
+        return self.world > 1 or _FLAT_1 or not self.params[0].is_cuda
+
+    def _grads(self) -> List[torch.Tensor]:
+        return [p.grad for p in self.params if p.grad is not None]
+
     def _fwd_bwd(self, image1, image2, flow, valid):
-        self.flat.zero_()
+        if self.flat is not None:
+            self.flat.zero_()
+        else:
+            for p in self.params:  # the backward allocates (in the graph's pool when captured)
+                p.grad = None
         preds = self.model(image1, image2, iters=self.iters)
         loss, metrics = self.loss_fn(preds, flow, valid, self.gamma)
         loss.backward()
@@ -83,9 +103,15 @@ class GraphedTrainStep:
     def _update(self):
         if self.world > 1:
             self.flat.div_(self.world)
-        norm = torch.linalg.vector_norm(self.flat)
-        coef = (self.clip / (norm + 1e-6)).clamp(max=1.0)
-        self.flat.mul_(coef)
+        if self.flat is not None:
+            norm = torch.linalg.vector_norm(self.flat)
+            coef = (self.clip / (norm + 1e-6)).clamp(max=1.0)
+            self.flat.mul_(coef)
+        else:
+            grads = self._grads()
+            norm = torch.linalg.vector_norm(torch.stack(torch._foreach_norm(grads)))
+            coef = (self.clip / (norm + 1e-6)).clamp(max=1.0)
+            torch._foreach_mul_(grads, coef)
         # failure guard without a host sync: a non-finite norm makes fused AdamW a no-op
         bad = (~torch.isfinite(norm)).float()
         self.skipped.add_(bad)
@@ -134,10 +160,16 @@ class GraphedTrainStep:
     def _capture(self, batch):
         dev = self.params[0].device
         self.static_in = [t.detach().clone() for t in batch]
-        self._bind_flat_grads()
+        if self._use_flat():
+            self._bind_flat_grads()
         self.skipped = torch.zeros((), device=dev)
         snap = self._snapshot()
-        side = torch.cuda.Stream(device=dev)
+        if _GRAPH_HP:
+            from ..ops.streams import step_stream
+
+            side = step_stream(dev)
+        else:
+            side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for _ in range(self.warmup):  # lazy init, MIOpen find, allocator warm-up
@@ -166,8 +198,9 @@ class GraphedTrainStep:
         """One optimizer step; returns (loss, metrics, grad_norm) device tensors."""
         batch = (image1, image2, flow, valid)
         if not (self.enabled and image1.is_cuda):
-            if self.flat is None:
-                self._bind_flat_grads()
+            if self.skipped is None:
+                if self._use_flat():
+                    self._bind_flat_grads()
                 self.skipped = torch.zeros((), device=image1.device)
             return self._eager(*batch)
         if self.static_in is None:
@@ -176,8 +209,21 @@ class GraphedTrainStep:
             for s, t in zip(self.static_in, batch):
                 if s.data_ptr() != t.data_ptr():
                     s.copy_(t, non_blocking=True)
+        if _GRAPH_HP:
+            from ..ops.streams import step_stream
+
+            cur = torch.cuda.current_stream(image1.device)
+            hp = step_stream(image1.device)
+            hp.wait_stream(cur)
+            with torch.cuda.stream(hp):
+                self._replay()
+            cur.wait_stream(hp)
+        else:
+            self._replay()
+        return self.out
+
+    def _replay(self):
         self.graphs[0].replay()
         if self.world > 1:
             self._allreduce()
             self.graphs[1].replay()
-        return self.out

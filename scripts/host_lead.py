@@ -106,6 +106,9 @@ def main():
             import cProfile
             import pstats
 
+            # the backward's Python (autograd Functions) runs on the engine's device thread,
+            # which cProfile does not see: run it on this thread for the profiled steps
+            torch.autograd.set_multithreading_enabled(False)
             pr = cProfile.Profile()
             pr.enable()
             for i in range(args.cprofile):

@@ -65,3 +65,36 @@ def test_fused_path_matches_fp32_module(cuda, small, shape):
         if err > 1.5 * floor + 0.02 * ref_norm:
             bad[n] = (err / ref_norm, floor / ref_norm)
     assert not bad, bad
+
+
+@pytest.mark.parametrize("alt", [False, True], ids=["dense", "alternate_corr"])
+def test_native_step_executor_matches_python_body(cuda, monkeypatch, alt):
+    """fused_step_fwd (the step's launches issued from C++) vs the Python body of
+    _Step.forward: the same kernels on the same operands, so the predictions are bitwise equal
+    (training, with the tail stream) and so are the inference outputs (test_mode: the steps
+    without upsampling); the gradients agree up to the backward's atomics."""
+    from raft_ros_amd.data.synthetic import synthetic_batch
+    from raft_ros_amd.ops import update_fused as uf
+
+    torch.manual_seed(0)
+    m = RAFT(Namespace(small=False, mixed_precision=True, amp_dtype="bf16", alternate_corr=alt)).to(cuda).train()
+    m.freeze_bn()
+    batch = synthetic_batch(2, 128, 192, max_disp=6, seed=3, device=cuda)
+    outs = {}
+    for native in (False, True):
+        monkeypatch.setattr(uf, "NATIVE_STEP", native)
+        preds, grads = _run(m, batch, 4)
+        m.eval()
+        with torch.no_grad():
+            lo, up = m(batch[0], batch[1], iters=5, test_mode=True)
+        m.train()
+        m.freeze_bn()
+        outs[native] = (preds, grads, lo, up)
+    (p0, g0, lo0, up0), (p1, g1, lo1, up1) = outs[False], outs[True]
+    for a, b in zip(p0, p1):
+        assert torch.equal(a, b)
+    assert torch.equal(lo0, lo1) and torch.equal(up0, up1)
+    assert set(g0) == set(g1)
+    tol = 1e-2 if alt else 1e-3  # the local-correlation backward accumulates with atomics
+    for n in g0:
+        assert _rel(g1[n], g0[n]) < tol, n
