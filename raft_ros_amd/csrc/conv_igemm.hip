@@ -2296,6 +2296,110 @@ __global__ __launch_bounds__(256) void conv_flow7_kernel(const ConvFwdArgs a) {
   }
 }
 
+// ============================================================================ narrow input (Cin = 8)
+// flow_head.conv2's data gradient (3x3, the 2 flow gradients in an 8-channel row -> 256,
+// ReLU'-masked by the heads activation) has K = 72: on the GEMM tiles every 64-wide K step
+// re-derives its im2col taps (53 us in-step at config #2 for 0.8 GFLOP, on the critical path
+// of the step's backward).  With 8 channels per tap, an MFMA K block of 16 is exactly two taps,
+// so a lane's A fragment (8 consecutive k) is ONE 16-byte source row: the 64-pixel tile's halo
+// (6 x 18 rows) is staged in LDS and fragment (tap, pixel) is a single ds_read_b128; B
+// fragments are 16-byte weight-row loads (k contiguous).  Operands swapped (C^T blocks) so a
+// lane holds 4 consecutive output channels of one pixel: 8-byte masked stores.
+template <bool F16>
+__global__ __launch_bounds__(256) void conv_cin8_dgrad_kernel(const ConvFwdArgs a) {
+  constexpr int TH = 4, TW = 16, HH = TH + 2, HWD = TW + 2;
+  __shared__ __attribute__((aligned(16))) bf16x8 halo[HH * HWD + 1];  // + a zero row (tap 9)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, W = a.W;
+  const int tw = (W + TW - 1) / TW, th = (H + TH - 1) / TH;
+  const int nb_tiles = (a.N + 255) / 256;
+  int bid = blockIdx.x;
+  const int ntile = bid % nb_tiles;
+  bid /= nb_tiles;
+  const int b = bid / (tw * th);
+  bid -= b * tw * th;
+  const int y0 = (bid / tw) * TH, x0 = (bid - (bid / tw) * tw) * TW;
+  const long pbase = (long)b * H * W;
+  const long sst = a.src[0].stride;
+  for (int i = tid; i < HH * HWD + 1; i += 256) {
+    const int hy = i / HWD, hx = i - (i / HWD) * HWD;
+    const int y = y0 + hy - a.PH, x = x0 + hx - a.PW;
+    bf16x8 v{};
+    if (i < HH * HWD && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
+      v = *reinterpret_cast<const bf16x8*>(a.src[0].ptr + (pbase + (long)y * W + x) * sst);
+    halo[i] = v;
+  }
+  const int fr = lane & 31, fh = lane >> 5;
+  const int n0 = ntile * 256 + wave * 64;  // this wave's 64 output channels (2 blocks of 32)
+  // B fragments (become the MFMA's A operand: rows = output channels): weight row n, k = kb * 16
+  // + fh * 8 .. + 8 = tap 2 kb + fh, all 8 channels (taps >= 9 are zero)
+  bf16x8 wf[2][5];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + j * 32 + fr;
+#pragma unroll
+    for (int kb = 0; kb < 5; ++kb) {
+      const int tap = 2 * kb + fh;
+      wf[j][kb] = (n < a.N && tap < 9) ? *reinterpret_cast<const bf16x8*>(a.wt + (long)n * a.Kpad + tap * 8) : bf16x8{};
+    }
+  }
+  __syncthreads();
+  f32x16 acc[2][2];  // [pixel block][channel block]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = i * 32 + fr;  // tile pixel
+    const int ty = m / TW, tx = m - (m / TW) * TW;
+#pragma unroll
+    for (int kb = 0; kb < 5; ++kb) {
+      const int tap = 2 * kb + fh;
+      const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+      const bf16x8 xa = halo[tap < 9 ? (ty + ky) * HWD + tx + kx : HH * HWD];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mma16<F16>(wf[j][kb], xa, acc[i][j]);
+    }
+  }
+  // lane: pixel m = i * 32 + fr, channels n0 + j * 32 + 8 g + 4 fh .. + 4 (registers 4 g .. 4 g + 3)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = i * 32 + fr;
+    const int y = y0 + m / TW, x = x0 + m % TW;
+    if (y >= H || x >= W) continue;
+    const long p = pbase + (long)y * W + x;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + j * 32 + 8 * g + 4 * fh;
+        if (n >= a.N) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * g + e] * a.alpha;
+        if (a.mask) {
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          const bf16x4 mk = *reinterpret_cast<const bf16x4*>(a.mask + p * a.mask_stride + n);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (!(ld16(mk[e], F16) > 0.f)) v[e] = 0.f;
+        }
+        if (a.out_f32) {
+          *reinterpret_cast<f32x4*>(static_cast<float*>(a.out) + p * a.out_stride + n) = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          bf16x4 w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = st16(v[e], F16);
+          *reinterpret_cast<bf16x4*>(static_cast<__bf16*>(a.out) + p * a.out_stride + n) = w;
+        }
+      }
+  }
+}
+
 // ============================================================================ narrow output (N <= 2)
 // flow_head.conv2 (3x3, 256 -> 2) is a pair of 2,304-long dot products per pixel: a
 // bandwidth problem, not a GEMM (a 64-wide MFMA tile would be 97% padding).  LPP lanes
@@ -2464,6 +2568,19 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
     const long tiles = (long)a.B * ((a.H + 7) / 8) * ((a.W + 15) / 16);
     if (a.N == 128) hipLaunchKernelGGL((conv_flow7_kernel<128, F16>), dim3((unsigned)tiles), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((conv_flow7_kernel<64, F16>), dim3((unsigned)tiles), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
+  static const bool use_cin8 = [] {  // RAFT_CIN8=0: the GEMM tiles (A/B runs)
+    const char* e = std::getenv("RAFT_CIN8");
+    return !(e && e[0] == '0');
+  }();
+  if ((cfg == 69 || (cfg == 0 && use_cin8)) && a.KH == 3 && a.KW == 3 && a.nsrc == 1 && a.Cin == 8 &&
+      a.src[0].C == 8 && a.epi == 1 && a.acc_c0 >= a.N && a.split_g == 0 && a.N % 8 == 0 && a.Kpad >= 72 &&
+      a.PH == 1 && a.PW == 1 && a.src[0].stride % 8 == 0 && a.out_stride % 4 == 0 &&
+      (a.mask == nullptr || a.mask_stride % 4 == 0) && a.P < (1L << 31)) {
+    // narrow input (flow_head.conv2's data gradient): one-tap-pair MFMA K blocks from an LDS halo
+    const long tiles = (long)a.B * ((a.H + 3) / 4) * ((a.W + 15) / 16) * ((a.N + 255) / 256);
+    hipLaunchKernelGGL((conv_cin8_dgrad_kernel<F16>), dim3((unsigned)tiles), dim3(256), 0, s, a);
     return hipGetLastError();
   }
   if (cfg == 0 && a.N <= 2 && a.epi == 0 && a.nsrc == 1 && a.KH * a.KW <= 9 && a.src[0].C == a.Cin &&

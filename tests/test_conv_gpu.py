@@ -460,3 +460,26 @@ def test_convf1_direct_7x7_kernel(cuda, N, B, hw):
     out2 = torch.full((P, N), float("nan"), device=cuda, dtype=torch.bfloat16)
     C.conv_fwd([flow8], C.pack_fwd(w, [(2, 8)]), C.geom(B, H, W, 7, 7, 3, 3), N, out2, bias=bias, act=1, cfg=1)
     assert _rel(out.float(), out2.float()) < 1e-2
+
+
+@pytest.mark.parametrize("N,B,hw", [(256, 8, (46, 62)), (128, 2, (13, 19)), (256, 1, (27, 120))])
+def test_cin8_dgrad_direct_kernel(cuda, N, B, hw):
+    """The flow head's conv2 data gradient (3x3, an 8-channel gradient row -> N, ReLU' mask,
+    EPI_GRAD) on its direct kernel (automatic choice) vs the generic GEMM kernel (cfg 1) and
+    an fp32 conv2d of the flipped weights."""
+    torch.manual_seed(9)
+    H, W = hw
+    P = B * H * W
+    dy = torch.randn(P, 8, device=cuda).bfloat16()
+    w = torch.randn(8, N, 3, 3, device=cuda) / 72 ** 0.5  # forward conv N -> 8: dgrad maps 8 -> N
+    mask = torch.randn(P, N, device=cuda).bfloat16()
+    wd = C.pack_dgrad(w, [(N, N)])
+    outs = []
+    for cfg in (0, 1):
+        out = torch.full((P, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+        C.conv_fwd([dy], wd, C.geom(B, H, W, 3, 3, 1, 1), N, out, epi=C.EPI_GRAD, mask=mask, cfg=cfg)
+        outs.append(_from_pm(out, B, H, W))
+    ref = F.conv_transpose2d(_from_pm(dy, B, H, W), w.bfloat16().float(), padding=1)
+    ref = ref * (_from_pm(mask, B, H, W) > 0)
+    assert _rel(outs[0], ref) < 1e-2
+    assert _rel(outs[0], outs[1]) < 1e-2
