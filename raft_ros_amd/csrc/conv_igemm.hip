@@ -1362,6 +1362,14 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   constexpr int HWD = TW + KW - 1;                  // 2-D halo block pitch (pixels)
   constexpr int HROWS = (TH + KH - 1) * HWD;        // 2-D halo block pixels
   constexpr int SPW2 = (HROWS + 8 * NW - 1) / (8 * NW);  // its DMA pieces per wave
+  // LDS chunk swizzle of halo row r: (r >> 1) & 7 keeps a 16-lane ds_read_b128 group on 16
+  // distinct slots when its rows are consecutive, but a 3x3 tap on 16-wide tiles reads two tile
+  // rows 18 halo rows apart, and the row-parity / (r >> 1) pairs then collide (2-way on every
+  // group: 1.21 conflict cycles per LDS instruction, profiles/r5q_pmc_summary.txt).  Keyed on
+  // the halo COLUMN instead ((r % HWD) >> 1) those groups are conflict-free (the 1x5 / 5x1
+  // halo shapes keep the row key, conflict-free there).
+  constexpr bool COLSW = TW >= 16 && KW == 3;
+  auto fsw = [](int r) { return COLSW ? (((r % HWD) >> 1) & 7) : ((r >> 1) & 7); };
   static_assert(TW == 0 || (BM % TW == 0 && TW % 8 == 0 && SPW2 * 8 * NW <= CF::MAX_ROWS), "2-D tile");
   const int tilesN = (Nn + BN - 1) / BN;
   int tilesM;
@@ -1399,7 +1407,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
 #pragma unroll
       for (int tap = 0; tap < NT; ++tap) {
         const int row = (frow / TW + tap / KW) * HWD + frow % TW + tap % KW;
-        abase[tap][i] = lds0 + RING + (unsigned)row * 128u + ((((row >> 1) & 7) ^ fh) << 4);
+        abase[tap][i] = lds0 + RING + (unsigned)row * 128u + (((unsigned)fsw(row) ^ fh) << 4);
       }
       continue;
     }
@@ -1440,10 +1448,12 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   const int pstrip = m0 - halo_lo + wave * 8 + lrow;  // pixel of this lane's row in piece 0
   // 2-D: image pixel of this lane's halo row in each of its pieces (-1: outside the image)
   int spix[TW > 0 ? SPW2 : 1];
+  unsigned sswq[TW > 0 ? SPW2 : 1];  // 2-D: source chunk offset of this lane's row in each piece
   if constexpr (TW > 0) {
 #pragma unroll
     for (int q = 0; q < SPW2; ++q) {
       const int r = (wave + q * NW) * 8 + lrow;
+      sswq[q] = (unsigned)((lpc ^ fsw(r)) * 16);
       const int y = t2.y0 - PH + r / HWD, x = t2.x0 - PW + r % HWD;
       spix[q] = (r < HROWS && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) ? (int)t2.pbase + y * W + x
                                                                                      : -1;
@@ -1470,7 +1480,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
       if constexpr (TW > 0) {
 #pragma unroll
         for (int q = 0; q < SPW2; ++q) {
-          const unsigned voff = spix[q] >= 0 ? (unsigned)spix[q] * st + sswz : kOOB;
+          const unsigned voff = spix[q] >= 0 ? (unsigned)spix[q] * st + sswq[q] : kOOB;
           bload16(rs, reinterpret_cast<__bf16*>(sbuf + q * NW * 1024), voff, soff);
         }
       } else {
