@@ -1368,8 +1368,8 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   // group: 1.21 conflict cycles per LDS instruction, profiles/r5q_pmc_summary.txt).  Keyed on
   // the halo COLUMN instead ((r % HWD) >> 1) those groups are conflict-free (the 1x5 / 5x1
   // halo shapes keep the row key, conflict-free there).
-  constexpr bool COLSW = TW >= 16 && KW == 3;
-  auto fsw = [](int r) { return COLSW ? (((r % HWD) >> 1) & 7) : ((r >> 1) & 7); };
+  const bool colsw = TW >= 16 && KW == 3 && a.swz_col != 0;
+  auto fsw = [&](int r) { return colsw ? (((r % HWD) >> 1) & 7) : ((r >> 1) & 7); };
   static_assert(TW == 0 || (BM % TW == 0 && TW % 8 == 0 && SPW2 * 8 * NW <= CF::MAX_ROWS), "2-D tile");
   const int tilesN = (Nn + BN - 1) / BN;
   int tilesM;
@@ -2719,7 +2719,13 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s) {
+hipError_t launch_conv_fwd(const ConvFwdArgs& a_in, hipStream_t s) {
+  static const int swz_col = [] {  // RAFT_SWZ_COL=0: the row-keyed swizzle everywhere (A/B runs)
+    const char* e = std::getenv("RAFT_SWZ_COL");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  ConvFwdArgs a = a_in;
+  a.swz_col = swz_col;
   return a.f16 ? conv_fwd_dispatch<true>(a, s) : conv_fwd_dispatch<false>(a, s);
 }
 

@@ -1048,7 +1048,11 @@ hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s) {
     // v3 BK 32 at four per CU by default (cfg 0 / 6; 7: GM = 8): train shape 81 -> 69-73 us,
     // Sintel 56.5 -> 50.1 us, 1080p unchanged (1.26 ms, store-bound; profiles/r5n_bench_corr.log).
     // cfg 8: v3 BK 64, two per CU; cfg 2-5 / 9: v2 (GM overrides / automatic)
-    if (g.cfg == 0 || g.cfg == 6 || g.cfg == 7) {
+    static const bool v3 = [] {  // RAFT_CORR_V3=0: v2 for the automatic choice (A/B runs)
+      const char* e = std::getenv("RAFT_CORR_V3");
+      return !(e && e[0] == '0');
+    }();
+    if ((g.cfg == 0 && v3) || g.cfg == 6 || g.cfg == 7) {
       hipLaunchKernelGGL((corr_volume_v3_kernel<32, 4>), dim3((unsigned)tiles), dim3(256), 0, s, g);
     } else if (g.cfg == 8) {
       hipLaunchKernelGGL((corr_volume_v3_kernel<64, 2>), dim3((unsigned)tiles), dim3(256), 0, s, g);

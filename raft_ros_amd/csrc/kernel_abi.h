@@ -131,6 +131,7 @@ struct ConvFwdArgs {
   const __bf16* n2w;  // [2][n2_kpad] packed 3x3 weights of the follow-up conv (k = tap * n2_cols + c)
   float* n2y;         // [n2_cols / 64][18][P] fp32 partials
   int n2_kpad, n2_cols;
+  int swz_col;  // conv_fwd6 3x3 2-D tiles: LDS chunk swizzle keyed on the halo column (set by the launcher)
 };
 
 struct ConvWgradArgs {

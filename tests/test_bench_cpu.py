@@ -41,3 +41,28 @@ def test_bench_single_process_default():
     r = _bench()
     assert r["n_gpus"] == 1 and r["allreduce_ms"] == 0.0
     assert r["steps"] == 1 and r["warmup"] == 0
+
+
+@pytest.mark.timeout(600)
+def test_bench_under_torchrun_driver_launch():
+    """The driver's multi-GPU launch: python -m torch.distributed.run --nnodes=1
+    --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N (here gloo on
+    the CPU, N = 2): one JSON line from rank 0 with the world size and the global batch."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+           "--small", "--image_size", "128", "128", "--batch", "1", "--steps", "1", "--warmup", "0", "--iters", "2"]
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        e.pop(k, None)
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=500, cwd=ROOT, env=e)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 2
+    assert r["scaling"] == "weak" and r["allreduce_ms"] > 0
