@@ -67,6 +67,7 @@ class _PyramidState:
         self.dlevels: Optional[List[torch.Tensor]] = None
         self.sizes = []                        # (Hl, Wl, off) per level
         self.tail = None                       # stream of fused-step lookup backwards (to join)
+        self.tail_event = None                 # or the point of it to join (work queued after it is not ours)
         self.ld = 0
         self.shape = None
         self.pending: List[tuple] = []         # deferred (coords, window gradient) of each lookup
@@ -195,7 +196,12 @@ class _BuildPyramid(torch.autograd.Function):
         fmap1, fmap2 = ctx.saved_tensors
         tail = getattr(state, "tail", None)
         if tail is not None:  # lookups' backward ran on the fused step's tail stream
-            torch.cuda.current_stream().wait_stream(tail)
+            ev = getattr(state, "tail_event", None)
+            if ev is not None:  # only up to the work queued before the batched weight gradients
+                torch.cuda.current_stream().wait_event(ev)
+                state.tail_event = None
+            else:
+                torch.cuda.current_stream().wait_stream(tail)
             state.tail = None
             if state.dbuf is not None:
                 state.dbuf.record_stream(tail)

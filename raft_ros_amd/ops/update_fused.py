@@ -135,6 +135,7 @@ class _Run:
         self.bias: Dict[str, torch.Tensor] = {}
         self.cout: Dict[str, int] = {}
         self.n2y: Optional[torch.Tensor] = None  # folded flow-head partials (native step), per run
+        self.wg_final: Optional[List[torch.Tensor]] = None  # weight gradients issued at the loop's end
         # every layer's operands in one launch
         mods_of = [(name, mods(block)) for name, mods, _, _, _ in _LAYERS]
         packed = C.pack_weights_multi([([m.weight for m in ms], [m.bias for m in ms], segs, scale, dgrad)
@@ -285,6 +286,13 @@ NATIVE_STEP = os.environ.get("RAFT_NATIVE_STEP", "1") != "0"
 EARLY_WGRAD = os.environ.get("RAFT_EARLY_WGRAD", "1") != "0"
 # the batched weight gradients on 1 (tail) or 2 (tail + wgrad) streams
 WGRAD_STREAMS = int(os.environ.get("RAFT_WGRAD_STREAMS", "1"))
+# RAFT_WGRAD_AT_LOOP_END=1: the batched weight gradients issued by the last refinement step's
+# backward (before the host issues the pyramid / encoder backward) instead of by the weight
+# token's backward after it.  They then overlap the encoder backward instead of running after
+# it alone (profiles/r5w_phases.txt vs r5x_phases.txt), but every kernel runs slower beside the
+# other stream's and the step time is unchanged (430.0 / 430.4 vs 430.9 / 430.5 pairs/s,
+# r5x_bench*.json): the tail of the step is throughput-bound, not dependency-bound.  Off.
+WGRAD_AT_LOOP_END = os.environ.get("RAFT_WGRAD_AT_LOOP_END", "0") == "1"
 # cost-balanced halves (per-layer wgrad time at config #2, profiles/r2_bench_convs_v5_all.log)
 _WGRAD_GROUP_A = {"zr1", "zr2", "heads", "convc1", "fh2", "convf2"}
 _WGRAD_GROUP_B = {"q1", "q2", "convc2", "conv", "mask2", "convf1"}
@@ -343,6 +351,14 @@ class _PackWeights(torch.autograd.Function):
         if run is None:  # the token's forward pass never reached the update loop
             return (None,) * (len(ctx.needs_input_grad))
         cur = torch.cuda.current_stream() if run.inp_bf.is_cuda else None
+        wg = getattr(run, "wg_final", None)
+        if wg is not None and cur is not None:  # issued at the end of the loop's backward
+            cur.wait_stream(_tail_stream(cur.device))
+            run.wg_final = None
+            run.grad_out = None
+            run.arena.bufs.clear()
+            run.tail = None
+            return (None, *wg)
         ev = getattr(run, "steps_done", None)
         if ev is not None and run.wgrads is None and cur is not None:
             ws = _tail_stream(cur.device)
@@ -670,6 +686,21 @@ class _Step(torch.autograd.Function):
                 run.grad_out = run.alloc_weight_grads()
                 run.steps_done = torch.cuda.Event()
                 run.steps_done.record(torch.cuda.current_stream(dev))
+                if WGRAD_AT_LOOP_END and WGRAD_STREAMS == 1 and run.wgrads is None and len(run.done) == run.iters:
+                    # issue the batched weight gradients NOW, on the tail stream: issued from the
+                    # token's backward they reached the GPU only after the host had issued the
+                    # whole encoder backward, and ran after it, alone (profiles/r5w_phases.txt:
+                    # 3.6 ms of weight-gradient kernels on one stream after the encoders).  The
+                    # pyramid backward joins the tail stream through an event recorded before
+                    # them, so it does not wait for them.
+                    ws = _tail_stream(dev)
+                    if run.pyr is not None and getattr(run.pyr, "tail", None) is ws:
+                        tail_ev = torch.cuda.Event()
+                        tail_ev.record(ws)
+                        run.pyr.tail_event = tail_ev
+                    ws.wait_event(run.steps_done)
+                    with torch.cuda.stream(ws):
+                        run.wg_final = run.weight_grads(out_bufs=run.grad_out)
             done = sorted(run.done)
             gi = run.g_all[:, :, HID:2 * HID] if len(done) == run.iters else run.g_all[done][:, :, HID:2 * HID]
             d_inp = _nchw(gi.sum(0), B, H, W)
