@@ -1283,17 +1283,22 @@ constexpr int kLdsMax = 160 * 1024;
 // Flat strips (TW == 0) take the whole 160 KB (their strip length depends on the image width);
 // 2-D tiles size the strip buffers to their halo block, so a small tile (BM = 128) fits two
 // workgroups per CU -- two waves per SIMD, and a grid quantised over 512 slots instead of 256.
-template <int BM, int BN, int NW, int KH, int KW, int TW>
+// NSX: weight-ring stages = K steps of DMA lead (3; 4 on the 2-D tiles with a halo padded to
+// 8-row pieces, so a 128 x 64 tile still fits two workgroups per CU at 78 KB)
+template <int BM, int BN, int NW, int KH, int KW, int TW, int NSX = 3>
 struct Fwd6Cfg {
   static constexpr int NT = KH * KW;
-  static constexpr int NS = 3;                        // weight ring stages
-  static constexpr int U = (NT % 3 == 0) ? 2 : 6;     // chunks per unrolled block: U * NT % 6 == 0,
-                                                      // so stage (step % 3), register set (step & 1)
-                                                      // and strip parity (chunk & 1) are compile-time
+  static constexpr int NS = NSX;                      // weight ring stages
+  static_assert(NS == 3 || (NS == 4 && TW > 0 && NT % 2 == 1), "ring depth");
+  // chunks per unrolled block: U * NT % lcm(NS, 2) == 0 and U even, so the stage (step % NS),
+  // register set (step & 1) and strip parity (chunk & 1) are compile-time
+  static constexpr int U = NS == 4 ? 4 : (NT % 3 == 0) ? 2 : 6;
   static constexpr int RING = NS * BN * 128;
   // strip rows: a 2-D tile's halo block; a flat 1 x KW strip's BM + KW - 1 pixels (independent of
   // the image width); other flat strips take what the 160 KB leave
-  static constexpr int HALO = TW > 0   ? fwd6_halo_rows(BM / (TW > 0 ? TW : 1), TW, KH, KW, NW)
+  static constexpr int HROWS2 = TW > 0 ? (BM / (TW > 0 ? TW : 1) + KH - 1) * (TW + KW - 1) : 0;
+  static constexpr int HALO = TW > 0   ? (NS == 4 ? (HROWS2 + 7) / 8 * 8
+                                                 : fwd6_halo_rows(BM / (TW > 0 ? TW : 1), TW, KH, KW, NW))
                               : KH == 1 ? (BM + KW - 1 + 8 * NW - 1) / (8 * NW) * (8 * NW)
                                         : 0;
   static constexpr int SB = HALO > 0 && BM <= 128 ? (HALO + 1) * 128 : fwd6_sb(BN);  // odd strip = +SB
@@ -1328,13 +1333,13 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {
 // strip of BM + (KH-1) W + KW-1 rows no longer fits in LDS): the strip is the tile's halo
 // block of (BM/TW + KH-1) x (TW + KW-1) pixels with pitch TW + KW-1, so a tap is still one
 // constant row shift, and pixels outside the image are DMA'd as zeros (no per-tap masking).
-template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW = 0, bool F16 = false>
+template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW = 0, bool F16 = false, int NSX = 3>
 __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwdArgs a, int strip_rows) {
   constexpr int NW = WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;  // wave tile
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int NT = KH * KW;
-  using CF = Fwd6Cfg<BM, BN, WGM * WGN, KH, KW, TW>;
+  using CF = Fwd6Cfg<BM, BN, WGM * WGN, KH, KW, TW, NSX>;
   constexpr int NS = CF::NS, SB = CF::SB, RING = CF::RING;
   constexpr int BI = BN / (8 * NW);  // weight pieces (8 rows x 128 B) per wave per step
   constexpr int BSTAGE = BN * 128;
@@ -1361,7 +1366,10 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   constexpr int TH = TW > 0 ? BM / TW : 1;          // 2-D tile rows
   constexpr int HWD = TW + KW - 1;                  // 2-D halo block pitch (pixels)
   constexpr int HROWS = (TH + KH - 1) * HWD;        // 2-D halo block pixels
-  constexpr int SPW2 = (HROWS + 8 * NW - 1) / (8 * NW);  // its DMA pieces per wave
+  constexpr int SPW2 = (HROWS + 8 * NW - 1) / (8 * NW);  // its DMA pieces per wave (at most)
+  // 8-row pieces of the halo block: all SPW2 * NW with the 3-stage ring (the halo is padded to
+  // them), only those holding halo rows with the 4-stage ring (HALO padded to 8 rows)
+  constexpr int NPIECE = NS == 4 ? (HROWS + 7) / 8 : SPW2 * NW;
   // LDS chunk swizzle of halo row r: (r >> 1) & 7 keeps a 16-lane ds_read_b128 group on 16
   // distinct slots when its rows are consecutive, but a 3x3 tap on 16-wide tiles reads two tile
   // rows 18 halo rows apart, and the row-parity / (r >> 1) pairs then collide (2-way on every
@@ -1370,7 +1378,7 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   // halo shapes keep the row key, conflict-free there).
   const bool colsw = TW >= 16 && KW == 3 && a.swz_col != 0;
   auto fsw = [&](int r) { return colsw ? (((r % HWD) >> 1) & 7) : ((r >> 1) & 7); };
-  static_assert(TW == 0 || (BM % TW == 0 && TW % 8 == 0 && SPW2 * 8 * NW <= CF::MAX_ROWS), "2-D tile");
+  static_assert(TW == 0 || (BM % TW == 0 && TW % 8 == 0 && NPIECE * 8 <= CF::MAX_ROWS), "2-D tile");
   const int tilesN = (Nn + BN - 1) / BN;
   int tilesM;
   if constexpr (TW == 0) tilesM = (P + BM - 1) / BM;
@@ -1442,8 +1450,8 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
     bvoff[i] = (n0 + row < Nn) ? (unsigned)((n0 + row) * Kpad * 2 + swz(row, lpc) * 16) : kOOB;
   }
   const int nchunks = Cin / 64;
-  // strip pieces per wave (strip_rows % (8 NW) == 0)
-  const int spw = TW > 0 ? SPW2 : strip_rows / (8 * NW);
+  // strip pieces of this wave (flat: strip_rows % (8 NW) == 0; 2-D: pieces wave, wave + NW, ...)
+  const int spw = TW > 0 ? (NPIECE - wave + NW - 1) / NW : strip_rows / (8 * NW);
   const unsigned sswz = (unsigned)((lpc ^ (((wave & 1) << 2) | (lrow >> 1))) * 16);
   const int pstrip = m0 - halo_lo + wave * 8 + lrow;  // pixel of this lane's row in piece 0
   // 2-D: image pixel of this lane's halo row in each of its pieces (-1: outside the image)
@@ -1480,8 +1488,10 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
       if constexpr (TW > 0) {
 #pragma unroll
         for (int q = 0; q < SPW2; ++q) {
-          const unsigned voff = spix[q] >= 0 ? (unsigned)spix[q] * st + sswq[q] : kOOB;
-          bload16(rs, reinterpret_cast<__bf16*>(sbuf + q * NW * 1024), voff, soff);
+          if (NPIECE == SPW2 * NW || wave + q * NW < NPIECE) {  // uniform per wave
+            const unsigned voff = spix[q] >= 0 ? (unsigned)spix[q] * st + sswq[q] : kOOB;
+            bload16(rs, reinterpret_cast<__bf16*>(sbuf + q * NW * 1024), voff, soff);
+          }
         }
       } else {
         for (int q = 0; q < spw; ++q) {
@@ -1536,11 +1546,9 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
             std::integral_constant<int, (GU / NT) & 1>{});
   };
 
-  // prologue: steps 0, 1, 2 in flight (NT >= 5: all in chunk 0), fragments of step 0
-  issue_g(0, std::integral_constant<int, 0>{});
-  issue_g(0, std::integral_constant<int, 1>{});
-  issue_g(0, std::integral_constant<int, 2>{});
-  wait_vmcnt<2 * BI>();
+  // prologue: steps 0 .. NS-1 in flight (NT >= 5: all in chunk 0), fragments of step 0
+  static_for<NS>([&](auto gc) __attribute__((always_inline)) { issue_g(0, gc); });
+  wait_vmcnt<(NS - 1) * BI>();
   __syncthreads();  // also publishes the zero rows
   read(std::integral_constant<int, 0>{});
 
@@ -1549,19 +1557,34 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
     constexpr int G = decltype(gc)::value;
     const bool has1 = cb + (G + 1) / NT < nchunks;  // step t+1 exists
     const bool has2 = cb + (G + 2) / NT < nchunks;  // step t+2 exists (issued one step ago)
+    const bool hasl = cb + (G + NS - 1) / NT < nchunks;  // the last step in flight exists
     // sched_barrier(0) fences keep the compiler from sinking each MFMA next to its fragment
     // read (it would otherwise trade the one-step read-ahead for registers)
     __builtin_amdgcn_sched_barrier(0);
     if (has1) {
-      // step t+1 landed; step t+2 may stay in flight (BI pieces, + the strip when it opens a chunk)
-      if (!has2) wait_vmcnt<0>();
-      else if constexpr ((G + 2) % NT == 0) wait_vmcnt_le<40>(BI + spw);
-      else wait_vmcnt<BI>();
+      // step t+1 landed; steps t+2 .. t+NS-1 may stay in flight (BI pieces each, + the strip
+      // of the one that opens a chunk)
+      constexpr int OPEN = ((G + 2) % NT == 0 ? 1 : 0) + (NS == 4 && (G + 3) % NT == 0 ? 1 : 0);
+      if constexpr (NS == 3) {
+        if (!has2) wait_vmcnt<0>();
+        else if constexpr (OPEN) wait_vmcnt_le<40>(BI + spw);
+        else wait_vmcnt<BI>();
+      } else {
+        if (!has2) {
+          wait_vmcnt<0>();
+        } else if (!hasl) {  // only t+2 in flight
+          if constexpr ((G + 2) % NT == 0) wait_vmcnt_le<40>(BI + spw);
+          else wait_vmcnt<BI>();
+        } else {
+          if constexpr (OPEN) wait_vmcnt_le<40>(2 * BI + spw);
+          else wait_vmcnt<2 * BI>();
+        }
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      // step t+3 into the stage of step t (its fragments were read before this barrier)
-      issue_g(cb, std::integral_constant<int, G + 3>{});
+      // step t+NS into the stage of step t (its fragments were read before this barrier)
+      issue_g(cb, std::integral_constant<int, G + NS>{});
       __builtin_amdgcn_sched_barrier(0);
       // MFMA sub-step s of step t, then the sub-step-s reads of step t+1: every MFMA group
       // precedes the reads issued after it, so the compiler's lgkmcnt (at most 15 in flight)
@@ -2493,9 +2516,9 @@ __global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
 }  // namespace
 
 namespace {
-template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW, bool F16>
+template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW, bool F16, int NSX = 3>
 bool launch_fwd6_t(const ConvFwdArgs& a, hipStream_t s) {
-  using CF = Fwd6Cfg<BM, BN, WGM * WGN, KH, KW, TW>;
+  using CF = Fwd6Cfg<BM, BN, WGM * WGN, KH, KW, TW, NSX>;
   constexpr int NW = WGM * WGN;
   int rows = 0;
   long tiles;
@@ -2508,8 +2531,9 @@ bool launch_fwd6_t(const ConvFwdArgs& a, hipStream_t s) {
     tiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
   }
   const dim3 grid((unsigned)(tiles * ((a.N + BN - 1) / BN)));
-  set_lds_limit((const void*)conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, TW, F16>, CF::LDS);
-  hipLaunchKernelGGL((conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, TW, F16>), grid, dim3(NW * 64), CF::LDS, s, a, rows);
+  set_lds_limit((const void*)conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, TW, F16, NSX>, CF::LDS);
+  hipLaunchKernelGGL((conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, TW, F16, NSX>), grid, dim3(NW * 64), CF::LDS, s, a,
+                     rows);
   return true;
 }
 // v6 tiles (forced with cfg, chosen per shape by launch_conv_fwd): 41 = 256x64 flat strip (4x1
@@ -2552,6 +2576,10 @@ bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
       return t51 && launch_fwd6_t<128, 64, 4, 1, 5, 1, 16, F16>(a, s);
     case 65:  // 1x5 as a flat 128-pixel strip (132 halo rows at any width), two workgroups per CU
       return t15 && launch_fwd6_t<128, 64, 4, 1, 1, 5, 0, F16>(a, s);
+    case 70:  // 62 with a 4-stage weight ring (one more K step of DMA lead), still two per CU
+      if (t33) return launch_fwd6_t<128, 64, 4, 1, 3, 3, 16, F16, 4>(a, s);
+      if (t15) return launch_fwd6_t<128, 64, 4, 1, 1, 5, 64, F16, 4>(a, s);
+      return t51 && launch_fwd6_t<128, 64, 4, 1, 5, 1, 8, F16, 4>(a, s);
 
     default:
       return false;
@@ -2629,7 +2657,7 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
   bool ok5 = a.KH * a.KW > 1 && a.Cin % 64 == 0 && a.N >= 64 && a.P < (1L << 30);
   for (int i = 0; i < a.nsrc; ++i) ok5 = ok5 && a.src[i].C % 64 == 0;
   int v5 = cfg >= 20 ? cfg : 0;
-  if (cfg == 41 || cfg == 45 || (cfg >= 59 && cfg <= 65)) {  // v6 tiles (tests / microbenchmarks)
+  if (cfg == 41 || cfg == 45 || (cfg >= 59 && cfg <= 65) || cfg == 70) {  // v6 tiles (tests / microbenchmarks)
     // (a strip buffer pair per chunk needs >= 3 taps per chunk: no 1x1 variant)
     const bool shape6 = (a.KH == 3 && a.KW == 3) || (a.KH * a.KW == 5 && (a.KH == 1 || a.KW == 1));
     if (!ok5 || !shape6 || a.PH != a.KH / 2 || a.PW != a.KW / 2) return hipErrorInvalidValue;
@@ -2640,7 +2668,12 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
     // shape (the rule and its measurements: choose_fwd6 in kernel_abi.h, unit-tested on the
     // host; profiles/r5b_conv6_*.log).  Before round 5: 256 x 64 / 256 x 128 one-workgroup
     // tiles (profiles/r3_bench_conv6_*.log, r4_bench_conv6_16x16.log), now forced variants.
-    const int v6 = choose_fwd6(a.KH, a.KW, a.N, a.B, a.H, a.W);
+    static const bool ns4 = [] {  // RAFT_FWD6_NS4=1: cfg 62 -> 70 (4-stage weight ring), A/B runs
+      const char* e = std::getenv("RAFT_FWD6_NS4");
+      return e && e[0] == '1';
+    }();
+    int v6 = choose_fwd6(a.KH, a.KW, a.N, a.B, a.H, a.W);
+    if (v6 == 62 && ns4) v6 = 70;
     if (v6 && launch_conv_fwd6<F16>(a, v6, s)) return hipGetLastError();
   }
   if (ok5 && v5 == 0 && cfg == 0) {

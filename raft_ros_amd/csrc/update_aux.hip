@@ -123,39 +123,35 @@ __global__ __launch_bounds__(256) void apply_delta_kernel(const float* __restric
 // fused with apply_delta: delta[o] = bias[o] + sum_s sum_t y[s][o * 9 + t][p + off_t] (taps
 // outside the image are the conv's zero padding), then coords_out / flow_out as apply_delta;
 // delta itself is stored when requested (tests)
-__global__ __launch_bounds__(64) void n2_apply_kernel(const float* __restrict__ y, int nslot,
+__global__ __launch_bounds__(256) void n2_apply_kernel(const float* __restrict__ y, int nslot,
                                                        const float* __restrict__ bias,
                                                        const float* __restrict__ coords1,
                                                        float* __restrict__ coords_out, float* __restrict__ flow_out,
                                                        float* __restrict__ delta, long sd, int B, int H, int W) {
+  // wave w sums slot w of 64 consecutive pixels (coalesced plane rows), the 4 slot partials
+  // meet in LDS: four times the waves of a thread-per-pixel form, whose single wave per
+  // 64 pixels left each CU ~2 waves to hide the loads' latency
+  __shared__ float part[4][2][64];
   const int HW = H * W;
   const long P = (long)B * HW;
-  const long p = (long)blockIdx.x * 64 + threadIdx.x;
-  if (p >= P) return;
-  const int b = p / HW;
-  const int s = p - (long)b * HW;
+  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const long p = (long)blockIdx.x * 64 + lane;
+  const bool in = p < P;
+  const int b = in ? (int)(p / HW) : 0;
+  const int s = in ? (int)(p - (long)b * HW) : 0;
   const int py = s / W, px = s - py * W;
-  float d0 = bias ? bias[0] : 0.f, d1 = bias ? bias[1] : 0.f;
-  // branch-free taps (clamped offset, zero weight outside the image) so every slot's 18
-  // loads are issued back to back instead of one bounds-checked branch at a time
-  long off[9];
-  float keep[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int dy = t / 3 - 1, dx = t % 3 - 1;
-    const bool in = (unsigned)(py + dy) < (unsigned)H && (unsigned)(px + dx) < (unsigned)W;
-    off[t] = in ? (long)dy * W + dx : 0;
-    keep[t] = in ? 1.f : 0.f;
-  }
-#pragma unroll
-  for (int sl = 0; sl < 4; ++sl) {
-    if (sl >= nslot) break;
+  float d0 = 0.f, d1 = 0.f;
+  if (in && sl < nslot) {
     const float* ys = y + (long)sl * 18 * P + p;
-    float v[18];
+    float v[18], keep[9];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      v[t] = ys[t * P + off[t]];
-      v[9 + t] = ys[(9 + t) * P + off[t]];
+    for (int t = 0; t < 9; ++t) {  // branch-free taps: clamped offset, zero weight outside the image
+      const int dy = t / 3 - 1, dx = t % 3 - 1;
+      const bool ok = (unsigned)(py + dy) < (unsigned)H && (unsigned)(px + dx) < (unsigned)W;
+      const long off = ok ? (long)dy * W + dx : 0;
+      keep[t] = ok ? 1.f : 0.f;
+      v[t] = ys[t * P + off];
+      v[9 + t] = ys[(9 + t) * P + off];
     }
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
@@ -163,6 +159,12 @@ __global__ __launch_bounds__(64) void n2_apply_kernel(const float* __restrict__ 
       d1 += keep[t] * v[9 + t];
     }
   }
+  part[sl][0][lane] = d0;
+  part[sl][1][lane] = d1;
+  __syncthreads();
+  if (sl != 0 || !in) return;
+  d0 = (bias ? bias[0] : 0.f) + ((part[0][0][lane] + part[1][0][lane]) + (part[2][0][lane] + part[3][0][lane]));
+  d1 = (bias ? bias[1] : 0.f) + ((part[0][1][lane] + part[1][1][lane]) + (part[2][1][lane] + part[3][1][lane]));
   if (delta) {
     delta[p * sd] = d0;
     delta[p * sd + 1] = d1;
@@ -273,8 +275,8 @@ hipError_t launch_n2_apply(const float* y, int nslot, const float* bias, const f
   const long P = (long)B * H * W;
   if (!P) return hipSuccess;
   if (nslot > 4) return hipErrorInvalidValue;
-  // 64-thread workgroups: a 1080p frame is 32,400 pixels, 507 workgroups over 256 CUs
-  hipLaunchKernelGGL(n2_apply_kernel, dim3((unsigned)((P + 63) / 64)), dim3(64), 0, s, y, nslot, bias, coords1,
+  // 64 pixels x 4 slots per workgroup: a 1080p frame is 32,400 pixels, 507 workgroups of 4 waves
+  hipLaunchKernelGGL(n2_apply_kernel, dim3((unsigned)((P + 63) / 64)), dim3(256), 0, s, y, nslot, bias, coords1,
                      coords_out, flow_out, delta, sd, B, H, W);
   return hipGetLastError();
 }

@@ -169,7 +169,7 @@ def test_gru_epilogues(cuda):
     assert _rel(_from_pm(hn, B, H, W), hn_ref) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 1, 8, 9, 41, 45, 59, 60, 61, 62, 63, 64, 65, 67])
+@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 1, 8, 9, 41, 45, 59, 60, 61, 62, 63, 64, 65, 67, 70])
 @pytest.mark.parametrize("segs,cout,kh,kw,hw", [
     ([(256, 256)], 192, 3, 3, (46, 62)),
     ([(128, 128), (128, 128), (128, 128)], 256, 1, 5, (46, 62)),
