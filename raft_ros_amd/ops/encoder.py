@@ -244,10 +244,13 @@ class _Prepack:
 
 def _prepack(L, x0, split: bool, f16: bool, stream_name: str):
     """Issue the ahead-of-time packing of ``L``'s weight operands (None: disabled / too many
-    input shapes seen / inside a HIP-graph capture: launches cost nothing there, and the
-    forked packing stream (first design) crashed capture_end in
-    test_model_gpu.py::test_graphed_inference_matches_eager)."""
-    if not PREPACK or x0.device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+    input shapes seen).  Inside a HIP-graph capture only an already-built plan is used (a
+    rebuild uploads the job table, a host copy that cannot be captured; the warm-up forward
+    before the capture builds it) and never the forked packing stream, which crashed
+    capture_end in test_model_gpu.py::test_graphed_inference_matches_eager.  (Per-conv packing
+    inside the graph was ~32 serial 6 us launches per 1080p pair.)"""
+    capturing = torch.cuda.is_current_stream_capturing() if x0.device.type == "cuda" else False
+    if not PREPACK or x0.device.type != "cuda" or (capturing and _PREPACK_FORK):
         return None
     from .streams import aux_stream
 
@@ -256,9 +259,11 @@ def _prepack(L, x0, split: bool, f16: bool, stream_name: str):
     cache = L.__dict__.setdefault("prepacks", {})
     pk = cache.get(key)
     if pk is None:
-        if len(cache) >= _Prepack._MAX_SHAPES:
+        if capturing or len(cache) >= _Prepack._MAX_SHAPES:
             return None
         pk = cache[key] = _Prepack(L, L.params, x0.shape[1], x0.shape[2], split, f16, need_bwd, x0.device)
+    if capturing and tuple(p.data_ptr() for p in L.params) != pk.ptrs:
+        return None
     return pk.issue(L.params, aux_stream(x0.device, stream_name) if _PREPACK_FORK else None)
 
 

@@ -420,11 +420,16 @@ class _Step(torch.autograd.Function):
         ar = run.arena
         g = run.geom
 
-        # hidden state: slot t of the "h" arena (slot t+1 = this step's output)
-        h0 = ar.take("h", t, HID, slots=run.iters + 1)
+        # hidden state: slot t of the "h" arena (slot t+1 = this step's output).  Without the
+        # arena (inference) the previous step's output rows are used as they are: a fresh slot
+        # would cost a copy of the hidden state per iteration (32 copies of 8 MB per 1080p pair)
         net_pm = _pm(net)
-        if net_pm.data_ptr() != h0.data_ptr():
-            h0.copy_(net_pm)
+        if not ar.keep and net_pm.dtype == run.dt16 and net_pm.is_contiguous():
+            h0 = net_pm
+        else:
+            h0 = ar.take("h", t, HID, slots=run.iters + 1)
+            if net_pm.data_ptr() != h0.data_ptr():
+                h0.copy_(net_pm)
         if NATIVE_STEP and dev.type == "cuda":
             return _Step._native_forward(ctx, run, t, up, h0, coords1, corr_in, net.dtype)
         # correlation features

@@ -169,10 +169,13 @@ class _Step(torch.autograd.Function):
         ar = run.arena
         g = run.geom
 
-        h0 = ar.take("h", t, HID, slots=run.iters + 1)
         net_pm = _pm(net)
-        if net_pm.data_ptr() != h0.data_ptr():
-            h0.copy_(net_pm)
+        if not ar.keep and net_pm.dtype == run.dt16 and net_pm.is_contiguous():
+            h0 = net_pm  # inference: the previous step's output rows, no copy per iteration
+        else:
+            h0 = ar.take("h", t, HID, slots=run.iters + 1)
+            if net_pm.data_ptr() != h0.data_ptr():
+                h0.copy_(net_pm)
         corr = ar.take("corr", t, CORR_PAD)
         flow8 = ar.take("flow8", t, 8)
         motion = run.motion(t)
