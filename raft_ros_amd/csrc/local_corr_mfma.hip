@@ -100,31 +100,61 @@ __device__ __forceinline__ void tile_level_geometry(const LocalCorrArgs& a, Tile
   }
 }
 
-// Stage one 64-channel slice: query tile rows (32 x 64) and window chunk rows (256 x 64).
-// F1 = false: the window rows only (the dF1-only backward does not read the query tile).
-template <bool F1 = true>
-__device__ __forceinline__ void stage_tiles(const LocalCorrArgs& a, const TileGeo& g, int b, int l, int chunk, int c0,
-                                            __bf16* sF1, __bf16* sW, int tid) {
-  if constexpr (F1) {  // 32 rows x 8 chunks of 16 B = 256 pieces, one per thread
+// Staging of one 64-channel slice -- query tile rows (32 x 64; F1 = false: not needed by the
+// dF1-only backward) and window chunk rows (256 x 64) -- split into offsets (per level and
+// window chunk), loads (per slice, into registers) and LDS stores, so the next slice's global
+// loads are in flight while the MFMAs of the current one run (loading and storing each slice
+// in place exposed 16-32 round trips per tile and level); the window rows' division by the
+// box width is done once per chunk.
+struct StageOff {
+  long f1;    // element offset of this thread's query-tile piece (-1: none)
+  long w[8];  // element offsets of its 8 window pieces from the level base (-1: zeros)
+};
+struct StageRegs {
+  bf16x8_t f1;
+  bf16x8_t w[8];
+};
+template <bool F1>
+__device__ __forceinline__ void stage_offsets(const LocalCorrArgs& a, const TileGeo& g, int l, int chunk, int tid,
+                                              StageOff& o) {
+  o.f1 = -1;
+  if constexpr (F1) {
     const int row = tid >> 3, pc = tid & 7;
-    bf16x8_t v{};
-    if (g.pix[row] >= 0) v = *reinterpret_cast<const bf16x8_t*>(a.f1 + (long)g.pix[row] * a.C + c0 + pc * 8);
-    *reinterpret_cast<bf16x8_t*>(sF1 + row * FP + pc * 8) = v;
+    if (g.pix[row] >= 0) o.f1 = (long)g.pix[row] * a.C + pc * 8;
   }
-  const __bf16* f2l = a.f2 + b * a.f2_bstride + (long)a.off[l] * a.C;
   const int area = g.bw * g.bh;
-#pragma unroll 4
-  for (int i = 0; i < 8; ++i) {  // 256 rows x 8 pieces = 2048 pieces
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
     const int piece = tid + 256 * i;
     const int row = piece >> 3, pc = piece & 7;
     const int n = chunk * WCAP + row;
-    bf16x8_t v{};
+    o.w[i] = -1;
     if (n < area) {
       const int wy = n / g.bw, wx = n - (n / g.bw) * g.bw;
-      const int y = g.by0 + wy, x = g.bx0 + wx;
-      v = *reinterpret_cast<const bf16x8_t*>(f2l + ((long)y * a.w[l] + x) * a.C + c0 + pc * 8);
+      o.w[i] = ((long)(g.by0 + wy) * a.w[l] + g.bx0 + wx) * a.C + pc * 8;
     }
-    *reinterpret_cast<bf16x8_t*>(sW + row * FP + pc * 8) = v;
+  }
+}
+template <bool F1>
+__device__ __forceinline__ void stage_load(const LocalCorrArgs& a, const __bf16* f2l, const StageOff& o, int c0,
+                                           StageRegs& r) {
+  if constexpr (F1) {
+    r.f1 = bf16x8_t{};
+    if (o.f1 >= 0) r.f1 = *reinterpret_cast<const bf16x8_t*>(a.f1 + o.f1 + c0);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    r.w[i] = bf16x8_t{};
+    if (o.w[i] >= 0) r.w[i] = *reinterpret_cast<const bf16x8_t*>(f2l + o.w[i] + c0);
+  }
+}
+template <bool F1>
+__device__ __forceinline__ void stage_store(const StageRegs& r, __bf16* sF1, __bf16* sW, int tid) {
+  if constexpr (F1) *reinterpret_cast<bf16x8_t*>(sF1 + (tid >> 3) * FP + (tid & 7) * 8) = r.f1;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int piece = tid + 256 * i;
+    *reinterpret_cast<bf16x8_t*>(sW + (piece >> 3) * FP + (piece & 7) * 8) = r.w[i];
   }
 }
 
@@ -172,6 +202,7 @@ __global__ __launch_bounds__(256) void local_corr_mfma_fwd_kernel(const LocalCor
     for (int i = tid; i < NQ * win; i += 256) taps[i] = 0.f;
     __syncthreads();
     const int nchunks = (g.bw * g.bh + WCAP - 1) / WCAP;
+    const __bf16* f2l = a.f2 + b * a.f2_bstride + (long)a.off[l] * a.C;
     for (int chunk = 0; chunk < nchunks; ++chunk) {
       // S (32 x 256) = F1tile . F2win^T: wave w owns window pixels [64w, 64w + 64) (2 N-tiles)
       f32x16 acc[2];
@@ -179,9 +210,14 @@ __global__ __launch_bounds__(256) void local_corr_mfma_fwd_kernel(const LocalCor
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+      StageOff so;
+      StageRegs sr;
+      stage_offsets<true>(a, g, l, chunk, tid, so);
+      stage_load<true>(a, f2l, so, 0, sr);
       for (int c0 = 0; c0 < a.C; c0 += KC) {
-        stage_tiles(a, g, b, l, chunk, c0, sF1, sW, tid);
+        stage_store<true>(sr, sF1, sW, tid);
         __syncthreads();
+        if (c0 + KC < a.C) stage_load<true>(a, f2l, so, c0 + KC, sr);  // in flight during the MFMAs
 #pragma unroll
         for (int ks = 0; ks < KC / 16; ++ks) {
           const int fr = lane & 31, fk = (lane >> 5) * 8;
@@ -297,9 +333,15 @@ __global__ __launch_bounds__(256) void local_corr_mfma_bwd_kernel(const LocalCor
         G[q * GP + n] = static_cast<__bf16>(v * a.scale);
       }
       __syncthreads();
+      StageOff so;
+      StageRegs sr;
+      const __bf16* f2l = a.f2 + b * a.f2_bstride + (long)a.off[l] * a.C;
+      stage_offsets<DF2>(a, g, l, chunk, tid, so);
+      stage_load<DF2>(a, f2l, so, 0, sr);
       for (int s = 0; s < nkc; ++s) {
-        stage_tiles<DF2>(a, g, b, l, chunk, s * KC, sF1, sW, tid);
+        stage_store<DF2>(sr, sF1, sW, tid);
         __syncthreads();
+        if (s + 1 < nkc) stage_load<DF2>(a, f2l, so, (s + 1) * KC, sr);  // in flight during the MFMAs
         // dF1[q][c] += sum_n G[q][n] F2win[n][c]: M = 32 q (2 x 16), N = 16 channels (wave),
         // K = 256 window pixels.  A = G rows (k contiguous); B[k = n][col = c] = F2win column
         // -> transposed read of the [n][c] tile.
@@ -309,11 +351,13 @@ __global__ __launch_bounds__(256) void local_corr_mfma_bwd_kernel(const LocalCor
           for (int m = 0; m < 2; ++m) {
             const bf16x8 af = *reinterpret_cast<const bf16x8*>(G + (m * 16 + (lane & 15)) * GP + ks * 32 +
                                                                (lane >> 4) * 8);
-            // B fragment (16x16x32): lane holds B[k = 8 * (lane >> 4) + j][col = lane & 15]
-            const int col = wave * 16 + (lane & 15);
-            bf16x8 bfr;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) bfr[j] = sW[(ks * 32 + (lane >> 4) * 8 + j) * FP + col];
+            // B fragment (16x16x32): lane holds B[k = 8 * (lane >> 4) + j][col = lane & 15]: two
+            // transposed reads of 4 window rows x the wave's 16 channels (lane 4q + p of a 16-lane
+            // group addresses row q, channels 4p .. 4p + 3), instead of 8 scalar 16-bit reads
+            const int tr_row = ks * 32 + (lane >> 4) * 8 + ((lane & 15) >> 2), tr_col = wave * 16 + 4 * (lane & 3);
+            const s16x4 blo = tr_read(sW + tr_row * FP + tr_col);
+            const s16x4 bhi = tr_read(sW + (tr_row + 4) * FP + tr_col);
+            const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7));
             acc1[s][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc1[s][m], 0, 0, 0);
           }
         }
