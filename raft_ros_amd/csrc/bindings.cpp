@@ -1024,8 +1024,20 @@ int wgrad3_mt5() {
   return v;
 }
 
+// RAFT_WGRAD_DIV=d: plan the update-block weight gradients for 1/d of the workgroups (they run
+// beside the encoder backward, which is the step's critical path; A/B runs)
+int wgrad_grid_div() {
+  static const int v = [] {
+    const char* e = std::getenv("RAFT_WGRAD_DIV");
+    const int d = e ? std::atoi(e) : 1;
+    return d >= 1 && d <= 8 ? d : 1;
+  }();
+  return v;
+}
+
 std::tuple<at::Tensor, at::Tensor, WgradPlan> run_wgrad(ConvWgradArgs& a, bool with_bias, const at::Tensor& like) {
   a.mt5 = wgrad3_mt5();
+  a.grid_div = wgrad_grid_div();
   const WgradPlan pl = plan_conv_wgrad(a);
   auto opts = like.options().dtype(at::kFloat);
   auto slab = at::empty({(long)pl.nsplit * pl.Npad * a.Kpad}, opts);

@@ -150,6 +150,7 @@ struct ConvWgradArgs {
   int xcd_g;      // >0: XCD-grouped split mapping with xcd_g splits per XCD (set by the launcher)
   int f16;        // fp16 operands (see ConvFwdArgs::f16)
   int mt5;        // wgrad v3 on 1x5 / 5x1 convs: 1 = 64-row workgroups, 2 = 128 rows on 4 waves, 3 = 128 rows on 8 waves
+  int grid_div;   // > 1: plan for 1 / grid_div of the workgroups (leave CUs to the work beside it)
 };
 
 // Plan of one weight-gradient launch (the caller sizes the slabs from it).
@@ -493,7 +494,8 @@ inline WgradPlan plan_conv_wgrad3(const ConvWgradArgs& a) {
   const int TH = sq ? 8 : (a.KH == 5 ? 16 : 1), TW = 64 / TH;
   const long ntiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
   long splits, g;
-  choose_splits((long)pl.tilesM * pl.tilesN, ntiles, splits, g, (!sq && a.mt5 == 3) ? 256 : 512);
+  choose_splits((long)pl.tilesM * pl.tilesN, ntiles, splits, g,
+                ((!sq && a.mt5 == 3) ? 256 : 512) / std::max(1, a.grid_div));
   long per = (ntiles + splits - 1) / splits;
   if ((ntiles + per - 1) / per != splits) g = 0;
   pl.nsplit = (int)((ntiles + per - 1) / per);
@@ -515,7 +517,7 @@ inline WgradPlan plan_conv_wgrad(const ConvWgradArgs& a) {
   pl.tilesN = (a.K + pl.BN - 1) / pl.BN;
   pl.Npad = pl.tilesM * pl.BM;
   long splits, g;
-  choose_splits((long)pl.tilesM * pl.tilesN, (a.P + 255) / 256, splits, g);
+  choose_splits((long)pl.tilesM * pl.tilesN, (a.P + 255) / 256, splits, g, 256 / std::max(1, a.grid_div));
   long per = (a.P + splits - 1) / splits;
   per = (per + kWgradBK - 1) / kWgradBK * kWgradBK;
   if ((a.P + per - 1) / per != splits) g = 0;  // rounding dropped a split: plain mapping

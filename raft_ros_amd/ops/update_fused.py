@@ -293,6 +293,9 @@ WGRAD_STREAMS = int(os.environ.get("RAFT_WGRAD_STREAMS", "1"))
 # other stream's and the step time is unchanged (430.0 / 430.4 vs 430.9 / 430.5 pairs/s,
 # r5x_bench*.json): the tail of the step is throughput-bound, not dependency-bound.  Off.
 WGRAD_AT_LOOP_END = os.environ.get("RAFT_WGRAD_AT_LOOP_END", "0") == "1"
+# diagnostics: a list collects (main-stream event at the token's backward, weight-gradient
+# start, end) event triples on the tail stream (scripts/host_lead.py --wgrad_timing)
+WGRAD_TIMING: Optional[list] = None
 # cost-balanced halves (per-layer wgrad time at config #2, profiles/r2_bench_convs_v5_all.log)
 _WGRAD_GROUP_A = {"zr1", "zr2", "heads", "convc1", "fh2", "convf2"}
 _WGRAD_GROUP_B = {"q1", "q2", "convc2", "conv", "mask2", "convf1"}
@@ -375,7 +378,14 @@ class _PackWeights(torch.autograd.Function):
                 cur.wait_stream(ws2)
             else:
                 with torch.cuda.stream(ws):
+                    if WGRAD_TIMING is not None:  # scripts/host_lead.py --wgrad_timing
+                        evs = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                        evs[0].record(cur)  # main stream: the encoder backward queued before this point
+                        evs[1].record(ws)
                     grads = run.weight_grads(out_bufs=run.grad_out)
+                    if WGRAD_TIMING is not None:
+                        evs[2].record(ws)
+                        WGRAD_TIMING.append(evs)
             cur.wait_stream(ws)
             # no record_stream: the gradients were allocated on this stream before the event the
             # tail stream waited for, and the arena (this stream's memory too) is released only

@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--host_pad_ms", type=float, default=0.0, help="host sleep before each step")
     ap.add_argument("--max_lead", type=int, default=0,
                     help="> 0: before issuing step i, wait for step i - max_lead - 1 to finish on the GPU")
+    ap.add_argument("--wgrad_timing", action="store_true",
+                    help="per step: when the batched weight gradients start / end on the tail stream, relative "
+                         "to the step's backward start and to the main stream reaching the weight token")
     ap.add_argument("--cprofile", type=int, default=0,
                     help="> 0: also profile the host side of this many steps (cProfile, top functions)")
     args = ap.parse_args()
@@ -84,6 +87,10 @@ def main():
             torch.cuda._sleep(cycles)
         return th
 
+    if args.wgrad_timing:
+        from raft_ros_amd.ops import update_fused
+
+        update_fused.WGRAD_TIMING = []
     with torch.cuda.stream(stream):
         for i in range(5):
             step(i, [torch.cuda.Event(enable_timing=True) for _ in range(8)])
@@ -118,6 +125,19 @@ def main():
             st = pstats.Stats(pr)
             st.sort_stats("tottime").print_stats(45)
             st.sort_stats("cumulative").print_stats(45)
+    if args.wgrad_timing:
+        from raft_ros_amd.ops import update_fused
+
+        tl = update_fused.WGRAD_TIMING[-args.steps:]
+        rows = []
+        for i, (e_tok, e0, e1) in enumerate(tl):
+            # relative to the step's backward start (evs[i][2]: after the loss) and its end (evs[i][3])
+            b0 = evs[i][2]
+            rows.append((b0.elapsed_time(e0), b0.elapsed_time(e1), b0.elapsed_time(e_tok), b0.elapsed_time(evs[i][3])))
+        n = len(rows)
+        m = [sum(r[k] for r in rows) / n for k in range(4)]
+        print(f"weight gradients (ms after the backward start): start {m[0]:.2f}, end {m[1]:.2f}; main stream "
+              f"at the weight token {m[2]:.2f}; backward end (main) {m[3]:.2f}")
     keys = ("num_device_alloc", "num_device_free", "num_alloc_retries", "num_sync_all_streams", "num_ooms")
     print("caching allocator over the timed steps:", {k: m1.get(k, 0) - m0.get(k, 0) for k in keys},
           f"reserved {m0['reserved_bytes.all.current'] / 2**30:.2f} -> {m1['reserved_bytes.all.current'] / 2**30:.2f} GiB")
