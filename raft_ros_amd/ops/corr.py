@@ -41,6 +41,9 @@ import torch.nn.functional as F
 from . import reference as ref
 from ._ext import ops, use_native
 
+# RAFT_CORR_BWD_BLAS=0: the pyramid backward GEMMs on the generic MFMA kernel (A/B runs)
+BWD_BLAS = os.environ.get("RAFT_CORR_BWD_BLAS", "1") != "0"
+
 # Lookup backward mode (see _PyramidState.add_grad): deferred row accumulation (default) or
 # one read-modify-write pass per lookup (RAFT_DEFER_LOOKUP_GRADS=0, for A/B measurements)
 DEFER_LOOKUP_GRADS = os.environ.get("RAFT_DEFER_LOOKUP_GRADS", "1") != "0"
@@ -218,14 +221,24 @@ class _BuildPyramid(torch.autograd.Function):
         alpha = 1.0 / math.sqrt(C)
         f2t = k.pyramid_operand(fmap2.detach(), state.segments(), ld, True, True)  # (B, C, ld)
         f1t = k.pyramid_operand(fmap1.detach(), [0, H, W], _pad_to(HW, 8), False, True)  # (B, C, HW + pad)
-        d1 = torch.empty(B, HW, C, device=fmap1.device)
-        G = torch.empty(B, ld, C, device=fmap1.device)
-        # dF1 = alpha * dL . f2cat            (M = HW, N = C, K = all levels)
-        k.corr_gemm(dbuf, f2t, d1, HW, C, ld, B, ld, HW * ld, ld, C * ld, C, HW * C, alpha, False, split, 0)
-        # G = alpha * dL^T . f1  per level row (M = all levels, N = C, K = HW; A read transposed),
-        # dF2 = sum_l unpool_l(G_l)
-        k.corr_gemm(dbuf, f1t, G, ld, C, HW, B, ld, HW * ld, f1t.shape[2], C * f1t.shape[2], C, ld * C, alpha,
-                    True, split, 0)
+        if not split and dbuf.dtype == torch.bfloat16 and BWD_BLAS:
+            # bf16 level gradients: both are plain batched GEMMs (the unpool is its own pass), on
+            # hipBLASLt -- the generic MFMA GEMM ran them at ~9-12 % of peak (215 + 158 us per step
+            # at config #2, profiles/r5o_bf16_kernels.txt) on the backward's critical path
+            dL, bf = dbuf.view(B, HW, ld), torch.bfloat16
+            d1 = torch.baddbmm(torch.empty(B, HW, C, device=fmap1.device, dtype=bf), dL,
+                               f2t.to(bf).transpose(1, 2), beta=0.0, alpha=alpha)
+            G = torch.baddbmm(torch.empty(B, ld, C, device=fmap1.device, dtype=bf), dL.transpose(1, 2),
+                              f1t[:, :, :HW].to(bf).transpose(1, 2), beta=0.0, alpha=alpha).float()
+        else:
+            d1 = torch.empty(B, HW, C, device=fmap1.device)
+            G = torch.empty(B, ld, C, device=fmap1.device)
+            # dF1 = alpha * dL . f2cat            (M = HW, N = C, K = all levels)
+            k.corr_gemm(dbuf, f2t, d1, HW, C, ld, B, ld, HW * ld, ld, C * ld, C, HW * C, alpha, False, split, 0)
+            # G = alpha * dL^T . f1  per level row (M = all levels, N = C, K = HW; A read transposed),
+            # dF2 = sum_l unpool_l(G_l)
+            k.corr_gemm(dbuf, f1t, G, ld, C, HW, B, ld, HW * ld, f1t.shape[2], C * f1t.shape[2], C, ld * C, alpha,
+                        True, split, 0)
         d2 = k.pyramid_unpool(G, H, W, state.segments(), True)
         state.release()
         g1 = d1.view(B, H, W, C).permute(0, 3, 1, 2)
