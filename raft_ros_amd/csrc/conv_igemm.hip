@@ -1623,14 +1623,16 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
 // lane's DMA offsets are computed once and the K step rides in the scalar soffset; the
 // fwd6 pipeline (3-stage ring, fragments of step t+1 read behind the MFMAs of step t, raw
 // barriers, counted vmcnt); 128 x 64 tiles in 72 KB so two workgroups share a CU.
-template <int BM, int BN, int WGM, int WGN, bool F16 = false>
-__global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd7_kernel(const ConvFwdArgs a) {
+// NS = 2: a 2-stage ring (48 KB, three workgroups per CU; one step of DMA in flight).
+template <int BM, int BN, int WGM, int WGN, bool F16 = false, int NS = 3>
+__global__ __launch_bounds__(WGM * WGN * 64) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 3 : 1)))
+void conv_fwd7_kernel(const ConvFwdArgs a) {
   constexpr int NW = WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);  // DMA pieces per wave per step
   constexpr int STAGE = (BM + BN) * 128;                 // bytes
-  constexpr int NS = 3;
+  static_assert(NS == 2 || NS == 3, "ring depth");
   static_assert(AI >= 1 && BI >= 1 && TM >= 1 && TN >= 1, "tile");
   static_assert(NS * STAGE >= BM * (BN + 4) * 4, "epilogue tile must fit the ring");
   extern __shared__ __attribute__((aligned(1024))) __bf16 dsm[];
@@ -1705,8 +1707,8 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd7_kernel(const ConvFwd
   constexpr int G = AI + BI;
   issue(0, 0);
   if (nk > 1) issue(1, 1);
-  if (nk > 2) issue(2, 2);
-  if (nk > 2) wait_vmcnt<2 * G>();
+  if (NS == 3 && nk > 2) issue(2, 2);
+  if (NS == 3 && nk > 2) wait_vmcnt<2 * G>();
   else if (nk > 1) wait_vmcnt<G>();
   else wait_vmcnt<0>();
   __syncthreads();
@@ -1715,12 +1717,12 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd7_kernel(const ConvFwd
     constexpr int R = decltype(rc)::value;
     __builtin_amdgcn_sched_barrier(0);
     if (t + 1 < nk) {
-      if (t + 2 < nk) wait_vmcnt<G>();  // step t+1 landed, t+2 may stay in flight
+      if (NS == 3 && t + 2 < nk) wait_vmcnt<G>();  // step t+1 landed, t+2 may stay in flight
       else wait_vmcnt<0>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      if (t + 3 < nk) issue(t + 3, t % NS);  // into the stage step t was read from
+      if (t + NS < nk) issue(t + NS, t % NS);  // into the stage step t was read from
       __builtin_amdgcn_sched_barrier(0);
       const unsigned off = (unsigned)(((t + 1) % NS) * STAGE);
 #pragma unroll
@@ -2592,6 +2594,11 @@ static const bool kUseV7 = [] {
   const char* e = std::getenv("RAFT_CONV_V7");
   return !(e && e[0] == '0');
 }();
+// RAFT_V7_RING2=1: v7 on the 2-stage ring (cfg 71) for the automatic 1x1 choice
+static const bool kV7Ring2 = [] {
+  const char* e = std::getenv("RAFT_V7_RING2");
+  return e && e[0] == '1';
+}();
 
 template <bool F16>
 hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
@@ -2737,6 +2744,13 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
   // v7 (lean 1x1 GEMM, 128 x 64 tiles, two workgroups per CU) for single-source 1x1 convs
   const bool v7ok = a.KH == 1 && a.KW == 1 && a.nsrc == 1 && a.src[0].C == a.Cin && a.N >= 64 &&
                     (a.src[0].stride % 8) == 0 && a.P * a.src[0].stride * 2 < (1L << 31);
+  if (cfg == 71 || (cfg == 0 && v7ok && kUseV7 && kV7Ring2)) {  // 2-stage ring, 3 WGs per CU
+    if (!v7ok) return hipErrorInvalidValue;
+    constexpr int lds7 = 2 * (128 + 64) * 128;
+    set_lds_limit((const void*)conv_fwd7_kernel<128, 64, 4, 1, F16, 2>, lds7);
+    hipLaunchKernelGGL((conv_fwd7_kernel<128, 64, 4, 1, F16, 2>), dim3(tiles(128, 64)), dim3(256), lds7, s, a);
+    return hipGetLastError();
+  }
   if (cfg == 67 || (cfg == 0 && v7ok && kUseV7)) {
     if (!v7ok) return hipErrorInvalidValue;
     constexpr int lds7 = 3 * (128 + 64) * 128;
