@@ -906,6 +906,8 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
 // part [B][R][4][N] (no atomics; fixed reduction order).
 
 
+// MODE: 0 bf16, 1 fp16, 2 split-bf16 rows (one code path per instantiation)
+template <int MODE>
 __global__ __launch_bounds__(256) void enc_norm_bwd_reduce_kernel(const NormBwdArgs a) {
   __shared__ float red[8 * (256 + 32)];
   const int r = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
@@ -918,11 +920,11 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_reduce_kernel(const NormBwdA
   const bool active = pr < PPB;
   const int n = cg * 8;
   const int chunk = (a.HW + a.R - 1) / a.R;
-  const long rs = a.split ? 3L * N : N;  // row pitch (split rows: hi / lo / hi planes of N)
+  const long rs = MODE == 2 ? 3L * N : N;  // row pitch (split rows: hi / lo / hi planes of N)
   const int pb = r * chunk, pe = min(a.HW, pb + chunk);
   auto ld8 = [&](const __bf16* q, float* v) __attribute__((always_inline)) {
-    if (a.split) load8_split(q, N, v, a.split);
-    else load8(q, v, a.f16 != 0);
+    if constexpr (MODE == 2) load8_split(q, N, v, a.split);
+    else load8(q, v, MODE == 1);
   };
   float S[4][8];
 #pragma unroll
@@ -930,15 +932,14 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_reduce_kernel(const NormBwdA
 #pragma unroll
     for (int e = 0; e < 8; ++e) S[qd][e] = 0.f;
   if (active) {
-    float sc0[8], sh0[8], rs0[8], mu0[8], rs1[8], mu1[8];
+    // the rstd factor of S2 is applied once after the loop (fewer live registers in it)
+    float sc0[8], sh0[8], mu0[8], mu1[8];
     const float* c0 = a.c0 + (long)b * 4 * N;
     loadf8(c0 + n, sc0);
     loadf8(c0 + N + n, sh0);
-    loadf8(c0 + 2 * N + n, rs0);
     loadf8(c0 + 3 * N + n, mu0);
     if (a.a1) {
       const float* c1 = a.c1 + (long)b * 4 * N;
-      loadf8(c1 + 2 * N + n, rs1);
       loadf8(c1 + 3 * N + n, mu1);
     }
     const long base = (long)b * a.HW;
@@ -961,16 +962,25 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_reduce_kernel(const NormBwdA
         for (int e = 0; e < 8; ++e) {
           const float dy = (a.relu0 && !(av[u][e] * sc0[e] + sh0[e] > 0.f)) ? 0.f : gv[u][e];
           S[0][e] += dy;
-          S[1][e] += dy * (av[u][e] - mu0[e]) * rs0[e];
+          S[1][e] += dy * (av[u][e] - mu0[e]);
         }
         if (a.a1) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             S[2][e] += gv[u][e];
-            S[3][e] += gv[u][e] * (dv[u][e] - mu1[e]) * rs1[e];
+            S[3][e] += gv[u][e] * (dv[u][e] - mu1[e]);
           }
         }
       }
+    }
+    float rs[8];
+    loadf8(c0 + 2 * N + n, rs);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) S[1][e] *= rs[e];
+    if (a.a1) {
+      loadf8(a.c1 + (long)b * 4 * N + 2 * N + n, rs);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) S[3][e] *= rs[e];
     }
   }
   const int nq = a.a1 ? 4 : 2;
@@ -1045,47 +1055,55 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_finalize_kernel(const NormBw
   }
 }
 
-// pass 3: da_j = k1 * dy_j + k2 * xhat_j + k3
+// pass 3: da_j = k1 * dy_j + k2 * xhat_j + k3, as k1 * dy_j + A_j * a_j + C_j with
+// A = k2 * rstd, C = k3 - A * mean folded per image (five coefficient vectors per branch held
+// across the pixel loop put the kernel at 173 VGPRs, two waves per SIMD, on a streaming pass)
+// MODE: 0 bf16, 1 fp16, 2 split-bf16 rows (one code path per instantiation)
+template <int MODE>
 __global__ __launch_bounds__(256) void enc_norm_bwd_apply_kernel(const NormBwdArgs a) {
   const int N = a.N, G = N / 8;
   const PixWalk w = pix_walk(G);
   if (w.p < 0) return;
   const int n = w.n, P = a.B * a.HW;
-  const long rp = a.split ? 3L * N : N;  // row pitch (split rows: hi / lo / hi planes of N)
+  const long rp = MODE == 2 ? 3L * N : N;  // row pitch (split rows: hi / lo / hi planes of N)
   auto ld8 = [&](const __bf16* q, float* v) __attribute__((always_inline)) {
-    if (a.split) load8_split(q, N, v, a.split);
-    else load8(q, v, a.f16 != 0);
+    if constexpr (MODE == 2) load8_split(q, N, v, a.split);
+    else load8(q, v, MODE == 1);
   };
   auto st8 = [&](__bf16* q, const float* v) __attribute__((always_inline)) {
-    if (a.split) store8_split(q, N, v, a.split);
-    else store8(q, v, a.f16 != 0);
+    if constexpr (MODE == 2) store8_split(q, N, v, a.split);
+    else store8(q, v, MODE == 1);
+  };
+  // k, A, C of branch j at j * 3 + {0, 1, 2}; loaded per image
+  auto coefs = [&](int b, int j, float* k, float* A, float* Cc) __attribute__((always_inline)) {
+    const float* cj = (j ? a.c1 : a.c0) + (long)b * 4 * N;
+    const float* bc = a.bcoef + ((long)b * 2 + j) * 3 * N;
+    float k2[8], k3[8], rs[8], mu[8];
+    loadf8(bc + n, k);
+    loadf8(bc + N + n, k2);
+    loadf8(bc + 2 * N + n, k3);
+    loadf8(cj + 2 * N + n, rs);
+    loadf8(cj + 3 * N + n, mu);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      A[e] = k2[e] * rs[e];
+      Cc[e] = k3[e] - A[e] * mu[e];
+    }
   };
   int bend = 0;
-  float k1[8], k2[8], k3[8], rs[8], mu[8], sc[8], sh[8];
-  float q1[8], q2[8], q3[8], rs1[8], mu1[8];
+  float k1[8], A1[8], C1[8], sc[8], sh[8];
+  float q1[8], A2[8], C2[8];
   for (int p = w.p; p < P; p += w.stride) {
     if (p >= bend) {  // next image: its coefficients
       const int b = p / a.HW;
       bend = (b + 1) * a.HW;
-      const float* c0 = a.c0 + (long)b * 4 * N;
-      const float* bc = a.bcoef + (long)b * 2 * 3 * N;
-      loadf8(bc + n, k1);
-      loadf8(bc + N + n, k2);
-      loadf8(bc + 2 * N + n, k3);
-      loadf8(c0 + 2 * N + n, rs);
-      loadf8(c0 + 3 * N + n, mu);
+      coefs(b, 0, k1, A1, C1);
       if (a.relu0) {
+        const float* c0 = a.c0 + (long)b * 4 * N;
         loadf8(c0 + n, sc);
         loadf8(c0 + N + n, sh);
       }
-      if (a.a1) {
-        const float* c1 = a.c1 + (long)b * 4 * N;
-        loadf8(bc + 3 * N + n, q1);
-        loadf8(bc + 4 * N + n, q2);
-        loadf8(bc + 5 * N + n, q3);
-        loadf8(c1 + 2 * N + n, rs1);
-        loadf8(c1 + 3 * N + n, mu1);
-      }
+      if (a.a1) coefs(b, 1, q1, A2, C2);
     }
     float gv[8], av[8], o[8];
     ld8(a.g + (long)p * rp + n, gv);
@@ -1094,17 +1112,17 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_apply_kernel(const NormBwdAr
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float dy = (av[e] * sc[e] + sh[e] > 0.f) ? gv[e] : 0.f;
-        o[e] = k1[e] * dy + k2[e] * (av[e] - mu[e]) * rs[e] + k3[e];
+        o[e] = k1[e] * dy + A1[e] * av[e] + C1[e];
       }
     } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = k1[e] * gv[e] + k2[e] * (av[e] - mu[e]) * rs[e] + k3[e];
+      for (int e = 0; e < 8; ++e) o[e] = k1[e] * gv[e] + A1[e] * av[e] + C1[e];
     }
     st8(a.out0 + (long)p * rp + n, o);
     if (a.a1) {
       ld8(a.a1 + (long)p * rp + n, av);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = q1[e] * gv[e] + q2[e] * (av[e] - mu1[e]) * rs1[e] + q3[e];
+      for (int e = 0; e < 8; ++e) o[e] = q1[e] * gv[e] + A2[e] * av[e] + C2[e];
       st8(a.out1 + (long)p * rp + n, o);
     }
   }
@@ -1461,7 +1479,10 @@ hipError_t launch_enc_apply(const void* a, const float* ca, bool relu_a, const v
 
 hipError_t launch_enc_norm_bwd_stages(const NormBwdArgs& a, int stages, int b_fin, hipStream_t s) {
   if (stages & 1) {
-    hipLaunchKernelGGL(enc_norm_bwd_reduce_kernel, dim3(a.R, a.B), dim3(256), 0, s, a);
+    const dim3 g(a.R, a.B);
+    if (a.split) hipLaunchKernelGGL(enc_norm_bwd_reduce_kernel<2>, g, dim3(256), 0, s, a);
+    else if (a.f16) hipLaunchKernelGGL(enc_norm_bwd_reduce_kernel<1>, g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(enc_norm_bwd_reduce_kernel<0>, g, dim3(256), 0, s, a);
     RAFT_HIP_CHECK(hipGetLastError());
   }
   if (stages & 2) {
@@ -1475,7 +1496,10 @@ hipError_t launch_enc_norm_bwd_stages(const NormBwdArgs& a, int stages, int b_fi
   }
   if (stages & 4) {
     if (a.N % 8 != 0 || a.N / 8 > 256 || (long)a.B * a.HW >= (1L << 31)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(enc_norm_bwd_apply_kernel, dim3(grid_pix(a.B, a.HW, a.N)), dim3(256), 0, s, a);
+    const dim3 g(grid_pix(a.B, a.HW, a.N));
+    if (a.split) hipLaunchKernelGGL(enc_norm_bwd_apply_kernel<2>, g, dim3(256), 0, s, a);
+    else if (a.f16) hipLaunchKernelGGL(enc_norm_bwd_apply_kernel<1>, g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(enc_norm_bwd_apply_kernel<0>, g, dim3(256), 0, s, a);
     RAFT_HIP_CHECK(hipGetLastError());
   }
   return hipSuccess;
