@@ -843,6 +843,9 @@ __device__ __forceinline__ PixWalk pix_walk(int G) {
   return w;
 }
 
+// SPL: split-bf16 rows (fp32 training) -- one code path per instantiation keeps the bf16 /
+// fp16 kernel's registers (and so its occupancy) free of the split path's
+template <bool SPL>
 __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict__ a, const float* __restrict__ ca,
                                                         int relu_a, const __bf16* __restrict__ r,
                                                         const float* __restrict__ cr, int relu_out,
@@ -850,8 +853,7 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
   const int G = N / 8;
   const bool f16 = (split & 2) != 0;
   const int mode = (split & 4) ? 2 : 1;  // split-plane mode (store8_split)
-  split &= 1;
-  const int rs = split ? 3 * N : N;  // row stride: split rows hold three planes
+  const int rs = SPL ? 3 * N : N;  // row stride: split rows hold three planes
   const PixWalk w = pix_walk(G);
   if (w.p < 0) return;
   const int n = w.n, P = B * HW;
@@ -869,7 +871,7 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
       }
     }
     float v[8];
-    if (split)
+    if (SPL)
       load8_split(a + (long)p * rs + n, N, v, mode);
     else
       load8(a + (long)p * N + n, v, f16);
@@ -880,7 +882,7 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
     }
     if (r) {
       float rv[8];
-      if (split)
+      if (SPL)
         load8_split(r + (long)p * rs + n, N, rv, mode);
       else
         load8(r + (long)p * N + n, rv, f16);
@@ -893,7 +895,7 @@ __global__ __launch_bounds__(256) void enc_apply_kernel(const __bf16* __restrict
     if (relu_out)
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-    if (split)
+    if (SPL)
       store8_split(out + (long)p * rs + n, N, v, mode);
     else
       store8(out + (long)p * N + n, v, f16);
@@ -1471,9 +1473,14 @@ hipError_t launch_enc_norm_finalize(const NormFinArgs& a, hipStream_t s) {
 hipError_t launch_enc_apply(const void* a, const float* ca, bool relu_a, const void* r, const float* cr,
                             bool relu_out, void* out, int B, int HW, int N, int split, hipStream_t s) {
   if (N % 8 != 0 || N / 8 > 256 || (long)B * HW >= (1L << 31)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(enc_apply_kernel, dim3(grid_pix(B, HW, N)), dim3(256), 0, s, static_cast<const __bf16*>(a), ca,
-                     relu_a ? 1 : 0, static_cast<const __bf16*>(r), cr, relu_out ? 1 : 0, static_cast<__bf16*>(out), B,
-                     HW, N, split);
+  if (split & 1)
+    hipLaunchKernelGGL(enc_apply_kernel<true>, dim3(grid_pix(B, HW, N)), dim3(256), 0, s,
+                       static_cast<const __bf16*>(a), ca, relu_a ? 1 : 0, static_cast<const __bf16*>(r), cr,
+                       relu_out ? 1 : 0, static_cast<__bf16*>(out), B, HW, N, split);
+  else
+    hipLaunchKernelGGL(enc_apply_kernel<false>, dim3(grid_pix(B, HW, N)), dim3(256), 0, s,
+                       static_cast<const __bf16*>(a), ca, relu_a ? 1 : 0, static_cast<const __bf16*>(r), cr,
+                       relu_out ? 1 : 0, static_cast<__bf16*>(out), B, HW, N, split);
   return hipGetLastError();
 }
 
