@@ -1060,9 +1060,11 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_finalize_kernel(const NormBw
 // pass 3: da_j = k1 * dy_j + k2 * xhat_j + k3, as k1 * dy_j + A_j * a_j + C_j with
 // A = k2 * rstd, C = k3 - A * mean folded per image (five coefficient vectors per branch held
 // across the pixel loop put the kernel at 173 VGPRs, two waves per SIMD, on a streaming pass)
-// MODE: 0 bf16, 1 fp16, 2 split-bf16 rows (one code path per instantiation)
-template <int MODE>
-__global__ __launch_bounds__(256) void enc_norm_bwd_apply_kernel(const NormBwdArgs a) {
+// MODE: 0 bf16, 1 fp16, 2 split-bf16 rows; TWO: the second (downsample) branch -- one code
+// path per instantiation, so the one-branch kernels do not carry the second's coefficients
+template <int MODE, bool TWO>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO || MODE == 2 ? 1 : 5)))
+void enc_norm_bwd_apply_kernel(const NormBwdArgs a) {
   const int N = a.N, G = N / 8;
   const PixWalk w = pix_walk(G);
   if (w.p < 0) return;
@@ -1105,7 +1107,7 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_apply_kernel(const NormBwdAr
         loadf8(c0 + n, sc);
         loadf8(c0 + N + n, sh);
       }
-      if (a.a1) coefs(b, 1, q1, A2, C2);
+      if constexpr (TWO) coefs(b, 1, q1, A2, C2);
     }
     float gv[8], av[8], o[8];
     ld8(a.g + (long)p * rp + n, gv);
@@ -1121,7 +1123,7 @@ __global__ __launch_bounds__(256) void enc_norm_bwd_apply_kernel(const NormBwdAr
       for (int e = 0; e < 8; ++e) o[e] = k1[e] * gv[e] + A1[e] * av[e] + C1[e];
     }
     st8(a.out0 + (long)p * rp + n, o);
-    if (a.a1) {
+    if constexpr (TWO) {
       ld8(a.a1 + (long)p * rp + n, av);
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = q1[e] * gv[e] + A2[e] * av[e] + C2[e];
@@ -1504,9 +1506,13 @@ hipError_t launch_enc_norm_bwd_stages(const NormBwdArgs& a, int stages, int b_fi
   if (stages & 4) {
     if (a.N % 8 != 0 || a.N / 8 > 256 || (long)a.B * a.HW >= (1L << 31)) return hipErrorInvalidValue;
     const dim3 g(grid_pix(a.B, a.HW, a.N));
-    if (a.split) hipLaunchKernelGGL(enc_norm_bwd_apply_kernel<2>, g, dim3(256), 0, s, a);
-    else if (a.f16) hipLaunchKernelGGL(enc_norm_bwd_apply_kernel<1>, g, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(enc_norm_bwd_apply_kernel<0>, g, dim3(256), 0, s, a);
+    const bool two = a.a1 != nullptr;
+    if (a.split && two) hipLaunchKernelGGL((enc_norm_bwd_apply_kernel<2, true>), g, dim3(256), 0, s, a);
+    else if (a.split) hipLaunchKernelGGL((enc_norm_bwd_apply_kernel<2, false>), g, dim3(256), 0, s, a);
+    else if (a.f16 && two) hipLaunchKernelGGL((enc_norm_bwd_apply_kernel<1, true>), g, dim3(256), 0, s, a);
+    else if (a.f16) hipLaunchKernelGGL((enc_norm_bwd_apply_kernel<1, false>), g, dim3(256), 0, s, a);
+    else if (two) hipLaunchKernelGGL((enc_norm_bwd_apply_kernel<0, true>), g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((enc_norm_bwd_apply_kernel<0, false>), g, dim3(256), 0, s, a);
     RAFT_HIP_CHECK(hipGetLastError());
   }
   return hipSuccess;
