@@ -317,17 +317,23 @@ def fetch_dataloader(args, TRAIN_DS: str = "C+T+K+S+H"):
 
     world = int(getattr(args, "world_size", 1) or 1)
     rank = int(getattr(args, "rank", 0) or 0)
-    if args.stage == "synthetic":  # device-resident pool (data/synthetic.py DeviceSyntheticLoader)
+    pool = int(getattr(args, "synthetic_pool", 8) or 0)
+    if args.stage == "synthetic" and pool > 0:  # device-resident pool (data/synthetic.py DeviceSyntheticLoader)
         from .synthetic import DeviceSyntheticLoader
 
         sizes = rank_batch_sizes(args.batch_size, world, getattr(args, "batch_split", "balanced"))
         steps = 100000 // args.batch_size
         if rank == 0:
-            print("Training with %d synthetic image pairs (device-resident pool)" % (steps * args.batch_size))
+            # a throughput stage, not a dataset: each rank replays `pool` fixed batches of its own
+            # (seeded by rank), so only pool * batch_size distinct pairs are ever seen and the
+            # global-batch alignment of GlobalBatchSampler does not apply (--synthetic_pool 0:
+            # 100000 distinct pairs generated by the CPU DataLoader, globally aligned)
+            print("Training on a device-resident synthetic pool: %d batches per rank replayed for %d steps per epoch "
+                  "(%d distinct pairs on rank 0)" % (pool, steps, pool * max(sizes[0], 1)))
         if sizes[rank] == 0:
             return IdleLoader(GlobalBatchSampler(steps * args.batch_size, sizes, rank))
         device = getattr(args, "device", None) or ("cuda" if torch.cuda.is_available() else "cpu")
-        return DeviceSyntheticLoader(sizes[rank], args.image_size, device,
+        return DeviceSyntheticLoader(sizes[rank], args.image_size, device, pool=pool,
                                      seed=int(getattr(args, "seed", 1234)) + 1000 * rank, steps=steps)
     dataset, specs = build_train_dataset(args.stage, args.image_size, TRAIN_DS)
     workers = int(getattr(args, "num_workers", 4))

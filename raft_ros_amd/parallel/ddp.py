@@ -144,6 +144,20 @@ def all_reduce_mean(values: Dict[str, float], info: DistInfo) -> Dict[str, float
     return dict(zip(keys, t.tolist()))
 
 
+def broadcast_buffers(model: torch.nn.Module, info: DistInfo, src: int = 0) -> None:
+    """Copy every buffer (BatchNorm running statistics, ...) of ``model`` from rank ``src``.
+
+    GradSync broadcasts parameters and buffers once, at construction; after that each rank's
+    running statistics follow its own batches (and stay at their initial values on a rank
+    that never had a sample).  Called before sharded validation, so every rank scores its
+    share with the same statistics."""
+    if not info.distributed:
+        return
+    with torch.no_grad():
+        for b in model.buffers():
+            dist.broadcast(b.data, src)
+
+
 def barrier(info: DistInfo) -> None:
     if info.distributed:
         if info.device.type == "cuda":

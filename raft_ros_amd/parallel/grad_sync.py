@@ -20,10 +20,13 @@ hook, no copy), then after ``backward()``:
 
 A parameter that no rank computed a gradient for keeps ``p.grad = None`` (so AdamW skips
 it, as in single-process training and DDP).  Which parameters receive gradients is found
-once, on the first ``sync()``: a per-parameter "had a gradient" count rides in the same
+on the first ``sync()``: a per-parameter "had a gradient" count rides in the same
 all-reduce and is read back on the host that one time (RAFT uses every parameter in every
 step; a rank with no sample of the global batch -- parallel/batching.py -- has no gradient
-at all and sends zeros).
+at all and sends zeros).  A later step in which a parameter marked unused has a local
+gradient raises instead of silently dropping it; after a collective change of the trainable
+set (unfreezing a branch) every rank calls ``reset_usage()`` and the next ``sync()`` finds
+the flags again.
 
 At 21 MB the ring all-reduce over 8 MI355X is ~0.1-0.2 ms: one large collective is the cheap
 case on point-to-point xGMI links.  ``bf16=True`` halves the bytes on the wire (the buffer is
@@ -55,6 +58,7 @@ class GradSync:
         # + one "had a gradient" slot per parameter (used by the first sync only)
         self.flat = torch.empty(total + len(self.params), device=dev, dtype=torch.float32)
         self.used: Optional[List[bool]] = None
+        self.unused_idx: List[int] = []
         self.views: List[torch.Tensor] = []
         off = 0
         for p in self.params:
@@ -68,12 +72,25 @@ class GradSync:
                 for t in list(model.parameters()) + list(model.buffers()):
                     dist.broadcast(t.data, 0, group=group)
 
+    def reset_usage(self) -> None:
+        """Re-detect on the next ``sync()`` which parameters receive gradients (collective:
+        every rank calls it before the same step)."""
+        self.used = None
+
     def sync(self) -> None:
         """Average ``p.grad`` over the ranks (call after ``backward()``, before unscale / clip /
         the optimizer).  A parameter without a gradient contributes zeros (every rank must
         send the same buffer) and gets the averaged gradient of the others; one that no rank
         has a gradient for stays ``None``."""
         first = self.used is None
+        if not first:
+            # host-only check (no sync): a gradient on a parameter found unused on the first
+            # step would be dropped by the p.grad = None below
+            for i in self.unused_idx:
+                if self.params[i].grad is not None:
+                    raise RuntimeError(
+                        f"GradSync: parameter {i} received no gradient on any rank when usage was detected but has "
+                        "one now; call reset_usage() on every rank after changing the set of trained parameters")
         if first:
             flags = torch.tensor([0.0 if p.grad is None else 1.0 for p in self.params], dtype=torch.float32)
             self.flat[self.total:].copy_(flags)
@@ -105,6 +122,7 @@ class GradSync:
                 flat.mul_(1.0 / self.world)
         if first:  # one host read, on the first step only
             self.used = (self.flat[self.total:] > 0).tolist()
+            self.unused_idx = [i for i, u in enumerate(self.used) if not u]
         for p, v, u in zip(self.params, self.views, self.used):
             p.grad = v if u else None
 

@@ -60,6 +60,17 @@ def _dummy_batch(image_size):
     return (torch.zeros(1, 3, h, w), torch.zeros(1, 3, h, w), torch.zeros(1, 2, h, w), torch.zeros(1, h, w))
 
 
+def init_idle_scaler(scaler, device) -> None:
+    """Initialise an enabled GradScaler's scale on a rank that has no sample this step.
+
+    ``GradScaler.scale()`` creates the scale tensor lazily; a GradSync rank without a sample
+    never calls it, and ``unscale_`` would then fail ('_scale is None') while the other ranks
+    wait in the next all-reduce.  Scaling a zero keeps the scale at its current value on every
+    rank (the update after ``step`` sees the same all-reduced gradients everywhere)."""
+    if scaler.is_enabled():
+        scaler.scale(torch.zeros((), device=device))
+
+
 def train(args: Namespace, on_finish=None) -> str:
     info = ddp.init_distributed()
     args.rank, args.world_size = info.rank, info.world_size
@@ -138,6 +149,9 @@ def train(args: Namespace, on_finish=None) -> str:
                 stdv = np.random.uniform(0.0, 5.0)  # drawn on every rank: same RNG stream
             if idle and gsync is not None:
                 metrics = {k: torch.zeros((), device=dev) for k in METRIC_KEYS}
+                # no loss to scale here, but GradScaler.unscale_ below needs its scale tensor:
+                # the idle rank must run the same unscale / step / update as the busy ones
+                init_idle_scaler(scaler, dev)
             else:
                 image1, image2, flow, valid = [x.to(dev, non_blocking=True) for x in data_blob]
                 if args.add_noise:
@@ -183,6 +197,10 @@ def train(args: Namespace, on_finish=None) -> str:
             if info.is_main:
                 checkpoint.save_weights(model, path)
                 checkpoint.save_state(checkpoint.state_path(path), optimizer, scheduler, scaler, total_steps + 1)
+            # validation is sharded over the ranks and each rank scores its share with its own
+            # BatchNorm running statistics: take rank 0's (the reference's replica-0 statistics,
+            # train.py:138), which also covers ranks that sat idle and never updated theirs
+            ddp.broadcast_buffers(model, info)
             results = run_validation(model, args.validation, rank=info.rank, world=info.world_size)
             logger.write_dict(results)
             model.train()

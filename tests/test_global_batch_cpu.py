@@ -175,3 +175,149 @@ def test_train_two_ranks_replicas_in_sync_rank0_writes(batch, split):
         assert torch.equal(ck["module." + k], s0[k]), k
         moved += int(not torch.equal(s0[k], init[k]))
     assert moved > 50  # the optimizer did update the (rank-0-broadcast) weights
+
+
+def _bn_train_worker(rank, world, port, tmpdir):
+    """RAFT-base, chairs stage (trainable BatchNorm), global batch 1 on 2 ranks: rank 1 is idle."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    import train as train_cli
+    from raft_ros_amd.data import datasets
+    from raft_ros_amd.train import trainer
+
+    ck = os.path.join(tmpdir, f"ckpt{rank}")
+    args = train_cli.build_parser().parse_args(
+        ["--name", "bn", "--stage", "chairs", "--batch_size", "1", "--image_size", "128", "128",
+         "--num_steps", "1", "--iters", "2", "--num_workers", "0", "--ckpt_dir", ck,
+         "--log_dir", os.path.join(tmpdir, f"runs{rank}"), "--lr", "4e-4"])
+    torch.manual_seed(args.seed + rank)
+    os.makedirs(ck, exist_ok=True)
+
+    def fetch(a):  # the chairs stage's BN semantics on synthetic batches (no dataset here)
+        b = Namespace(**vars(a))
+        b.stage = "synthetic"
+        return datasets.fetch_dataloader(b)
+
+    trainer.fetch_dataloader = fetch
+    trainer.VAL_FREQ = 2  # a checkpoint + (empty) validation after the second step
+
+    def dump(model, info):
+        torch.save({k: v.detach().clone() for k, v in model.state_dict().items()},
+                   os.path.join(tmpdir, f"final{rank}.pt"))
+
+    trainer.train(args, on_finish=dump)
+
+
+@pytest.mark.timeout(900)
+def test_idle_rank_bn_statistics_broadcast_before_validation():
+    """an idle GradSync rank never runs a forward, so its BatchNorm running
+    statistics stay at 0 / 1 and its shard of a sharded validation would be scored with them.
+    The trainer broadcasts rank 0's buffers before validating: both ranks end with rank 0's
+    (trained, non-initial) statistics."""
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_bn_train_worker, args=(2, ddp.free_port(), tmp), nprocs=2, start_method="spawn")
+        s0 = torch.load(os.path.join(tmp, "final0.pt"), weights_only=True)
+        s1 = torch.load(os.path.join(tmp, "final1.pt"), weights_only=True)
+    bn = [k for k in s0 if k.startswith("cnet.") and k.endswith("running_mean")]
+    assert bn
+    assert any(float(s0[k].abs().max()) > 0 for k in bn)  # rank 0 did update them
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
+
+
+def _scaler_worker(rank, world, port, tmpdir, init_idle):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from raft_ros_amd.train.trainer import init_idle_scaler
+
+    info = ddp.init_distributed(device_type="cpu")
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(8, 8), torch.nn.ReLU(), torch.nn.Linear(8, 2))
+    _, gsync = ddp.data_parallel(model, info, impl="sync")
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2)
+    scaler = torch.amp.GradScaler("cpu", init_scale=1024.0, enabled=True)
+    err = ""
+    for step in range(3):
+        opt.zero_grad(set_to_none=True)
+        if rank == 0:  # the one busy rank of a global batch of 1
+            x = torch.randn(4, 8, generator=torch.Generator().manual_seed(step))
+            scaler.scale(model(x).square().mean() * world).backward()
+        elif init_idle:
+            init_idle_scaler(scaler, torch.device("cpu"))
+        gsync.sync()
+        try:
+            scaler.unscale_(opt)
+        except Exception as e:  # noqa: BLE001 -- the failure mode under test
+            err = repr(e)
+            break
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        scaler.step(opt)
+        scaler.update()
+    torch.save({"state": model.state_dict(), "err": err, "scale": float(scaler.get_scale())},
+               os.path.join(tmpdir, f"s{rank}.pt"))
+    if not err:
+        ddp.barrier(info)
+    ddp.cleanup()
+
+
+@pytest.mark.timeout(300)
+def test_fp16_gradscaler_with_an_idle_rank():
+    """with --amp_dtype fp16 the GradScaler is enabled, and a GradSync rank with
+    no sample never called scaler.scale(), so unscale_ failed ('_scale is None') while the busy
+    ranks waited.  The trainer initialises the idle rank's scaler: both ranks step in lockstep and
+    end bitwise equal with the same scale.  Without it, the idle rank's unscale_ raises."""
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_scaler_worker, args=(2, ddp.free_port(), tmp, True), nprocs=2, start_method="spawn")
+        r = [torch.load(os.path.join(tmp, f"s{i}.pt"), weights_only=True) for i in range(2)]
+    assert r[0]["err"] == "" and r[1]["err"] == ""
+    assert r[0]["scale"] == r[1]["scale"]
+    for k in r[0]["state"]:
+        assert torch.equal(r[0]["state"][k], r[1]["state"][k]), k
+    # negative control, one rank only (no collective for the failing rank to strand)
+    sc = torch.amp.GradScaler("cpu", enabled=True)
+    lin = torch.nn.Linear(2, 2)
+    for p in lin.parameters():
+        p.grad = torch.zeros_like(p)
+    with pytest.raises(Exception):
+        sc.unscale_(torch.optim.AdamW(lin.parameters()))
+
+
+def _usage_worker(rank, world, port, tmpdir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    info = ddp.init_distributed(device_type="cpu")
+    a, b = torch.nn.Linear(4, 4), torch.nn.Linear(4, 4)
+    model = torch.nn.ModuleList([a, b])
+    _, gsync = ddp.data_parallel(model, info, impl="sync")
+    x = torch.randn(2, 4)
+    a(x).sum().backward()  # step 1: b unused
+    gsync.sync()
+    out = {"b_none": b.weight.grad is None}
+    model.zero_grad(set_to_none=True)
+    b(a(x)).sum().backward()  # b joins (every rank): a silent drop before the fix
+    try:
+        gsync.sync()
+        out["raised"] = False
+    except RuntimeError:
+        out["raised"] = True
+    gsync.reset_usage()  # collective re-detection
+    gsync.sync()
+    out["b_after_reset"] = b.weight.grad is not None
+    torch.save(out, os.path.join(tmpdir, f"u{rank}.pt"))
+    ddp.barrier(info)
+    ddp.cleanup()
+
+
+@pytest.mark.timeout(300)
+def test_gradsync_refuses_to_drop_a_late_gradient():
+    """a parameter without a gradient on the first sync was frozen to
+    p.grad = None and a later gradient dropped silently; now the sync raises, and
+    reset_usage() re-detects the trained set."""
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_usage_worker, args=(2, ddp.free_port(), tmp), nprocs=2, start_method="spawn")
+        for r in range(2):
+            out = torch.load(os.path.join(tmp, f"u{r}.pt"), weights_only=True)
+            assert out == {"b_none": True, "raised": True, "b_after_reset": True}, out

@@ -74,6 +74,10 @@ def build_parser() -> argparse.ArgumentParser:
                         "per-rank statistics, like the reference's DataParallel replicas)")
     g.add_argument("--ddp_bf16_grads", action="store_true",
                    help="all-reduce gradients in bf16 (halves xGMI traffic)")
+    g.add_argument("--synthetic_pool", type=int, default=8,
+                   help="--stage synthetic: batches per rank in the device-resident pool that is replayed "
+                        "(a throughput check: only pool x batch distinct pairs); 0 = 100000 distinct pairs "
+                        "generated by CPU DataLoader workers (~200 pairs/s on one MI355X), globally aligned")
     g.add_argument("--profile_dir", default=None, help="capture a torch.profiler trace of steps 5-7 here")
     return p
 
