@@ -278,11 +278,6 @@ def run(args):
     for i in range(args.warmup):
         loss, metrics = step(i)
         lead.step_done(device)
-    if os.environ.get("RAFT_GC_FREEZE", "0") == "1":  # experiment: no full GC scans of the model / setup objects
-        import gc
-
-        gc.collect()
-        gc.freeze()
     _sync(device)
     if distributed:
         dist.barrier()

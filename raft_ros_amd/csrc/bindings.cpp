@@ -29,6 +29,7 @@ enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 
 // launchers (defined in the .hip translation units)
 hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s);
+hipError_t launch_corr_bwd_pair(const CorrGemmArgs& g1, const CorrGemmArgs& gt, hipStream_t s);
 hipError_t launch_fixed_to_float(const long long* in, float* out, long n, const float* fix_scale, hipStream_t s);
 hipError_t launch_local_corr_mfma(const LocalCorrArgs& a, bool backward, hipStream_t s);
 bool local_corr_gather_ok(const LocalCorrArgs& a);
@@ -211,6 +212,36 @@ void corr_gemm(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, in
   HIP_OK(launch_corr_gemm(g, cur_stream()));
 }
 
+// The AMP pyramid backward's two GEMMs in one launch (csrc/corr_volume.hip corr_bwd_pair_kernel):
+//   d1 (B, HW, C) bf16 = alpha * dL . f2t^T      dL (B, HW, ld) bf16, f2t (B, C, ld) bf16
+//   G  (B, ld, C) fp32 = alpha * dL^T . f1t^T    f1t (B, C, hp >= HW) bf16
+void corr_pyramid_bwd(const at::Tensor& dL, const at::Tensor& f2t, const at::Tensor& f1t, const at::Tensor& d1,
+                      const at::Tensor& G, double alpha) {
+  for (const auto* t : {&dL, &f2t, &f1t, &d1, &G}) check_gpu(*t, "corr_pyramid_bwd operand");
+  TORCH_CHECK(dL.scalar_type() == at::kBFloat16 && f2t.scalar_type() == at::kBFloat16 &&
+                  f1t.scalar_type() == at::kBFloat16 && d1.scalar_type() == at::kBFloat16 && G.scalar_type() == at::kFloat,
+              "raft_amd::corr_pyramid_bwd: bf16 dL / f2t / f1t / d1, fp32 G");
+  TORCH_CHECK(f2t.dim() == 3 && f1t.dim() == 3 && d1.dim() == 3 && G.dim() == 3, "raft_amd::corr_pyramid_bwd: 3-d operands");
+  for (const auto* t : {&dL, &f2t, &f1t, &d1, &G}) TORCH_CHECK(t->is_contiguous(), "raft_amd::corr_pyramid_bwd: contiguous operands");
+  const long B = f2t.size(0), C = f2t.size(1), ld = f2t.size(2), HW = d1.size(1), hp = f1t.size(2);
+  TORCH_CHECK(f1t.size(0) == B && f1t.size(1) == C && hp >= HW && d1.size(0) == B && d1.size(2) == C &&
+                  G.size(0) == B && G.size(1) == ld && G.size(2) == C && dL.numel() == B * HW * ld,
+              "raft_amd::corr_pyramid_bwd: shape mismatch");
+  TORCH_CHECK(ld % 8 == 0 && hp % 8 == 0, "raft_amd::corr_pyramid_bwd: ld and the f1t pitch must be multiples of 8");
+  if (B == 0 || HW == 0 || C == 0) return;
+  CorrGemmArgs g1{}, gt{};
+  g1.A = dL.data_ptr(); g1.lda = ld; g1.sA = HW * ld;
+  g1.B = f2t.data_ptr(); g1.ldb = ld; g1.sB = C * ld;
+  g1.C = d1.data_ptr(); g1.ldc = C; g1.sC = HW * C;
+  g1.M = (int)HW; g1.N = (int)C; g1.K = (int)ld; g1.batch = (int)B; g1.alpha = (float)alpha; g1.c_bf16 = 1; g1.cfg = 10;
+  gt.A = dL.data_ptr(); gt.lda = ld; gt.sA = HW * ld; gt.a_trans = 1;
+  gt.B = f1t.data_ptr(); gt.ldb = hp; gt.sB = C * hp;
+  gt.C = G.data_ptr(); gt.ldc = C; gt.sC = ld * C;
+  gt.M = (int)ld; gt.N = (int)C; gt.K = (int)HW; gt.batch = (int)B; gt.alpha = (float)alpha; gt.c_bf16 = 0; gt.cfg = 10;
+  const c10::DeviceGuard guard(dL.device());
+  HIP_OK(launch_corr_bwd_pair(g1, gt, cur_stream()));
+}
+
 at::Tensor gemm_nt(const at::Tensor& A, const at::Tensor& B, double alpha, at::ScalarType out_dtype) {
   check_gpu(A, "A");
   check_gpu(B, "B");
@@ -255,7 +286,8 @@ at::Tensor pyramid_unpool(const at::Tensor& G, int64_t H, int64_t W, at::IntArra
 
 // Dense-pyramid GEMM operand straight from a feature map (B, C, H, W) of any strides, bf16 or
 // fp32: levels [off, h, w] (2x2 average pools, floor), fp32 (B, ld, C) or (B, C, ld) (nchw).
-at::Tensor pyramid_operand(const at::Tensor& fmap, at::IntArrayRef segs, int64_t ld, bool blocked, bool nchw) {
+at::Tensor pyramid_operand(const at::Tensor& fmap, at::IntArrayRef segs, int64_t ld, bool blocked, bool nchw,
+                           bool bf16_out) {
   check_gpu(fmap, "fmap");
   TORCH_CHECK(fmap.dim() == 4 && (fmap.scalar_type() == at::kFloat || fmap.scalar_type() == at::kBFloat16),
               "raft_amd::pyramid_operand: fmap must be (B, C, H, W) fp32 or bf16");
@@ -278,9 +310,10 @@ at::Tensor pyramid_operand(const at::Tensor& fmap, at::IntArrayRef segs, int64_t
   a.src_bf16 = fmap.scalar_type() == at::kBFloat16 ? 1 : 0;
   a.sB = fmap.stride(0); a.sC = fmap.stride(1); a.sH = fmap.stride(2); a.sW = fmap.stride(3);
   const c10::DeviceGuard guard(fmap.device());
-  auto out = nchw ? at::empty({a.B, a.C, ld}, fmap.options().dtype(at::kFloat))
-                  : at::empty({a.B, ld, a.C}, fmap.options().dtype(at::kFloat));
-  a.out = out.data_ptr<float>();
+  const auto odt = bf16_out ? at::kBFloat16 : at::kFloat;
+  auto out = nchw ? at::empty({a.B, a.C, ld}, fmap.options().dtype(odt)) : at::empty({a.B, ld, a.C}, fmap.options().dtype(odt));
+  if (bf16_out) a.out16 = reinterpret_cast<__bf16*>(out.data_ptr());
+  else a.out = out.data_ptr<float>();
   HIP_OK(launch_pyramid_operand(a, cur_stream()));
   return out;
 }
@@ -1012,32 +1045,12 @@ ConvWgradArgs wgrad_args(at::TensorList srcs, const at::Tensor& dy, at::IntArray
 // (scripts/bench_convs.py, profiles/r4_convs_wgrad_mt.log) but +0.4 % on the training step
 // (5 of 5 interleaved A/B pairs, profiles/r4_bench_wgrad_mt_ab.log): half the workgroups, so the
 // tail stream leaves more of the chip to the encoders' backward running beside it.
-// RAFT_WGRAD3_MT=1: 64-row workgroups; 3: the 128-row tile on 8 waves (two per SIMD, where the
-// default 4-wave one holds 274 registers per lane, one wave per SIMD) -- measured 1.3 % slower
-// on the training step (451.1 / 451.2 vs 457.3 / 457.0 pairs/s, profiles/r5o_bench_*.json).
-int wgrad3_mt5() {
-  static const int v = [] {
-    const char* e = std::getenv("RAFT_WGRAD3_MT");
-    const int m = e ? std::atoi(e) : 2;
-    return (m == 1 || m == 3) ? m : 2;
-  }();
-  return v;
-}
-
-// RAFT_WGRAD_DIV=d: plan the update-block weight gradients for 1/d of the workgroups (they run
-// beside the encoder backward, which is the step's critical path; A/B runs)
-int wgrad_grid_div() {
-  static const int v = [] {
-    const char* e = std::getenv("RAFT_WGRAD_DIV");
-    const int d = e ? std::atoi(e) : 1;
-    return d >= 1 && d <= 8 ? d : 1;
-  }();
-  return v;
-}
-
+// (Measured and dropped: the 128-row tile on 8 waves, -1.3 % on the training step,
+// profiles/r5o_bench_mt2*.json; planning the weight gradients for fewer workgroups, -0.5 /
+// -1.9 %, profiles/r5ad_*.json.)
 std::tuple<at::Tensor, at::Tensor, WgradPlan> run_wgrad(ConvWgradArgs& a, bool with_bias, const at::Tensor& like) {
-  a.mt5 = wgrad3_mt5();
-  a.grid_div = wgrad_grid_div();
+  a.mt5 = 2;
+  a.grid_div = 1;
   const WgradPlan pl = plan_conv_wgrad(a);
   auto opts = like.options().dtype(at::kFloat);
   auto slab = at::empty({(long)pl.nsplit * pl.Npad * a.Kpad}, opts);
@@ -1676,8 +1689,9 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def(
       "corr_gemm(Tensor A, Tensor B, Tensor(a!) C, int M, int N, int K, int batch, int lda, int sA, int ldb, int sB, "
       "int ldc, int sC, float alpha, bool a_trans, bool split, int epi, int cfg=0) -> ()");
+  m.def("corr_pyramid_bwd(Tensor dL, Tensor f2t, Tensor f1t, Tensor(a!) d1, Tensor(b!) G, float alpha) -> ()");
   m.def("pyramid_unpool(Tensor G, int H, int W, int[] segs, bool blocked=False) -> Tensor");
-  m.def("pyramid_operand(Tensor fmap, int[] segs, int ld, bool blocked, bool nchw) -> Tensor");
+  m.def("pyramid_operand(Tensor fmap, int[] segs, int ld, bool blocked, bool nchw, bool bf16_out=False) -> Tensor");
   m.def("corr_lookup_split_into(Tensor[] pyramid, Tensor coords, int radius, Tensor(a!) out, int G, Tensor(b!)? flow8, "
         "Tensor(c!)? motion, int G_m) -> ()");
   m.def("convex_upsample(Tensor flow, Tensor mask) -> Tensor");
@@ -1703,6 +1717,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("corr_lookup_backward_", &raft_amd::corr_lookup_backward_);
   m.impl("corr_lookup_grad_rows", &raft_amd::corr_lookup_grad_rows);
   m.impl("corr_gemm", &raft_amd::corr_gemm);
+  m.impl("corr_pyramid_bwd", &raft_amd::corr_pyramid_bwd);
   m.impl("pyramid_unpool", &raft_amd::pyramid_unpool);
   m.impl("convex_upsample", &raft_amd::convex_upsample);
   m.impl("pyramid_operand", &raft_amd::pyramid_operand);

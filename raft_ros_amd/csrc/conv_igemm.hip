@@ -1283,22 +1283,20 @@ constexpr int kLdsMax = 160 * 1024;
 // Flat strips (TW == 0) take the whole 160 KB (their strip length depends on the image width);
 // 2-D tiles size the strip buffers to their halo block, so a small tile (BM = 128) fits two
 // workgroups per CU -- two waves per SIMD, and a grid quantised over 512 slots instead of 256.
-// NSX: weight-ring stages = K steps of DMA lead (3; 4 on the 2-D tiles with a halo padded to
-// 8-row pieces, so a 128 x 64 tile still fits two workgroups per CU at 78 KB)
-template <int BM, int BN, int NW, int KH, int KW, int TW, int NSX = 3>
+// NS: weight-ring stages = K steps of DMA lead.  (A 4-stage ring on the 2-D tiles measured -1 %,
+// profiles/r5y_bench_ns4*.json: the convs are not DMA-latency bound.)
+template <int BM, int BN, int NW, int KH, int KW, int TW>
 struct Fwd6Cfg {
   static constexpr int NT = KH * KW;
-  static constexpr int NS = NSX;                      // weight ring stages
-  static_assert(NS == 3 || (NS == 4 && TW > 0 && NT % 2 == 1), "ring depth");
+  static constexpr int NS = 3;                        // weight ring stages
   // chunks per unrolled block: U * NT % lcm(NS, 2) == 0 and U even, so the stage (step % NS),
   // register set (step & 1) and strip parity (chunk & 1) are compile-time
-  static constexpr int U = NS == 4 ? 4 : (NT % 3 == 0) ? 2 : 6;
+  static constexpr int U = (NT % 3 == 0) ? 2 : 6;
   static constexpr int RING = NS * BN * 128;
   // strip rows: a 2-D tile's halo block; a flat 1 x KW strip's BM + KW - 1 pixels (independent of
   // the image width); other flat strips take what the 160 KB leave
   static constexpr int HROWS2 = TW > 0 ? (BM / (TW > 0 ? TW : 1) + KH - 1) * (TW + KW - 1) : 0;
-  static constexpr int HALO = TW > 0   ? (NS == 4 ? (HROWS2 + 7) / 8 * 8
-                                                 : fwd6_halo_rows(BM / (TW > 0 ? TW : 1), TW, KH, KW, NW))
+  static constexpr int HALO = TW > 0   ? fwd6_halo_rows(BM / (TW > 0 ? TW : 1), TW, KH, KW, NW)
                               : KH == 1 ? (BM + KW - 1 + 8 * NW - 1) / (8 * NW) * (8 * NW)
                                         : 0;
   static constexpr int SB = HALO > 0 && BM <= 128 ? (HALO + 1) * 128 : fwd6_sb(BN);  // odd strip = +SB
@@ -1333,13 +1331,13 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {
 // strip of BM + (KH-1) W + KW-1 rows no longer fits in LDS): the strip is the tile's halo
 // block of (BM/TW + KH-1) x (TW + KW-1) pixels with pitch TW + KW-1, so a tap is still one
 // constant row shift, and pixels outside the image are DMA'd as zeros (no per-tap masking).
-template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW = 0, bool F16 = false, int NSX = 3>
+template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW = 0, bool F16 = false>
 __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwdArgs a, int strip_rows) {
   constexpr int NW = WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;  // wave tile
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int NT = KH * KW;
-  using CF = Fwd6Cfg<BM, BN, WGM * WGN, KH, KW, TW, NSX>;
+  using CF = Fwd6Cfg<BM, BN, WGM * WGN, KH, KW, TW>;
   constexpr int NS = CF::NS, SB = CF::SB, RING = CF::RING;
   constexpr int BI = BN / (8 * NW);  // weight pieces (8 rows x 128 B) per wave per step
   constexpr int BSTAGE = BN * 128;
@@ -1367,9 +1365,8 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   constexpr int HWD = TW + KW - 1;                  // 2-D halo block pitch (pixels)
   constexpr int HROWS = (TH + KH - 1) * HWD;        // 2-D halo block pixels
   constexpr int SPW2 = (HROWS + 8 * NW - 1) / (8 * NW);  // its DMA pieces per wave (at most)
-  // 8-row pieces of the halo block: all SPW2 * NW with the 3-stage ring (the halo is padded to
-  // them), only those holding halo rows with the 4-stage ring (HALO padded to 8 rows)
-  constexpr int NPIECE = NS == 4 ? (HROWS + 7) / 8 : SPW2 * NW;
+  // 8-row pieces of the halo block: all SPW2 * NW (the halo is padded to them)
+  constexpr int NPIECE = SPW2 * NW;
   // LDS chunk swizzle of halo row r: (r >> 1) & 7 keeps a 16-lane ds_read_b128 group on 16
   // distinct slots when its rows are consecutive, but a 3x3 tap on 16-wide tiles reads two tile
   // rows 18 halo rows apart, and the row-parity / (r >> 1) pairs then collide (2-way on every
@@ -1557,29 +1554,16 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
     constexpr int G = decltype(gc)::value;
     const bool has1 = cb + (G + 1) / NT < nchunks;  // step t+1 exists
     const bool has2 = cb + (G + 2) / NT < nchunks;  // step t+2 exists (issued one step ago)
-    const bool hasl = cb + (G + NS - 1) / NT < nchunks;  // the last step in flight exists
     // sched_barrier(0) fences keep the compiler from sinking each MFMA next to its fragment
     // read (it would otherwise trade the one-step read-ahead for registers)
     __builtin_amdgcn_sched_barrier(0);
     if (has1) {
       // step t+1 landed; steps t+2 .. t+NS-1 may stay in flight (BI pieces each, + the strip
       // of the one that opens a chunk)
-      constexpr int OPEN = ((G + 2) % NT == 0 ? 1 : 0) + (NS == 4 && (G + 3) % NT == 0 ? 1 : 0);
-      if constexpr (NS == 3) {
-        if (!has2) wait_vmcnt<0>();
-        else if constexpr (OPEN) wait_vmcnt_le<40>(BI + spw);
-        else wait_vmcnt<BI>();
-      } else {
-        if (!has2) {
-          wait_vmcnt<0>();
-        } else if (!hasl) {  // only t+2 in flight
-          if constexpr ((G + 2) % NT == 0) wait_vmcnt_le<40>(BI + spw);
-          else wait_vmcnt<BI>();
-        } else {
-          if constexpr (OPEN) wait_vmcnt_le<40>(2 * BI + spw);
-          else wait_vmcnt<2 * BI>();
-        }
-      }
+      constexpr int OPEN = (G + 2) % NT == 0 ? 1 : 0;
+      if (!has2) wait_vmcnt<0>();
+      else if constexpr (OPEN) wait_vmcnt_le<40>(BI + spw);
+      else wait_vmcnt<BI>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
@@ -1622,17 +1606,16 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
 // and read its fragments in front of the MFMAs.  v7: a single source row per pixel, so every
 // lane's DMA offsets are computed once and the K step rides in the scalar soffset; the
 // fwd6 pipeline (3-stage ring, fragments of step t+1 read behind the MFMAs of step t, raw
-// barriers, counted vmcnt); 128 x 64 tiles in 72 KB so two workgroups share a CU.
-// NS = 2: a 2-stage ring (48 KB, three workgroups per CU; one step of DMA in flight).
-template <int BM, int BN, int WGM, int WGN, bool F16 = false, int NS = 3>
-__global__ __launch_bounds__(WGM * WGN * 64) __attribute__((amdgpu_waves_per_eu(NS == 2 ? 3 : 1)))
-void conv_fwd7_kernel(const ConvFwdArgs a) {
+// barriers, counted vmcnt); 128 x 64 tiles in 72 KB so two workgroups share a CU.  (A 2-stage
+// ring at three workgroups per CU ran faster alone but -1.2 % in-step, profiles/r5ai_*.)
+template <int BM, int BN, int WGM, int WGN, bool F16 = false>
+__global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd7_kernel(const ConvFwdArgs a) {
+  constexpr int NS = 3;
   constexpr int NW = WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);  // DMA pieces per wave per step
   constexpr int STAGE = (BM + BN) * 128;                 // bytes
-  static_assert(NS == 2 || NS == 3, "ring depth");
   static_assert(AI >= 1 && BI >= 1 && TM >= 1 && TN >= 1, "tile");
   static_assert(NS * STAGE >= BM * (BN + 4) * 4, "epilogue tile must fit the ring");
   extern __shared__ __attribute__((aligned(1024))) __bf16 dsm[];
@@ -1707,8 +1690,8 @@ void conv_fwd7_kernel(const ConvFwdArgs a) {
   constexpr int G = AI + BI;
   issue(0, 0);
   if (nk > 1) issue(1, 1);
-  if (NS == 3 && nk > 2) issue(2, 2);
-  if (NS == 3 && nk > 2) wait_vmcnt<2 * G>();
+  if (nk > 2) issue(2, 2);
+  if (nk > 2) wait_vmcnt<2 * G>();
   else if (nk > 1) wait_vmcnt<G>();
   else wait_vmcnt<0>();
   __syncthreads();
@@ -1717,7 +1700,7 @@ void conv_fwd7_kernel(const ConvFwdArgs a) {
     constexpr int R = decltype(rc)::value;
     __builtin_amdgcn_sched_barrier(0);
     if (t + 1 < nk) {
-      if (NS == 3 && t + 2 < nk) wait_vmcnt<G>();  // step t+1 landed, t+2 may stay in flight
+      if (t + 2 < nk) wait_vmcnt<G>();  // step t+1 landed, t+2 may stay in flight
       else wait_vmcnt<0>();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -2518,9 +2501,9 @@ __global__ __launch_bounds__(256) void conv_n2_fwd_kernel(const ConvFwdArgs a) {
 }  // namespace
 
 namespace {
-template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW, bool F16, int NSX = 3>
+template <int BM, int BN, int WGM, int WGN, int KH, int KW, int TW, bool F16>
 bool launch_fwd6_t(const ConvFwdArgs& a, hipStream_t s) {
-  using CF = Fwd6Cfg<BM, BN, WGM * WGN, KH, KW, TW, NSX>;
+  using CF = Fwd6Cfg<BM, BN, WGM * WGN, KH, KW, TW>;
   constexpr int NW = WGM * WGN;
   int rows = 0;
   long tiles;
@@ -2533,8 +2516,8 @@ bool launch_fwd6_t(const ConvFwdArgs& a, hipStream_t s) {
     tiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
   }
   const dim3 grid((unsigned)(tiles * ((a.N + BN - 1) / BN)));
-  set_lds_limit((const void*)conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, TW, F16, NSX>, CF::LDS);
-  hipLaunchKernelGGL((conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, TW, F16, NSX>), grid, dim3(NW * 64), CF::LDS, s, a,
+  set_lds_limit((const void*)conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, TW, F16>, CF::LDS);
+  hipLaunchKernelGGL((conv_fwd6_kernel<BM, BN, WGM, WGN, KH, KW, TW, F16>), grid, dim3(NW * 64), CF::LDS, s, a,
                      rows);
   return true;
 }
@@ -2578,11 +2561,6 @@ bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
       return t51 && launch_fwd6_t<128, 64, 4, 1, 5, 1, 16, F16>(a, s);
     case 65:  // 1x5 as a flat 128-pixel strip (132 halo rows at any width), two workgroups per CU
       return t15 && launch_fwd6_t<128, 64, 4, 1, 1, 5, 0, F16>(a, s);
-    case 70:  // 62 with a 4-stage weight ring (one more K step of DMA lead), still two per CU
-      if (t33) return launch_fwd6_t<128, 64, 4, 1, 3, 3, 16, F16, 4>(a, s);
-      if (t15) return launch_fwd6_t<128, 64, 4, 1, 1, 5, 64, F16, 4>(a, s);
-      return t51 && launch_fwd6_t<128, 64, 4, 1, 5, 1, 8, F16, 4>(a, s);
-
     default:
       return false;
   }
@@ -2593,11 +2571,6 @@ bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
 static const bool kUseV7 = [] {
   const char* e = std::getenv("RAFT_CONV_V7");
   return !(e && e[0] == '0');
-}();
-// RAFT_V7_RING2=1: v7 on the 2-stage ring (cfg 71) for the automatic 1x1 choice
-static const bool kV7Ring2 = [] {
-  const char* e = std::getenv("RAFT_V7_RING2");
-  return e && e[0] == '1';
 }();
 
 template <bool F16>
@@ -2615,11 +2588,7 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
     else hipLaunchKernelGGL((conv_flow7_kernel<64, F16>), dim3((unsigned)tiles), dim3(256), 0, s, a);
     return hipGetLastError();
   }
-  static const bool use_cin8 = [] {  // RAFT_CIN8=0: the GEMM tiles (A/B runs)
-    const char* e = std::getenv("RAFT_CIN8");
-    return !(e && e[0] == '0');
-  }();
-  if ((cfg == 69 || (cfg == 0 && use_cin8)) && a.KH == 3 && a.KW == 3 && a.nsrc == 1 && a.Cin == 8 &&
+  if ((cfg == 69 || cfg == 0) && a.KH == 3 && a.KW == 3 && a.nsrc == 1 && a.Cin == 8 &&
       a.src[0].C == 8 && a.epi == 1 && a.acc_c0 >= a.N && a.split_g == 0 && a.N % 8 == 0 && a.Kpad >= 72 &&
       a.PH == 1 && a.PW == 1 && a.src[0].stride % 8 == 0 && a.out_stride % 4 == 0 &&
       (a.mask == nullptr || a.mask_stride % 4 == 0) && a.P < (1L << 31)) {
@@ -2664,7 +2633,7 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
   bool ok5 = a.KH * a.KW > 1 && a.Cin % 64 == 0 && a.N >= 64 && a.P < (1L << 30);
   for (int i = 0; i < a.nsrc; ++i) ok5 = ok5 && a.src[i].C % 64 == 0;
   int v5 = cfg >= 20 ? cfg : 0;
-  if (cfg == 41 || cfg == 45 || (cfg >= 59 && cfg <= 65) || cfg == 70) {  // v6 tiles (tests / microbenchmarks)
+  if (cfg == 41 || cfg == 45 || (cfg >= 59 && cfg <= 65)) {  // v6 tiles (tests / microbenchmarks)
     // (a strip buffer pair per chunk needs >= 3 taps per chunk: no 1x1 variant)
     const bool shape6 = (a.KH == 3 && a.KW == 3) || (a.KH * a.KW == 5 && (a.KH == 1 || a.KW == 1));
     if (!ok5 || !shape6 || a.PH != a.KH / 2 || a.PW != a.KW / 2) return hipErrorInvalidValue;
@@ -2675,12 +2644,7 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
     // shape (the rule and its measurements: choose_fwd6 in kernel_abi.h, unit-tested on the
     // host; profiles/r5b_conv6_*.log).  Before round 5: 256 x 64 / 256 x 128 one-workgroup
     // tiles (profiles/r3_bench_conv6_*.log, r4_bench_conv6_16x16.log), now forced variants.
-    static const bool ns4 = [] {  // RAFT_FWD6_NS4=1: cfg 62 -> 70 (4-stage weight ring), A/B runs
-      const char* e = std::getenv("RAFT_FWD6_NS4");
-      return e && e[0] == '1';
-    }();
-    int v6 = choose_fwd6(a.KH, a.KW, a.N, a.B, a.H, a.W);
-    if (v6 == 62 && ns4) v6 = 70;
+    const int v6 = choose_fwd6(a.KH, a.KW, a.N, a.B, a.H, a.W);
     if (v6 && launch_conv_fwd6<F16>(a, v6, s)) return hipGetLastError();
   }
   if (ok5 && v5 == 0 && cfg == 0) {
@@ -2744,13 +2708,6 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
   // v7 (lean 1x1 GEMM, 128 x 64 tiles, two workgroups per CU) for single-source 1x1 convs
   const bool v7ok = a.KH == 1 && a.KW == 1 && a.nsrc == 1 && a.src[0].C == a.Cin && a.N >= 64 &&
                     (a.src[0].stride % 8) == 0 && a.P * a.src[0].stride * 2 < (1L << 31);
-  if (cfg == 71 || (cfg == 0 && v7ok && kUseV7 && kV7Ring2)) {  // 2-stage ring, 3 WGs per CU
-    if (!v7ok) return hipErrorInvalidValue;
-    constexpr int lds7 = 2 * (128 + 64) * 128;
-    set_lds_limit((const void*)conv_fwd7_kernel<128, 64, 4, 1, F16, 2>, lds7);
-    hipLaunchKernelGGL((conv_fwd7_kernel<128, 64, 4, 1, F16, 2>), dim3(tiles(128, 64)), dim3(256), lds7, s, a);
-    return hipGetLastError();
-  }
   if (cfg == 67 || (cfg == 0 && v7ok && kUseV7)) {
     if (!v7ok) return hipErrorInvalidValue;
     constexpr int lds7 = 3 * (128 + 64) * 128;
@@ -2782,14 +2739,10 @@ hipError_t conv_wgrad_dispatch(const ConvWgradArgs& a, const WgradPlan& pl, hipS
   if (pl.kind == 3) {
     if (a.KH == 3)
       hipLaunchKernelGGL((conv_wgrad3_kernel<3, 3, 8, 8, 1, 3, F16>), grid, dim3(256), 0, s, a);
-    else if (a.KH == 5 && pl.BM == 128 && a.mt5 == 3)
-      hipLaunchKernelGGL((conv_wgrad3_kernel<5, 1, 16, 4, 1, 3, F16, 8>), grid, dim3(512), 0, s, a);
     else if (a.KH == 5 && pl.BM == 128)
       hipLaunchKernelGGL((conv_wgrad3_kernel<5, 1, 16, 4, 2, 3, F16>), grid, dim3(256), 0, s, a);
     else if (a.KH == 5)
       hipLaunchKernelGGL((conv_wgrad3_kernel<5, 1, 16, 4, 1, 3, F16>), grid, dim3(256), 0, s, a);
-    else if (pl.BM == 128 && a.mt5 == 3)
-      hipLaunchKernelGGL((conv_wgrad3_kernel<1, 5, 1, 64, 1, 3, F16, 8>), grid, dim3(512), 0, s, a);
     else if (pl.BM == 128)
       hipLaunchKernelGGL((conv_wgrad3_kernel<1, 5, 1, 64, 2, 3, F16>), grid, dim3(256), 0, s, a);
     else

@@ -505,6 +505,191 @@ __global__ __launch_bounds__(256, OCC) void corr_volume_v3_kernel(const CorrGemm
   }
 }
 
+// ---------------------------------------------------------------------------- pyramid backward
+// The two GEMMs of the AMP pyramid backward, straight from the bf16 level gradients dL
+// (B x HW x ld, every level's columns side by side; the reference differentiates through
+// its fp32 matmul + avg_pool, core/corr.py:53-60):
+//     dF1 = alpha * dL . f2cat        (M = HW,  N = C, K = ld; A rows K-contiguous)
+//     G   = alpha * dL^T . f1         (M = ld,  N = C, K = HW; A read TRANSPOSED from dL)
+// dL is 180 MB at config #2 and K is long (2.9-3.9k), so both are dL-streaming GEMMs: the
+// kernel is built to read dL once at DMA speed and keep the MFMAs fed.
+//   * 128x128 tiles, 4 waves of 64x64, 32-deep K steps in a 3-stage LDS ring filled by
+//     buffer_load ... lds (two steps of DMA lead; one barrier per step), 48 KB per workgroup;
+//     the two N tiles of an M tile are adjacent in the XCD-aware order, so the second reads its
+//     dL tile from L2;
+//   * non-transposed operands: 64-byte rows, 16-byte chunk slot = chunk ^ ((row >> 2) & 3)
+//     through the SOURCE address (conflict-free ds_read_b128 fragments, as corr_volume_v3);
+//   * transposed A (G): the DMA copies dL rows (fixed query pixel p, 128 level columns) as
+//     [k = p][m] 256-byte LDS rows, chunk slot = chunk ^ ((row & 3) << 2); the MFMA A fragment
+//     (8 consecutive k of one m per lane) is two ds_read_b64_tr_b16 -- the four rows a 16-lane
+//     group touches land on four disjoint 64-byte bank groups;
+//   * the K tail (K % 32) and the M / N edges are zero-filled by the DMA's range check (the
+//     per-chunk offset is set past the buffer), no masking in the MFMA loop.
+// Replaces hipBLASLt (torch.baddbmm) and the register-staged generic GEMM on this path.
+namespace cbw {
+constexpr int BM = 128, BN = 128, BK = 32, NS = 3;
+constexpr int TILE = 128 * BK;             // bf16 elements of one operand tile
+constexpr int STAGE = 2 * TILE;            // A + B
+}  // namespace cbw
+
+template <bool AT>
+__device__ __forceinline__ void corr_bwd_tile(const CorrGemmArgs& g, __bf16* smem, int bid) {
+  using namespace cbw;
+  const int tilesM = (g.M + BM - 1) / BM, tilesN = (g.N + BN - 1) / BN;
+  const int per_b = tilesM * tilesN;
+  const int wg = xcd_remap(bid, per_b * g.batch);
+  const int b = wg / per_b, t = wg - b * per_b;
+  const int m0 = (t / tilesN) * BM, n0 = (t - (t / tilesN) * tilesN) * BN;
+  const __bf16* A = static_cast<const __bf16*>(g.A) + (long)b * g.sA;
+  const __bf16* B = static_cast<const __bf16*>(g.B) + (long)b * g.sB;
+  const __amdgpu_buffer_rsrc_t ra =
+      vrsrc(A, (unsigned)((AT ? (long)g.K * g.lda : (long)g.M * g.lda) * 2));
+  const __amdgpu_buffer_rsrc_t rb = vrsrc(B, (unsigned)((long)g.N * g.ldb * 2));
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // DMA pieces: 8 instructions (1 KB) per operand tile and stage, 2 per wave
+  //   rows-of-K layout (A non-trans, B): instr j -> rows 16j .. 16j+15, lane -> row 16j + lane/4
+  //   transposed A: instr j -> k rows 4j .. 4j+3, lane -> k row 4j + lane/16, m chunk slot lane%16
+  unsigned abase[2], bbase[2];
+  int akc[2], bkc[2];  // k (element) offset of this lane's chunk within a K step (non-trans)
+  int akr[2];          // transposed A: k row of this lane within a K step
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int j = wave * 2 + i;
+    {
+      const int row = 16 * j + (lane >> 2), slot = lane & 3;
+      const int sc = slot ^ ((row >> 2) & 3);
+      bkc[i] = sc * 8;
+      bbase[i] = n0 + row < g.N ? (unsigned)((long)(n0 + row) * g.ldb * 2 + sc * 16) : kVOOB;
+      if constexpr (!AT) {
+        akc[i] = sc * 8;
+        abase[i] = m0 + row < g.M ? (unsigned)((long)(m0 + row) * g.lda * 2 + sc * 16) : kVOOB;
+      }
+    }
+    if constexpr (AT) {
+      const int row = 4 * j + (lane >> 4), slot = lane & 15;
+      const int sc = slot ^ ((row & 3) << 2);
+      akr[i] = row;
+      abase[i] = m0 + sc * 8 < g.M ? (unsigned)((long)row * g.lda * 2 + (m0 + sc * 8) * 2) : kVOOB;
+      akc[i] = 0;
+    }
+  }
+  auto issue = [&](int k0, int stage) __attribute__((always_inline)) {
+    const __bf16* sA = smem + stage * STAGE;
+    const __bf16* sB = sA + TILE;
+    const int kv = g.K - k0;  // valid k of this step (>= 1)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if constexpr (AT) {
+        const unsigned vo = (akr[i] < kv && abase[i] != kVOOB) ? abase[i] : kVOOB;
+        vbload16(ra, sA + (wave * 2 + i) * 512, vo, (unsigned)((long)k0 * g.lda * 2));
+      } else {
+        const unsigned vo = (akc[i] < kv && abase[i] != kVOOB) ? abase[i] : kVOOB;
+        vbload16(ra, sA + (wave * 2 + i) * 512, vo, (unsigned)k0 * 2);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const unsigned vo = (bkc[i] < kv && bbase[i] != kVOOB) ? bbase[i] : kVOOB;
+      vbload16(rb, sB + (wave * 2 + i) * 512, vo, (unsigned)k0 * 2);
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  const int fr = lane & 31, fh = lane >> 5;
+  const unsigned lds0 = (unsigned)(reinterpret_cast<uintptr_t>(smem) & 0xffffffffu);
+  // rows-of-K fragment (row r, 16-deep sub-step s): 8 consecutive k of row r
+  auto frag = [&](unsigned base, int row, int s) __attribute__((always_inline)) {
+    const int chunk = (2 * s + fh) ^ ((row >> 2) & 3);
+    return *(const vlds_bf16x8*)(uintptr_t)(base + (unsigned)(row * BK * 2 + chunk * 16));
+  };
+  // transposed A fragment of 32-row block i, sub-step s from the [k][m] tile
+  const int gi = (lane >> 4) & 1, q4 = (lane & 15) >> 2, pq = lane & 3;
+  auto tfrag = [&](unsigned base, int i, int s) __attribute__((always_inline)) {
+    const int chunk = (wm * 8 + i * 4 + gi * 2 + (pq >> 1)) ^ (q4 << 2);
+    const unsigned off = (unsigned)(chunk * 16 + (pq & 1) * 8);
+    const int r0 = s * 16 + fh * 8 + q4;
+    const s16x4 lo = tr_read(reinterpret_cast<const __bf16*>((uintptr_t)(base + (unsigned)(r0 * 256) + off)));
+    const s16x4 hi = tr_read(reinterpret_cast<const __bf16*>((uintptr_t)(base + (unsigned)((r0 + 4) * 256) + off)));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+
+  const int nk = (g.K + BK - 1) / BK;
+  issue(0, 0);
+  if (nk > 1) issue(BK, 1);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // step kt landed, kt+1 in flight
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of step kt landed; step kt-1's stage is free
+    if (kt + 2 < nk) issue((kt + 2) * BK, (kt + 2) % NS);
+    const unsigned sa = lds0 + (unsigned)((kt % NS) * STAGE * 2), sb = sa + TILE * 2;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if constexpr (AT) af[i] = tfrag(sa, i, s);
+        else af[i] = frag(sa, wm * 64 + i * 32 + fr, s);
+        bfr[i] = frag(sb, wn * 64 + i * 32 + fr, s);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // epilogue: lane = column n (32 consecutive per half-wave), registers = rows
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wn * 64 + j * 32 + fr;
+    if (n >= g.N) continue;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        if (m >= g.M) continue;
+        const float v = g.alpha * acc[i][j][r];
+        if (g.c_bf16) static_cast<__bf16*>(g.C)[(long)b * g.sC + (long)m * g.ldc + n] = static_cast<__bf16>(v);
+        else static_cast<float*>(g.C)[(long)b * g.sC + (long)m * g.ldc + n] = v;
+      }
+  }
+}
+
+__host__ __device__ inline int corr_bwd_tiles(const CorrGemmArgs& g) {
+  return ((g.M + cbw::BM - 1) / cbw::BM) * ((g.N + cbw::BN - 1) / cbw::BN) * g.batch;
+}
+
+template <bool AT>
+__global__ __launch_bounds__(256, 2) void corr_bwd_kernel(const CorrGemmArgs g) {
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[cbw::NS * cbw::STAGE];
+  corr_bwd_tile<AT>(g, smem, blockIdx.x);
+}
+
+// Both GEMMs of the pyramid backward in ONE grid: workgroups [0, n1) run dF1 (the longer K,
+// first), [n1, n1 + tiles(G)) run G.  Alone, each under-fills the chip (368 / 496 workgroups of
+// 4 waves at config #2, each latency-bound on its DMA ring); together they keep ~3 workgroups
+// per CU and share dL's lines in L2 / the Infinity Cache.  n1 is padded to a multiple of 8 so
+// blockIdx - n1 keeps the XCD of blockIdx (xcd_remap works on the local index).
+__global__ __launch_bounds__(256, 2) void corr_bwd_pair_kernel(const CorrGemmArgs g1, const CorrGemmArgs gt, int n1) {
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[cbw::NS * cbw::STAGE];
+  const int bid = blockIdx.x;
+  if (bid < n1) {
+    if (bid < corr_bwd_tiles(g1)) corr_bwd_tile<false>(g1, smem, bid);
+  } else {
+    corr_bwd_tile<true>(gt, smem, bid - n1);
+  }
+}
+
 __global__ __launch_bounds__(256) void pyramid_unpool_kernel(const UnpoolArgs u) {
   const long total = (long)u.B * u.H * u.W * u.C;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -633,11 +818,24 @@ __global__ __launch_bounds__(256) void pyramid_operand_t_kernel(const PyrOperand
   }
   __syncthreads();
   const int qs = (tid & 15) * 4;
-  const bool vst = (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
+  const bool vst = (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(a.out16 ? (void*)a.out16 : (void*)a.out) & 15) == 0;
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
     const int cl = (tid >> 4) + 16 * pass, c = c0 + cl;
     if (c >= a.C) break;
+    if (a.out16) {
+      __bf16* o16 = a.out16 + ((long)b * a.C + c) * ld + q0 + qs;
+      if (vst && q0 + qs + 4 <= ld) {
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<bf16x4*>(o16) = bf16x4{static_cast<__bf16>(tile[cl][qs]), static_cast<__bf16>(tile[cl][qs + 1]),
+                                                 static_cast<__bf16>(tile[cl][qs + 2]), static_cast<__bf16>(tile[cl][qs + 3])};
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (q0 + qs + j < ld) o16[j] = static_cast<__bf16>(tile[cl][qs + j]);
+      }
+      continue;
+    }
     float* o = a.out + ((long)b * a.C + c) * ld + q0 + qs;
     if (vst && q0 + qs + 4 <= ld) {
       *reinterpret_cast<f32x4*>(o) = f32x4{tile[cl][qs], tile[cl][qs + 1], tile[cl][qs + 2], tile[cl][qs + 3]};
@@ -660,6 +858,12 @@ __global__ __launch_bounds__(256) void pyramid_operand_kernel(const PyrOperandAr
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
   if (pyr_column(a, q, l, y, x))
     v = pyr_vec(a) ? pyr_value4<true>(a, l, b, c, y, x) : pyr_value4<false>(a, l, b, c, y, x);
+  if (a.out16) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<bf16x4*>(a.out16 + (long)i * 4) =
+        bf16x4{static_cast<__bf16>(v[0]), static_cast<__bf16>(v[1]), static_cast<__bf16>(v[2]), static_cast<__bf16>(v[3])};
+    return;
+  }
   *reinterpret_cast<f32x4*>(a.out + (long)i * 4) = v;
 }
 
@@ -1035,8 +1239,22 @@ inline int grid_for(long total) {
 
 }  // namespace
 
+static bool corr_bwd_ok(const CorrGemmArgs& g) {
+  return !g.split && !g.a_f32 && !g.b_f32 && g.epi == 0 && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
+         (g.a_trans ? g.M % 8 == 0 : g.K % 8 == 0) &&
+         (g.a_trans ? (long)g.K * g.lda : (long)g.M * g.lda) * 2 < (1L << 31) && (long)g.N * g.ldb * 2 < (1L << 31);
+}
+
 hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s) {
   if (g.M == 0 || g.N == 0 || g.batch == 0) return hipSuccess;
+  // cfg 10: the pyramid-backward kernel (bf16 operands, store epilogue, 32-bit DMA offsets)
+  if (g.cfg == 10) {
+    if (!corr_bwd_ok(g)) return hipErrorInvalidValue;
+    const long tiles = corr_bwd_tiles(g);
+    if (g.a_trans) hipLaunchKernelGGL((corr_bwd_kernel<true>), dim3((unsigned)tiles), dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((corr_bwd_kernel<false>), dim3((unsigned)tiles), dim3(256), 0, s, g);
+    return hipGetLastError();
+  }
   // bf16 x bf16 -> bf16 store (the AMP volume build): the store-oriented v2 kernel, when its
   // 16-byte DMA / store granules and 32-bit buffer offsets fit
   const bool v2 = !g.split && !g.a_trans && !g.a_f32 && !g.b_f32 && g.c_bf16 && g.epi == 0 && g.K % VBK == 0 &&
@@ -1069,6 +1287,15 @@ hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s) {
     if (g.a_trans) hipLaunchKernelGGL((corr_gemm_kernel<false, true>), grid, blk, 0, s, g);
     else hipLaunchKernelGGL((corr_gemm_kernel<false, false>), grid, blk, 0, s, g);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_corr_bwd_pair(const CorrGemmArgs& g1, const CorrGemmArgs& gt, hipStream_t s) {
+  if (g1.a_trans || !gt.a_trans || !corr_bwd_ok(g1) || !corr_bwd_ok(gt)) return hipErrorInvalidValue;
+  const int n1 = (corr_bwd_tiles(g1) + 7) / 8 * 8;
+  const long total = (long)n1 + corr_bwd_tiles(gt);
+  if (corr_bwd_tiles(g1) == 0 || corr_bwd_tiles(gt) == 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(corr_bwd_pair_kernel, dim3((unsigned)total), dim3(256), 0, s, g1, gt, n1);
   return hipGetLastError();
 }
 

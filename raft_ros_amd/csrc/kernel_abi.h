@@ -149,7 +149,7 @@ struct ConvWgradArgs {
   int Npad;       // slab rows (N rounded up to the row tile)
   int xcd_g;      // >0: XCD-grouped split mapping with xcd_g splits per XCD (set by the launcher)
   int f16;        // fp16 operands (see ConvFwdArgs::f16)
-  int mt5;        // wgrad v3 on 1x5 / 5x1 convs: 1 = 64-row workgroups, 2 = 128 rows on 4 waves, 3 = 128 rows on 8 waves
+  int mt5;        // wgrad v3 on 1x5 / 5x1 convs: 1 = 64-row workgroups, 2 = 128 rows on 4 waves (the default)
   int grid_div;   // > 1: plan for 1 / grid_div of the workgroups (leave CUs to the work beside it)
 };
 
@@ -406,6 +406,7 @@ struct PyrOperandArgs {
   int blk, nchw;
   long ld;
   float* out;
+  __bf16* out16;  // non-null: bf16 output instead (the bf16 GEMM operands, no conversion pass)
 };
 
 struct LocalCorrArgs {
@@ -485,7 +486,6 @@ inline WgradPlan plan_conv_wgrad3(const ConvWgradArgs& a) {
   // wgrads 1.2-1.3x faster, 1x5/5x1 1.05-1.1x)
   // 1x5 / 5x1 (a.mt5 == 2): 128 output channels per workgroup -- twice the MFMAs per staged
   // dY tile and halo block for the 5-tap convs, whose 64-channel steps are short
-  // (a.mt5 == 3: the 128-row tile on 8 waves, one 96 KB workgroup per CU: one round of 256)
   pl.BM = (!sq && a.mt5 >= 2) ? 128 : 64;
   pl.BN = 64 * a.KH * a.KW;
   pl.tilesM = (a.N + pl.BM - 1) / pl.BM;
@@ -495,7 +495,7 @@ inline WgradPlan plan_conv_wgrad3(const ConvWgradArgs& a) {
   const long ntiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
   long splits, g;
   choose_splits((long)pl.tilesM * pl.tilesN, ntiles, splits, g,
-                ((!sq && a.mt5 == 3) ? 256 : 512) / std::max(1, a.grid_div));
+                512 / std::max(1, a.grid_div));
   long per = (ntiles + splits - 1) / splits;
   if ((ntiles + per - 1) / per != splits) g = 0;
   pl.nsplit = (int)((ntiles + per - 1) / per);

@@ -46,9 +46,9 @@ def register() -> None:
         return coords.new_empty((B, H, W, och), dtype=out_dtype)
 
     @fake(lib + "pyramid_operand")
-    def _(fmap, segs, ld, blocked, nchw):
+    def _(fmap, segs, ld, blocked, nchw, bf16_out=False):
         B, C = fmap.shape[:2]
-        return fmap.new_empty((B, C, ld) if nchw else (B, ld, C), dtype=torch.float32)
+        return fmap.new_empty((B, C, ld) if nchw else (B, ld, C), dtype=torch.bfloat16 if bf16_out else torch.float32)
 
     @fake(lib + "convex_upsample")
     def _(flow, mask):
@@ -207,6 +207,6 @@ def register() -> None:
     # mutating ops: nothing to infer
     for name in ("conv_fwd", "conv_wgrad", "conv_wgrad_params", "gru_bwd_a", "gru_bwd_b", "masked_cast",
                  "pack_flow", "apply_delta", "n2_apply", "corr_lookup_into", "corr_lookup_split_into", "convex_upsample_backward_into",
-                 "corr_lookup_backward_", "corr_lookup_grad_rows", "corr_gemm", "local_corr_mfma", "local_corr_mfma_backward",
+                 "corr_lookup_backward_", "corr_lookup_grad_rows", "corr_gemm", "corr_pyramid_bwd", "local_corr_mfma", "local_corr_mfma_backward",
                  "enc_conv_wgrad", "enc_pack_multi"):
         fake(lib + name)(lambda *args, **kwargs: None)

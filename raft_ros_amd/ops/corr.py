@@ -41,8 +41,9 @@ import torch.nn.functional as F
 from . import reference as ref
 from ._ext import ops, use_native
 
-# RAFT_CORR_BWD_BLAS=0: the pyramid backward GEMMs on the generic MFMA kernel (A/B runs)
-BWD_BLAS = os.environ.get("RAFT_CORR_BWD_BLAS", "1") != "0"
+# RAFT_CORR_BWD_BLAS=1: the bf16 pyramid-backward GEMMs on hipBLASLt (torch.baddbmm) instead of
+# the hand-written corr_bwd_kernel (csrc/corr_volume.hip) -- an A/B switch only
+BWD_BLAS = os.environ.get("RAFT_CORR_BWD_BLAS", "0") == "1"
 
 # Lookup backward mode (see _PyramidState.add_grad): deferred row accumulation (default) or
 # one read-modify-write pass per lookup (RAFT_DEFER_LOOKUP_GRADS=0, for A/B measurements)
@@ -179,7 +180,7 @@ class _BuildPyramid(torch.autograd.Function):
         ld = off
         state.sizes, state.ld = sizes, ld
         # pooled fmap2 levels in blocked order, (B, ld, C): one HIP launch (== _concat_levels(_pooled))
-        f2cat = k.pyramid_operand(fmap2.detach(), state.segments(), ld, True, False).to(op_dt)
+        f2cat = k.pyramid_operand(fmap2.detach(), state.segments(), ld, True, False, op_dt == torch.bfloat16)
         # AMP (not split): the volume is stored in bf16 -- its lookups feed bf16 convs, and the
         # lookup kernels are bound by the bytes they gather; split mode keeps it fp32-faithful
         buf = torch.empty(B * HW, ld, device=f1.device, dtype=torch.float32 if split else torch.bfloat16)
@@ -199,12 +200,7 @@ class _BuildPyramid(torch.autograd.Function):
         fmap1, fmap2 = ctx.saved_tensors
         tail = getattr(state, "tail", None)
         if tail is not None:  # lookups' backward ran on the fused step's tail stream
-            ev = getattr(state, "tail_event", None)
-            if ev is not None:  # only up to the work queued before the batched weight gradients
-                torch.cuda.current_stream().wait_event(ev)
-                state.tail_event = None
-            else:
-                torch.cuda.current_stream().wait_stream(tail)
+            torch.cuda.current_stream().wait_stream(tail)
             state.tail = None
             if state.dbuf is not None:
                 state.dbuf.record_stream(tail)
@@ -219,17 +215,28 @@ class _BuildPyramid(torch.autograd.Function):
         HW, ld = H * W, state.ld
         k = ops()
         alpha = 1.0 / math.sqrt(C)
-        f2t = k.pyramid_operand(fmap2.detach(), state.segments(), ld, True, True)  # (B, C, ld)
-        f1t = k.pyramid_operand(fmap1.detach(), [0, H, W], _pad_to(HW, 8), False, True)  # (B, C, HW + pad)
-        if not split and dbuf.dtype == torch.bfloat16 and BWD_BLAS:
+        bf_ops = not split and dbuf.dtype == torch.bfloat16
+        # (B, C, ld) / (B, C, HW + pad) K-contiguous B operands, bf16 straight from the kernel
+        f2t = k.pyramid_operand(fmap2.detach(), state.segments(), ld, True, True, bf_ops)
+        f1t = k.pyramid_operand(fmap1.detach(), [0, H, W], _pad_to(HW, 8), False, True, bf_ops)
+        if bf_ops and not BWD_BLAS:
+            # bf16 level gradients: both GEMMs in ONE launch of the hand-written DMA-ring MFMA
+            # kernel (csrc/corr_volume.hip corr_bwd_pair_kernel):
+            #   dF1 = alpha * dL . f2cat   (M = HW, N = C, K = every level column)
+            #   G   = alpha * dL^T . f1    (M = every level column, N = C, K = HW; dL read
+            #                               transposed through ds_read_b64_tr_b16, no dL^T copy)
+            d1 = torch.empty(B, HW, C, device=fmap1.device, dtype=torch.bfloat16)
+            G = torch.empty(B, ld, C, device=fmap1.device)
+            k.corr_pyramid_bwd(dbuf.view(B, HW, ld), f2t, f1t, d1, G, alpha)
+        elif bf_ops:
             # bf16 level gradients: both are plain batched GEMMs (the unpool is its own pass), on
             # hipBLASLt -- the generic MFMA GEMM ran them at ~9-12 % of peak (215 + 158 us per step
             # at config #2, profiles/r5o_bf16_kernels.txt) on the backward's critical path
             dL, bf = dbuf.view(B, HW, ld), torch.bfloat16
             d1 = torch.baddbmm(torch.empty(B, HW, C, device=fmap1.device, dtype=bf), dL,
-                               f2t.to(bf).transpose(1, 2), beta=0.0, alpha=alpha)
+                               f2t.transpose(1, 2), beta=0.0, alpha=alpha)
             G = torch.baddbmm(torch.empty(B, ld, C, device=fmap1.device, dtype=bf), dL.transpose(1, 2),
-                              f1t[:, :, :HW].to(bf).transpose(1, 2), beta=0.0, alpha=alpha).float()
+                              f1t[:, :, :HW].transpose(1, 2), beta=0.0, alpha=alpha).float()
         else:
             d1 = torch.empty(B, HW, C, device=fmap1.device)
             G = torch.empty(B, ld, C, device=fmap1.device)

@@ -36,9 +36,9 @@ _NONE, _INSTANCE, _BATCH_TRAIN, _BATCH_EVAL = 0, 1, 2, 3
 
 # pack every conv's weight operand (forward, and the data-gradient operands of the backward) with
 # two launches at the start of the encoder forward instead of one packing launch in front of each
-# conv (RAFT_ENC_PREPACK=0: per-conv packing; =fork: the two launches on an auxiliary stream)
+# conv (RAFT_ENC_PREPACK=0: per-conv packing; the two launches on an auxiliary stream measured
+# -1.6 % and were removed, profiles/r4_enc_prepack_ab.log)
 PREPACK = os.environ.get("RAFT_ENC_PREPACK", "1") != "0"
-_PREPACK_FORK = os.environ.get("RAFT_ENC_PREPACK", "1") == "fork"
 # fp32 training: three-plane (fp32-exact) encoder forward; RAFT_ENC_SPLIT3=0 keeps the round-4
 # two-plane forward (A/B, tests)
 SPLIT3 = os.environ.get("RAFT_ENC_SPLIT3", "1") != "0"
@@ -159,9 +159,7 @@ class _Prepack:
     The job plans (the kernel arguments of every job, uploaded once) hold the parameters' data
     pointers and are rebuilt when those change.
 
-    RAFT_ENC_PREPACK=fork issues the two launches on an auxiliary stream (the block convs
-    wait on ``fwd_ready``, the end of the forward joins ``bwd_ready``); measured no faster
-    than the consumer stream at config #2 (profiles/r4_enc_prepack_ab.log).  The buffer is
+    The launches run on the consumer stream.  The buffer is
     allocated on the consuming stream and kept, so no allocator event is recorded per step;
     each step's packing follows the consumer's queued work, which includes every earlier read
     of the buffer."""
@@ -188,7 +186,6 @@ class _Prepack:
         self.device = device
         self.buf = None
         self.ptrs = None
-        self.fwd_ready = self.bwd_ready = None
 
     def _build(self, P):
         """Job plans and the packed buffer (first use, and whenever a parameter moved)."""
@@ -219,26 +216,16 @@ class _Prepack:
             self.bwd = {id(cds[0]): self.buf[a:a + n] for (cds, _, _), a, (_, n, _) in
                         zip(self.bwd_jobs, offs[len(fj):], bj)}
 
-    def issue(self, P, stream):
+    def issue(self, P):
         o = ops()
         ptrs = tuple(p.data_ptr() for p in P)
         if ptrs != self.ptrs:
             self._build(P)
             self.ptrs = ptrs
-        if stream is None:  # on the consumer stream: ordered by the stream itself
-            o.enc_pack_multi(self.fwd_plan[0], self.fwd_plan[1], self.fwd_plan[2], self.buf)
-            if self.bwd_jobs:
-                o.enc_pack_multi(self.bwd_plan[0], self.bwd_plan[1], self.bwd_plan[2], self.buf)
-            return self
-        stream.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(stream):
-            o.enc_pack_multi(self.fwd_plan[0], self.fwd_plan[1], self.fwd_plan[2], self.buf)
-            self.fwd_ready = torch.cuda.Event()
-            self.fwd_ready.record(stream)
-            if self.bwd_jobs:
-                o.enc_pack_multi(self.bwd_plan[0], self.bwd_plan[1], self.bwd_plan[2], self.buf)
-                self.bwd_ready = torch.cuda.Event()
-                self.bwd_ready.record(stream)
+        # on the consumer stream: ordered by the stream itself
+        o.enc_pack_multi(self.fwd_plan[0], self.fwd_plan[1], self.fwd_plan[2], self.buf)
+        if self.bwd_jobs:
+            o.enc_pack_multi(self.bwd_plan[0], self.bwd_plan[1], self.bwd_plan[2], self.buf)
         return self
 
 
@@ -246,13 +233,11 @@ def _prepack(L, x0, split: bool, f16: bool, stream_name: str):
     """Issue the ahead-of-time packing of ``L``'s weight operands (None: disabled / too many
     input shapes seen).  Inside a HIP-graph capture only an already-built plan is used (a
     rebuild uploads the job table, a host copy that cannot be captured; the warm-up forward
-    before the capture builds it) and never the forked packing stream, which crashed
-    capture_end in test_model_gpu.py::test_graphed_inference_matches_eager.  (Per-conv packing
-    inside the graph was ~32 serial 6 us launches per 1080p pair.)"""
+    before the capture builds it).  (Per-conv packing inside the graph was ~32 serial 6 us
+    launches per 1080p pair.)"""
     capturing = torch.cuda.is_current_stream_capturing() if x0.device.type == "cuda" else False
-    if not PREPACK or x0.device.type != "cuda" or (capturing and _PREPACK_FORK):
+    if not PREPACK or x0.device.type != "cuda":
         return None
-    from .streams import aux_stream
 
     need_bwd = torch.is_grad_enabled()
     key = (x0.shape[1], x0.shape[2], split, f16, need_bwd)
@@ -264,7 +249,7 @@ def _prepack(L, x0, split: bool, f16: bool, stream_name: str):
         pk = cache[key] = _Prepack(L, L.params, x0.shape[1], x0.shape[2], split, f16, need_bwd, x0.device)
     if capturing and tuple(p.data_ptr() for p in L.params) != pk.ptrs:
         return None
-    return pk.issue(L.params, aux_stream(x0.device, stream_name) if _PREPACK_FORK else None)
+    return pk.issue(L.params)
 
 
 def _forward(L, x0, P, split: bool = False, pk=None):
@@ -273,8 +258,6 @@ def _forward(L, x0, P, split: bool = False, pk=None):
     o = ops()
     sc, sn = L.stem
     a0, st = _conv(x0, sc, P, True, split)
-    if pk is not None and pk.fwd_ready is not None:
-        torch.cuda.current_stream(x0.device).wait_event(pk.fwd_ready)
     c0 = _stats(a0, st, sn, P, split)
     h = o.enc_apply(a0, c0, True, None, None, False, split)
     stem_rec = (x0, a0, c0, h)
@@ -302,10 +285,6 @@ def _forward(L, x0, P, split: bool = False, pk=None):
             h = o.enc_apply(acts[-1], coefs[-1], True, hin, None, True, split)
         recs.append((ins, acts, coefs, drec, h))
     y, _ = _conv(h, L.out, P, False, split, pk)
-    if pk is not None and pk.bwd_ready is not None:
-        # join the packing stream here (its data-gradient packs ran beside the blocks): nothing
-        # it writes is left in flight past the forward, whether or not a backward follows
-        torch.cuda.current_stream(x0.device).wait_event(pk.bwd_ready)
     return y, stem_rec, recs
 
 

@@ -135,7 +135,6 @@ class _Run:
         self.bias: Dict[str, torch.Tensor] = {}
         self.cout: Dict[str, int] = {}
         self.n2y: Optional[torch.Tensor] = None  # folded flow-head partials (native step), per run
-        self.wg_final: Optional[List[torch.Tensor]] = None  # weight gradients issued at the loop's end
         # every layer's operands in one launch
         mods_of = [(name, mods(block)) for name, mods, _, _, _ in _LAYERS]
         packed = C.pack_weights_multi([([m.weight for m in ms], [m.bias for m in ms], segs, scale, dgrad)
@@ -279,26 +278,17 @@ HEAD_STREAM = True  # upsampler / head backward ahead of the d-net chain (see _S
 # a separate 3x3 256 -> 2 conv that re-reads the 256-channel activation 9 times
 FOLD_N2 = os.environ.get("RAFT_FOLD_N2", "1") != "0"
 # the step's forward issued by one native op (csrc/bindings.cpp fused_step_fwd) instead of ~17
-# Python-side op calls; RAFT_NATIVE_STEP=0 keeps the Python body (A/B, and the reference for the
-# native path's tests)
-NATIVE_STEP = os.environ.get("RAFT_NATIVE_STEP", "1") != "0"
+# Python-side op calls (neutral on the GPU, profiles/r5o_bench_native*.json: the launches, not
+# Python, are the host cost); tests set it False to compare with the Python body bitwise
+NATIVE_STEP = True
 # batched weight gradients on the tail stream beside the encoders' backward (see WeightToken)
 EARLY_WGRAD = os.environ.get("RAFT_EARLY_WGRAD", "1") != "0"
-# the batched weight gradients on 1 (tail) or 2 (tail + wgrad) streams
-WGRAD_STREAMS = int(os.environ.get("RAFT_WGRAD_STREAMS", "1"))
-# RAFT_WGRAD_AT_LOOP_END=1: the batched weight gradients issued by the last refinement step's
-# backward (before the host issues the pyramid / encoder backward) instead of by the weight
-# token's backward after it.  They then overlap the encoder backward instead of running after
-# it alone (profiles/r5w_phases.txt vs r5x_phases.txt), but every kernel runs slower beside the
-# other stream's and the step time is unchanged (430.0 / 430.4 vs 430.9 / 430.5 pairs/s,
-# r5x_bench*.json): the tail of the step is throughput-bound, not dependency-bound.  Off.
-WGRAD_AT_LOOP_END = os.environ.get("RAFT_WGRAD_AT_LOOP_END", "0") == "1"
+# (Measured and dropped: the batched weight gradients split over two streams, neutral,
+# profiles/r4_bench_wgrad_mt_ab.log; issued from the last step's backward instead of the weight
+# token's, neutral, profiles/r5x_bench*.json -- the tail of the step is throughput-bound.)
 # diagnostics: a list collects (main-stream event at the token's backward, weight-gradient
 # start, end) event triples on the tail stream (scripts/host_lead.py --wgrad_timing)
 WGRAD_TIMING: Optional[list] = None
-# cost-balanced halves (per-layer wgrad time at config #2, profiles/r2_bench_convs_v5_all.log)
-_WGRAD_GROUP_A = {"zr1", "zr2", "heads", "convc1", "fh2", "convf2"}
-_WGRAD_GROUP_B = {"q1", "q2", "convc2", "conv", "mask2", "convf1"}
 
 
 def _head_stream(device) -> torch.cuda.Stream:
@@ -354,38 +344,19 @@ class _PackWeights(torch.autograd.Function):
         if run is None:  # the token's forward pass never reached the update loop
             return (None,) * (len(ctx.needs_input_grad))
         cur = torch.cuda.current_stream() if run.inp_bf.is_cuda else None
-        wg = getattr(run, "wg_final", None)
-        if wg is not None and cur is not None:  # issued at the end of the loop's backward
-            cur.wait_stream(_tail_stream(cur.device))
-            run.wg_final = None
-            run.grad_out = None
-            run.arena.bufs.clear()
-            run.tail = None
-            return (None, *wg)
         ev = getattr(run, "steps_done", None)
         if ev is not None and run.wgrads is None and cur is not None:
             ws = _tail_stream(cur.device)
             ws.wait_event(ev)  # the steps' backward on the main stream (the tail stream is ordered)
-            if WGRAD_STREAMS > 1 and len(run.done) == run.iters:
-                # the layers in two cost-balanced groups on two streams (tail, wgrad): after the
-                # encoders' backward the weight gradients are all that is left of the step
-                ws2 = aux_stream(cur.device, "wgrad")
-                ws2.wait_event(ev)
-                with torch.cuda.stream(ws):
-                    run.weight_grads(out_bufs=run.grad_out, only=_WGRAD_GROUP_A)
-                with torch.cuda.stream(ws2):
-                    grads = run.weight_grads(out_bufs=run.grad_out, only=_WGRAD_GROUP_B)
-                cur.wait_stream(ws2)
-            else:
-                with torch.cuda.stream(ws):
-                    if WGRAD_TIMING is not None:  # scripts/host_lead.py --wgrad_timing
-                        evs = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-                        evs[0].record(cur)  # main stream: the encoder backward queued before this point
-                        evs[1].record(ws)
-                    grads = run.weight_grads(out_bufs=run.grad_out)
-                    if WGRAD_TIMING is not None:
-                        evs[2].record(ws)
-                        WGRAD_TIMING.append(evs)
+            with torch.cuda.stream(ws):
+                if WGRAD_TIMING is not None:  # scripts/host_lead.py --wgrad_timing
+                    evs = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                    evs[0].record(cur)  # main stream: the encoder backward queued before this point
+                    evs[1].record(ws)
+                grads = run.weight_grads(out_bufs=run.grad_out)
+                if WGRAD_TIMING is not None:
+                    evs[2].record(ws)
+                    WGRAD_TIMING.append(evs)
             cur.wait_stream(ws)
             # no record_stream: the gradients were allocated on this stream before the event the
             # tail stream waited for, and the arena (this stream's memory too) is released only
@@ -701,21 +672,6 @@ class _Step(torch.autograd.Function):
                 run.grad_out = run.alloc_weight_grads()
                 run.steps_done = torch.cuda.Event()
                 run.steps_done.record(torch.cuda.current_stream(dev))
-                if WGRAD_AT_LOOP_END and WGRAD_STREAMS == 1 and run.wgrads is None and len(run.done) == run.iters:
-                    # issue the batched weight gradients NOW, on the tail stream: issued from the
-                    # token's backward they reached the GPU only after the host had issued the
-                    # whole encoder backward, and ran after it, alone (profiles/r5w_phases.txt:
-                    # 3.6 ms of weight-gradient kernels on one stream after the encoders).  The
-                    # pyramid backward joins the tail stream through an event recorded before
-                    # them, so it does not wait for them.
-                    ws = _tail_stream(dev)
-                    if run.pyr is not None and getattr(run.pyr, "tail", None) is ws:
-                        tail_ev = torch.cuda.Event()
-                        tail_ev.record(ws)
-                        run.pyr.tail_event = tail_ev
-                    ws.wait_event(run.steps_done)
-                    with torch.cuda.stream(ws):
-                        run.wg_final = run.weight_grads(out_bufs=run.grad_out)
             done = sorted(run.done)
             gi = run.g_all[:, :, HID:2 * HID] if len(done) == run.iters else run.g_all[done][:, :, HID:2 * HID]
             d_inp = _nchw(gi.sum(0), B, H, W)

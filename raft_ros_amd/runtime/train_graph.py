@@ -27,20 +27,16 @@ that the next replay overwrites.
 """
 from __future__ import annotations
 
-import os
 from typing import Callable, Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
 # one process: the gradients are the tensors the captured backward allocates (autograd steals
-# them: no accumulate kernels -- a pre-bound flat buffer costs one add kernel per parameter,
-# ~0.5 ms/step at config #2); RAFT_GRAPH_FLAT=1 binds the flat buffer anyway (A/B)
-_FLAT_1 = os.environ.get("RAFT_GRAPH_FLAT", "0") == "1"
-# RAFT_GRAPH_HP=1: capture and replay on the high-priority step stream (ops/streams.py
-# step_stream), as the eager step runs.  Off: it made the replay much slower on MI355X
-# (284-292 vs 402 pairs/s default-priority, profiles/r5n_bench_graph*.json)
-_GRAPH_HP = os.environ.get("RAFT_GRAPH_HP", "0") == "1"
+# them: no accumulate kernels; a pre-bound flat buffer costs one add kernel per parameter and
+# measured no faster, profiles/r5n_bench_graph_flat.json).  The graphs are captured and replayed
+# at default priority: on the high-priority step stream the replay ran 284-292 vs 402 pairs/s
+# (profiles/r5n_bench_graph*.json).
 
 
 class GraphedTrainStep:
@@ -84,7 +80,7 @@ class GraphedTrainStep:
             o += n
 
     def _use_flat(self) -> bool:
-        return self.world > 1 or _FLAT_1 or not self.params[0].is_cuda
+        return self.world > 1 or not self.params[0].is_cuda
 
     def _grads(self) -> List[torch.Tensor]:
         return [p.grad for p in self.params if p.grad is not None]
@@ -164,12 +160,7 @@ class GraphedTrainStep:
             self._bind_flat_grads()
         self.skipped = torch.zeros((), device=dev)
         snap = self._snapshot()
-        if _GRAPH_HP:
-            from ..ops.streams import step_stream
-
-            side = step_stream(dev)
-        else:
-            side = torch.cuda.Stream(device=dev)
+        side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for _ in range(self.warmup):  # lazy init, MIOpen find, allocator warm-up
@@ -209,17 +200,7 @@ class GraphedTrainStep:
             for s, t in zip(self.static_in, batch):
                 if s.data_ptr() != t.data_ptr():
                     s.copy_(t, non_blocking=True)
-        if _GRAPH_HP:
-            from ..ops.streams import step_stream
-
-            cur = torch.cuda.current_stream(image1.device)
-            hp = step_stream(image1.device)
-            hp.wait_stream(cur)
-            with torch.cuda.stream(hp):
-                self._replay()
-            cur.wait_stream(hp)
-        else:
-            self._replay()
+        self._replay()
         return self.out
 
     def _replay(self):

@@ -122,7 +122,7 @@ static void test_wgrad_plans() {
             if (Cin % nsrc || (Cin / nsrc) % (nsrc > 1 ? 128 : 8)) continue;
             ConvWgradArgs a = make_args(d[0], d[1], d[2], s[0], s[1], Cin, N, nsrc);
             if (!wgrad_supported(a)) continue;
-            for (int mt5 = 1; mt5 <= 3; ++mt5) {  // 64- / 128-row (4- / 8-wave) workgroups of the 1x5 / 5x1 v3 kernel
+            for (int mt5 = 1; mt5 <= 2; ++mt5) {  // 64- / 128-row workgroups of the 1x5 / 5x1 v3 kernel
               a.mt5 = mt5;
               check_plan(a);
               if (s[0] * s[1] == 5 && plan_conv_wgrad(a).kind == 3)

@@ -51,6 +51,37 @@ def test_corr_volume_v2_matches_generic(cuda, M, N, K, batch):
         assert (out - outs[1]).abs().max().item() <= 2 * want.abs().max().item() * 2 ** -8, cfg
 
 
+@pytest.mark.parametrize("HW,ld,C,batch", [(2852, 3936, 256, 2), (130, 200, 72, 3), (21, 48, 136, 1)])
+def test_corr_bwd_kernel_matches_fp32(cuda, HW, ld, C, batch):
+    """The pyramid-backward GEMMs on corr_bwd_kernel (cfg 10) vs fp32 matmuls of the same bf16
+    operands: dF1 = a dL . f2t^T (bf16 out) and G = a dL^T . f1t^T (A read transposed, fp32 out),
+    with K tails (HW % 32, ld % 32), partial M / N tiles and a padded f1t pitch; the outputs start
+    as NaN so an unwritten element fails."""
+    torch.manual_seed(9)
+    ops = _ops()
+    a = 0.0625
+    dL = torch.randn(batch, HW, ld, device=cuda).bfloat16()
+    f2t = torch.randn(batch, C, ld, device=cuda).bfloat16()
+    hp = (HW + 7) // 8 * 8
+    f1t = torch.zeros(batch, C, hp, device=cuda).bfloat16()
+    f1t[:, :, :HW] = torch.randn(batch, C, HW, device=cuda).bfloat16()
+    d1 = torch.full((batch, HW, C), float("nan"), device=cuda, dtype=torch.bfloat16)
+    ops.corr_gemm(dL, f2t, d1, HW, C, ld, batch, ld, HW * ld, ld, C * ld, C, HW * C, a, False, False, 0, 10)
+    want1 = a * torch.matmul(dL.float(), f2t.float().transpose(1, 2))
+    assert torch.isfinite(d1.float()).all()
+    torch.testing.assert_close(d1.float(), want1, rtol=1e-2, atol=1e-2 * want1.abs().max().item())
+    G = torch.full((batch, ld, C), float("nan"), device=cuda)
+    ops.corr_gemm(dL, f1t, G, ld, C, HW, batch, ld, HW * ld, hp, C * hp, C, ld * C, a, True, False, 0, 10)
+    want2 = a * torch.matmul(dL.float().transpose(1, 2), f1t[:, :, :HW].float().transpose(1, 2))
+    assert torch.isfinite(G).all()
+    torch.testing.assert_close(G, want2, rtol=1e-3, atol=1e-3 * want2.abs().max().item())
+    # both GEMMs in one launch (the training path): the same tiles, bitwise
+    d1p = torch.full_like(d1, float("nan"))
+    Gp = torch.full_like(G, float("nan"))
+    ops.corr_pyramid_bwd(dL, f2t, f1t, d1p, Gp, a)
+    assert torch.equal(d1p, d1) and torch.equal(Gp, G)
+
+
 def test_gemm_nt_identity_asymmetric(cuda):
     M, K = 128, 128
     A = torch.eye(M, K, device=cuda).bfloat16()[None]
