@@ -211,7 +211,11 @@ def run(args):
             from raft_ros_amd.parallel.grad_sync import GradSync
 
             gsync = GradSync(model)
-    optimizer, scheduler = fetch_optimizer(oargs, model, capturable=train_graph)
+    # eager bf16 / fp32 steps: clip + AdamW as one native op (ops/optim.py), as the trainer runs it
+    native_opt = args.impl == "native" and not train_graph and args.mode == "train" and (
+        args.fp32 or args.amp_dtype == "bf16") and device.type == "cuda"
+    optimizer, scheduler = fetch_optimizer(oargs, model, capturable=train_graph, clip=1.0 if native_opt else None)
+    native_opt = not isinstance(optimizer, torch.optim.AdamW)
     scaler = torch.amp.GradScaler("cuda", enabled=args.amp_dtype == "fp16" and not args.fp32 and device.type == "cuda")
 
     H, W = args.image_size
@@ -241,11 +245,14 @@ def run(args):
         scaler.scale(loss).backward()
         if gsync is not None:
             gsync.sync()
-        scaler.unscale_(optimizer)
-        torch.nn.utils.clip_grad_norm_(params, 1.0)
-        scaler.step(optimizer)
+        if native_opt:
+            optimizer.step()  # clip (1.0) + AdamW
+        else:
+            scaler.unscale_(optimizer)
+            torch.nn.utils.clip_grad_norm_(params, 1.0)
+            scaler.step(optimizer)
+            scaler.update()
         scheduler.step()
-        scaler.update()
         return loss, metrics
 
     if train_graph:
@@ -344,6 +351,7 @@ def run(args):
                 "mode": args.mode,
                 "alternate_corr": args.alternate_corr,
                 "hip_graph": bool(train_graph or (args.graph is not False and args.mode == "infer")),
+                "optimizer": "native clip+AdamW (2 launches)" if native_opt else "torch clip_grad_norm_ + AdamW",
             },
             "final_loss": round(float(loss.item()), 4),
             "epe_synthetic": round(float(metrics["epe"].item()), 4),

@@ -593,6 +593,24 @@ inline bool up_seg_ok(unsigned long addr, int esz, long sN, long sC, long sH, lo
 // ============================================================================ correlation build
 // Row tiles per group of the v2 volume build's tile order (cfg 2-5 force 1 / 2 / 4 / 16):
 // 8 while one image's B operand (N x K bf16) fits 8 MB, 4 beyond (the 1080p store stream).
+// Clip + AdamW optimizer step (optim.hip): parameter chunks of kAdamChunk elements, one block
+// each; gradients of up to kAdamGrads tensors per launch travel in the kernel arguments.
+constexpr int kAdamChunk = 16384;
+constexpr int kAdamGrads = 128;
+struct AdamArgs {
+  const float* g[kAdamGrads];  // gradients of tensors [t0, t0 + kAdamGrads)
+  int t0;
+  const long long* ptrs;       // [ntensor][3]: parameter, exp_avg, exp_avg_sq (fp32, grad layout)
+  const int* blocks;           // [nblocks][3]: tensor, first element, length
+  int blk0, nblocks;           // first block of this launch; blocks of the whole parameter set
+  float* partial;              // [nblocks] sums of squared gradients
+  float* steps;                // [2] step counter slots: read [par], block 0 writes [par ^ 1]
+  int par;
+  float lr, beta1, beta2, eps, wd, max_norm;  // max_norm <= 0: no clipping
+  float* norm_out;             // the total gradient norm (may be null)
+  float* skipped;              // += 1 when the norm is not finite (may be null)
+};
+
 RAFT_HD inline int corr_group_rows(long N, long K, int cfg) {
   if (cfg >= 2 && cfg <= 5) return cfg == 2 ? 1 : cfg == 3 ? 2 : cfg == 4 ? 4 : 16;
   if (cfg == 7) return 8;
@@ -605,6 +623,8 @@ RAFT_HD inline int corr_group_rows(long N, long K, int cfg) {
 #include <hip/hip_runtime_api.h>
 
 namespace raft_amd {
+// optim.hip
+hipError_t launch_adamw(const AdamArgs& a, int nblk, bool update, hipStream_t s);
 // conv_igemm.hip
 hipError_t launch_conv_fwd(const ConvFwdArgs& a, hipStream_t s);
 hipError_t launch_conv_wgrad(ConvWgradArgs a, const WgradPlan& pl, hipStream_t s);

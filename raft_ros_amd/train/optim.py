@@ -14,11 +14,23 @@ def count_parameters(model) -> int:
     return sum(p.numel() for p in model.parameters() if p.requires_grad)
 
 
-def fetch_optimizer(args, model, capturable: bool = False):
+def fetch_optimizer(args, model, capturable: bool = False, clip: float | None = None):
     """``capturable=True`` (GPU): lr lives in a device tensor and the step counter on the
     device, so the optimizer step can be captured in a HIP graph
-    (``runtime.GraphedTrainStep``); the scheduler updates the lr tensor in place."""
+    (``runtime.GraphedTrainStep``); the scheduler updates the lr tensor in place.
+
+    ``clip`` (eager GPU training without a GradScaler): the native clip + AdamW step
+    (ops/optim.py ``ClipAdamW``: clip_grad_norm_(clip) and AdamW in two launches, ~2.5 ms less
+    host time per step); its ``step(skipped=...)`` clips, and returns the gradient norm."""
     params = [p for p in model.parameters() if p.requires_grad]
+    if clip is not None and not capturable:
+        from ..ops.optim import ClipAdamW, usable
+
+        if usable(params):
+            optimizer = ClipAdamW(params, lr=args.lr, weight_decay=args.wdecay, eps=args.epsilon, max_norm=float(clip))
+            scheduler = optim.lr_scheduler.OneCycleLR(optimizer, args.lr, args.num_steps + 100, pct_start=0.05,
+                                                      cycle_momentum=False, anneal_strategy="linear")
+            return optimizer, scheduler
     fused = bool(params) and params[0].is_cuda
     capturable = capturable and fused
     lr = torch.tensor(float(args.lr), device=params[0].device) if capturable else args.lr

@@ -107,8 +107,10 @@ def train(args: Namespace, on_finish=None) -> str:
 
     args.device = str(dev)  # batched augmentation runs on the rank's device
     train_loader = fetch_dataloader(args)
-    optimizer, scheduler = fetch_optimizer(args, model)
     use_scaler = bool(args.mixed_precision) and getattr(args, "amp_dtype", "bf16") == "fp16" and dev.type == "cuda"
+    # without a GradScaler the clip + AdamW step is one native op (ops/optim.py ClipAdamW)
+    optimizer, scheduler = fetch_optimizer(args, model, clip=None if use_scaler else args.clip)
+    native_opt = not isinstance(optimizer, torch.optim.AdamW)
     scaler = torch.amp.GradScaler("cuda", enabled=use_scaler)
     logger = Logger(model, scheduler, log_dir=os.path.join(args.log_dir, args.name), enabled=info.is_main,
                     pairs_per_step=args.batch_size,
@@ -171,11 +173,16 @@ def train(args: Namespace, on_finish=None) -> str:
                 with trace_range("grad_sync"):
                     gsync.sync()
             scaler.unscale_(optimizer)
-            gnorm = torch.nn.utils.clip_grad_norm_(clip_params, args.clip)
-            if use_scaler:
+            if native_opt:
+                # clip + AdamW in two launches; a non-finite norm skips the update on device and
+                # counts in `skipped` (no host sync)
+                optimizer.step(skipped=skipped)
+            elif use_scaler:
+                torch.nn.utils.clip_grad_norm_(clip_params, args.clip)
                 scaler.step(optimizer)  # GradScaler already skips non-finite steps
                 scaler.update()
             else:
+                gnorm = torch.nn.utils.clip_grad_norm_(clip_params, args.clip)
                 # failure guard without a host sync: a non-finite gradient norm (identical on all
                 # ranks after the all-reduce) turns the fused AdamW update into a no-op on device
                 bad = (~torch.isfinite(gnorm)).float()

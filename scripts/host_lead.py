@@ -33,6 +33,10 @@ def main():
     ap.add_argument("--wgrad_timing", action="store_true",
                     help="per step: when the batched weight gradients start / end on the tail stream, relative "
                          "to the step's backward start and to the main stream reaching the weight token")
+    ap.add_argument("--torch_opt", action="store_true",
+                    help="torch clip_grad_norm_ + fused AdamW instead of the native clip + AdamW op")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--image_size", type=int, nargs=2, default=[368, 496])
     ap.add_argument("--cprofile", type=int, default=0,
                     help="> 0: also profile the host side of this many steps (cProfile, top functions)")
     args = ap.parse_args()
@@ -45,8 +49,11 @@ def main():
     torch.cuda.set_device(dev)
     model = RAFT(Namespace(small=False, mixed_precision=True, amp_dtype="bf16", dropout=0.0)).to(dev)
     model = model.to(memory_format=torch.channels_last).train()
-    opt, sched = fetch_optimizer(Namespace(lr=4e-4, wdecay=1e-4, epsilon=1e-8, num_steps=100000), model)
-    pool = [synthetic_batch(8, 368, 496, seed=i, device=dev) for i in range(4)]
+    opt, sched = fetch_optimizer(Namespace(lr=4e-4, wdecay=1e-4, epsilon=1e-8, num_steps=100000), model,
+                                 clip=None if args.torch_opt else 1.0)
+    native_opt = not isinstance(opt, torch.optim.AdamW)
+    print("optimizer:", type(opt).__name__)
+    pool = [synthetic_batch(args.batch, *args.image_size, seed=i, device=dev) for i in range(4)]
     stream = torch.cuda.Stream(device=dev, priority=-1) if args.hp else torch.cuda.current_stream(dev)
     phases = ["forward", "loss", "backward", "clip", "optimizer"]
 
@@ -76,7 +83,8 @@ def main():
         loss.backward()
         th.append(time.perf_counter())
         ev[3].record()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        if not native_opt:  # (the native op clips inside its step)
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
         th.append(time.perf_counter())
         ev[4].record()
         opt.step()

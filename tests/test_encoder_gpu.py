@@ -228,16 +228,13 @@ def test_split_encoder_inference_is_fp32_faithful(name):
     assert err < 2e-4, (name, err)  # measured 1e-5 (basic) .. 5.5e-5 (small)
 
 
-@pytest.mark.parametrize("mode", ["bf16", "f16", "split", "split_infer", "bf16_fork", "split_fork"])
+@pytest.mark.parametrize("mode", ["bf16", "f16", "split", "split_infer"])
 @pytest.mark.parametrize("name", ["basic_batch", "small_instance"])
 def test_prepacked_weights_match_per_conv_packing(name, mode, monkeypatch):
-    """Weights packed ahead by the one-launch multi-conv packing (ops/encoder.py _Prepack; _fork:
-    on an auxiliary stream) give bit-identical outputs and gradients to the per-conv packing,
-    also after an in-place weight update (the optimizer step the next forward's packing must
-    see)."""
+    """Weights packed ahead by the one-launch multi-conv packing (ops/encoder.py _Prepack) give
+    bit-identical outputs and gradients to the per-conv packing, also after an in-place weight
+    update (the optimizer step the next forward's packing must see)."""
     from raft_ros_amd.ops import encoder as enc_native
-    monkeypatch.setattr(enc_native, "_PREPACK_FORK", mode.endswith("_fork"))
-    mode = mode.replace("_fork", "")
     torch.manual_seed(0)
     base = _encoders()[name]().to(cuda).to(memory_format=torch.channels_last).train()
     nets = {flag: copy.deepcopy(base) for flag in (True, False)}
