@@ -380,7 +380,8 @@ __global__ __launch_bounds__(256, 2) void corr_volume_bf16_kernel(const CorrGemm
 // columns of one row), so the epilogue writes the LDS tile as 8-byte runs instead of 2-byte
 // scattered stores.  Swizzle for BK-deep rows: R = 128 / BK rows share a 256-byte bank line,
 // 16-byte chunk slot = chunk ^ ((row / R) & (BK / 8 - 1)).
-template <int BK, int OCC>
+// NT: the 16-byte output stores carry the nontemporal hint (streamed past the caches; cfg 11)
+template <int BK, int OCC, bool NT = false>
 __global__ __launch_bounds__(256, OCC) void corr_volume_v3_kernel(const CorrGemmArgs g) {
   constexpr int CH = BK / 8, R = 128 / BK, RPI = 512 / BK;  // chunks / row, rows / bank line, rows / DMA instr
   constexpr int STAGE = (VBM + VBN) * BK;                      // bf16 elements
@@ -496,7 +497,8 @@ __global__ __launch_bounds__(256, OCC) void corr_volume_v3_kernel(const CorrGemm
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(ct + row * VCP + c8);
     __bf16* dst = C + (long)m * g.ldc + n;
     if (n + 8 <= g.N) {
-      *reinterpret_cast<bf16x8*>(dst) = v;
+      if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(dst));
+      else *reinterpret_cast<bf16x8*>(dst) = v;
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e)
@@ -1270,10 +1272,23 @@ hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s) {
       const char* e = std::getenv("RAFT_CORR_V3");
       return !(e && e[0] == '0');
     }();
-    if ((g.cfg == 0 && v3) || g.cfg == 6 || g.cfg == 7) {
+    // nontemporal output stores for volumes larger than the 256 MB Infinity Cache (1080p: 2.8 GB,
+    // 1286 -> 1144 us standalone, profiles/r6g_bench_corr.log; the training volume, 180 MB, is
+    // read back by the lookups right away and keeps its cache lines: 68.5 vs 70.4 us with NT).
+    // RAFT_CORR_NT=1 / 0 forces it on / off (A/B).
+    static const int nt_env = [] {
+      const char* e = std::getenv("RAFT_CORR_NT");
+      return e ? (e[0] == '1' ? 1 : 0) : -1;
+    }();
+    const bool nt = nt_env >= 0 ? nt_env == 1 : (long)g.M * g.batch * g.ldc * 2 > (256L << 20);
+    if (g.cfg == 0 && v3 && nt) {
+      hipLaunchKernelGGL((corr_volume_v3_kernel<32, 4, true>), dim3((unsigned)tiles), dim3(256), 0, s, g);
+    } else if ((g.cfg == 0 && v3) || g.cfg == 6 || g.cfg == 7) {
       hipLaunchKernelGGL((corr_volume_v3_kernel<32, 4>), dim3((unsigned)tiles), dim3(256), 0, s, g);
     } else if (g.cfg == 8) {
       hipLaunchKernelGGL((corr_volume_v3_kernel<64, 2>), dim3((unsigned)tiles), dim3(256), 0, s, g);
+    } else if (g.cfg == 11) {
+      hipLaunchKernelGGL((corr_volume_v3_kernel<32, 4, true>), dim3((unsigned)tiles), dim3(256), 0, s, g);
     } else {
       hipLaunchKernelGGL(corr_volume_bf16_kernel, dim3((unsigned)tiles), dim3(256), 0, s, g);
     }

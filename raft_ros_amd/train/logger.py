@@ -49,7 +49,8 @@ class Logger:
         return self.writer or None
 
     def _lr(self) -> float:
-        return self.scheduler.get_last_lr()[0] if self.scheduler is not None else 0.0
+        # float(): a capturable optimizer (train.py --graph) keeps lr in a device tensor
+        return float(self.scheduler.get_last_lr()[0]) if self.scheduler is not None else 0.0
 
     def _print_training_status(self):
         keys = sorted(self.running_loss)

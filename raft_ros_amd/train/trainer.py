@@ -101,16 +101,38 @@ def train(args: Namespace, on_finish=None) -> str:
         convert_sync_bn(model.cnet)
     if args.stage != "chairs":
         model.freeze_bn()
-    net, gsync = ddp.data_parallel(model, info, impl=getattr(args, "dp_impl", "sync"),
-                                   bucket_cap_mb=getattr(args, "bucket_mb", 10.0),
-                                   bf16_grads=getattr(args, "ddp_bf16_grads", False))
+    use_scaler = bool(args.mixed_precision) and getattr(args, "amp_dtype", "bf16") == "fp16" and dev.type == "cuda"
+    # --graph: the whole step replayed as HIP graph(s) (runtime/train_graph.py), which does its own
+    # flat-buffer gradient all-reduce between two graphs -- no GradSync / DDP wrapper
+    use_graph = bool(getattr(args, "graph", False)) and dev.type == "cuda" and not use_scaler
+    if use_graph:
+        net, gsync = model, None
+    else:
+        net, gsync = ddp.data_parallel(model, info, impl=getattr(args, "dp_impl", "sync"),
+                                       bucket_cap_mb=getattr(args, "bucket_mb", 10.0),
+                                       bf16_grads=getattr(args, "ddp_bf16_grads", False))
 
     args.device = str(dev)  # batched augmentation runs on the rank's device
     train_loader = fetch_dataloader(args)
-    use_scaler = bool(args.mixed_precision) and getattr(args, "amp_dtype", "bf16") == "fp16" and dev.type == "cuda"
-    # without a GradScaler the clip + AdamW step is one native op (ops/optim.py ClipAdamW)
-    optimizer, scheduler = fetch_optimizer(args, model, clip=None if use_scaler else args.clip)
+    # without a GradScaler the eager clip + AdamW step is one native op (ops/optim.py ClipAdamW);
+    # the graphed step captures torch's capturable fused AdamW (device lr and step count)
+    optimizer, scheduler = fetch_optimizer(args, model, capturable=use_graph,
+                                           clip=None if (use_scaler or use_graph) else args.clip)
     native_opt = not isinstance(optimizer, torch.optim.AdamW)
+    runner = None
+    if use_graph:
+        from ..runtime import GraphedTrainStep
+
+        w = 0.0 if sizes[info.rank] == 0 else weight  # an idle rank replays a zero-weight dummy sample
+
+        def weighted_loss(preds, flow, valid, gamma):
+            loss, m = sequence_loss(preds, flow, valid, gamma)
+            if w != 1.0:
+                loss = loss * w
+                m = {k: v * w for k, v in m.items()}
+            return loss, m
+
+        runner = GraphedTrainStep(model, optimizer, weighted_loss, iters=args.iters, clip=args.clip, gamma=args.gamma)
     scaler = torch.amp.GradScaler("cuda", enabled=use_scaler)
     logger = Logger(model, scheduler, log_dir=os.path.join(args.log_dir, args.name), enabled=info.is_main,
                     pairs_per_step=args.batch_size,
@@ -138,8 +160,49 @@ def train(args: Namespace, on_finish=None) -> str:
     prof = maybe_profiler(getattr(args, "profile_dir", None))
     profiler = prof.__enter__()
     clip_params = [p for p in model.parameters() if p.requires_grad]  # walked once, not per step
+
+    def _after_step(step: int) -> int:
+        """Checkpoint + validation every VAL_FREQ steps (reference train.py:186-199); -> step + 1."""
+        total_steps = step
+        if total_steps % VAL_FREQ == VAL_FREQ - 1:
+            path = os.path.join(args.ckpt_dir, "%d_%s.pth" % (total_steps + 1, args.name))
+            if info.is_main:
+                checkpoint.save_weights(model, path)
+                checkpoint.save_state(checkpoint.state_path(path), optimizer, scheduler, scaler, total_steps + 1)
+            # validation is sharded over the ranks and each rank scores its share with its own
+            # BatchNorm running statistics: take rank 0's (the reference's replica-0 statistics,
+            # train.py:138), which also covers ranks that sat idle and never updated theirs
+            ddp.broadcast_buffers(model, info)
+            results = run_validation(model, args.validation, rank=info.rank, world=info.world_size)
+            logger.write_dict(results)
+            model.train()
+            if args.stage != "chairs":
+                model.freeze_bn()
+            ddp.barrier(info)
+        return total_steps + 1
+
     for data_blob in _infinite(train_loader, set_epoch):
         injector.before_step(total_steps)
+        if runner is not None:
+            # --graph: the step is one graph replay (two around the gradient all-reduce); an idle
+            # rank replays its zero-weight dummy sample to stay in the collective
+            if data_blob is None:
+                data_blob = _dummy_batch(args.image_size)
+            image1, image2, flow, valid = [x.to(dev, non_blocking=True) for x in data_blob]
+            if args.add_noise:
+                stdv = np.random.uniform(0.0, 5.0)  # drawn on every rank: same RNG stream
+                image1 = (image1 + stdv * torch.randn_like(image1)).clamp(0.0, 255.0)
+                image2 = (image2 + stdv * torch.randn_like(image2)).clamp(0.0, 255.0)
+            _, metrics, _ = runner(image1, image2, flow, valid)
+            scheduler.step()  # writes the captured optimizer's device lr
+            logger.push(metrics)
+            if profiler is not None:
+                profiler.step()
+            lead.step_done(dev)
+            total_steps = _after_step(total_steps)
+            if total_steps > args.num_steps:
+                break
+            continue
         # the step on the high-priority step stream (ops/streams.py; RAFT_HP_MAIN=0 disables)
         with step_context(dev):
             optimizer.zero_grad(set_to_none=True)
@@ -198,32 +261,16 @@ def train(args: Namespace, on_finish=None) -> str:
             if profiler is not None:
                 profiler.step()
         lead.step_done(dev)
-
-        if total_steps % VAL_FREQ == VAL_FREQ - 1:
-            path = os.path.join(args.ckpt_dir, "%d_%s.pth" % (total_steps + 1, args.name))
-            if info.is_main:
-                checkpoint.save_weights(model, path)
-                checkpoint.save_state(checkpoint.state_path(path), optimizer, scheduler, scaler, total_steps + 1)
-            # validation is sharded over the ranks and each rank scores its share with its own
-            # BatchNorm running statistics: take rank 0's (the reference's replica-0 statistics,
-            # train.py:138), which also covers ranks that sat idle and never updated theirs
-            ddp.broadcast_buffers(model, info)
-            results = run_validation(model, args.validation, rank=info.rank, world=info.world_size)
-            logger.write_dict(results)
-            model.train()
-            if args.stage != "chairs":
-                model.freeze_bn()
-            ddp.barrier(info)
-
-        total_steps += 1
+        total_steps = _after_step(total_steps)
         if total_steps > args.num_steps:
             break
 
     prof.__exit__(None, None, None)
+    nskip = runner.skipped if runner is not None and runner.skipped is not None else skipped
     if info.is_main:
         dt = time.perf_counter() - t0
         print(f"trained {total_steps} steps in {dt:.1f}s ({args.batch_size * total_steps / dt:.2f} "
-              f"pairs/s, {int(skipped.item())} non-finite steps skipped)")
+              f"pairs/s, {int(nskip.item())} non-finite steps skipped)")
     logger.close()
     path = os.path.join(args.ckpt_dir, "%s.pth" % args.name)
     if info.is_main:

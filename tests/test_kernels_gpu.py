@@ -39,7 +39,7 @@ def test_corr_volume_v2_matches_generic(cuda, M, N, K, batch):
     A = torch.randn(batch, M, K, device=cuda).bfloat16()
     B = torch.randn(batch, N, K, device=cuda).bfloat16()
     outs = []
-    cfgs = (0, 1, 7, 8, 9)  # 0 / 7 / 8: the v3 kernel (BK 32 at four per CU, GM 8, BK 64); 9: v2
+    cfgs = (0, 1, 7, 8, 9, 11)  # 0 / 7 / 8: the v3 kernel (BK 32 at four per CU, GM 8, BK 64); 9: v2; 11: v3 + NT stores
     for cfg in cfgs:
         C = torch.full((batch, M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
         ops.corr_gemm(A, B, C, M, N, K, batch, K, M * K, K, N * K, N, M * N, 0.0625, False, False, 0, cfg)

@@ -73,3 +73,38 @@ def test_graphed_step_replay_matches_eager_gpu(cuda):
     d = torch.cat([(a - b).abs().flatten() for a, b in zip(m1.parameters(), m2.parameters())])
     assert float((d > OARGS.lr).float().mean()) < 0.01, float(d.max())
     assert float(graphed.skipped) == 0.0
+
+
+@pytest.mark.gpu
+def test_trainer_graph_mode_runs_and_tracks_eager(cuda, tmp_path):
+    """train.py --graph (the trainer's graphed step: static synthetic batches, capturable AdamW)
+    trains like the eager trainer step (native clip + AdamW) from the same initial weights."""
+    import train as train_cli
+    from raft_ros_amd.train import trainer
+
+    finals = {}
+    for graph in (False, True):
+        argv = ["--name", f"g{int(graph)}", "--stage", "synthetic", "--batch_size", "1", "--image_size", "128", "160",
+                "--num_steps", "3", "--iters", "3", "--num_workers", "0", "--mixed_precision", "--lr", "4e-4",
+                "--ckpt_dir", str(tmp_path / f"ck{int(graph)}"), "--log_dir", str(tmp_path / f"runs{int(graph)}"),
+                "--gpus", "0"]
+        if graph:
+            argv.append("--graph")
+        args = train_cli.build_parser().parse_args(argv)
+        torch.manual_seed(args.seed)
+        (tmp_path / f"ck{int(graph)}").mkdir()
+
+        def keep(model, info, graph=graph):
+            finals[graph] = {k: v.detach().float().clone() for k, v in model.state_dict().items()}
+
+        trainer.train(args, on_finish=keep)
+    moved = 0
+    for k, a in finals[True].items():
+        b = finals[False][k]
+        assert torch.isfinite(a).all(), k
+        if a.is_floating_point() and a.numel() > 1:
+            d = (a - b).abs()
+            # early AdamW updates are ~lr * sign(g): allow a few round-off sign flips
+            assert float((d > 4e-4).float().mean()) < 0.02, (k, float(d.max()))
+            moved += 1
+    assert moved > 50

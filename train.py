@@ -74,6 +74,11 @@ def build_parser() -> argparse.ArgumentParser:
                         "per-rank statistics, like the reference's DataParallel replicas)")
     g.add_argument("--ddp_bf16_grads", action="store_true",
                    help="all-reduce gradients in bf16 (halves xGMI traffic)")
+    g.add_argument("--graph", action="store_true",
+                   help="replay each training step as captured HIP graph(s) (static crops; the gradient "
+                        "all-reduce runs between two graphs).  Pays off where a rank trains 1-2 pairs per "
+                        "step (train_standard.sh on 8 GPUs) and the eager step is host-bound: 368x768 batch 1 "
+                        "125.9 vs 113.0 pairs/s, batch 2 196.3 vs 151.8 (profiles/r6c_*); at batch 8 eager wins")
     g.add_argument("--synthetic_pool", type=int, default=8,
                    help="--stage synthetic: batches per rank in the device-resident pool that is replayed "
                         "(a throughput check: only pool x batch distinct pairs); 0 = 100000 distinct pairs "
