@@ -6,7 +6,7 @@
                  backward runs once after the last of them)
   tail           .. last kernel before the optimizer (pyramid backward, encoder backward, the
                  batched weight gradients beside it)
-  optimizer      clip + fused AdamW (multi_tensor_apply kernels)
+  optimizer      clip + AdamW (the native adamw_* kernels, or torch's multi_tensor_apply ones)
   forward        step k+1's forward, up to its loss (encoders, pyramid, 12 refinement steps)
 
 with each phase's wall time, summed kernel time (busy), and the kernels that own most of it;
@@ -39,7 +39,11 @@ def main():
     step = rows[idx[-2]:idx[-1]]
     t_start = step[0][1]
     names = [r[0] for r in step]
-    is_opt = lambda n: "multi_tensor_apply" in n or "FusedOptimizer" in n  # noqa: E731
+    # the native clip + AdamW op (ops/optim.py) when present, else torch's fused AdamW launches
+    if any("adamw_norm_kernel" in n for n in names):
+        is_opt = lambda n: "adamw_norm_kernel" in n or "adamw_update_kernel" in n  # noqa: E731
+    else:
+        is_opt = lambda n: "multi_tensor_apply" in n or "FusedOptimizer" in n  # noqa: E731
     i_bwd = next(i for i, n in enumerate(names) if "seq_loss_bwd" in n)
     i_rows = max((i for i, n in enumerate(names) if "lookup_grad_rows" in n or "lc_gather" in n), default=i_bwd)
     opts = [i for i, n in enumerate(names) if is_opt(n) and i > i_rows]

@@ -76,9 +76,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="all-reduce gradients in bf16 (halves xGMI traffic)")
     g.add_argument("--graph", action="store_true",
                    help="replay each training step as captured HIP graph(s) (static crops; the gradient "
-                        "all-reduce runs between two graphs).  Pays off where a rank trains 1-2 pairs per "
-                        "step (train_standard.sh on 8 GPUs) and the eager step is host-bound: 368x768 batch 1 "
-                        "125.9 vs 113.0 pairs/s, batch 2 196.3 vs 151.8 (profiles/r6c_*); at batch 8 eager wins")
+                        "all-reduce runs between two graphs; no host issue per step).  Off by default: since "
+                        "the native clip + AdamW op the eager step is GPU-bound down to batch 1 and keeps its "
+                        "stream priorities (368x768 batch 1: eager 134.0 vs graph 124.2 pairs/s, batch 8 at "
+                        "368x496: 471 vs 436; profiles/r6s_*, r6c_*)")
     g.add_argument("--synthetic_pool", type=int, default=8,
                    help="--stage synthetic: batches per rank in the device-resident pool that is replayed "
                         "(a throughput check: only pool x batch distinct pairs); 0 = 100000 distinct pairs "
