@@ -2749,10 +2749,16 @@ hipError_t conv_wgrad_dispatch(const ConvWgradArgs& a, const WgradPlan& pl, hipS
       hipLaunchKernelGGL((conv_wgrad3_kernel<1, 5, 1, 64, 1, 3, F16>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
   }
-  if (pl.BM == 128)
+  if (a.wg2_stages == 2) {  // two workgroups per CU (see ConvWgradArgs::wg2_stages)
+    if (pl.BM == 128)
+      hipLaunchKernelGGL((conv_wgrad2_kernel<128, 128, 2, F16>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_wgrad2_kernel<64, 128, 2, F16>), grid, dim3(256), 0, s, a);
+  } else if (pl.BM == 128) {
     hipLaunchKernelGGL((conv_wgrad2_kernel<128, 128, 3, F16>), grid, dim3(256), 0, s, a);
-  else
+  } else {
     hipLaunchKernelGGL((conv_wgrad2_kernel<64, 128, 3, F16>), grid, dim3(256), 0, s, a);
+  }
   return hipGetLastError();
 }
 

@@ -1289,6 +1289,8 @@ hipError_t launch_corr_gemm(const CorrGemmArgs& g, hipStream_t s) {
       hipLaunchKernelGGL((corr_volume_v3_kernel<64, 2>), dim3((unsigned)tiles), dim3(256), 0, s, g);
     } else if (g.cfg == 11) {
       hipLaunchKernelGGL((corr_volume_v3_kernel<32, 4, true>), dim3((unsigned)tiles), dim3(256), 0, s, g);
+    } else if (g.cfg == 12) {
+      hipLaunchKernelGGL((corr_volume_v3_kernel<64, 2, true>), dim3((unsigned)tiles), dim3(256), 0, s, g);
     } else {
       hipLaunchKernelGGL(corr_volume_bf16_kernel, dim3((unsigned)tiles), dim3(256), 0, s, g);
     }

@@ -151,6 +151,8 @@ struct ConvWgradArgs {
   int f16;        // fp16 operands (see ConvFwdArgs::f16)
   int mt5;        // wgrad v3 on 1x5 / 5x1 convs: 1 = 64-row workgroups, 2 = 128 rows on 4 waves (the default)
   int grid_div;   // > 1: plan for 1 / grid_div of the workgroups (leave CUs to the work beside it)
+  int wg2_stages; // wgrad v2 (1x1 / generic) DMA ring stages: 3 (0 = 3; 98 KB at 128 x 128, one
+                  // workgroup per CU) or 2 (64 KB, two per CU: the plan targets 512 workgroups)
 };
 
 // Plan of one weight-gradient launch (the caller sizes the slabs from it).
@@ -517,7 +519,8 @@ inline WgradPlan plan_conv_wgrad(const ConvWgradArgs& a) {
   pl.tilesN = (a.K + pl.BN - 1) / pl.BN;
   pl.Npad = pl.tilesM * pl.BM;
   long splits, g;
-  choose_splits((long)pl.tilesM * pl.tilesN, (a.P + 255) / 256, splits, g, 256 / std::max(1, a.grid_div));
+  choose_splits((long)pl.tilesM * pl.tilesN, (a.P + 255) / 256, splits, g,
+                (a.wg2_stages == 2 ? 512 : 256) / std::max(1, a.grid_div));
   long per = (a.P + splits - 1) / splits;
   per = (per + kWgradBK - 1) / kWgradBK * kWgradBK;
   if ((a.P + per - 1) / per != splits) g = 0;  // rounding dropped a split: plain mapping

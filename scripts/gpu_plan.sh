@@ -1,34 +1,16 @@
 #!/bin/bash
 # The current GPU session plan (one gpurun call): steps run in order by scripts/gpu_step.sh,
 # each "<timeout s> <log under gpurun_out/> <command>"; the first crash / time-out ends it.
-# (This one: the round's configuration sweep -- full GPU suite, smoke, every config's bench.)
 export TMPDIR=/tmp
-T="python -u -m pytest tests -m gpu -q -rf --tb=short --timeout 200 --timeout-method thread"
-I="python bench.py --mode infer --image_size 1080 1920 --iters 32 --batch 1 --steps 10 --warmup 3"
-P=r6s
+T="python -u -m pytest -q --timeout 200 --timeout-method thread"
 bash scripts/gpu_step.sh \
- "900 ${P}_gputests.log $T" \
- "300 ${P}_smoke.log python -c 'import __graft_entry__ as g; g.smoke()'" \
- "200 ${P}_bench_a.json python bench.py" \
- "200 ${P}_bench_1080_a.json $I" \
- "200 ${P}_bench_b.json python bench.py" \
- "200 ${P}_bench_1080_b.json $I" \
- "200 ${P}_bench_c.json python bench.py --steps 40" \
- "200 ${P}_bench_alt.json python bench.py --alternate_corr --batch 3 --image_size 376 1248 --steps 15" \
- "200 ${P}_bench_kitti_dense.json python bench.py --batch 3 --image_size 376 1248 --steps 15" \
- "200 ${P}_bench_sintel.json python bench.py --batch 6 --image_size 368 768" \
- "200 ${P}_bench_full.json python bench.py --batch 6 --image_size 440 1024 --steps 15" \
- "200 ${P}_bench_fp16.json python bench.py --amp_dtype fp16" \
- "200 ${P}_bench_fp32.json python bench.py --fp32 --steps 10" \
- "200 ${P}_bench_infer_sintel.json python bench.py --mode infer --image_size 440 1024 --iters 32 --batch 1 --steps 20 --warmup 3" \
- "200 ${P}_bench_ros_fp32.json python bench.py --mode infer --fp32 --image_size 440 1024 --iters 20 --batch 1 --steps 20 --warmup 3" \
- "200 ${P}_bench_small.json python bench.py --small" \
- "200 ${P}_b1_368x768.json python bench.py --batch 1 --image_size 368 768 --steps 40" \
- "200 ${P}_b1_368x768_graph.json python bench.py --batch 1 --image_size 368 768 --steps 40 --graph" \
- "200 ${P}_b2_368x768.json python bench.py --batch 2 --image_size 368 768 --steps 40" \
- "200 ${P}_b2_368x768_graph.json python bench.py --batch 2 --image_size 368 768 --steps 40 --graph" \
- "200 ${P}_b1_400x720.json python bench.py --batch 1 --image_size 400 720 --steps 40" \
- "200 ${P}_b1_400x720_graph.json python bench.py --batch 1 --image_size 400 720 --steps 40 --graph" \
- "200 ${P}_b2_400x720.json python bench.py --batch 2 --image_size 400 720 --steps 40" \
- "200 ${P}_b2_400x720_graph.json python bench.py --batch 2 --image_size 400 720 --steps 40 --graph" \
- "200 ${P}_b6_400x720.json python bench.py --batch 6 --image_size 400 720"
+ "300 r6l_tests.log env RAFT_WGRAD2_STAGES=2 $T tests/test_conv_gpu.py -k wgrad" \
+ "200 r6l_base.json python bench.py" \
+ "200 r6l_s2.json env RAFT_WGRAD2_STAGES=2 python bench.py" \
+ "200 r6l_mt1.json env RAFT_WGRAD3_MT=1 python bench.py" \
+ "200 r6l_base_b.json python bench.py" \
+ "200 r6l_s2_b.json env RAFT_WGRAD2_STAGES=2 python bench.py" \
+ "200 r6l_mt1_b.json env RAFT_WGRAD3_MT=1 python bench.py" \
+ "300 r6l_prof.log env RAFT_WGRAD2_STAGES=2 rocprofv3 --kernel-trace -d gpurun_out/pk -o run -- python3 bench.py --steps 4 --warmup 3" \
+ "120 r6l_kernels.txt python scripts/rocpd_summary.py gpurun_out/pk/run_results.db --boundary seq_loss_fwd --steps 3 --top 40" \
+ "30 r6l_rm.log rm -rf gpurun_out/pk"
