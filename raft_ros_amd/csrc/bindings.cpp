@@ -242,25 +242,6 @@ void corr_pyramid_bwd(const at::Tensor& dL, const at::Tensor& f2t, const at::Ten
   HIP_OK(launch_corr_bwd_pair(g1, gt, cur_stream()));
 }
 
-// A HIP stream whose kernels may only use ``ncu`` of the device's compute units (hipExt CU
-// mask), spread evenly: blocks of 8 consecutive CU ids, every (total / ncu)-th block, so both a
-// round-robin and a contiguous CU-id -> XCD numbering give every XCD the same share.  Returns the
-// raw stream handle (torch.cuda.ExternalStream wraps it; the stream lives for the process).
-int64_t cu_mask_stream(int64_t device, int64_t ncu) {
-  int total = 0;
-  HIP_OK(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, (int)device));
-  TORCH_CHECK(ncu >= 8 && ncu <= total && total % ncu == 0 && (total / ncu) <= total / 8 + 1,
-              "raft_amd::cu_mask_stream: ncu must divide the CU count (", total, ") in blocks of 8");
-  const int stride = total / (int)ncu;
-  std::vector<uint32_t> mask((total + 31) / 32, 0u);
-  for (int i = 0; i < total; ++i)
-    if ((i / 8) % stride == 0) mask[i / 32] |= 1u << (i % 32);
-  const c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
-  hipStream_t st = nullptr;
-  HIP_OK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
-  return reinterpret_cast<int64_t>(st);
-}
-
 at::Tensor gemm_nt(const at::Tensor& A, const at::Tensor& B, double alpha, at::ScalarType out_dtype) {
   check_gpu(A, "A");
   check_gpu(B, "B");
@@ -1717,7 +1698,6 @@ TORCH_LIBRARY(raft_amd, m) {
       "corr_gemm(Tensor A, Tensor B, Tensor(a!) C, int M, int N, int K, int batch, int lda, int sA, int ldb, int sB, "
       "int ldc, int sC, float alpha, bool a_trans, bool split, int epi, int cfg=0) -> ()");
   m.def("corr_pyramid_bwd(Tensor dL, Tensor f2t, Tensor f1t, Tensor(a!) d1, Tensor(b!) G, float alpha) -> ()");
-  m.def("cu_mask_stream(int device, int ncu) -> int", &raft_amd::cu_mask_stream);  // no tensors: catch-all
   m.def("pyramid_unpool(Tensor G, int H, int W, int[] segs, bool blocked=False) -> Tensor");
   m.def("pyramid_operand(Tensor fmap, int[] segs, int ld, bool blocked, bool nchw, bool bf16_out=False) -> Tensor");
   m.def("corr_lookup_split_into(Tensor[] pyramid, Tensor coords, int radius, Tensor(a!) out, int G, Tensor(b!)? flow8, "

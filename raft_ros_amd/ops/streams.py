@@ -71,23 +71,6 @@ def aux_stream(device, name: str) -> torch.cuda.Stream:
     return _STREAMS[key]
 
 
-_CU_STREAMS: Dict[Tuple[torch.device, int], torch.cuda.ExternalStream] = {}
-
-
-def cu_limited_stream(device, ncu: int):
-    """A stream whose kernels run on only ``ncu`` of the device's CUs (hipExt CU mask, spread
-    over every XCD; csrc/bindings.cpp cu_mask_stream).  Long-running background grids -- the
-    batched update-block weight gradients beside the encoders' backward -- then leave the other
-    CUs to the critical chain instead of holding every CU with workgroups that run for ~100 us."""
-    from ._ext import ops
-
-    key = (torch.device(device), int(ncu))
-    if key not in _CU_STREAMS:
-        ptr = ops().cu_mask_stream(key[0].index if key[0].index is not None else torch.cuda.current_device(), key[1])
-        _CU_STREAMS[key] = torch.cuda.ExternalStream(ptr, device=key[0])
-    return _CU_STREAMS[key]
-
-
 class LeadLimiter:
     """Bound how far the host runs ahead of the GPU: ``step_done()`` after issuing a step
     records an event on the current stream and waits for the one of ``max_lead`` steps ago.

@@ -38,7 +38,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from . import conv as C
-from .streams import aux_stream, cu_limited_stream
+from .streams import aux_stream
 from ._ext import ops
 
 HID = 128
@@ -286,10 +286,9 @@ EARLY_WGRAD = os.environ.get("RAFT_EARLY_WGRAD", "1") != "0"
 # (Measured and dropped: the batched weight gradients split over two streams, neutral,
 # profiles/r4_bench_wgrad_mt_ab.log; issued from the last step's backward instead of the weight
 # token's, neutral, profiles/r5x_bench*.json -- the tail of the step is throughput-bound.)
-# RAFT_WGRAD_CUS=n: the batched weight gradients on a stream limited to n CUs (ops/streams.py
-# cu_limited_stream), so their long-running workgroups leave the rest of the chip to the
-# encoders' backward beside them (A/B; 0 = the unmasked tail stream)
-WGRAD_CUS = int(os.environ.get("RAFT_WGRAD_CUS", "0"))
+# (Measured and dropped: the batched weight gradients on a CU-masked stream -- 128 / 64 / 32 of
+# the 256 CUs: 374 / 290 / 210 vs 450 pairs/s, profiles/r6j_*.json.  They share the encoders'
+# backward window as throughput work; starving them lengthens the step.)
 # diagnostics: a list collects (main-stream event at the token's backward, weight-gradient
 # start, end) event triples on the tail stream (scripts/host_lead.py --wgrad_timing)
 WGRAD_TIMING: Optional[list] = None
@@ -351,11 +350,6 @@ class _PackWeights(torch.autograd.Function):
         ev = getattr(run, "steps_done", None)
         if ev is not None and run.wgrads is None and cur is not None:
             ws = _tail_stream(cur.device)
-            if WGRAD_CUS > 0:
-                # on a CU-masked stream, after the tail stream's queued work (the dY it wrote)
-                tail = ws
-                ws = cu_limited_stream(cur.device, WGRAD_CUS)
-                ws.wait_stream(tail)
             ws.wait_event(ev)  # the steps' backward on the main stream (the tail stream is ordered)
             with torch.cuda.stream(ws):
                 if WGRAD_TIMING is not None:  # scripts/host_lead.py --wgrad_timing
