@@ -1365,8 +1365,8 @@ __global__ __launch_bounds__(WGM * WGN * 64) void conv_fwd6_kernel(const ConvFwd
   constexpr int HWD = TW + KW - 1;                  // 2-D halo block pitch (pixels)
   constexpr int HROWS = (TH + KH - 1) * HWD;        // 2-D halo block pixels
   constexpr int SPW2 = (HROWS + 8 * NW - 1) / (8 * NW);  // its DMA pieces per wave (at most)
-  // 8-row pieces of the halo block: all SPW2 * NW (the halo is padded to them)
-  constexpr int NPIECE = SPW2 * NW;
+  // 8-row pieces of the halo block (the halo is padded to whole pieces, not to SPW2 * NW)
+  constexpr int NPIECE = (HROWS + 7) / 8;
   // LDS chunk swizzle of halo row r: (r >> 1) & 7 keeps a 16-lane ds_read_b128 group on 16
   // distinct slots when its rows are consecutive, but a 3x3 tap on 16-wide tiles reads two tile
   // rows 18 halo rows apart, and the row-parity / (r >> 1) pairs then collide (2-way on every
@@ -2561,6 +2561,17 @@ bool launch_conv_fwd6(const ConvFwdArgs& a, int cfg, hipStream_t s) {
       return t51 && launch_fwd6_t<128, 64, 4, 1, 5, 1, 16, F16>(a, s);
     case 65:  // 1x5 as a flat 128-pixel strip (132 halo rows at any width), two workgroups per CU
       return t15 && launch_fwd6_t<128, 64, 4, 1, 1, 5, 0, F16>(a, s);
+    // 64 x 64 2-D tiles, 2x2 waves of 32 x 32, <= 53.5 KB of LDS: three workgroups per CU and
+    // twice the workgroups of the 128 x 64 tiles (small grids: batch 1-2 per GPU).
+    // 74: 3x3 as 4 x 16, 1x5 as 1 x 64, 5x1 as 8 x 8;  75: 3x3 as 8 x 8, 1x5 as 2 x 32, 5x1 as 4 x 16
+    case 74:
+      if (t33) return launch_fwd6_t<64, 64, 2, 2, 3, 3, 16, F16>(a, s);
+      if (t15) return launch_fwd6_t<64, 64, 2, 2, 1, 5, 64, F16>(a, s);
+      return t51 && launch_fwd6_t<64, 64, 2, 2, 5, 1, 8, F16>(a, s);
+    case 75:
+      if (t33) return launch_fwd6_t<64, 64, 2, 2, 3, 3, 8, F16>(a, s);
+      if (t15) return launch_fwd6_t<64, 64, 2, 2, 1, 5, 32, F16>(a, s);
+      return t51 && launch_fwd6_t<64, 64, 2, 2, 5, 1, 16, F16>(a, s);
     default:
       return false;
   }
@@ -2633,18 +2644,22 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
   bool ok5 = a.KH * a.KW > 1 && a.Cin % 64 == 0 && a.N >= 64 && a.P < (1L << 30);
   for (int i = 0; i < a.nsrc; ++i) ok5 = ok5 && a.src[i].C % 64 == 0;
   int v5 = cfg >= 20 ? cfg : 0;
-  if (cfg == 41 || cfg == 45 || (cfg >= 59 && cfg <= 65)) {  // v6 tiles (tests / microbenchmarks)
+  if (cfg == 41 || cfg == 45 || (cfg >= 59 && cfg <= 65) || cfg == 74 || cfg == 75) {  // v6 tiles (tests / microbenchmarks)
     // (a strip buffer pair per chunk needs >= 3 taps per chunk: no 1x1 variant)
     const bool shape6 = (a.KH == 3 && a.KW == 3) || (a.KH * a.KW == 5 && (a.KH == 1 || a.KW == 1));
     if (!ok5 || !shape6 || a.PH != a.KH / 2 || a.PW != a.KW / 2) return hipErrorInvalidValue;
     return launch_conv_fwd6<F16>(a, cfg, s) ? hipGetLastError() : hipErrorInvalidValue;
   }
   if (ok5 && cfg == 0 && a.PH == a.KH / 2 && a.PW == a.KW / 2) {
-    // v6 on 128 x 64 tiles, two workgroups per CU, for every 3x3 / 1x5 / 5x1 update-block
-    // shape (the rule and its measurements: choose_fwd6 in kernel_abi.h, unit-tested on the
-    // host; profiles/r5b_conv6_*.log).  Before round 5: 256 x 64 / 256 x 128 one-workgroup
+    // v6 on 128 x 64 tiles (two workgroups per CU) or 64 x 64 tiles (three per CU) for every
+    // 3x3 / 1x5 / 5x1 update-block shape (the rule and its measurements: choose_fwd6 in
+    // kernel_abi.h, unit-tested on the host; profiles/r5b_conv6_*.log, r6t_conv6_*.log).  Before round 5: 256 x 64 / 256 x 128 one-workgroup
     // tiles (profiles/r3_bench_conv6_*.log, r4_bench_conv6_16x16.log), now forced variants.
-    const int v6 = choose_fwd6(a.KH, a.KW, a.N, a.B, a.H, a.W);
+    static const bool small_tiles = [] {  // RAFT_FWD6_SMALL=0: 128 x 64 tiles only (A/B runs)
+      const char* e = std::getenv("RAFT_FWD6_SMALL");
+      return !(e && e[0] == '0');
+    }();
+    const int v6 = choose_fwd6(a.KH, a.KW, a.N, a.B, a.H, a.W, small_tiles);
     if (v6 && launch_conv_fwd6<F16>(a, v6, s)) return hipGetLastError();
   }
   if (ok5 && v5 == 0 && cfg == 0) {

@@ -550,37 +550,62 @@ RAFT_HD inline int fwd6_strip_rows(int BM, int NW, int KH, int KW, int W, int ma
 }
 
 // 2-D tile of TH x TW output pixels: its halo block of (TH + KH - 1) x (TW + KW - 1) pixels,
-// padded to whole DMA pieces
+// padded to whole 8-row DMA pieces (the NW waves take pieces wave, wave + NW, ...; the last
+// round may leave some waves without one).  Padding to 8 rows instead of 8 * NW keeps the 64 x 64
+// tiles' LDS under a third of the CU (three workgroups per CU).
 RAFT_HD constexpr int fwd6_halo_rows(int TH, int TW, int KH, int KW, int NW) {
   const int rows = (TH + KH - 1) * (TW + KW - 1);
-  return (rows + 8 * NW - 1) / (8 * NW) * (8 * NW);
+  return NW > 0 ? (rows + 7) / 8 * 8 : 0;
 }
 
 // v6 variant the forward dispatcher picks for a multi-tap stride-1 conv of N outputs over
-// B x H x W pixels (0: v5 / v4).  Since round 5 every update-block shape takes a 128 x 64 tile
-// whose LDS (halo block + 3-stage weight ring, <= 74 KB) lets two workgroups share a CU: two
-// waves per SIMD hide each other's DMA / barrier waits, and the grid is quantised over 512
-// workgroup slots instead of 256 (scripts/bench_conv6.py, profiles/r5b_conv6_*.log: config #2
-// 3x3 / 1x5 / 5x1 forward and data-gradient shapes 10-29 % faster than the round-4 choice,
-// 1080p 5x1 z||r 54.3 -> 36.5 us, 3x3 conv 37.2 -> 24.0 us):
-//   62 = 2-D tiles: 3x3 as 8 x 16, 1x5 as 2 x 64, 5x1 as 16 x 8;  64 = 5x1 as 8 x 16;
-//   65 = 1x5 as a flat 128-pixel strip (132 halo rows at any width: wide images).
-// The 5x1 tile is the one with fewer 512-slot rounds of workgroups (16 x 8: less halo per
-// pixel, 8 x 16: fewer tiles on 1080p's 135-row planes).  The round-3/4 one-workgroup tiles
-// (41 / 45 / 59 / 60 / 61, 256 x 64 / 256 x 128) remain as forced variants (tests, benches).
+// B x H x W pixels (0: v5 / v4).  Two tile families:
+//   128 x 64 (4 waves of 32 x 64, <= 74 KB of LDS: two workgroups per CU, 512 slots):
+//     62 = 2-D tiles: 3x3 as 8 x 16, 1x5 as 2 x 64, 5x1 as 16 x 8;  64 = 5x1 as 8 x 16;
+//     65 = 1x5 as a flat 128-pixel strip (132 halo rows at any width: wide images);
+//   64 x 64 (2x2 waves of 32 x 32, <= 53.5 KB: three workgroups per CU, 768 slots):
+//     74 = 3x3 as 4 x 16, 5x1 as 8 x 8;  75 = 1x5 as 2 x 32.
+// The choice is the lower modelled time of the two families (fwd6_grid_cost): whole rounds of
+// workgroups over the slots cost 1 each, a partial round of fraction f costs 0.35 + 0.65 f (its
+// workgroups share their CUs with fewer others), and a 64 x 64 round costs 0.83 of a 128 x 64
+// round.  Fitted on scripts/bench_conv6.py over the update-block forward / data-gradient shapes
+// at batch 8 x 46 x 62, 1 and 2 x 46 x 96 and 1080p (profiles/r6t_conv6_*.log): 64 x 64 wins
+// 10-30 % at batch 1-2 per GPU (70-300 workgroups of 128 x 64 for 512 slots) and on the batch-8
+// shapes with < 1.2 or 2.2-2.9 rounds of 128 x 64 workgroups; 4 % below automatic over the 72
+// measured cases, 0.7 % above the per-case best.
 RAFT_HD inline int fwd6_tiles2d(int B, int H, int W, int TH, int TW) {
   return B * ((H + TH - 1) / TH) * ((W + TW - 1) / TW);
 }
-RAFT_HD inline int choose_fwd6(int KH, int KW, int N, int B, int H, int W) {
-  const int tn = (N + 63) / 64;
-  if (KH == 3 && KW == 3) return 62;
-  if (KH == 1 && KW == 5) return W <= 64 ? 62 : 65;
-  if (KH == 5 && KW == 1) {
-    const long r62 = ((long)fwd6_tiles2d(B, H, W, 16, 8) * tn + 511) / 512;
-    const long r64 = ((long)fwd6_tiles2d(B, H, W, 8, 16) * tn + 511) / 512;
-    return r64 < r62 ? 64 : 62;
+RAFT_HD inline double fwd6_grid_cost(long wgs, int slots) {
+  const long full = wgs / slots;
+  const double f = (double)(wgs - full * slots) / slots;
+  return (double)full + (f > 0.0 ? 0.35 + 0.65 * f : 0.0);
+}
+RAFT_HD inline int choose_fwd6(int KH, int KW, int N, int B, int H, int W, bool small_tiles = true) {
+  const long tn = (N + 63) / 64;
+  int base;
+  long wb, ws;  // workgroups of the 128 x 64 choice / of the 64 x 64 one
+  if (KH == 3 && KW == 3) {
+    base = 62;
+    wb = fwd6_tiles2d(B, H, W, 8, 16) * tn;
+    ws = fwd6_tiles2d(B, H, W, 4, 16) * tn;
+  } else if (KH == 1 && KW == 5) {
+    base = W <= 64 ? 62 : 65;
+    wb = (base == 62 ? (long)fwd6_tiles2d(B, H, W, 2, 64) : ((long)B * H * W + 127) / 128) * tn;
+    ws = fwd6_tiles2d(B, H, W, 2, 32) * tn;
+  } else if (KH == 5 && KW == 1) {
+    // 16 x 8 or 8 x 16: fewer 512-slot rounds (16 x 8: less halo per pixel, 8 x 16: fewer tiles
+    // on 1080p's 135-row planes)
+    const long r62 = (fwd6_tiles2d(B, H, W, 16, 8) * tn + 511) / 512;
+    const long r64 = (fwd6_tiles2d(B, H, W, 8, 16) * tn + 511) / 512;
+    base = r64 < r62 ? 64 : 62;
+    wb = (base == 62 ? fwd6_tiles2d(B, H, W, 16, 8) : fwd6_tiles2d(B, H, W, 8, 16)) * tn;
+    ws = fwd6_tiles2d(B, H, W, 8, 8) * tn;
+  } else {
+    return 0;
   }
-  return 0;
+  const int small = KH == 1 ? 75 : 74;
+  return small_tiles && 0.83 * fwd6_grid_cost(ws, 768) < fwd6_grid_cost(wb, 512) ? small : base;
 }
 
 // ============================================================================ convex upsampling

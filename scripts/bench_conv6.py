@@ -3,7 +3,8 @@
 shapes at config #2 (8 x 46 x 62 pixels): bitwise / numeric agreement and time per launch.
 
     python scripts/bench_conv6.py [--cfgs 41,45,59,60] [--batch 8] [--hw 46 62]
-cfg 41 = 256x64 flat strip, 45 = 256x128 flat strip, 59 / 60 = 256x64 as 2-D 4x64 / 8x32 tiles.
+cfg 41 = 256x64 flat strip, 45 = 256x128 flat strip, 59 / 60 = 256x64 as 2-D 4x64 / 8x32 tiles,
+62-65 = 128x64 2-D / flat tiles (two workgroups per CU), 74 / 75 = 64x64 2-D tiles (three per CU).
 (The probe variants behind profiles/r3_conv6_probe.log -- no MFMA / DMA / reads / barrier /
 epilogue -- were removed after the measurement.)
 """
@@ -48,7 +49,7 @@ SHAPES = {
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cfgs", default="41,45,59,60,62,63,64")
+    ap.add_argument("--cfgs", default="62,63,64,65,74,75")
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--hw", type=int, nargs=2, default=[46, 62])
     ap.add_argument("--only", default="")

@@ -1,16 +1,24 @@
-#!/bin/bash
-# The current GPU session plan (one gpurun call): steps run in order by scripts/gpu_step.sh,
-# each "<timeout s> <log under gpurun_out/> <command>"; the first crash / time-out ends it.
-export TMPDIR=/tmp
-T="python -u -m pytest -q --timeout 200 --timeout-method thread"
-bash scripts/gpu_step.sh \
- "300 r6l_tests.log env RAFT_WGRAD2_STAGES=2 $T tests/test_conv_gpu.py -k wgrad" \
- "200 r6l_base.json python bench.py" \
- "200 r6l_s2.json env RAFT_WGRAD2_STAGES=2 python bench.py" \
- "200 r6l_mt1.json env RAFT_WGRAD3_MT=1 python bench.py" \
- "200 r6l_base_b.json python bench.py" \
- "200 r6l_s2_b.json env RAFT_WGRAD2_STAGES=2 python bench.py" \
- "200 r6l_mt1_b.json env RAFT_WGRAD3_MT=1 python bench.py" \
- "300 r6l_prof.log env RAFT_WGRAD2_STAGES=2 rocprofv3 --kernel-trace -d gpurun_out/pk -o run -- python3 bench.py --steps 4 --warmup 3" \
- "120 r6l_kernels.txt python scripts/rocpd_summary.py gpurun_out/pk/run_results.db --boundary seq_loss_fwd --steps 3 --top 40" \
- "30 r6l_rm.log rm -rf gpurun_out/pk"
+# round-6 plan: 64 x 64 conv tiles -- correctness, then interleaved A/B of RAFT_FWD6_SMALL
+set -o pipefail
+mkdir -p gpurun_out/u
+export PYTHONUNBUFFERED=1
+T="timeout -k 10"
+$T 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_gpu.py tests/test_update_fused_gpu.py tests/test_golden_gpu.py > gpurun_out/u/tests.log 2>&1 || { tail -30 gpurun_out/u/tests.log; exit 1; }
+tail -2 gpurun_out/u/tests.log
+run() {  # tag env bench-args
+  tag=$1; shift; e=$1; shift
+  env $e $T 300 python -u bench.py "$@" > gpurun_out/u/$tag.json 2> gpurun_out/u/$tag.err || { echo "$tag failed"; tail -5 gpurun_out/u/$tag.err; exit 1; }
+  echo "$tag $(grep -o '"value": [0-9.]*' gpurun_out/u/$tag.json)"
+}
+for r in a b; do
+  run b8_new_$r RAFT_FWD6_SMALL=1 --steps 30 --warmup 5
+  run b8_old_$r RAFT_FWD6_SMALL=0 --steps 30 --warmup 5
+  run b1_new_$r RAFT_FWD6_SMALL=1 --steps 40 --warmup 5 --batch 1 --image_size 368 768
+  run b1_old_$r RAFT_FWD6_SMALL=0 --steps 40 --warmup 5 --batch 1 --image_size 368 768
+  run b2_new_$r RAFT_FWD6_SMALL=1 --steps 40 --warmup 5 --batch 2 --image_size 368 768
+  run b2_old_$r RAFT_FWD6_SMALL=0 --steps 40 --warmup 5 --batch 2 --image_size 368 768
+done
+run b1t_new RAFT_FWD6_SMALL=1 --steps 40 --warmup 5 --batch 1 --image_size 400 720
+run b1t_old RAFT_FWD6_SMALL=0 --steps 40 --warmup 5 --batch 1 --image_size 400 720
+run inf1080_new RAFT_FWD6_SMALL=1 --mode infer --batch 1 --image_size 1080 1920 --iters 32 --steps 20 --warmup 5
+run inf1080_old RAFT_FWD6_SMALL=0 --mode infer --batch 1 --image_size 1080 1920 --iters 32 --steps 20 --warmup 5

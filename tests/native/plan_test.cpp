@@ -138,38 +138,58 @@ static void test_wgrad_plans() {
 // conv_fwd6 selection: the measured choices at the benchmark shapes, and every chosen variant's
 // strip / halo block fits the LDS the kernel allocates, at any image width
 static void test_fwd6_plan() {
-  // every update-block shape on the 128 x 64 two-workgroups-per-CU tiles: config #2 (8 x 46 x
-  // 62): 3x3 -> 62, 1x5 (W <= 64) -> 62, 5x1 -> 62 (16 x 8 and 8 x 16 tie on rounds)
-  EXPECT(choose_fwd6(3, 3, 126, 8, 46, 62) == 62, "conv");
-  EXPECT(choose_fwd6(3, 3, 192, 8, 46, 62) == 62, "convc2");
+  // config #2 (8 x 46 x 62), measured per shape (profiles/r6t_conv6_b8.log): 64 x 64 tiles where
+  // the 128 x 64 grid leaves a partial round (conv 384, convc2 576 workgroups for 512 slots) ...
+  EXPECT(choose_fwd6(3, 3, 126, 8, 46, 62) == 74, "conv");
+  EXPECT(choose_fwd6(3, 3, 192, 8, 46, 62) == 74, "convc2");
+  EXPECT(choose_fwd6(3, 3, 64, 8, 46, 62) == 74, "convf2");
+  EXPECT(choose_fwd6(1, 5, 128, 8, 46, 62) == 75, "q 1x5");
+  EXPECT(choose_fwd6(5, 1, 384, 8, 46, 62) == 74, "5x1 data gradient");
+  // ... and 128 x 64 on whole rounds (heads: 1536 = 3 x 512)
   EXPECT(choose_fwd6(3, 3, 512, 8, 46, 62) == 62, "heads");
-  EXPECT(choose_fwd6(1, 5, 128, 8, 46, 62) == 62, "q 1x5");
-  EXPECT(choose_fwd6(1, 5, 256, 8, 46, 62) == 62, "z||r 1x5");
-  EXPECT(choose_fwd6(5, 1, 256, 8, 46, 62) == 62, "z||r 5x1");
-  EXPECT(choose_fwd6(5, 1, 384, 8, 46, 62) == 62, "5x1 data gradient");
+  // (N = 256: 768 vs 1536 workgroups model and measure as a tie, 21.9 vs 22.3 us)
+  // batch 1 at 368 x 768 (46 x 96, the per-rank work of train_standard.sh on 8 GPUs): 64 x 64
+  for (int N : {64, 126, 192, 256, 384, 512}) {
+    EXPECT(choose_fwd6(3, 3, N, 1, 46, 96) == 74, "b1 3x3 N=%d", N);
+    EXPECT(choose_fwd6(1, 5, N, 1, 46, 96) == 75, "b1 1x5 N=%d", N);
+  }
+  // batch 2: the N = 384 data gradients stay on 128 x 64 (864 / 1104 small workgroups > 768)
+  EXPECT(choose_fwd6(5, 1, 384, 2, 46, 96) == 62, "b2 5x1 data gradient");
+  EXPECT(choose_fwd6(1, 5, 384, 2, 46, 96) == 65, "b2 1x5 data gradient");
+  EXPECT(choose_fwd6(3, 3, 512, 2, 46, 96) == 74, "b2 heads");
   // 1080p (1 x 135 x 240): flat 1x5 strips; the 5x1 z||r on 8 x 16 (1020 vs 1080 workgroups)
   EXPECT(choose_fwd6(1, 5, 256, 1, 135, 240) == 65, "1080p 1x5");
   EXPECT(choose_fwd6(5, 1, 256, 1, 135, 240) == 64, "1080p 5x1 z||r");
   EXPECT(choose_fwd6(5, 1, 128, 1, 135, 240) == 64, "1080p 5x1 q");
   EXPECT(choose_fwd6(3, 3, 126, 1, 135, 240) == 62, "1080p conv");
   EXPECT(choose_fwd6(7, 7, 128, 1, 135, 240) == 0, "7x7 -> v4");
-  // every choice fits: 2-D halo blocks / the flat 1x5 strip within the two-workgroup budget
+  // every choice fits: 2-D halo blocks / the flat 1x5 strip within the LDS of two (128 x 64) or
+  // three (64 x 64) workgroups per CU
   const int taps[3][2] = {{3, 3}, {1, 5}, {5, 1}};
-  for (int W = 1; W <= 400; ++W)
-    for (int H = 1; H <= 140; H += 13)
-      for (const auto& t : taps)
-        for (int N = 64; N <= 576; N += 64) {
-          const int kh = t[0], kw = t[1];
-          const int c = choose_fwd6(kh, kw, N, 2, H, W);
-          EXPECT(c == 62 || c == 64 || c == 65, "cfg %d", c);
-          if (c == 64) EXPECT(kh == 5, "64 is a 5x1 tile");
-          if (c == 65) EXPECT(kh == 1 && W > 64, "65: wide 1x5");
-          const int halo = c == 65 ? (128 + 4 + 31) / 32 * 32
-                           : c == 64 ? fwd6_halo_rows(8, 16, kh, kw, 4)
-                           : kh == 3 ? fwd6_halo_rows(8, 16, 3, 3, 4)
-                           : kh == 1 ? fwd6_halo_rows(2, 64, 1, 5, 4) : fwd6_halo_rows(16, 8, 5, 1, 4);
-          EXPECT(3 * 64 * 128 + 2 * (halo + 1) * 128 <= kFwd6Lds / 2, "two workgroups per CU: halo %d", halo);
-        }
+  for (int B : {1, 2, 8})
+    for (int W = 1; W <= 400; W += (B == 2 ? 1 : 7))
+      for (int H = 1; H <= 140; H += 13)
+        for (const auto& t : taps)
+          for (int N = 64; N <= 576; N += 64) {
+            const int kh = t[0], kw = t[1];
+            const int c = choose_fwd6(kh, kw, N, B, H, W);
+            EXPECT(c == 62 || c == 64 || c == 65 || c == 74 || c == 75, "cfg %d", c);
+            if (c == 64) EXPECT(kh == 5, "64 is a 5x1 tile");
+            if (c == 65) EXPECT(kh == 1 && W > 64, "65: wide 1x5");
+            if (c == 74) EXPECT(kw == 3 || kh == 5, "74: 3x3 / 5x1");
+            if (c == 75) EXPECT(kh == 1, "75: 1x5");
+            if (c >= 74) {
+              const int halo = kh == 3 ? fwd6_halo_rows(4, 16, 3, 3, 4)
+                               : kh == 5 ? fwd6_halo_rows(8, 8, 5, 1, 4) : fwd6_halo_rows(2, 32, 1, 5, 4);
+              EXPECT(3 * 64 * 128 + 2 * (halo + 1) * 128 <= kFwd6Lds / 3, "three workgroups per CU: halo %d", halo);
+              continue;
+            }
+            const int halo = c == 65 ? (128 + 4 + 31) / 32 * 32
+                             : c == 64 ? fwd6_halo_rows(8, 16, kh, kw, 4)
+                             : kh == 3 ? fwd6_halo_rows(8, 16, 3, 3, 4)
+                             : kh == 1 ? fwd6_halo_rows(2, 64, 1, 5, 4) : fwd6_halo_rows(16, 8, 5, 1, 4);
+            EXPECT(3 * 64 * 128 + 2 * (halo + 1) * 128 <= kFwd6Lds / 2, "two workgroups per CU: halo %d", halo);
+          }
   EXPECT(2 * fwd6_sb(128) + 3 * 128 * 128 <= kFwd6Lds && fwd6_sb(64) <= 65408, "LDS layout");
 }
 

@@ -169,7 +169,7 @@ def test_gru_epilogues(cuda):
     assert _rel(_from_pm(hn, B, H, W), hn_ref) < 1e-2
 
 
-@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 1, 8, 9, 41, 45, 59, 60, 61, 62, 63, 64, 65, 67])
+@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 1, 8, 9, 41, 45, 59, 60, 61, 62, 63, 64, 65, 67, 74, 75])
 @pytest.mark.parametrize("segs,cout,kh,kw,hw", [
     ([(256, 256)], 192, 3, 3, (46, 62)),
     ([(128, 128), (128, 128), (128, 128)], 256, 1, 5, (46, 62)),
@@ -199,7 +199,8 @@ def test_fwd_every_variant_full_size(cuda, cfg, segs, cout, kh, kw, hw):
     if cfg in v6_flat and v6_flat[cfg][0] + (kh - 1) * W + kw - 1 > v6_flat[cfg][1]:
         pytest.skip("v6 flat strip does not fit in LDS at this width (2-D tiles cover it)")
     # v6 tap shapes: 45 = 3x3 / 1x5, 59 (2-D) = 3x3 / 1x5, 60 (2-D) = 5x1, 61 (2-D) = 3x3 / 5x1
-    # 62 / 63 (128 x 64 2-D tiles, two workgroups per CU) = every tap shape, 64 = 5x1
+    # 62 / 63 (128 x 64 2-D tiles, two workgroups per CU) = every tap shape, 64 = 5x1; 74 / 75
+    # (64 x 64 2-D tiles, three workgroups per CU) = every tap shape
     if ((cfg in (60, 64) and (kh, kw) != (5, 1)) or (cfg in (45, 59) and (kh, kw) not in ((3, 3), (1, 5)))
             or (cfg == 65 and (kh, kw) != (1, 5)) or (cfg == 67) != ((kh, kw) == (1, 1)) and cfg >= 41
             or (cfg == 61 and (kh, kw) not in ((3, 3), (5, 1)))):
@@ -257,7 +258,7 @@ def test_wgrad_params_periodic_source_and_param_layout(cuda):
     assert torch.equal(gz, gz2)
 
 
-@pytest.mark.parametrize("cfg", [0, 8, 25, 26, 41, 59])
+@pytest.mark.parametrize("cfg", [0, 8, 25, 26, 41, 59, 62, 74, 75])
 def test_gru_backward_epilogues_match_unfused(cuda, cfg):
     """EPI_GRU_BWD_A / _B / _LAST (gate backward fused into the data-gradient epilogue) vs
     the plain EPI_GRAD store followed by the separate gru_bwd_a / gru_bwd_b / masked_cast
@@ -405,7 +406,7 @@ def test_split_gru_stage_is_fp32_faithful(cuda):
     assert _rel(_from_pm(_split_read(zr, Hd, 2 * Hd), B, H, W), torch.cat([z, r], 1)) < 3e-5
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 8, 9, 20, 21, 24, 25, 26, 41, 45, 59, 61, 62, 63])
+@pytest.mark.parametrize("cfg", [0, 1, 8, 9, 20, 21, 24, 25, 26, 41, 45, 59, 61, 62, 63, 74, 75])
 @pytest.mark.parametrize("N,B,hw", [(256, 2, (46, 62)), (512, 1, (27, 120)), (256, 1, (23, 31))])
 def test_flow_head_conv2_folded_into_heads_epilogue(cuda, cfg, N, B, hw):
     """heads conv (3x3 128 -> N, ReLU, bf16) with flow_head.conv2 (3x3 256 -> 2) folded into
