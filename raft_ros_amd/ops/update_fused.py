@@ -82,6 +82,14 @@ def _nchw(t: torch.Tensor, B: int, H: int, W: int) -> torch.Tensor:
     return t.reshape(B, H, W, t.shape[1]).permute(0, 3, 1, 2)
 
 
+# backward arena buffers (name, channels) and the buffer order of fused_step_bwd (csrc/bindings.cpp
+# step_exec::BwdBuf)
+_BWD_ARENA = (("dmask", 576), ("dd8", 8), ("dhd", 512), ("dq1", HID), ("dq2", HID), ("dzr1", 2 * HID),
+              ("dzr2", 2 * HID), ("dmo", HID), ("dcf", 256), ("dc1", 256), ("df1", 128))
+_BWD_BUFS = ("hd", "mask", "h", "h1", "zr1", "zr2", "q1", "q2", "motion", "cf", "c1", "f1", "dmask", "dd8", "dhd",
+             "dq1", "dq2", "dzr1", "dzr2", "dmo", "dcf", "dc1", "df1")
+
+
 class _Arena:
     """Per-forward storage: one (slots * P, C) buffer per name, slot t at rows [t*P, (t+1)*P).
 
@@ -135,6 +143,7 @@ class _Run:
         self.bias: Dict[str, torch.Tensor] = {}
         self.cout: Dict[str, int] = {}
         self.n2y: Optional[torch.Tensor] = None  # folded flow-head partials (native step), per run
+        self.bwd_bufs: Optional[List[torch.Tensor]] = None  # arena bases handed to fused_step_bwd
         # every layer's operands in one launch
         mods_of = [(name, mods(block)) for name, mods, _, _, _ in _LAYERS]
         packed = C.pack_weights_multi([([m.weight for m in ms], [m.bias for m in ms], segs, scale, dgrad)
@@ -145,6 +154,14 @@ class _Run:
             self.cout[name] = sum(m.weight.shape[0] for m in ms)
         # context features: constant over the iterations -> one bf16 pixel-major copy
         self.inp_bf = _pm(inp.detach().to(dt16).contiguous(memory_format=torch.channels_last))
+
+    def release(self):
+        """Drop the arena (and the native backward's references to its buffers) once the batched
+        weight gradients are queued: the run object itself may live on (autograd contexts,
+        reference cycles) until a later collection."""
+        self.arena.bufs.clear()
+        self.bwd_bufs = None
+        self.wd_list = None
 
     def geom(self, kh, kw, T: int = 1):
         B, H, W = self.dims
@@ -281,6 +298,10 @@ FOLD_N2 = os.environ.get("RAFT_FOLD_N2", "1") != "0"
 # Python-side op calls (neutral on the GPU, profiles/r5o_bench_native*.json: the launches, not
 # Python, are the host cost); tests set it False to compare with the Python body bitwise
 NATIVE_STEP = True
+# the step's backward issued by one native op (csrc/bindings.cpp fused_step_bwd) instead of ~11
+# conv_fwd calls and ~30 arena views from Python (~0.28 ms of host time per iteration, which is
+# step time at batch 1-2 per GPU); tests set it False to compare with the Python body bitwise
+NATIVE_BWD = os.environ.get("RAFT_NATIVE_BWD", "1") != "0"
 # batched weight gradients on the tail stream beside the encoders' backward (see WeightToken)
 EARLY_WGRAD = os.environ.get("RAFT_EARLY_WGRAD", "1") != "0"
 # (Measured and dropped: the batched weight gradients split over two streams, neutral,
@@ -368,7 +389,7 @@ class _PackWeights(torch.autograd.Function):
             # the recorded stream when it is freed: ~70 of them, ~0.5 ms of GPU time, used to
             # land on the main stream at every optimizer.zero_grad.)
             run.grad_out = None
-            run.arena.bufs.clear()
+            run.release()
             run.tail = None
             return (None, *grads)
         if run.tail is not None:  # the steps' motion-encoder backward wrote dY on the tail stream
@@ -388,7 +409,7 @@ class _PackWeights(torch.autograd.Function):
                 b.record_stream(ws)
         else:
             grads = run.weight_grads()
-        run.arena.bufs.clear()
+        run.release()
         run.wgrads = None
         return (None, *grads)
 
@@ -547,6 +568,49 @@ class _Step(torch.autograd.Function):
         return _nchw(h_out, B, H, W), res[2], coords_out
 
     @staticmethod
+    def _native_backward(ctx, g_net, g_flow_up):
+        """The backward below as one native op call (csrc/bindings.cpp fused_step_bwd): the same
+        launches, streams and arena slots, issued from C++."""
+        run: _Run = ctx.run
+        t = ctx.t
+        B, H, W = run.dims
+        ar = run.arena
+        dev = run.inp_bf.device
+        main = torch.cuda.current_stream(dev)
+        head = _head_stream(dev) if HEAD_STREAM else None
+        if head is not None:
+            ready = getattr(g_flow_up, "_raft_ready", None) if g_flow_up is not None else None
+            if ready is not None:
+                head.wait_event(ready)
+            else:
+                head.wait_stream(main)
+            if g_flow_up is not None:
+                g_flow_up.record_stream(head)
+        if run.bwd_bufs is None:  # every backward arena buffer at once, then the views' bases
+            for name, C in _BWD_ARENA:
+                ar.take(name, 0, C)
+            run.bwd_bufs = [ar.bufs[n] for n in _BWD_BUFS]
+            none16 = torch.empty(0, device=dev, dtype=run.dt16)
+            run.wd_list = [run.wd[name] if run.wd[name] is not None else none16 for name, _, _, _, _ in _LAYERS]
+            run.g_all = torch.empty(run.iters, run.P, 3 * HID, device=dev, dtype=torch.float32)
+        dense = not ctx.has_corr_in and run.pyr is not None and bool(run.pyr.levels)
+        if dense and not run.pyr.deferrable():
+            run.pyr.grad_buffers()  # allocated (zeroed) on the main stream
+        tail = _tail_stream(dev) if dense and TAIL_STREAM else None
+        if tail is not None:
+            run.tail = run.pyr.tail = tail
+        d_net, dcorr = ops().fused_step_bwd(run.bwd_bufs, run.wd_list, run.g_all, run.flows[t], g_net, g_flow_up,
+                                            [B, H, W, t, head.cuda_stream if head is not None else 0,
+                                             tail.cuda_stream if tail is not None else 0])
+        if dense:
+            if run.pyr.deferrable():
+                run.pyr.pending.append((run.coords[t], dcorr.view(B, H, W, CORR_PAD)))
+            else:
+                with torch.cuda.stream(tail) if tail is not None else contextlib.nullcontext():
+                    run.pyr.add_grad(run.coords[t], dcorr.view(B, H, W, CORR_PAD))
+        return d_net, dcorr
+
+    @staticmethod
     def backward(ctx, g_net, g_flow_up, _g_coords):
         run: _Run = ctx.run
         t = ctx.t
@@ -557,6 +621,9 @@ class _Step(torch.autograd.Function):
         k = ops()
         ar = run.arena
         gd = run.geom_d
+        if NATIVE_BWD and dev.type == "cuda" and ar.keep:
+            d_net, dcorr = _Step._native_backward(ctx, g_net, g_flow_up)
+            return _Step._backward_tail(ctx, d_net, dcorr)
 
         def R(name):  # this step's slot of a forward arena
             return ar.rows(name, t, t + 1)
@@ -662,11 +729,20 @@ class _Step(torch.autograd.Function):
             dgrad("convc1", dc1, 1, 1, dcorr, CORR_PAD)
             if dense:
                 run.pyr.add_grad(run.coords[t], dcorr.reshape(B, H, W, CORR_PAD))
+        return _Step._backward_tail(ctx, d_net, dcorr)
+
+    @staticmethod
+    def _backward_tail(ctx, d_net, dcorr):
+        run: _Run = ctx.run
+        t = ctx.t
+        B, H, W = run.dims
+        dev = d_net.device
+        ar = run.arena
         run.done.add(t)
         run.early_weight_grads(t)
 
         d_corr_in = dcorr.reshape(B, H, W, CORR_PAD) if ctx.has_corr_in else None
-        d_net = _nchw(d_net if ctx.net_dtype == bf else d_net.to(ctx.net_dtype), B, H, W)
+        d_net = _nchw(d_net if ctx.net_dtype == run.dt16 else d_net.to(ctx.net_dtype), B, H, W)
         d_inp = None
         if t == 0:  # the last step backward to run (every other step's d net feeds it)
             if EARLY_WGRAD and dev.type == "cuda" and ar.keep:
