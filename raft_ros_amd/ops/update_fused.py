@@ -365,6 +365,12 @@ class _PackWeights(torch.autograd.Function):
     def backward(ctx, gtoken):
         h = ctx.holder
         run: _Run = h.run if isinstance(h, WeightToken) else h
+        # break the token <-> graph reference cycle (token.tensor.grad_fn holds this ctx, whose
+        # holder is the token): without it every step's run (~28 MB of device tensors at config #2)
+        # stayed reachable until the next cyclic garbage collection (scripts/mem_growth.py)
+        ctx.holder = None
+        if isinstance(h, WeightToken):
+            h.run = None
         if run is None:  # the token's forward pass never reached the update loop
             return (None,) * (len(ctx.needs_input_grad))
         cur = torch.cuda.current_stream() if run.inp_bf.is_cuda else None

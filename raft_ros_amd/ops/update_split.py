@@ -299,6 +299,9 @@ class _SplitToken(torch.autograd.Function):
     def backward(ctx, gtoken):
         h = ctx.holder
         run = h.run if isinstance(h, SplitWeightToken) else h
+        ctx.holder = None  # break the token <-> graph cycle (see ops/update_fused.py _PackWeights)
+        if isinstance(h, SplitWeightToken):
+            h.run = None
         if run is None:
             return (None,) * len(ctx.needs_input_grad)
         ev = getattr(run, "steps_done", None)
