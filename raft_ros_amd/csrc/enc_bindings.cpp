@@ -509,7 +509,7 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
       ConvParamDesc d{};
       d.w[0] = dw.data_ptr<float>();
       for (int k = 0; k < 4; ++k) d.ws[0][k] = dw.stride(k);
-      d.b[0] = with_b ? db->data_ptr<float>() : nullptr;
+      d.b[0] = want_db ? db->data_ptr<float>() : nullptr;  // db_zero: the reduce writes 0 (no partials)
       d.rows[0] = N;
       d.nseg = 1;
       d.seg_real[0] = d.seg_pad[0] = Cin;
@@ -519,7 +519,6 @@ void enc_conv_wgrad(const at::Tensor& x, const at::Tensor& dy, at::Tensor dw, co
       check(launch_wgrad_reduce_params(w.slab, pl.nsplit, pl.Npad, w.Kpad, w.dbslab, pl.nsplit * pl.tilesN, d, N,
                                        accumulate ? 1 : 0, stream()),
             "wgrad_reduce_params (encoder)");
-      if (want_db && db_zero && !accumulate) db->zero_();  // exact zero in front of IN / BN-train
       return;
     }
   }

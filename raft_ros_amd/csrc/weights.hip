@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_params_kernel(const float* _
   } else {
     const int n = (int)(blk - (long)N * kch) * 64 + lane;
     float v = 0.f;
-    if (n < N)
+    if (n < N && dbslab)
       for (int j = wave; j < ndb; j += 4) v += dbslab[(long)j * Npad + n];
     v = combine4(v, red);
     if (wave != 0 || n >= N) return;
@@ -325,7 +325,9 @@ hipError_t launch_pack_conv_weights_multi(const PackJobs& js, hipStream_t s) {
 hipError_t launch_wgrad_reduce_params(const float* slab, int nsplit, int Npad, int Kpad, const float* dbslab, int ndb,
                                       const ConvParamDesc& d, int N, int accumulate, hipStream_t s) {
   const long kch = (d.KH * d.KW * (d.fold ? 2 : 1) * d.Cin_pad + 63) / 64;
-  const long blocks = (long)N * kch + (dbslab ? (N + 63) / 64 : 0);
+  // bias blocks also without partials: they write the exact zero bias gradient (convs in front of
+  // InstanceNorm / training BatchNorm) in this launch instead of a separate fill
+  const long blocks = (long)N * kch + ((dbslab || d.b[0] || d.b[1]) ? (N + 63) / 64 : 0);
   hipLaunchKernelGGL(wgrad_reduce_params_kernel, dim3((unsigned)blocks), dim3(256), 0, s, slab, nsplit, Npad, Kpad,
                      dbslab, ndb, d, N, accumulate);
   return hipGetLastError();

@@ -192,7 +192,7 @@ class _BuildPyramid(torch.autograd.Function):
         ctx.state, ctx.split = state, split
         ctx.save_for_backward(fmap1, fmap2)
         ctx.set_materialize_grads(False)  # the token gradient is never used (may be None)
-        return fmap1.new_zeros((), dtype=torch.float32)
+        return fmap1.new_empty((), dtype=torch.float32)  # ordering token: never read (no fill launch)
 
     @staticmethod
     def backward(ctx, gtoken):

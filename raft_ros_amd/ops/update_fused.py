@@ -359,7 +359,7 @@ class _PackWeights(torch.autograd.Function):
     def forward(ctx, holder, *params):
         ctx.holder = holder  # a _Run, or a WeightToken whose run is filled in later
         ctx.set_materialize_grads(False)  # the steps send no token gradient (None): no zero fills
-        return params[0].new_zeros(())
+        return params[0].new_empty(())  # ordering token: its value is never read (no fill launch)
 
     @staticmethod
     def backward(ctx, gtoken):

@@ -293,7 +293,7 @@ class _SplitToken(torch.autograd.Function):
     def forward(ctx, holder, *params):
         ctx.holder = holder  # a run, or a SplitWeightToken whose run is filled in later
         ctx.set_materialize_grads(False)
-        return params[0].new_zeros(())
+        return params[0].new_empty(())  # ordering token: its value is never read (no fill launch)
 
     @staticmethod
     def backward(ctx, gtoken):
