@@ -47,6 +47,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--global_batch", type=int, default=0,
+                    help="> 0: strong scaling at this GLOBAL batch, split over the ranks as the trainer does "
+                         "(parallel/batching.py: the reference's DataParallel semantics; train_standard.sh on 8 "
+                         "GPUs = --global_batch 6 -> 1,1,1,1,1,1,0,0 with loss weights, idle ranks still in the "
+                         "all-reduce and the optimizer step); --batch is then ignored")
     ap.add_argument("--image_size", type=int, nargs=2, default=[368, 496])
     ap.add_argument("--iters", type=int, default=12)
     ap.add_argument("--impl", choices=["native", "reference"], default="native")
@@ -185,6 +190,7 @@ def run(args):
     from raft_ros_amd.ops import _ext
     from raft_ros_amd.train.loss import sequence_loss
     from raft_ros_amd.train.optim import fetch_optimizer
+    from raft_ros_amd.train.trainer import init_idle_scaler
 
     _ext.set_backend(args.impl)
     torch.backends.cudnn.benchmark = True
@@ -219,7 +225,19 @@ def run(args):
     scaler = torch.amp.GradScaler("cuda", enabled=args.amp_dtype == "fp16" and not args.fp32 and device.type == "cuda")
 
     H, W = args.image_size
-    pool = [synthetic_batch(args.batch, H, W, seed=rank * 97 + i, device=device) for i in range(2 if H * W > 1e6 else 4)]
+    # strong scaling (--global_batch): this rank's share of the global batch and its loss weight
+    sizes = None
+    if args.global_batch > 0:
+        from raft_ros_amd.parallel.batching import loss_weight, rank_batch_sizes
+
+        if args.mode != "train" or train_graph or (distributed and args.dp_impl == "ddp"):
+            raise SystemExit("bench.py: --global_batch measures eager training with --dp_impl sync")
+        sizes = rank_batch_sizes(args.global_batch, world)
+        args.batch = sizes[rank]
+    weight = loss_weight(sizes, rank) if sizes is not None else 1.0
+    idle = args.batch == 0
+    pool = [synthetic_batch(max(args.batch, 1), H, W, seed=rank * 97 + i, device=device)
+            for i in range(2 if H * W > 1e6 else 4)]
 
     if args.mode == "infer":
         from raft_ros_amd.runtime import GraphedRAFT
@@ -240,9 +258,16 @@ def run(args):
     def train_step(i):
         i1, i2, flow, valid = pool[i % len(pool)]
         optimizer.zero_grad(set_to_none=True)
-        preds = ddp(i1, i2, iters=args.iters)
-        loss, metrics = sequence_loss(preds, flow, valid, gamma=0.8)
-        scaler.scale(loss).backward()
+        if idle:  # no sample of the global batch here: zero gradients into the all-reduce
+            loss = torch.zeros((), device=device)
+            metrics = {"epe": torch.zeros((), device=device)}
+            init_idle_scaler(scaler, device)
+        else:
+            preds = ddp(i1, i2, iters=args.iters)
+            loss, metrics = sequence_loss(preds, flow, valid, gamma=0.8)
+            if weight != 1.0:
+                loss = loss * weight
+            scaler.scale(loss).backward()
         if gsync is not None:
             gsync.sync()
         if native_opt:
@@ -315,7 +340,7 @@ def run(args):
     elapsed = float(t.item())
     ar_ms = _allreduce_ms(model, device, world)
     enc_path, upd_path = _paths(model, pool[0][0], args)
-    pairs = args.batch * world * args.steps
+    pairs = (args.global_batch if sizes is not None else args.batch * world) * args.steps
     value = pairs / elapsed
     if rank == 0:
         out = {
@@ -327,16 +352,17 @@ def run(args):
             "warmup": args.warmup,
             "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sizes is not None else "weak",
             "vs_baseline": (round(value / (BASELINE_PAIRS_PER_SEC * world), 3)
                             if BASELINE_PAIRS_PER_SEC and args.impl == "native" and args.mode == "train" and not args.fp32
                             and not args.small and not args.alternate_corr and (H, W) == (368, 496)
-                            and args.iters == 12 and args.batch == 8 else None),
+                            and args.iters == 12 and args.batch == 8 and sizes is None else None),
             "dtype": args.amp_dtype if device.type == "cuda" and not args.fp32 else "fp32",
             "data": "synthetic (textured pairs warped by known smooth flow; random-init weights)",
             "config": {
                 "model": "RAFT-small" if args.small else "RAFT-base",
-                "global_batch": args.batch * world,
+                "global_batch": args.global_batch if sizes is not None else args.batch * world,
+                "rank_batches": sizes,
                 "seq_len": args.iters,
                 "image_size": [H, W],
                 "iters": args.iters,

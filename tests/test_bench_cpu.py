@@ -66,3 +66,15 @@ def test_bench_under_torchrun_driver_launch():
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 2
     assert r["scaling"] == "weak" and r["allreduce_ms"] > 0
+
+
+@pytest.mark.timeout(600)
+def test_bench_global_batch_strong_scaling_with_idle_rank():
+    """--global_batch: the trainer's global-batch split (train_standard.sh on 8 GPUs runs batch 6
+    as 1,1,1,1,1,1,0,0); here 1 pair over 2 ranks leaves rank 1 idle -- it still joins the
+    gradient all-reduce and the optimizer step, and the job reports strong scaling."""
+    r = _bench("--gpus", "2", "--global_batch", "1", "--steps", "2")
+    assert r["scaling"] == "strong" and r["n_gpus"] == 2
+    assert r["config"]["global_batch"] == 1 and r["config"]["rank_batches"] == [1, 0]
+    assert r["vs_baseline"] is None
+    assert abs(r["value"] - 1 * 2 / (r["ms_per_step"] * 2 / 1000.0)) / r["value"] < 1e-2
