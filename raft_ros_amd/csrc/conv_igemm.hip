@@ -2323,14 +2323,20 @@ __global__ __launch_bounds__(256) void conv_flow7_kernel(const ConvFwdArgs a) {
 // (6 x 18 rows) is staged in LDS and fragment (tap, pixel) is a single ds_read_b128; B
 // fragments are 16-byte weight-row loads (k contiguous).  Operands swapped (C^T blocks) so a
 // lane holds 4 consecutive output channels of one pixel: 8-byte masked stores.
-template <bool F16>
+// NPW: output channels per wave (4 waves per workgroup).  32 (128 channels per workgroup): twice
+// the workgroups of NPW = 64 (384 -> 768 at config #2, ~1.5 -> 3 waves per SIMD), and the ReLU'
+// mask of the epilogue is loaded before the MFMAs -- the kernel is latency-bound (0.2 GFLOP,
+// 24 MB of traffic in ~30 us per call with NPW = 64).
+template <bool F16, int NPW = 32>
 __global__ __launch_bounds__(256) void conv_cin8_dgrad_kernel(const ConvFwdArgs a) {
   constexpr int TH = 4, TW = 16, HH = TH + 2, HWD = TW + 2;
+  constexpr int JB = NPW / 32;  // 32-channel blocks per wave
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) bf16x8 halo[HH * HWD + 1];  // + a zero row (tap 9)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, W = a.W;
   const int tw = (W + TW - 1) / TW, th = (H + TH - 1) / TH;
-  const int nb_tiles = (a.N + 255) / 256;
+  const int nb_tiles = (a.N + 4 * NPW - 1) / (4 * NPW);
   int bid = blockIdx.x;
   const int ntile = bid % nb_tiles;
   bid /= nb_tiles;
@@ -2348,12 +2354,12 @@ __global__ __launch_bounds__(256) void conv_cin8_dgrad_kernel(const ConvFwdArgs 
     halo[i] = v;
   }
   const int fr = lane & 31, fh = lane >> 5;
-  const int n0 = ntile * 256 + wave * 64;  // this wave's 64 output channels (2 blocks of 32)
+  const int n0 = ntile * 4 * NPW + wave * NPW;  // this wave's NPW output channels (JB blocks of 32)
   // B fragments (become the MFMA's A operand: rows = output channels): weight row n, k = kb * 16
   // + fh * 8 .. + 8 = tap 2 kb + fh, all 8 channels (taps >= 9 are zero)
-  bf16x8 wf[2][5];
+  bf16x8 wf[JB][5];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < JB; ++j) {
     const int n = n0 + j * 32 + fr;
 #pragma unroll
     for (int kb = 0; kb < 5; ++kb) {
@@ -2361,12 +2367,30 @@ __global__ __launch_bounds__(256) void conv_cin8_dgrad_kernel(const ConvFwdArgs 
       wf[j][kb] = (n < a.N && tap < 9) ? *reinterpret_cast<const bf16x8*>(a.wt + (long)n * a.Kpad + tap * 8) : bf16x8{};
     }
   }
+  // the epilogue's ReLU' mask, loaded ahead of the MFMAs (lane: pixel i * 32 + fr, channels
+  // n0 + j * 32 + 8 g + 4 fh .. + 4)
+  bf16x4 mk[2][JB][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = i * 32 + fr;
+    const int y = y0 + m / TW, x = x0 + m % TW;
+    const bool in = y < H && x < W;
+    const long p = pbase + (long)y * W + x;
+#pragma unroll
+    for (int j = 0; j < JB; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + j * 32 + 8 * g + 4 * fh;
+        mk[i][j][g] = (a.mask && in && n < a.N) ? *reinterpret_cast<const bf16x4*>(a.mask + p * a.mask_stride + n)
+                                                 : bf16x4{};
+      }
+  }
   __syncthreads();
-  f32x16 acc[2][2];  // [pixel block][channel block]
+  f32x16 acc[2][JB];  // [pixel block][channel block]
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < JB; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 #pragma unroll
@@ -2379,7 +2403,7 @@ __global__ __launch_bounds__(256) void conv_cin8_dgrad_kernel(const ConvFwdArgs 
       const int ky = tap / 3, kx = tap - (tap / 3) * 3;
       const bf16x8 xa = halo[tap < 9 ? (ty + ky) * HWD + tx + kx : HH * HWD];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = mma16<F16>(wf[j][kb], xa, acc[i][j]);
+      for (int j = 0; j < JB; ++j) acc[i][j] = mma16<F16>(wf[j][kb], xa, acc[i][j]);
     }
   }
   // lane: pixel m = i * 32 + fr, channels n0 + j * 32 + 8 g + 4 fh .. + 4 (registers 4 g .. 4 g + 3)
@@ -2390,7 +2414,7 @@ __global__ __launch_bounds__(256) void conv_cin8_dgrad_kernel(const ConvFwdArgs 
     if (y >= H || x >= W) continue;
     const long p = pbase + (long)y * W + x;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < JB; ++j)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int n = n0 + j * 32 + 8 * g + 4 * fh;
@@ -2399,16 +2423,13 @@ __global__ __launch_bounds__(256) void conv_cin8_dgrad_kernel(const ConvFwdArgs 
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * g + e] * a.alpha;
         if (a.mask) {
-          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-          const bf16x4 mk = *reinterpret_cast<const bf16x4*>(a.mask + p * a.mask_stride + n);
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            if (!(ld16(mk[e], F16) > 0.f)) v[e] = 0.f;
+            if (!(ld16(mk[i][j][g][e], F16) > 0.f)) v[e] = 0.f;
         }
         if (a.out_f32) {
           *reinterpret_cast<f32x4*>(static_cast<float*>(a.out) + p * a.out_stride + n) = f32x4{v[0], v[1], v[2], v[3]};
         } else {
-          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
           bf16x4 w;
 #pragma unroll
           for (int e = 0; e < 4; ++e) w[e] = st16(v[e], F16);
@@ -2604,7 +2625,7 @@ hipError_t conv_fwd_dispatch(const ConvFwdArgs& a, hipStream_t s) {
       a.PH == 1 && a.PW == 1 && a.src[0].stride % 8 == 0 && a.out_stride % 4 == 0 &&
       (a.mask == nullptr || a.mask_stride % 4 == 0) && a.P < (1L << 31)) {
     // narrow input (flow_head.conv2's data gradient): one-tap-pair MFMA K blocks from an LDS halo
-    const long tiles = (long)a.B * ((a.H + 3) / 4) * ((a.W + 15) / 16) * ((a.N + 255) / 256);
+    const long tiles = (long)a.B * ((a.H + 3) / 4) * ((a.W + 15) / 16) * ((a.N + 127) / 128);  // NPW = 32
     hipLaunchKernelGGL((conv_cin8_dgrad_kernel<F16>), dim3((unsigned)tiles), dim3(256), 0, s, a);
     return hipGetLastError();
   }
