@@ -1,22 +1,11 @@
-#!/bin/bash
-# Round-6 end-of-round check on the final tree: full GPU suite, smoke, config #2 and batch-1 bench.
-set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/end
-mkdir -p $OUT
+set -o pipefail
+mkdir -p gpurun_out/fb
 export PYTHONUNBUFFERED=1
-step() {
-  local name=$1 lim=$2; shift 2
-  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
-  local rc=$?
-  echo "$name rc=$rc $(grep -o '"value": [0-9.]*' $OUT/$name.log | head -1) $(tail -n 1 $OUT/$name.log | cut -c1-100)"
-  if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
-}
-step pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --tb=short --timeout 200 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step b8_a 300 python bench.py --steps 30 --warmup 5
-step b8_b 300 python bench.py --steps 30 --warmup 5
-step b1 300 python bench.py --batch 1 --image_size 368 768 --steps 100 --warmup 10
-step b6 300 python bench.py --batch 6 --image_size 368 768 --steps 20 --warmup 5
-step infer1080 300 python bench.py --mode infer --image_size 1080 1920 --iters 32 --batch 1 --steps 10 --warmup 3
-echo done
+T="timeout -k 10"
+$T 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_update_fused_gpu.py tests/test_golden_gpu.py tests/test_train_graph.py tests/test_split_train_gpu.py tests/test_model_gpu.py > gpurun_out/fb/tests.log 2>&1 || { tail -30 gpurun_out/fb/tests.log; exit 1; }
+tail -1 gpurun_out/fb/tests.log
+$T 300 python -u scripts/host_lead.py --batch 1 --image_size 368 768 --steps 30 --cprofile 20 > gpurun_out/fb/host_b1.log 2>&1 && grep -E "wall|forward|backward|fused_step_fwd}|update_fused.py.*forward" gpurun_out/fb/host_b1.log | head -8
+for r in a b; do
+$T 300 python -u bench.py --steps 30 --warmup 5 > gpurun_out/fb/b8_$r.json 2>/dev/null && grep -o '"value": [0-9.]*' gpurun_out/fb/b8_$r.json
+$T 300 python -u bench.py --batch 1 --image_size 368 768 --steps 100 --warmup 10 > gpurun_out/fb/b1_$r.json 2>/dev/null && grep -o '"value": [0-9.]*' gpurun_out/fb/b1_$r.json
+done
