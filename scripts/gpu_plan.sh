@@ -1,5 +1,8 @@
 set -o pipefail
-mkdir -p gpurun_out/conv
+mkdir -p gpurun_out/f32
 export PYTHONUNBUFFERED=1
-timeout -k 10 1000 python -u scripts/convergence.py --impl native --steps 3000 > gpurun_out/conv/native_bf16.jsonl 2> gpurun_out/conv/native_bf16.err || { tail -5 gpurun_out/conv/native_bf16.err; exit 1; }
-tail -2 gpurun_out/conv/native_bf16.jsonl
+for r in a b; do
+for v in 1 0; do
+timeout -k 10 300 env RAFT_ENC_SPLIT3=$v python -u bench.py --fp32 --steps 10 --warmup 3 > gpurun_out/f32/split3_${v}_$r.json 2>/dev/null && echo "split3=$v $(grep -o '"value": [0-9.]*' gpurun_out/f32/split3_${v}_$r.json)"
+done
+done
