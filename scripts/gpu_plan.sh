@@ -1,8 +1,5 @@
 set -o pipefail
-mkdir -p gpurun_out/f32
+mkdir -p gpurun_out/ref
 export PYTHONUNBUFFERED=1
-for r in a b; do
-for v in 1 0; do
-timeout -k 10 300 env RAFT_ENC_SPLIT3=$v python -u bench.py --fp32 --steps 10 --warmup 3 > gpurun_out/f32/split3_${v}_$r.json 2>/dev/null && echo "split3=$v $(grep -o '"value": [0-9.]*' gpurun_out/f32/split3_${v}_$r.json)"
-done
-done
+timeout -k 10 600 python -u bench.py --impl reference --steps 10 --warmup 3 > gpurun_out/ref/reference_b8.json 2> gpurun_out/ref/reference_b8.err && grep -o '"value": [0-9.]*' gpurun_out/ref/reference_b8.json
+timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 > gpurun_out/ref/native_b8.json 2>/dev/null && grep -o '"value": [0-9.]*' gpurun_out/ref/native_b8.json
